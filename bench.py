@@ -1,0 +1,264 @@
+#!/usr/bin/env python3
+"""bench.py -- MI355X merge-path fp64 SpMV (+ CG) benchmark; prints ONE JSON line on rank 0.
+
+Workload (BASELINE.json configs[1], "merge-based CSR SpMV fp64, 1 RHS, pwtk/rma10 on
+1xMI355X"): a STEP is one SpMV over each matrix of a batch of 4 distinct synthetic
+pwtk-shaped matrices (m = 217,918, nnz = 11,524,432, band +-10,000; SuiteSparse files are
+not available offline).  The batch (571 MB) exceeds the 256 MiB Infinity Cache, so every
+launch streams its matrix from HBM -- the regime the >= 70 %-of-HBM target is about.
+All inputs are resident in HBM before the timed region.
+
+  value      = 2 * nnz * batch * steps * n_gpus / max-over-ranks(time)   [GFLOP/s, whole job]
+  roofline   = algorithmic bytes per SpMV launch (12 nnz + 4 (m+1) + 8 n + 8 m)
+               / average duration of the merge-tile kernel, HIP events on its stream,
+               recorded inside the timed region; peak 8 TB/s (MI355X HBM3E)
+  cpu_baseline = the reference's own OmpMergeCsrmm(num_vectors = 1) (== cpu_spmv.cpp
+               OmpMergeCsrmv) compiled from /root/reference (oracle/_ref), else the oracle
+               port, timed on the host cores for ~10 s on matrix #0 (rank 0, N = 1 only).
+
+Multi-GPU (--gpus N via torch.distributed.run): every rank runs its own batch on its own
+GPU (weak scaling; SpMV on row blocks needs no data-path collective); gloo carries only the
+barrier and the max-over-ranks time.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "sparse-matrix-linear-equations_amd")]
+
+import mspmv  # noqa: E402
+
+METRIC = "fp64 SpMV GFLOP/s + achieved HBM GB/s vs roofline; CG iters/sec"
+HBM_PEAK_GBS = 8000.0
+PWTK = dict(m=217918, nnz=11524432, half_band=10000)
+PARABOLIC_FEM = dict(m=525825, width=725)
+NLPKKT120 = dict(dims=(160, 135, 164))
+
+
+def spmv_bytes(m, n, nnz):
+    return 12 * nnz + 4 * (m + 1) + 8 * n + 8 * m
+
+
+def cg_iter_bytes(m, nnz, L=1):
+    return 12 * nnz + 4 * (m + 1) + 88 * m * L  # compulsory bytes per CG iteration
+
+
+def glibc_rhs(seed, n):
+    """srand(seed); b[i] = rand()/RAND_MAX -- the reference's RHS (cpu_singlecg.cpp:87-90)."""
+    libc = ctypes.CDLL("libc.so.6")
+    libc.srand(ctypes.c_uint(seed))
+    r = libc.rand
+    r.restype = ctypes.c_int
+    vals = np.fromiter((r() for _ in range(n)), dtype=np.float64, count=n)
+    return vals / 2147483647.0
+
+
+class Dist:
+    def __init__(self, want):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.td = None
+        if self.world > 1:
+            import torch.distributed as td
+            td.init_process_group("gloo")
+            self.td = td
+        if want != self.world and self.rank == 0:
+            print(f"warning: --gpus {want} but WORLD_SIZE {self.world}", file=sys.stderr)
+
+    def barrier(self):
+        if self.td:
+            self.td.barrier()
+
+    def max(self, v):
+        if not self.td:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.td.all_reduce(t, op=self.td.ReduceOp.MAX)
+        return float(t.item())
+
+
+def cpu_baseline(a, x, seconds):
+    """The reference's merge CsrMV on the host cores (bounded sample)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _oracle import REF_SO, Oracle, RefLib
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    if os.path.exists(REF_SO):
+        ref = RefLib()
+        kind = "reference"
+        X = np.ascontiguousarray(x[:, None])
+        fn = lambda: ref.merge_csrmm(a, X, threads)[:, 0]  # noqa: E731
+        what = "work_2025 OmpMergeCsrmm(num_vectors=1) == cpu_spmv.cpp OmpMergeCsrmv"
+    else:
+        orc = Oracle()
+        kind = "port"
+        fn = lambda: orc.merge_csrmv(a, x, threads)  # noqa: E731
+        what = "oracle port of cpu_spmv.cpp OmpMergeCsrmv"
+    y = fn()
+    calls, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        calls += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and calls >= 3:
+            break
+    gflops = 2.0 * a.num_nonzeros * calls / el / 1e9
+    return y, {"value": round(gflops, 3), "unit": "GFLOP/s", "cores": threads, "kind": kind,
+               "sample": f"{what}, P={threads} threads, pwtk-shaped matrix #0 (nnz={a.num_nonzeros}), "
+                         f"{calls} calls in {el:.1f} s"}
+
+
+def run_cg(dev, seconds_cpu, do_cpu):
+    """parabolic_fem-shaped single CG and nlpkkt120-shaped 8-RHS CG on one GPU."""
+    out = {}
+    pf = mspmv.CsrMatrix.synth_stencil(0, PARABOLIC_FEM["m"], PARABOLIC_FEM["width"])
+    n = pf.num_rows
+    b = glibc_rhs(42, n)
+    thr = float(np.sqrt(np.sum(b * b)) * 1e-5)  # calculate_threshold quirk, cpu_singlecg.cpp:92
+    with mspmv.GpuCsr(pf, device=dev) as g:
+        db, dx = mspmv.DeviceBuffer.from_array(b, dev), mspmv.DeviceBuffer(8 * n, dev)
+        g.cg_dev(db, dx, 1, 10000, thr)                     # warm (graph, workspace)
+        t0 = time.perf_counter()
+        it, _, st = g.cg_dev(db, dx, 1, 10000, thr)
+        el = time.perf_counter() - t0
+    ips = it / el
+    out["cg_single"] = {
+        "workload": f"CGSolveSingle, parabolic_fem-shaped SPD m={n} nnz={pf.num_nonzeros}, srand(42) RHS, "
+                    f"tol quirk 1e-5*||b||",
+        "iterations": it, "seconds": round(el, 5), "iters_per_s": round(ips, 1),
+        "achieved_GBps": round(cg_iter_bytes(n, pf.num_nonzeros) * ips / 1e9, 1), "status": st}
+    if do_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from _oracle import Oracle
+        orc = Oracle()
+        k = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds_cpu:
+            orc.cg_single(pf, b, 100, thr)
+            k += 100
+        el = time.perf_counter() - t0
+        out["cg_single"]["cpu_baseline"] = {
+            "iters_per_s": round(k / el, 1), "cores": orc.lib.orc_max_threads(), "kind": "port",
+            "sample": f"oracle CGSolveSingle restatement (reference CG needs <mkl.h>), {k} iterations"}
+    nx, ny, nz = NLPKKT120["dims"]
+    nk = mspmv.CsrMatrix.synth_stencil(1, nx * ny * nz, nx, ny, nz)
+    L = 8
+    n = nk.num_rows
+    B = np.random.default_rng(42).uniform(0, 1, (n, L))
+    flat = B.reshape(-1)
+    thr = float(np.sqrt(np.sum(flat[:n] ** 2)) * 1e-5)  # calculate_threshold(b, num_rows) on the flat buffer, cpu_multicg.cpp:168
+    with mspmv.GpuCsr(nk, device=dev) as g:
+        dB, dX = mspmv.DeviceBuffer.from_array(B, dev), mspmv.DeviceBuffer(8 * n * L, dev)
+        g.cg_dev(dB, dX, L, 50000, thr)
+        t0 = time.perf_counter()
+        it, _, st = g.cg_dev(dB, dX, L, 50000, thr)
+        el = time.perf_counter() - t0
+    ips = it / el
+    out["cg_multi"] = {
+        "workload": f"CGSolveMultiple L={L}, nlpkkt120-sized 27-pt SPD m={n} nnz={nk.num_nonzeros}, 1 GPU",
+        "iterations": it, "seconds": round(el, 4), "iters_per_s": round(ips, 1),
+        "achieved_GBps": round(cg_iter_bytes(n, nk.num_nonzeros, L) * ips / 1e9, 1), "status": st}
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=4)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-cg", action="store_true")
+    args = ap.parse_args()
+
+    d = Dist(args.gpus)
+    dev = d.local
+    if mspmv.device_count() <= dev:
+        raise SystemExit(f"rank {d.rank}: no HIP device {dev}")
+
+    mats, gs, dxs, dys, xs = [], [], [], [], []
+    for i in range(args.batch):
+        a = mspmv.CsrMatrix.synth_banded(PWTK["m"], PWTK["nnz"], PWTK["half_band"], seed=1 + i + 1000 * d.rank)
+        x = np.random.default_rng(2 + i + 1000 * d.rank).uniform(0.0, 1.0, a.num_cols)
+        g = mspmv.GpuCsr(a, device=dev)
+        mats.append(a)
+        gs.append(g)
+        xs.append(x)
+        dxs.append(mspmv.DeviceBuffer.from_array(x, dev))
+        dys.append(mspmv.DeviceBuffer(8 * a.num_rows, dev))
+    a0 = mats[0]
+
+    mspmv.time_spmm_batch(gs, dxs, dys, 1, max(args.warmup, 1))   # warmup (untimed)
+    for g in gs:
+        g.sync()
+    d.barrier()
+    t0 = time.perf_counter()
+    step_ms_ev, kern_ms, kps = mspmv.time_spmm_batch(gs, dxs, dys, 1, args.steps)
+    for g in gs:
+        g.sync()
+    el = time.perf_counter() - t0
+    d.barrier()
+    el = d.max(el)
+    kern_ms = d.max(kern_ms)
+
+    flops = 2.0 * a0.num_nonzeros * args.batch * args.steps * d.world
+    value = flops / el / 1e9
+    bytes_launch = spmv_bytes(a0.num_rows, a0.num_cols, a0.num_nonzeros)
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    # hot: one matrix back to back (MALL-resident: 143 MB < 256 MiB Infinity Cache)
+    hot_ms, hot_kern, _ = mspmv.time_spmm_batch(gs[:1], dxs[:1], dys[:1], 1, 200)
+    ref_eff = (a0.num_nonzeros * 20 + a0.num_rows * 12) / (kern_ms * 1e-3) / 1e9  # cpu_spmv.cpp:722-726
+
+    result = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GFLOP/s", "n_gpus": d.world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (pwtk-shaped banded CSR, splitmix64 values; SuiteSparse unavailable offline)",
+        "config": {"workload": f"merge-path CSR SpMV fp64, 1 RHS, batch of {args.batch} pwtk-shaped matrices "
+                               f"per step per GPU (configs[1])",
+                   "m": a0.num_rows, "nnz": a0.num_nonzeros, "batch": args.batch,
+                   "parallelism": f"independent row-block batches, {d.world} GPU(s)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "k_spmv_tile<8,false>", "bytes_per_launch": bytes_launch,
+                     "kernel_ms": round(kern_ms, 5), "kernels_per_step": kps},
+        "spmv_gflops_per_launch": round(2.0 * a0.num_nonzeros / (kern_ms * 1e-3) / 1e9, 2),
+        "reference_effective_GBps": round(ref_eff, 1),
+        "hot_single_matrix": {"ms_per_call": round(hot_ms, 5), "kernel_ms": round(hot_kern, 5),
+                              "GBps_vs_algorithmic": round(bytes_launch / (hot_kern * 1e-3) / 1e9, 1),
+                              "note": "one 143 MB matrix back to back: Infinity-Cache resident, not HBM-bound"},
+        "setup_ms": round(gs[0].setup_ms, 2),
+    }
+
+    if d.rank == 0 and d.world == 1 and not args.no_cpu:
+        y_cpu, cb = cpu_baseline(a0, xs[0], args.cpu_seconds)
+        result["cpu_baseline"] = cb
+        y_gpu = dys[0].download(a0.num_rows)
+        rel = float(np.max(np.abs(y_gpu - y_cpu) / np.maximum(np.abs(y_cpu), 1e-300)))
+        result["cpu_baseline"]["gpu_vs_cpu_max_rel_diff"] = rel
+        result["speedup_vs_cpu"] = round(value / cb["value"], 1)
+    if d.rank == 0 and d.world == 1 and not args.no_cg:
+        try:
+            result.update(run_cg(dev, min(args.cpu_seconds, 10.0), not args.no_cpu))
+        except Exception as e:  # the headline line must still print
+            result["cg_error"] = repr(e)
+
+    for g in gs:
+        g.close()
+    if d.rank == 0:
+        print(json.dumps(result), flush=True)
+    if d.td:
+        d.td.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

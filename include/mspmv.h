@@ -1,0 +1,174 @@
+/*
+ * mspmv.h -- C-ABI of the MI355X-native merge-path CSR SpMV/SpMM + CG library (libmspmv.so).
+ *
+ * This is the drop-in boundary for the reference's hot path
+ * (YuyaW-0118/Sparse-Matrix-Linear-Equations).  Each entry point names the reference
+ * interface it replaces (file:line in the reference checkout).  Plain pointers and sizes
+ * only; no C++ or torch types.  The header-only C++ facade in mspmv.hpp re-exposes the
+ * reference's own template names (CsrMatrix, OmpMergeCsrmv, OmpMergeCsrmm, CGSolveSingle,
+ * CGSolveMultiple) on top of these.
+ *
+ * Types: values fp64, indices int32 -- CsrMatrix<double,int> (sparse_matrix.h:633-653).
+ * Dense multi-vector panels are ROW-MAJOR n x L (X[c*L + j]), the layout of
+ * OmpMergeCsrmm / CGSolveMultiple (merge_based.hpp:97-100, utils_multiple.hpp:17).
+ *
+ * Threading: one handle per host thread.  Work is enqueued on the handle's own HIP
+ * stream; *_dev calls are asynchronous with respect to the host (use mspmv_sync);
+ * host-pointer calls copy in, compute, copy out and return synchronously.  There is no
+ * global mutable state except the thread-local last-error string.
+ *
+ * Errors: every call returns an mspmv_status; nothing calls exit() (unlike
+ * sparse_matrix.h:232,297,305).  mspmv_last_error() describes the last failure on the
+ * calling thread.
+ */
+#ifndef MSPMV_H
+#define MSPMV_H
+
+#include <stddef.h>
+
+#ifndef MSPMV_API
+#define MSPMV_API __attribute__((visibility("default")))
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum mspmv_status {
+    MSPMV_OK = 0,
+    MSPMV_ERR_INVALID = 1,       /* bad argument / shape */
+    MSPMV_ERR_HIP = 2,           /* a HIP runtime call failed */
+    MSPMV_ERR_OOM = 3,           /* device allocation failed */
+    MSPMV_ERR_BREAKDOWN = 4,     /* CG: p.Ap <= 0 or non-finite (the reference has no guard) */
+    MSPMV_ERR_RCCL = 5,          /* a collective failed */
+    MSPMV_ERR_UNSUPPORTED = 6,   /* e.g. L outside the compiled set */
+    MSPMV_ERR_IO = 7             /* MatrixMarket read/parse failure */
+} mspmv_status;
+
+/* Mirror of CsrMatrix<double,int> fields, sparse_matrix.h:648-653.  row_offsets has
+ * num_rows+1 entries; column indices sorted within each row as CsrMatrix::Init leaves
+ * them (stable_sort by (row,col), sparse_matrix.h:680); duplicates allowed. */
+typedef struct mspmv_csr_d {
+    int num_rows;
+    int num_cols;
+    int num_nonzeros;
+    const int *row_offsets;
+    const int *column_indices;
+    const double *values;
+} mspmv_csr_d;
+
+typedef struct mspmv_handle_s *mspmv_handle;
+
+/* Merge-path coordinate (CUB CoordinateT / the reference's int2, types.hpp:3-7). */
+typedef struct mspmv_coord {
+    int x; /* row index (merge list A = row end offsets) */
+    int y; /* nonzero index (merge list B = 0..nnz-1) */
+} mspmv_coord;
+
+/* SpmmKernel (work_2025/types.hpp:11-16).  Accepted for signature compatibility; the GPU
+ * always runs its merge-path kernel. */
+typedef enum mspmv_spmm_kernel { MSPMV_SIMPLE = 0, MSPMV_MERGE = 1, MSPMV_NONZERO_SPLIT = 2 } mspmv_spmm_kernel;
+
+/* ---- library / errors -------------------------------------------------------------- */
+MSPMV_API const char *mspmv_last_error(void);
+MSPMV_API const char *mspmv_version(void);
+/* Number of visible HIP devices (0 when none; never an error). */
+MSPMV_API int mspmv_device_count(void);
+
+/* ---- matrix handle ------------------------------------------------------------------ */
+/* Upload the CSR once to HBM on `device` and build its merge-path tile plans.  Replaces
+ * the per-call partitioning of OmpMergeCsrmv (cpu_spmv.cpp:379-389) and CUB's
+ * DeviceSpmvSearchKernel (dispatch_spmv_orig.cuh:99-143): the matrix is immutable, so the
+ * partition is computed once.  `host` arrays are only read during the call. */
+MSPMV_API mspmv_status mspmv_csr_create(const mspmv_csr_d *host, int device, mspmv_handle *out);
+/* Same, from arrays already resident in HBM (copied device-to-device). */
+MSPMV_API mspmv_status mspmv_csr_create_dev(const mspmv_csr_d *dev, int device, mspmv_handle *out);
+MSPMV_API mspmv_status mspmv_destroy(mspmv_handle h);
+MSPMV_API mspmv_status mspmv_shape(mspmv_handle h, int *num_rows, int *num_cols, int *num_nonzeros);
+/* Milliseconds spent in mspmv_csr_create (upload + partition), the reference's setup_ms
+ * (cpu_spmv.cpp:715-742). */
+MSPMV_API double mspmv_setup_ms(mspmv_handle h);
+/* Block until all work enqueued on the handle's stream has finished. */
+MSPMV_API mspmv_status mspmv_sync(mspmv_handle h);
+
+/* ---- merge-path partition ----------------------------------------------------------- */
+/* Coordinates of the num_parts+1 partition boundaries exactly as OmpMergeCsrmv computes
+ * them: diagonal_t = min(ceil((m+nnz)/P) * t, m+nnz), MergePathSearch over
+ * (row_offsets+1, 0..nnz-1) (cpu_spmv.cpp:208-235, :379-389).  Computed on the GPU, one
+ * lane per diagonal; bit-exact with the reference.  `coords` has num_parts+1 entries. */
+MSPMV_API mspmv_status mspmv_merge_coords(mspmv_handle h, int num_parts, mspmv_coord *coords);
+
+/* ---- SpMV / SpMM -------------------------------------------------------------------- */
+/* y = A x   (OmpMergeCsrmv, cpu_spmv.cpp:357-421; cub::DeviceSpmv::CsrMV with alpha=1,
+ * beta=0, device_spmv.cuh:129-164).  Host pointers: x[num_cols], y[num_rows]. */
+MSPMV_API mspmv_status mspmv_dspmv(mspmv_handle h, const double *x, double *y);
+/* Device pointers, asynchronous on the handle's stream. */
+MSPMV_API mspmv_status mspmv_dspmv_dev(mspmv_handle h, const double *d_x, double *d_y);
+/* Y = A X for L right-hand sides, row-major panels (OmpMergeCsrmm, merge_based.hpp:46-153).
+ * L in {1, 2, 4, 8, 16}. */
+MSPMV_API mspmv_status mspmv_dspmm(mspmv_handle h, const double *X, double *Y, int L);
+MSPMV_API mspmv_status mspmv_dspmm_dev(mspmv_handle h, const double *d_X, double *d_Y, int L);
+
+/* ---- CG ----------------------------------------------------------------------------- */
+/* Single-RHS CG, CGSolveSingle (work_2025/main/single_strategy.hpp:102-170): x0 = 0,
+ * r = p = b; stop after the update of r when sqrt(r.r)/||b|| < tolerance, counting that
+ * iteration; ||b|| == 0 -> 1.  `tolerance` has the reference's meaning (callers such as
+ * cpu_singlecg.cpp:92,101 pass tol*||b||; that quirk is the caller's).  Returns the
+ * iteration count in *iters.  resid_hist (optional, capacity hist_cap) receives
+ * sqrt(r.r)/||b|| per iteration.  Host pointers b[n], x[n]. */
+MSPMV_API mspmv_status mspmv_dcg_single(mspmv_handle h, const double *b, double *x, int max_iters, double tolerance,
+                              int *iters, double *resid_hist, int hist_cap);
+MSPMV_API mspmv_status mspmv_dcg_single_dev(mspmv_handle h, const double *d_b, double *d_x, int max_iters, double tolerance,
+                                  int *iters, double *resid_hist, int hist_cap);
+/* Block multi-RHS CG, CGSolveMultiple (work_2025/main/no_pretreatment.hpp:32-197): L
+ * lock-step recurrences on interleaved n x L panels, per-column converged masks
+ * (alpha = beta = 0 once converged), stop when all columns converged.  max_err_hist
+ * (optional) receives the per-iteration max over ALL columns of sqrt(r.r)/||b||
+ * (:132-155).  L in {1, 2, 4, 8, 16}. */
+MSPMV_API mspmv_status mspmv_dcg_multi(mspmv_handle h, const double *B, double *X, int L, int max_iters, double tolerance,
+                             mspmv_spmm_kernel kernel, int *iters, double *max_err_hist, int hist_cap);
+MSPMV_API mspmv_status mspmv_dcg_multi_dev(mspmv_handle h, const double *d_B, double *d_X, int L, int max_iters,
+                                 double tolerance, mspmv_spmm_kernel kernel, int *iters, double *max_err_hist,
+                                 int hist_cap);
+
+/* ---- measurement helpers (HIP events on the handle's stream) ------------------------ */
+/* Enqueue `reps` back-to-back SpMV (L == 1) or SpMM launches on device buffers and return
+ * the average milliseconds per call measured by hipEvents on the handle's stream.
+ * flush_bytes > 0 inserts a write of that many bytes to a scratch buffer before every
+ * call (outside the timed events) to evict the 256 MiB Infinity Cache ("cold" protocol,
+ * SURVEY 8(d)). */
+MSPMV_API mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y, int L, int reps,
+                                 size_t flush_bytes, double *avg_ms);
+/* Batch form for benchmarks: `reps` steps, each step one SpMM launch per handle (all handles
+ * on one device), every launch enqueued on hs[0]'s stream and bracketed by HIP events.
+ * *step_ms = average event time per step; *tile_kernel_ms = average duration of one merge
+ * tile kernel launch; *kernels_per_step = launches per step (tile + fix-up kernels). */
+MSPMV_API mspmv_status mspmv_time_spmm_batch_dev(int count, const mspmv_handle *hs, const double *const *d_X,
+                                                 double *const *d_Y, int L, int reps, double *step_ms,
+                                                 double *tile_kernel_ms, int *kernels_per_step);
+/* Per-kernel average duration (ms) of the dominant (merge tile) kernel over the last
+ * mspmv_time_spmm_dev call, and the number of kernels per SpMV/SpMM call. */
+MSPMV_API mspmv_status mspmv_last_kernel_ms(mspmv_handle h, double *tile_kernel_ms, int *kernels_per_call);
+
+/* ---- diagnostics ---------------------------------------------------------------------- */
+/* The tile plan the L-column kernels use: *num_tiles tiles of nominal *tile_items merge
+ * items; `bounds` (nullable, num_tiles+1 entries) receives the boundary coordinates after
+ * row snapping, *num_carries the number of boundaries a carry crosses.  Lets tests locate
+ * exactly which rows are split between threads (those are within tolerance, the rest are
+ * bit-identical to SpmvGold). */
+MSPMV_API mspmv_status mspmv_tile_plan(mspmv_handle h, int L, int *num_tiles, int *tile_items, int *num_carries,
+                                       mspmv_coord *bounds);
+
+/* ---- device memory helpers (so hosts need no HIP headers) ---------------------------- */
+MSPMV_API mspmv_status mspmv_device_malloc(int device, size_t bytes, void **d_ptr);
+MSPMV_API mspmv_status mspmv_device_free(void *d_ptr);
+MSPMV_API mspmv_status mspmv_memcpy_h2d(void *d_dst, const void *h_src, size_t bytes);
+MSPMV_API mspmv_status mspmv_memcpy_d2h(void *h_dst, const void *d_src, size_t bytes);
+MSPMV_API mspmv_status mspmv_memcpy_d2d(void *d_dst, const void *d_src, size_t bytes);
+MSPMV_API mspmv_status mspmv_memset_dev(void *d_dst, int byte_value, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MSPMV_H */

@@ -1,0 +1,44 @@
+/*
+ * mspmv_synth.h -- deterministic synthetic CSR generators for the benchmark shapes
+ * (SURVEY 8(d)): SuiteSparse matrices are not available offline, so bench.py and the
+ * tests build matrices of the same shapes.  Host-only (OpenMP), part of libmspmv.so.
+ * Every value is a pure function of (seed, index) via splitmix64, independent of the
+ * thread count.
+ */
+#ifndef MSPMV_SYNTH_H
+#define MSPMV_SYNTH_H
+
+#include "mspmv.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Banded non-symmetric pattern (cant / pwtk / rma10 shapes): exactly `nnz` nonzeros, row i
+ * holding floor((i+1)nnz/m) - floor(i nnz/m) of them, one per equal slice of the band
+ * [i-half_band, i+half_band] (clamped), so columns are unique and sorted; values
+ * U(0.5, 1.5).  Arrays: row_offsets[m+1], cols[nnz], vals[nnz] (caller-allocated).
+ * Requires half_band >= the longest row. */
+MSPMV_API mspmv_status mspmv_synth_banded(int m, long long nnz, int half_band, unsigned long long seed, int *row_offsets,
+                                int *cols, double *vals);
+
+/* Power-law row lengths with the same contract as mspmv_synth_banded: row lengths drawn
+ * from a Zipf-like law (a handful of rows hold a large share of nnz), columns spread over
+ * the whole matrix.  Exercises merge-path load balance and long-row carries. */
+MSPMV_API mspmv_status mspmv_synth_powerlaw(int m, int n, long long nnz, double exponent, unsigned long long seed,
+                                  int *row_offsets, int *cols, double *vals);
+
+/* SPD stencils (symmetric pattern, off-diagonals -U(0,1) symmetric in (i,j), diagonal =
+ * sum|off| + 1 -> strictly diagonally dominant).
+ *   kind 0: 2-D 7-point triangular-mesh stencil (P1 FEM; parabolic_fem shape) on a grid
+ *           `dim0` wide with m points in row-major order (last grid row may be partial);
+ *   kind 1: 3-D 27-point stencil on dim0 x dim1 x dim2 (nlpkkt120-sized, made SPD).
+ * Call with row_offsets only (cols/vals NULL) to size: fills row_offsets and *nnz_out. */
+MSPMV_API mspmv_status mspmv_synth_stencil(int kind, int m, int dim0, int dim1, int dim2, unsigned long long seed,
+                                 int *row_offsets, int *cols, double *vals, long long *nnz_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MSPMV_SYNTH_H */

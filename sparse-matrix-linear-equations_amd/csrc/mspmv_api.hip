@@ -1,0 +1,890 @@
+// mspmv_api.hip -- the C-ABI (include/mspmv.h): matrix handles, tile plans, SpMV/SpMM
+// entry points, and the CG drivers.  Host C++17 over the HIP runtime.
+#include "mspmv_internal.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+namespace mspmv {
+
+static thread_local std::string g_err;
+
+void set_error(const std::string &msg) { g_err = msg; }
+
+hipError_t launch_flush(void *p, size_t bytes, hipStream_t s);
+
+}  // namespace mspmv
+
+using namespace mspmv;
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess) {                                                                    \
+            set_error(std::string(#expr) + ": " + hipGetErrorString(_e));                          \
+            return (_e == hipErrorOutOfMemory) ? MSPMV_ERR_OOM : MSPMV_ERR_HIP;                    \
+        }                                                                                          \
+    } while (0)
+
+#define ST_TRY(expr)                                                                               \
+    do {                                                                                           \
+        mspmv_status _s = (expr);                                                                  \
+        if (_s != MSPMV_OK)                                                                        \
+            return _s;                                                                             \
+    } while (0)
+
+static mspmv_status invalid(const std::string &msg)
+{
+    set_error(msg);
+    return MSPMV_ERR_INVALID;
+}
+
+template <typename T>
+static mspmv_status dev_alloc(T **p, size_t count)
+{
+    *p = nullptr;
+    if (count == 0)
+        count = 1;
+    hipError_t e = hipMalloc((void **)p, count * sizeof(T));
+    if (e != hipSuccess) {
+        set_error(std::string("hipMalloc(") + std::to_string(count * sizeof(T)) + " B): " + hipGetErrorString(e));
+        *p = nullptr;
+        return e == hipErrorOutOfMemory ? MSPMV_ERR_OOM : MSPMV_ERR_HIP;
+    }
+    return MSPMV_OK;
+}
+
+template <typename T>
+static void dev_free(T *&p)
+{
+    if (p)
+        (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+__global__ void k_check_cols(const int *__restrict__ cols, long long nnz, int n, int *bad)
+{
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nnz; i += (long long)gridDim.x * blockDim.x) {
+        const int c = cols[i];
+        if (c < 0 || c >= n)
+            atomicOr(bad, 1);
+    }
+}
+
+static void free_plan(TilePlan &p)
+{
+    dev_free(p.d_bounds);
+    dev_free(p.d_split);
+    dev_free(p.d_carry_tiles);
+    dev_free(p.d_carry_rows);
+    dev_free(p.d_carry_val);
+}
+
+// Build (once) the tile plan for L right-hand sides, validating on the host every bound the
+// kernels rely on (monotone boundaries, <= 1.5 * tile_items merge items per tile) before any
+// tile kernel can run on it.
+static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out)
+{
+    const int tile = tile_items_for(L);
+    auto it = h->plans.find(tile);
+    if (it != h->plans.end()) {
+        *out = &it->second;
+        return MSPMV_OK;
+    }
+    TilePlan p;
+    p.tile_items = tile;
+    p.snap = tile / 2;
+    const long long total = (long long)h->m + h->nnz;
+    p.num_tiles = (int)((total + tile - 1) / tile);
+    const int T = p.num_tiles;
+    mspmv_status st;
+    if ((st = dev_alloc(&p.d_bounds, (size_t)T + 1)) != MSPMV_OK ||
+        (st = dev_alloc(&p.d_split, (size_t)T + 1)) != MSPMV_OK ||
+        (st = dev_alloc(&p.d_carry_val, (size_t)std::max(T, 1) * 16)) != MSPMV_OK) {
+        free_plan(p);
+        return st;
+    }
+    p.carry_L = 16;
+    auto fail = [&](mspmv_status s) {
+        free_plan(p);
+        return s;
+    };
+    hipError_t e = launch_merge_coords(h->d_row_offsets, h->m, h->nnz, tile, T, p.d_bounds, h->stream);
+    if (e == hipSuccess)
+        e = launch_snap(h->d_row_offsets, h->m, p.d_bounds, p.d_split, T, p.snap, h->stream);
+    std::vector<int2> hb((size_t)T + 1);
+    std::vector<unsigned char> hs((size_t)T + 1);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(hb.data(), p.d_bounds, sizeof(int2) * (T + 1), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(hs.data(), p.d_split, T + 1, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) {
+        set_error(std::string("tile plan: ") + hipGetErrorString(e));
+        return fail(MSPMV_ERR_HIP);
+    }
+    const int maxi = tile + tile / 2;
+    if (hb[0].x != 0 || hb[0].y != 0 || hb[T].x != h->m || hb[T].y != h->nnz) {
+        set_error("tile plan: bad end boundaries");
+        return fail(MSPMV_ERR_INVALID);
+    }
+    std::vector<int> ct, cr;
+    for (int t = 0; t < T; ++t) {
+        const int nr = hb[t + 1].x - hb[t].x, nz = hb[t + 1].y - hb[t].y;
+        if (nr < 0 || nz < 0 || nr + nz > maxi) {
+            set_error("tile plan: tile " + std::to_string(t) + " violates the merge bound");
+            return fail(MSPMV_ERR_INVALID);
+        }
+        if (hs[t + 1]) {
+            ct.push_back(t);
+            cr.push_back(hb[t + 1].x);
+        }
+    }
+    p.num_carries = (int)ct.size();
+    if (p.num_carries) {
+        if ((st = dev_alloc(&p.d_carry_tiles, ct.size())) != MSPMV_OK ||
+            (st = dev_alloc(&p.d_carry_rows, cr.size())) != MSPMV_OK)
+            return fail(st);
+        e = hipMemcpy(p.d_carry_tiles, ct.data(), sizeof(int) * ct.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(p.d_carry_rows, cr.data(), sizeof(int) * cr.size(), hipMemcpyHostToDevice);
+        if (e != hipSuccess) {
+            set_error(std::string("tile plan upload: ") + hipGetErrorString(e));
+            return fail(MSPMV_ERR_HIP);
+        }
+    }
+    auto res = h->plans.emplace(tile, p);
+    *out = &res.first->second;
+    return MSPMV_OK;
+}
+
+static mspmv_status validate_host_csr(const mspmv_csr_d *a)
+{
+    if (!a)
+        return invalid("null matrix");
+    if (a->num_rows < 0 || a->num_cols < 0 || a->num_nonzeros < 0)
+        return invalid("negative dimension");
+    if ((long long)a->num_rows + a->num_nonzeros > 0x7fffffffLL)
+        return invalid("num_rows + num_nonzeros must fit in int32 (merge-path diagonals)");
+    if (!a->row_offsets || (a->num_nonzeros > 0 && (!a->column_indices || !a->values)))
+        return invalid("null CSR array");
+    return MSPMV_OK;
+}
+
+static mspmv_status check_offsets_host(const int *ro, int m, int nnz)
+{
+    if (ro[0] != 0)
+        return invalid("row_offsets[0] != 0");
+    for (int i = 0; i < m; ++i)
+        if (ro[i + 1] < ro[i])
+            return invalid("row_offsets not monotone at row " + std::to_string(i));
+    if (ro[m] != nnz)
+        return invalid("row_offsets[num_rows] != num_nonzeros");
+    return MSPMV_OK;
+}
+
+static mspmv_status create_common(const mspmv_csr_d *a, int device, bool from_device, mspmv_handle *out)
+{
+    ST_TRY(validate_host_csr(a));
+    if (!out)
+        return invalid("null out handle");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+        set_error("no HIP device visible");
+        return MSPMV_ERR_HIP;
+    }
+    if (device < 0 || device >= ndev)
+        return invalid("device index out of range");
+    HIP_TRY(hipSetDevice(device));
+    const auto t0 = std::chrono::steady_clock::now();
+    auto *h = new mspmv_handle_s();
+    h->device = device;
+    h->m = a->num_rows;
+    h->n = a->num_cols;
+    h->nnz = a->num_nonzeros;
+    auto fail = [&](mspmv_status s) {
+        mspmv_destroy(h);
+        return s;
+    };
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        set_error("hipStreamCreate failed");
+        return fail(MSPMV_ERR_HIP);
+    }
+    mspmv_status st;
+    if ((st = dev_alloc(&h->d_row_offsets, (size_t)h->m + 1)) != MSPMV_OK ||
+        (st = dev_alloc(&h->d_cols, (size_t)h->nnz)) != MSPMV_OK ||
+        (st = dev_alloc(&h->d_vals, (size_t)h->nnz)) != MSPMV_OK)
+        return fail(st);
+    const hipMemcpyKind kind = from_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    std::vector<int> host_ro;
+    const int *ro = a->row_offsets;
+    if (from_device) {
+        host_ro.resize((size_t)h->m + 1);
+        if (hipMemcpy(host_ro.data(), a->row_offsets, sizeof(int) * (h->m + 1), hipMemcpyDeviceToHost) != hipSuccess) {
+            set_error("copy of device row_offsets failed");
+            return fail(MSPMV_ERR_HIP);
+        }
+        ro = host_ro.data();
+    }
+    if ((st = check_offsets_host(ro, h->m, h->nnz)) != MSPMV_OK)
+        return fail(st);
+    if (hipMemcpy(h->d_row_offsets, a->row_offsets, sizeof(int) * (h->m + 1), kind) != hipSuccess ||
+        (h->nnz && hipMemcpy(h->d_cols, a->column_indices, sizeof(int) * (size_t)h->nnz, kind) != hipSuccess) ||
+        (h->nnz && hipMemcpy(h->d_vals, a->values, sizeof(double) * (size_t)h->nnz, kind) != hipSuccess)) {
+        set_error("CSR upload failed");
+        return fail(MSPMV_ERR_HIP);
+    }
+    if (h->nnz) {  // column range check on the device (a bad index would fault a gather)
+        int *d_bad = nullptr;
+        if ((st = dev_alloc(&d_bad, 1)) != MSPMV_OK)
+            return fail(st);
+        int bad = 0;
+        hipError_t e = hipMemset(d_bad, 0, sizeof(int));
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_check_cols, dim3(1024), dim3(256), 0, h->stream, h->d_cols, (long long)h->nnz, h->n,
+                               d_bad);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(h->stream);
+        if (e == hipSuccess)
+            e = hipMemcpy(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost);
+        dev_free(d_bad);
+        if (e != hipSuccess) {
+            set_error(std::string("column check: ") + hipGetErrorString(e));
+            return fail(MSPMV_ERR_HIP);
+        }
+        if (bad)
+            return fail(invalid("column index out of [0, num_cols)"));
+    }
+    const TilePlan *plan = nullptr;
+    if ((st = get_plan(h, 1, &plan)) != MSPMV_OK)
+        return fail(st);
+    if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
+        set_error("hipEventCreate failed");
+        return fail(MSPMV_ERR_HIP);
+    }
+    if (hipStreamSynchronize(h->stream) != hipSuccess) {
+        set_error("setup sync failed");
+        return fail(MSPMV_ERR_HIP);
+    }
+    h->setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    *out = h;
+    return MSPMV_OK;
+}
+
+static mspmv_status check_handle(mspmv_handle h)
+{
+    if (!h)
+        return invalid("null handle");
+    HIP_TRY(hipSetDevice(h->device));
+    return MSPMV_OK;
+}
+
+static bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
+
+extern "C" {
+
+const char *mspmv_last_error(void) { return g_err.c_str(); }
+
+const char *mspmv_version(void) { return "mspmv 0.1.0 (gfx950, merge-path fp64)"; }
+
+int mspmv_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess)
+        return 0;
+    return n;
+}
+
+mspmv_status mspmv_csr_create(const mspmv_csr_d *host, int device, mspmv_handle *out)
+{
+    return create_common(host, device, false, out);
+}
+
+mspmv_status mspmv_csr_create_dev(const mspmv_csr_d *dev, int device, mspmv_handle *out)
+{
+    return create_common(dev, device, true, out);
+}
+
+mspmv_status mspmv_destroy(mspmv_handle h)
+{
+    if (!h)
+        return MSPMV_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream)
+        (void)hipStreamSynchronize(h->stream);
+    for (auto &kv : h->plans)
+        free_plan(kv.second);
+    dev_free(h->d_row_offsets);
+    dev_free(h->d_cols);
+    dev_free(h->d_vals);
+    dev_free(h->d_r);
+    dev_free(h->d_p0);
+    dev_free(h->d_p1);
+    dev_free(h->d_ap);
+    dev_free(h->d_partials);
+    dev_free(h->d_scal);
+    dev_free(h->d_conv);
+    dev_free(h->d_ctrl);
+    dev_free(h->d_hist);
+    if (h->d_flush)
+        (void)hipFree(h->d_flush);
+    if (h->h_ctrl)
+        (void)hipHostFree(h->h_ctrl);
+    if (h->ev0)
+        (void)hipEventDestroy(h->ev0);
+    if (h->ev1)
+        (void)hipEventDestroy(h->ev1);
+    if (h->stream)
+        (void)hipStreamDestroy(h->stream);
+    delete h;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_shape(mspmv_handle h, int *num_rows, int *num_cols, int *num_nonzeros)
+{
+    if (!h)
+        return invalid("null handle");
+    if (num_rows)
+        *num_rows = h->m;
+    if (num_cols)
+        *num_cols = h->n;
+    if (num_nonzeros)
+        *num_nonzeros = h->nnz;
+    return MSPMV_OK;
+}
+
+double mspmv_setup_ms(mspmv_handle h) { return h ? h->setup_ms : 0.0; }
+
+mspmv_status mspmv_sync(mspmv_handle h)
+{
+    ST_TRY(check_handle(h));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_merge_coords(mspmv_handle h, int num_parts, mspmv_coord *coords)
+{
+    ST_TRY(check_handle(h));
+    if (num_parts < 1 || !coords)
+        return invalid("num_parts must be >= 1 and coords non-null");
+    const long long total = (long long)h->m + h->nnz;
+    const long long step = (total + num_parts - 1) / num_parts;  // cpu_spmv.cpp:379
+    int2 *d = nullptr;
+    ST_TRY(dev_alloc(&d, (size_t)num_parts + 1));
+    hipError_t e = launch_merge_coords(h->d_row_offsets, h->m, h->nnz, step, num_parts, d, h->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(coords, d, sizeof(int2) * (num_parts + 1), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(h->stream);
+    dev_free(d);
+    if (e != hipSuccess) {
+        set_error(std::string("merge coords: ") + hipGetErrorString(e));
+        return MSPMV_ERR_HIP;
+    }
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_dspmm_dev(mspmv_handle h, const double *d_X, double *d_Y, int L)
+{
+    ST_TRY(check_handle(h));
+    if (!supported_L(L))
+        return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
+    if (h->m > 0 && (!d_X || !d_Y))
+        return invalid("null vector");
+    if (L > 1 && (!aligned16(d_X) || !aligned16(d_Y)))
+        return invalid("multi-vector panels must be 16-byte aligned");
+    if (h->m == 0)
+        return MSPMV_OK;
+    const TilePlan *plan = nullptr;
+    ST_TRY(get_plan(h, L, &plan));
+    int nk = 0;
+    HIP_TRY(launch_spmm(h, *plan, d_X, d_Y, L, &nk));
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_dspmv_dev(mspmv_handle h, const double *d_x, double *d_y)
+{
+    return mspmv_dspmm_dev(h, d_x, d_y, 1);
+}
+
+mspmv_status mspmv_dspmm(mspmv_handle h, const double *X, double *Y, int L)
+{
+    ST_TRY(check_handle(h));
+    if (!supported_L(L))
+        return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
+    if (h->m == 0)
+        return MSPMV_OK;
+    if (!X || !Y)
+        return invalid("null vector");
+    double *dX = nullptr, *dY = nullptr;
+    ST_TRY(dev_alloc(&dX, (size_t)h->n * L));
+    mspmv_status st = dev_alloc(&dY, (size_t)h->m * L);
+    if (st == MSPMV_OK) {
+        hipError_t e = hipMemcpyAsync(dX, X, sizeof(double) * h->n * L, hipMemcpyHostToDevice, h->stream);
+        if (e != hipSuccess) {
+            set_error(hipGetErrorString(e));
+            st = MSPMV_ERR_HIP;
+        }
+    }
+    if (st == MSPMV_OK)
+        st = mspmv_dspmm_dev(h, dX, dY, L);
+    if (st == MSPMV_OK) {
+        hipError_t e = hipMemcpyAsync(Y, dY, sizeof(double) * h->m * L, hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) {
+            set_error(hipGetErrorString(e));
+            st = MSPMV_ERR_HIP;
+        }
+    }
+    dev_free(dX);
+    dev_free(dY);
+    return st;
+}
+
+mspmv_status mspmv_dspmv(mspmv_handle h, const double *x, double *y) { return mspmv_dspmm(h, x, y, 1); }
+
+// ---- CG ------------------------------------------------------------------------------------
+static mspmv_status ensure_cg_workspace(mspmv_handle_s *h, int L, int nblk, int num_tiles, int hist_cap)
+{
+    const size_t elems = (size_t)h->m * L;
+    if (elems > h->cg_cap_elems) {
+        dev_free(h->d_r);
+        dev_free(h->d_p0);
+        dev_free(h->d_p1);
+        dev_free(h->d_ap);
+        h->cg_cap_elems = 0;
+        ST_TRY(dev_alloc(&h->d_r, elems));
+        ST_TRY(dev_alloc(&h->d_p0, elems));
+        ST_TRY(dev_alloc(&h->d_p1, elems));
+        ST_TRY(dev_alloc(&h->d_ap, elems));
+        h->cg_cap_elems = elems;
+    }
+    const size_t pcap = (size_t)std::max(nblk, num_tiles) * L;
+    if (pcap > h->partials_cap) {
+        dev_free(h->d_partials);
+        h->partials_cap = 0;
+        ST_TRY(dev_alloc(&h->d_partials, pcap));
+        h->partials_cap = pcap;
+    }
+    if (L > h->scal_cap) {
+        dev_free(h->d_scal);
+        dev_free(h->d_conv);
+        h->scal_cap = 0;
+        ST_TRY(dev_alloc(&h->d_scal, (size_t)L));
+        ST_TRY(dev_alloc(&h->d_conv, (size_t)L));
+        h->scal_cap = L;
+    }
+    if (!h->d_ctrl)
+        ST_TRY(dev_alloc(&h->d_ctrl, 1));
+    if (!h->h_ctrl)
+        HIP_TRY(hipHostMalloc((void **)&h->h_ctrl, sizeof(CgControl) * 2, hipHostMallocDefault));
+    if (hist_cap > h->hist_cap) {
+        dev_free(h->d_hist);
+        h->hist_cap = 0;
+        ST_TRY(dev_alloc(&h->d_hist, (size_t)hist_cap));
+        h->hist_cap = hist_cap;
+    }
+    return MSPMV_OK;
+}
+
+static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d_x, int L, int max_iters,
+                                 double tol, int *iters, double *hist, int hist_cap)
+{
+    if (h->m != h->n)
+        return invalid("CG needs a square matrix");
+    if (!supported_L(L))
+        return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
+    if (max_iters < 0)
+        return invalid("max_iters < 0");
+    if (h->m > 0 && (!d_b || !d_x))
+        return invalid("null vector");
+    if (!aligned16(d_b) || !aligned16(d_x))
+        return invalid("CG vectors must be 16-byte aligned");
+    if (iters)
+        *iters = 0;
+    if (h->m == 0)
+        return MSPMV_OK;
+    const TilePlan *plan = nullptr;
+    ST_TRY(get_plan(h, L, &plan));
+    const int nblk = cg_update_blocks((long long)h->m * L);
+    const int cap = hist ? std::max(hist_cap, 0) : 0;
+    ST_TRY(ensure_cg_workspace(h, L, nblk, plan->num_tiles, cap));
+    const int use_cap = hist ? cap : 0;
+    const int saved_cap = h->hist_cap;
+    h->hist_cap = use_cap;  // kernels record only what the caller asked for
+    HIP_TRY(hipMemsetAsync(h->d_ctrl, 0, sizeof(CgControl), h->stream));
+    HIP_TRY(launch_cg_init(h, d_b, d_x, L, tol, nblk));
+
+    constexpr int K = 32;  // iterations per graph replay (even: p buffers alternate)
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    mspmv_status st = MSPMV_OK;
+    if (max_iters >= K) {
+        hipError_t e = hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal);
+        for (int i = 0; i < K && e == hipSuccess; ++i)
+            e = launch_cg_iteration(h, *plan, d_x, L, i & 1, nblk, tol);
+        hipError_t e2 = hipStreamEndCapture(h->stream, &graph);
+        if (e == hipSuccess)
+            e = e2;
+        if (e == hipSuccess)
+            e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+        if (e != hipSuccess) {
+            set_error(std::string("CG graph capture: ") + hipGetErrorString(e));
+            st = MSPMV_ERR_HIP;
+        }
+    }
+    hipEvent_t evs[2] = {nullptr, nullptr};
+    if (st == MSPMV_OK && (hipEventCreateWithFlags(&evs[0], hipEventDisableTiming) != hipSuccess ||
+                           hipEventCreateWithFlags(&evs[1], hipEventDisableTiming) != hipSuccess)) {
+        set_error("hipEventCreate failed");
+        st = MSPMV_ERR_HIP;
+    }
+    // Pipelined: batch b+1 is queued before batch b's control word is inspected, so the GPU
+    // never idles on the host check; after convergence at most one batch of kernels runs,
+    // each returning at its first instruction (the `done` test).
+    int launched = 0, pending = 0, oldest = 0, slot = 0;
+    while (st == MSPMV_OK) {
+        const int k = std::min(K, max_iters - launched);
+        if (k > 0) {
+            hipError_t e = hipSuccess;
+            if (k == K && exec)
+                e = hipGraphLaunch(exec, h->stream);
+            else
+                for (int i = 0; i < k && e == hipSuccess; ++i)
+                    e = launch_cg_iteration(h, *plan, d_x, L, i & 1, nblk, tol);
+            if (e == hipSuccess)
+                e = hipMemcpyAsync(&h->h_ctrl[slot], h->d_ctrl, sizeof(CgControl), hipMemcpyDeviceToHost, h->stream);
+            if (e == hipSuccess)
+                e = hipEventRecord(evs[slot], h->stream);
+            if (e != hipSuccess) {
+                set_error(std::string("CG launch: ") + hipGetErrorString(e));
+                st = MSPMV_ERR_HIP;
+                break;
+            }
+            launched += k;
+            ++pending;
+            slot ^= 1;
+        }
+        if (pending == 0)
+            break;
+        if (pending == 2 || k <= 0) {
+            if (hipEventSynchronize(evs[oldest]) != hipSuccess) {
+                set_error("CG event sync failed");
+                st = MSPMV_ERR_HIP;
+                break;
+            }
+            --pending;
+            const bool done = h->h_ctrl[oldest].done != 0;
+            oldest ^= 1;
+            if (done)
+                break;
+        }
+    }
+    hipError_t e = hipStreamSynchronize(h->stream);
+    CgControl fin{};
+    if (e == hipSuccess)
+        e = hipMemcpy(&fin, h->d_ctrl, sizeof(CgControl), hipMemcpyDeviceToHost);
+    if (st == MSPMV_OK && e != hipSuccess) {
+        set_error(std::string("CG finish: ") + hipGetErrorString(e));
+        st = MSPMV_ERR_HIP;
+    }
+    for (auto &ev : evs)
+        if (ev)
+            (void)hipEventDestroy(ev);
+    if (exec)
+        (void)hipGraphExecDestroy(exec);
+    if (graph)
+        (void)hipGraphDestroy(graph);
+    h->hist_cap = saved_cap;
+    if (st != MSPMV_OK)
+        return st;
+    const int it = fin.done ? fin.iters_out : fin.iter;
+    if (iters)
+        *iters = it;
+    if (hist && use_cap > 0) {
+        const int nh = std::min(it, use_cap);
+        if (nh > 0)
+            HIP_TRY(hipMemcpy(hist, h->d_hist, sizeof(double) * nh, hipMemcpyDeviceToHost));
+    }
+    if (fin.breakdown) {
+        set_error("CG breakdown: p.Ap gave a non-finite alpha at iteration " + std::to_string(it));
+        return MSPMV_ERR_BREAKDOWN;
+    }
+    return MSPMV_OK;
+}
+
+static mspmv_status cg_solve_host(mspmv_handle h, const double *B, double *X, int L, int max_iters, double tol,
+                                  int *iters, double *hist, int hist_cap)
+{
+    ST_TRY(check_handle(h));
+    if (h->m == 0) {
+        if (iters)
+            *iters = 0;
+        return MSPMV_OK;
+    }
+    if (!B || !X)
+        return invalid("null vector");
+    double *dB = nullptr, *dX = nullptr;
+    const size_t bytes = sizeof(double) * (size_t)h->m * L;
+    ST_TRY(dev_alloc(&dB, (size_t)h->m * L));
+    mspmv_status st = dev_alloc(&dX, (size_t)h->m * L);
+    if (st == MSPMV_OK && hipMemcpy(dB, B, bytes, hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("B upload failed");
+        st = MSPMV_ERR_HIP;
+    }
+    if (st == MSPMV_OK)
+        st = cg_solve_dev(h, dB, dX, L, max_iters, tol, iters, hist, hist_cap);
+    if ((st == MSPMV_OK || st == MSPMV_ERR_BREAKDOWN) && hipMemcpy(X, dX, bytes, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error("X download failed");
+        st = MSPMV_ERR_HIP;
+    }
+    dev_free(dB);
+    dev_free(dX);
+    return st;
+}
+
+mspmv_status mspmv_dcg_single_dev(mspmv_handle h, const double *d_b, double *d_x, int max_iters, double tolerance,
+                                  int *iters, double *resid_hist, int hist_cap)
+{
+    ST_TRY(check_handle(h));
+    return cg_solve_dev(h, d_b, d_x, 1, max_iters, tolerance, iters, resid_hist, hist_cap);
+}
+
+mspmv_status mspmv_dcg_single(mspmv_handle h, const double *b, double *x, int max_iters, double tolerance,
+                              int *iters, double *resid_hist, int hist_cap)
+{
+    return cg_solve_host(h, b, x, 1, max_iters, tolerance, iters, resid_hist, hist_cap);
+}
+
+mspmv_status mspmv_dcg_multi_dev(mspmv_handle h, const double *d_B, double *d_X, int L, int max_iters,
+                                 double tolerance, mspmv_spmm_kernel kernel, int *iters, double *max_err_hist,
+                                 int hist_cap)
+{
+    (void)kernel;  // the GPU always runs the merge-path SpMM
+    ST_TRY(check_handle(h));
+    return cg_solve_dev(h, d_B, d_X, L, max_iters, tolerance, iters, max_err_hist, hist_cap);
+}
+
+mspmv_status mspmv_dcg_multi(mspmv_handle h, const double *B, double *X, int L, int max_iters, double tolerance,
+                             mspmv_spmm_kernel kernel, int *iters, double *max_err_hist, int hist_cap)
+{
+    (void)kernel;
+    if (!supported_L(L))
+        return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
+    return cg_solve_host(h, B, X, L, max_iters, tolerance, iters, max_err_hist, hist_cap);
+}
+
+// ---- measurement ---------------------------------------------------------------------------
+mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y, int L, int reps,
+                                 size_t flush_bytes, double *avg_ms)
+{
+    ST_TRY(check_handle(h));
+    if (reps < 1 || !avg_ms)
+        return invalid("reps >= 1 and avg_ms required");
+    if (!supported_L(L))
+        return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
+    if (L > 1 && (!aligned16(d_X) || !aligned16(d_Y)))
+        return invalid("multi-vector panels must be 16-byte aligned");
+    const TilePlan *plan = nullptr;
+    ST_TRY(get_plan(h, L, &plan));
+    if (flush_bytes && flush_bytes > h->flush_cap) {
+        if (h->d_flush)
+            (void)hipFree(h->d_flush);
+        h->d_flush = nullptr;
+        h->flush_cap = 0;
+        HIP_TRY(hipMalloc(&h->d_flush, flush_bytes));
+        h->flush_cap = flush_bytes;
+    }
+    std::vector<hipEvent_t> ev((size_t)reps * 2 + 2, nullptr);
+    for (auto &e : ev)
+        HIP_TRY(hipEventCreate(&e));
+    hipError_t e = hipSuccess;
+    for (int i = 0; i < reps && e == hipSuccess; ++i) {
+        if (flush_bytes)
+            e = launch_flush(h->d_flush, flush_bytes, h->stream);
+        if (e == hipSuccess)
+            e = hipEventRecord(ev[2 * i], h->stream);
+        if (e == hipSuccess)
+            e = launch_spmm_tile_only(h, *plan, d_X, d_Y, L);
+        if (e == hipSuccess)
+            e = hipEventRecord(ev[2 * i + 1], h->stream);
+        if (e == hipSuccess)
+            e = launch_fixup(h, *plan, d_Y, L);
+    }
+    if (e == hipSuccess)
+        e = hipEventRecord(ev[2 * reps], h->stream);
+    if (e == hipSuccess)
+        e = hipEventSynchronize(ev[2 * reps]);
+    double sum_tile = 0.0;
+    float ms = 0.f;
+    for (int i = 0; i < reps && e == hipSuccess; ++i) {
+        e = hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]);
+        sum_tile += ms;
+    }
+    float total = 0.f;
+    if (e == hipSuccess)
+        e = hipEventElapsedTime(&total, ev[0], ev[2 * reps]);
+    for (auto &x : ev)
+        (void)hipEventDestroy(x);
+    if (e != hipSuccess) {
+        set_error(std::string("timing: ") + hipGetErrorString(e));
+        return MSPMV_ERR_HIP;
+    }
+    h->last_tile_kernel_ms = sum_tile / reps;
+    h->last_kernels_per_call = 1 + (plan->num_carries ? 1 : 0);
+    *avg_ms = (double)total / reps;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_time_spmm_batch_dev(int count, const mspmv_handle *hs, const double *const *d_X,
+                                       double *const *d_Y, int L, int reps, double *step_ms, double *tile_kernel_ms,
+                                       int *kernels_per_step)
+{
+    if (count < 1 || !hs || !d_X || !d_Y || reps < 1 || !step_ms)
+        return invalid("bad batch timing arguments");
+    if (!supported_L(L))
+        return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
+    for (int i = 0; i < count; ++i) {
+        ST_TRY(check_handle(hs[i]));
+        if (hs[i]->device != hs[0]->device)
+            return invalid("batch handles must share a device");
+        if (L > 1 && (!aligned16(d_X[i]) || !aligned16(d_Y[i])))
+            return invalid("multi-vector panels must be 16-byte aligned");
+    }
+    ST_TRY(check_handle(hs[0]));
+    std::vector<const TilePlan *> plans(count);
+    int kps = 0;
+    for (int i = 0; i < count; ++i) {
+        ST_TRY(get_plan(hs[i], L, &plans[i]));
+        kps += (plans[i]->num_tiles ? 1 : 0) + (plans[i]->num_carries ? 1 : 0);
+    }
+    hipStream_t s = hs[0]->stream;
+    for (int i = 0; i < count; ++i)  // everything after this point is ordered on hs[0]'s stream
+        HIP_TRY(hipStreamSynchronize(hs[i]->stream));
+    const size_t nev = (size_t)reps * count * 2 + 2;
+    std::vector<hipEvent_t> ev(nev, nullptr);
+    for (auto &e : ev)
+        HIP_TRY(hipEventCreate(&e));
+    hipError_t e = hipEventRecord(ev[nev - 2], s);
+    size_t k = 0;
+    for (int r = 0; r < reps && e == hipSuccess; ++r)
+        for (int i = 0; i < count && e == hipSuccess; ++i) {
+            hipStream_t own = hs[i]->stream;
+            hs[i]->stream = s;
+            e = hipEventRecord(ev[k++], s);
+            if (e == hipSuccess)
+                e = launch_spmm_tile_only(hs[i], *plans[i], d_X[i], d_Y[i], L);
+            if (e == hipSuccess)
+                e = hipEventRecord(ev[k++], s);
+            if (e == hipSuccess)
+                e = launch_fixup(hs[i], *plans[i], d_Y[i], L);
+            hs[i]->stream = own;
+        }
+    if (e == hipSuccess)
+        e = hipEventRecord(ev[nev - 1], s);
+    if (e == hipSuccess)
+        e = hipEventSynchronize(ev[nev - 1]);
+    double sum = 0.0;
+    float ms = 0.f;
+    for (size_t j = 0; j + 1 < k && e == hipSuccess; j += 2) {
+        e = hipEventElapsedTime(&ms, ev[j], ev[j + 1]);
+        sum += ms;
+    }
+    float total = 0.f;
+    if (e == hipSuccess)
+        e = hipEventElapsedTime(&total, ev[nev - 2], ev[nev - 1]);
+    for (auto &x : ev)
+        (void)hipEventDestroy(x);
+    if (e != hipSuccess) {
+        set_error(std::string("batch timing: ") + hipGetErrorString(e));
+        return MSPMV_ERR_HIP;
+    }
+    *step_ms = (double)total / reps;
+    if (tile_kernel_ms)
+        *tile_kernel_ms = sum / ((double)reps * count);
+    if (kernels_per_step)
+        *kernels_per_step = kps;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_last_kernel_ms(mspmv_handle h, double *tile_kernel_ms, int *kernels_per_call)
+{
+    if (!h)
+        return invalid("null handle");
+    if (tile_kernel_ms)
+        *tile_kernel_ms = h->last_tile_kernel_ms;
+    if (kernels_per_call)
+        *kernels_per_call = h->last_kernels_per_call;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_tile_plan(mspmv_handle h, int L, int *num_tiles, int *tile_items, int *num_carries,
+                             mspmv_coord *bounds)
+{
+    ST_TRY(check_handle(h));
+    if (!supported_L(L))
+        return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
+    const TilePlan *plan = nullptr;
+    ST_TRY(get_plan(h, L, &plan));
+    if (num_tiles)
+        *num_tiles = plan->num_tiles;
+    if (tile_items)
+        *tile_items = plan->tile_items;
+    if (num_carries)
+        *num_carries = plan->num_carries;
+    if (bounds)
+        HIP_TRY(hipMemcpy(bounds, plan->d_bounds, sizeof(int2) * (plan->num_tiles + 1), hipMemcpyDeviceToHost));
+    return MSPMV_OK;
+}
+
+// ---- device memory helpers -----------------------------------------------------------------
+mspmv_status mspmv_device_malloc(int device, size_t bytes, void **d_ptr)
+{
+    if (!d_ptr)
+        return invalid("null out pointer");
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipMalloc(d_ptr, bytes ? bytes : 1));
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_device_free(void *d_ptr)
+{
+    if (d_ptr)
+        HIP_TRY(hipFree(d_ptr));
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_memcpy_h2d(void *d_dst, const void *h_src, size_t bytes)
+{
+    HIP_TRY(hipMemcpy(d_dst, h_src, bytes, hipMemcpyHostToDevice));
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_memcpy_d2h(void *h_dst, const void *d_src, size_t bytes)
+{
+    HIP_TRY(hipMemcpy(h_dst, d_src, bytes, hipMemcpyDeviceToHost));
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_memcpy_d2d(void *d_dst, const void *d_src, size_t bytes)
+{
+    HIP_TRY(hipMemcpy(d_dst, d_src, bytes, hipMemcpyDeviceToDevice));
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_memset_dev(void *d_dst, int byte_value, size_t bytes)
+{
+    HIP_TRY(hipMemset(d_dst, byte_value, bytes));
+    return MSPMV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,113 @@
+// mspmv_internal.h -- shared between the HIP kernels (mspmv_kernels.hip) and the C-ABI
+// implementation (mspmv_api.hip).  Not installed; the public boundary is include/mspmv.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <string>
+#include <vector>
+
+#include "mspmv.h"
+
+namespace mspmv {
+
+constexpr int kBlock = 256;  // 4 x 64-lane waves per workgroup
+
+// A merge-path tile plan for one nominal tile size (merge items per tile).
+//
+// Tile t covers the merge-path diagonals between boundary t and t+1.  A boundary whose
+// row was entered by at most `snap` nonzeros is moved back to that row's start ("row
+// snapped"): the row is then computed whole by the tile that completes it, so no carry
+// crosses that boundary.  Boundaries deeper inside a long row stay exact merge-path
+// coordinates ("split") and the tile before them writes a carry that a small fix-up
+// kernel adds in tile order.  Every tile holds at most tile_items + snap merge items.
+struct TilePlan {
+    int tile_items = 0;
+    int snap = 0;
+    int num_tiles = 0;
+    int2 *d_bounds = nullptr;           // [num_tiles+1] (row, nnz) boundary coordinates
+    unsigned char *d_split = nullptr;   // [num_tiles+1] 1 = split boundary (carry crosses it)
+    int num_carries = 0;                // tiles whose trailing boundary is split
+    int *d_carry_tiles = nullptr;       // [num_carries] tile ids, ascending
+    int *d_carry_rows = nullptr;        // [num_carries] row each carry belongs to
+    double *d_carry_val = nullptr;      // [num_tiles * L_max]
+    int carry_L = 0;                    // capacity (columns) of d_carry_val
+};
+
+// Device-resident CG scalars (one set per right-hand side column).
+struct CgScalars {
+    double rs_old;
+    double b_norm;
+    double alpha;
+    double beta;
+    double pAp;
+    double rs_new;
+};
+
+struct CgControl {
+    int iter;        // iterations completed
+    int done;        // 1 once every column converged (or breakdown)
+    int iters_out;   // iteration count to report (the reference's return value)
+    int breakdown;   // 1 if p.Ap <= 0 or non-finite was met
+    unsigned ticket_a;
+    unsigned ticket_b;
+    unsigned ticket_i;
+    unsigned pad;
+};
+
+}  // namespace mspmv
+
+struct mspmv_handle_s {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int m = 0, n = 0, nnz = 0;
+    int *d_row_offsets = nullptr;
+    int *d_cols = nullptr;
+    double *d_vals = nullptr;
+    double setup_ms = 0.0;
+    std::map<int, mspmv::TilePlan> plans;  // by nominal tile size
+    // CG workspace (grown on demand)
+    size_t cg_cap_elems = 0;
+    double *d_r = nullptr, *d_p0 = nullptr, *d_p1 = nullptr, *d_ap = nullptr;
+    double *d_partials = nullptr;
+    size_t partials_cap = 0;
+    mspmv::CgScalars *d_scal = nullptr;
+    unsigned char *d_conv = nullptr;   // per-column converged flags
+    mspmv::CgControl *d_ctrl = nullptr;
+    mspmv::CgControl *h_ctrl = nullptr;  // pinned mirror
+    double *d_hist = nullptr;
+    int hist_cap = 0;
+    int scal_cap = 0;
+    // timing
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    double last_tile_kernel_ms = 0.0;
+    int last_kernels_per_call = 1;
+    void *d_flush = nullptr;
+    size_t flush_cap = 0;
+};
+
+namespace mspmv {
+
+// ---- launchers (mspmv_kernels.hip) --------------------------------------------------
+void set_error(const std::string &msg);
+hipError_t launch_merge_coords(const int *d_row_offsets, int m, int nnz, long long diag_step, int num_parts,
+                               int2 *d_out, hipStream_t s);
+hipError_t launch_snap(const int *d_row_offsets, int m, int2 *d_bounds, unsigned char *d_split, int num_tiles,
+                       int snap, hipStream_t s);
+// y = A x (L == 1) or Y = A X (row-major panels), tile kernel + optional carry fix-up.
+hipError_t launch_spmm(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
+                       int *kernels_launched);
+hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L);
+hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L);
+// Nominal tile size (merge items per tile) used for L right-hand sides.
+int tile_items_for(int L);
+bool supported_L(int L);
+
+// CG pieces
+hipError_t launch_cg_init(mspmv_handle_s *h, const double *d_b, double *d_x, int L, double tol, int nblk);
+hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *d_x, int L, int parity, int nblk,
+                               double tol);
+int cg_update_blocks(long long elems);
+
+}  // namespace mspmv

@@ -1,0 +1,980 @@
+// mspmv_kernels.hip -- hand-written gfx950 (CDNA4) kernels for merge-path CSR SpMV/SpMM and
+// the fused CG iteration.  Compiled with -ffp-contract=off: every a*b+c is two roundings, as
+// in the reference built for the x86-64 baseline ISA, so rows that no tile/thread boundary
+// splits are bit-identical to SpmvGold (cpu_spmv.cpp:241-265).
+//
+// Algorithm (Merrill & Garland merge-path, re-derived for 64-lane waves):
+//   * the (row-end-offsets x nnz-index) merge path is cut into tiles of `tile_items` merge
+//     items at setup (k_merge_coords + k_snap, once per matrix -- the matrix is immutable);
+//   * one 256-thread workgroup per tile stages the tile's row end offsets and its
+//     products val*x[col] (SpMV) or its (col, val) pairs (SpMM) in LDS with fully
+//     coalesced loads, then every thread (SpMV) or every group of L/2 lanes (SpMM, one
+//     double2 of the row-major panel per lane) runs its own merge-path search in LDS and
+//     walks an equal share of merge items;
+//   * rows split between threads are closed in LDS in thread order; rows split between
+//     tiles (only inside rows longer than the snap distance) are closed by k_fixup in
+//     tile order.  All reductions are fixed-order: results are run-to-run deterministic.
+//   * tiles are dealt XCD-contiguously (blocks b and b+8 share an XCD), so each XCD's L2
+//     sees one contiguous band of x / X.
+#include "mspmv_internal.h"
+
+#include <cstdio>
+
+namespace mspmv {
+
+// ------------------------------------------------------------------------------------------
+// helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int xcd_tile(int b, int T)
+{
+    // Blocks are dealt round-robin over the 8 XCDs; give XCD k (= b % 8, a label only) the
+    // contiguous tile range [k*q + min(k,r), +q + (k<r)).  Bijective for any T.
+    const int q = T >> 3, r = T & 7;
+    const int k = b & 7, i = b >> 3;
+    return k * q + (k < r ? k : r) + i;
+}
+
+__device__ __forceinline__ void store_sc1(double *p, double v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double load_sc1(const double *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Merge-path search (cpu_spmv.cpp:208-235 semantics) over an LDS copy of the tile's row
+// end offsets, stored relative to the tile's first nonzero; list B is 0..b_len-1.
+__device__ __forceinline__ void lds_search(int d, const int *s_rowend, int a_len, int b_len, int &x, int &y)
+{
+    int lo = d - b_len > 0 ? d - b_len : 0;
+    int hi = d < a_len ? d : a_len;
+    while (lo < hi) {
+        const int pivot = (lo + hi) >> 1;
+        if (s_rowend[pivot] <= d - pivot - 1)
+            lo = pivot + 1;
+        else
+            hi = pivot;
+    }
+    x = lo;
+    y = d - lo;
+}
+
+// Lane 0 of each wave holds a deterministic butterfly sum; wave totals are combined in
+// wave order.  Call uniformly from every thread of the block; returns the total in all.
+__device__ __forceinline__ double block_sum(double v, double *s_red)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        v += __shfl_xor(v, off);
+    __syncthreads();  // s_red may still be read by a previous call
+    if ((threadIdx.x & 63) == 0)
+        s_red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = s_red[0];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w)
+        t += s_red[w];
+    return t;
+}
+
+// ------------------------------------------------------------------------------------------
+// partition: the reference's partition coordinates and the tile plan boundaries
+// ------------------------------------------------------------------------------------------
+__global__ void k_merge_coords(const int *__restrict__ row_offsets, int m, int nnz, long long step, int num_parts,
+                               int2 *__restrict__ out)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > num_parts)
+        return;
+    const long long total = (long long)m + nnz;
+    long long dl = step * (long long)t;
+    const int d = (int)(dl < total ? dl : total);
+    const int *a = row_offsets + 1;
+    int lo = d - nnz > 0 ? d - nnz : 0;
+    int hi = d < m ? d : m;
+    while (lo < hi) {
+        const int pivot = (lo + hi) >> 1;
+        if (a[pivot] <= d - pivot - 1)
+            lo = pivot + 1;
+        else
+            hi = pivot;
+    }
+    out[t] = make_int2(lo < m ? lo : m, d - lo);
+}
+
+__global__ void k_snap(const int *__restrict__ row_offsets, int m, int2 *__restrict__ b,
+                       unsigned char *__restrict__ split, int T, int snap)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > T)
+        return;
+    int2 c = b[t];
+    unsigned char s = 0;
+    if (t > 0 && t < T && c.x < m) {
+        const int start = row_offsets[c.x];
+        if (c.y - start <= snap)
+            c.y = start;  // row entered by <= snap nonzeros: the completing tile takes it whole
+        else
+            s = 1;        // deep inside a long row: exact merge coordinate, carry crosses it
+    }
+    b[t] = c;
+    split[t] = s;
+}
+
+// ------------------------------------------------------------------------------------------
+// tile kernels
+// ------------------------------------------------------------------------------------------
+struct TileArgs {
+    const int *__restrict__ row_offsets;
+    const int *__restrict__ cols;
+    const double *__restrict__ vals;
+    const double *__restrict__ x;      // SpMV/SpMM: x / X.   CG: r (residual)
+    const double *__restrict__ p_old;  // CG: previous search direction
+    double *__restrict__ p_new;        // CG: p = r + beta p, written for the tile's rows
+    double *__restrict__ y;            // SpMV/SpMM: y / Y.   CG: Ap
+    const int2 *__restrict__ bounds;
+    const unsigned char *__restrict__ split;
+    double *__restrict__ carry_val;
+    int num_tiles;
+    CgScalars *scal;                   // CG: per-column scalars
+    CgControl *ctrl;                   // CG: iteration control
+    const unsigned char *conv;         // CG: per-column converged flags
+    double *partials;                  // CG: per-tile partial dots [tile][L]
+};
+
+// Single right-hand side.  TILE = 256*IPT merge items nominal, up to 1.5*TILE after snapping.
+// CG: gathers p = r + beta*p_old on the fly (UpdatePSingle, single_strategy.hpp:89-97, fused
+// into the SpMV), writes p for its rows, Ap, and p.Ap by linearity; the last tile reduces
+// the partials in tile order and sets alpha = rs_old / pAp (single_strategy.hpp:140-141).
+template <int IPT, bool CG>
+__global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
+{
+    constexpr int TILE = kBlock * IPT;
+    constexpr int MAXI = TILE + TILE / 2;
+    constexpr int MAXJ = MAXI / kBlock;
+    __shared__ int s_rowend[MAXI];
+    __shared__ double s_prod[MAXI];
+    __shared__ int s_crow[kBlock];
+    __shared__ double s_cval[kBlock];
+    __shared__ double s_red[kBlock / 64];
+    __shared__ int s_last;
+
+    const int tid = threadIdx.x;
+    if (CG && a.ctrl->done)
+        return;
+    const int t = xcd_tile(blockIdx.x, a.num_tiles);
+    const int2 b0 = a.bounds[t];
+    const int2 b1 = a.bounds[t + 1];
+    const int r0 = b0.x, n0 = b0.y;
+    const int nrows = b1.x - r0;
+    const int nnzt = b1.y - n0;
+    const int items = nrows + nnzt;
+    const double beta = CG ? a.scal[0].beta : 0.0;
+
+    for (int i = tid; i < nrows; i += kBlock)
+        s_rowend[i] = a.row_offsets[r0 + 1 + i] - n0;
+    {
+        int c[MAXJ];
+        double v[MAXJ];
+#pragma unroll
+        for (int j = 0; j < MAXJ; ++j) {
+            const int k = tid + j * kBlock;
+            if (k < nnzt) {
+                c[j] = __builtin_nontemporal_load(a.cols + n0 + k);
+                v[j] = __builtin_nontemporal_load(a.vals + n0 + k);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < MAXJ; ++j) {
+            const int k = tid + j * kBlock;
+            if (k < nnzt) {
+                double xv = a.x[c[j]];
+                if (CG)
+                    xv = xv + beta * a.p_old[c[j]];
+                s_prod[k] = v[j] * xv;
+            }
+        }
+    }
+    __syncthreads();
+
+    const int ipt = (items + kBlock - 1) / kBlock;
+    const int d0 = min(tid * ipt, items);
+    const int d1 = min(d0 + ipt, items);
+    int cx, cy, ex, ey;
+    lds_search(d0, s_rowend, nrows, nnzt, cx, cy);
+    lds_search(d1, s_rowend, nrows, nnzt, ex, ey);
+    // Does this thread's first row hold nonzeros that earlier threads of the tile consumed?
+    const bool need_cin = (cx < ex) && (cy > (cx == 0 ? 0 : s_rowend[cx - 1]));
+
+    double dot = 0.0;
+    auto write_row = [&](int row, double val) {
+        const int R = r0 + row;
+        a.y[R] = val;
+        if (CG) {
+            const double pn = a.x[R] + beta * a.p_old[R];
+            a.p_new[R] = pn;
+            dot += pn * val;
+        }
+    };
+
+    double run = 0.0;
+    bool first = true, pend = false;
+    int prow = 0;
+    double pval = 0.0;
+    for (int k = cy; k < ey; ++k) {
+        while (cx < ex && s_rowend[cx] <= k) {
+            if (first && need_cin) {
+                pend = true;
+                prow = cx;
+                pval = run;
+            } else {
+                write_row(cx, run);
+            }
+            first = false;
+            run = 0.0;
+            ++cx;
+        }
+        run += s_prod[k];
+    }
+    while (cx < ex) {
+        if (first && need_cin) {
+            pend = true;
+            prow = cx;
+            pval = run;
+        } else {
+            write_row(cx, run);
+        }
+        first = false;
+        run = 0.0;
+        ++cx;
+    }
+    s_crow[tid] = ex;
+    s_cval[tid] = run;
+    __syncthreads();
+
+    if (pend) {  // close the row begun by earlier threads, summing their carries in thread order
+        int j0 = tid - 1;
+        while (j0 > 0 && s_crow[j0 - 1] == prow)
+            --j0;
+        double acc = s_cval[j0];
+        for (int u = j0 + 1; u < tid; ++u)
+            acc += s_cval[u];
+        write_row(prow, acc + pval);
+    }
+    if (tid == kBlock - 1 && a.split[t + 1]) {  // the tile's trailing partial row -> carry
+        int j0 = kBlock - 1;
+        while (j0 > 0 && s_crow[j0 - 1] == nrows)
+            --j0;
+        double acc = s_cval[j0];
+        for (int u = j0 + 1; u < kBlock; ++u)
+            acc += s_cval[u];
+        a.carry_val[t] = acc;
+        if (CG) {
+            const int R = r0 + nrows;
+            const double pn = a.x[R] + beta * a.p_old[R];
+            dot += pn * acc;
+        }
+    }
+
+    if (CG) {
+        const double tsum = block_sum(dot, s_red);
+        if (tid == 0) {
+            store_sc1(&a.partials[t], tsum);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned tk =
+                __hip_atomic_fetch_add(&a.ctrl->ticket_a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = (tk == gridDim.x - 1);
+        }
+        __syncthreads();
+        if (s_last) {
+            double v = 0.0;
+            for (int i = tid; i < a.num_tiles; i += kBlock)
+                v += load_sc1(&a.partials[i]);
+            const double pAp = block_sum(v, s_red);
+            if (tid == 0) {
+                __hip_atomic_store(&a.ctrl->ticket_a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                CgScalars &s = a.scal[0];
+                s.pAp = pAp;
+                const double alpha = a.conv[0] ? 0.0 : s.rs_old / pAp;
+                s.alpha = alpha;
+                if (!a.conv[0] && !(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
+                    a.ctrl->breakdown = 1;
+                    a.ctrl->done = 1;
+                    a.ctrl->iters_out = a.ctrl->iter + 1;
+                }
+            }
+        }
+    }
+}
+
+// Multi right-hand side (L = 2..16, row-major panels).  A group of L/2 lanes owns one merge
+// walk; each lane keeps a double2 of the L running totals (running_total[L],
+// merge_based.hpp:84-127).  TILE = (256/(L/2)) groups * IPTG items.
+template <int L, int IPTG, bool CG>
+__global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
+{
+    constexpr int GL = L / 2;
+    constexpr int NG = kBlock / GL;
+    constexpr int TILE = NG * IPTG;
+    constexpr int MAXI = TILE + TILE / 2;
+    constexpr int MAXJ = (MAXI + NG - 1) / NG;
+    constexpr int STG = (MAXI + kBlock - 1) / kBlock;
+    __shared__ int s_rowend[MAXI];
+    __shared__ int s_col[MAXI];
+    __shared__ double s_val[MAXI];
+    __shared__ int s_crow[NG];
+    __shared__ double2 s_cval[NG * GL];
+    __shared__ double2 s_red2[kBlock / 64][GL];
+    __shared__ int s_last;
+
+    const int tid = threadIdx.x;
+    const int g = tid / GL;
+    const int lane = tid % GL;
+    if (CG && a.ctrl->done)
+        return;
+    const int t = xcd_tile(blockIdx.x, a.num_tiles);
+    const int2 b0 = a.bounds[t];
+    const int2 b1 = a.bounds[t + 1];
+    const int r0 = b0.x, n0 = b0.y;
+    const int nrows = b1.x - r0;
+    const int nnzt = b1.y - n0;
+    const int items = nrows + nnzt;
+    double2 beta2 = make_double2(0.0, 0.0);
+    if (CG)
+        beta2 = make_double2(a.scal[2 * lane].beta, a.scal[2 * lane + 1].beta);
+
+    for (int i = tid; i < nrows; i += kBlock)
+        s_rowend[i] = a.row_offsets[r0 + 1 + i] - n0;
+#pragma unroll
+    for (int j = 0; j < STG; ++j) {
+        const int k = tid + j * kBlock;
+        if (k < nnzt) {
+            s_col[k] = __builtin_nontemporal_load(a.cols + n0 + k);
+            s_val[k] = __builtin_nontemporal_load(a.vals + n0 + k);
+        }
+    }
+    __syncthreads();
+
+    const int ipt = (items + NG - 1) / NG;
+    const int d0 = min(g * ipt, items);
+    const int d1 = min(d0 + ipt, items);
+    int cx, cy, ex, ey;
+    lds_search(d0, s_rowend, nrows, nnzt, cx, cy);
+    lds_search(d1, s_rowend, nrows, nnzt, ex, ey);
+    const bool need_cin = (cx < ex) && (cy > (cx == 0 ? 0 : s_rowend[cx - 1]));
+
+    // Gather this walk's panel rows up front (<= MAXJ independent 16-B loads in flight).
+    double2 xr[MAXJ];
+    double vv[MAXJ];
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+        const int k = cy + j;
+        if (k < ey) {
+            const int c = s_col[k];
+            vv[j] = s_val[k];
+            const size_t off = (size_t)c * L + 2 * lane;
+            double2 xv = *reinterpret_cast<const double2 *>(a.x + off);
+            if (CG) {
+                const double2 po = *reinterpret_cast<const double2 *>(a.p_old + off);
+                xv.x = xv.x + beta2.x * po.x;
+                xv.y = xv.y + beta2.y * po.y;
+            }
+            xr[j] = xv;
+        }
+    }
+
+    double2 dot = make_double2(0.0, 0.0);
+    auto write_row = [&](int row, double2 val) {
+        const size_t off = (size_t)(r0 + row) * L + 2 * lane;
+        *reinterpret_cast<double2 *>(a.y + off) = val;
+        if (CG) {
+            const double2 rr = *reinterpret_cast<const double2 *>(a.x + off);
+            const double2 po = *reinterpret_cast<const double2 *>(a.p_old + off);
+            double2 pn;
+            pn.x = rr.x + beta2.x * po.x;
+            pn.y = rr.y + beta2.y * po.y;
+            *reinterpret_cast<double2 *>(a.p_new + off) = pn;
+            dot.x += pn.x * val.x;
+            dot.y += pn.y * val.y;
+        }
+    };
+
+    double2 run = make_double2(0.0, 0.0);
+    bool first = true, pend = false;
+    int prow = 0;
+    double2 pval = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+        const int k = cy + j;
+        if (k < ey) {
+            while (cx < ex && s_rowend[cx] <= k) {
+                if (first && need_cin) {
+                    pend = true;
+                    prow = cx;
+                    pval = run;
+                } else {
+                    write_row(cx, run);
+                }
+                first = false;
+                run = make_double2(0.0, 0.0);
+                ++cx;
+            }
+            run.x += vv[j] * xr[j].x;
+            run.y += vv[j] * xr[j].y;
+        }
+    }
+    while (cx < ex) {
+        if (first && need_cin) {
+            pend = true;
+            prow = cx;
+            pval = run;
+        } else {
+            write_row(cx, run);
+        }
+        first = false;
+        run = make_double2(0.0, 0.0);
+        ++cx;
+    }
+    if (lane == 0)
+        s_crow[g] = ex;
+    s_cval[g * GL + lane] = run;
+    __syncthreads();
+
+    if (pend) {
+        int j0 = g - 1;
+        while (j0 > 0 && s_crow[j0 - 1] == prow)
+            --j0;
+        double2 acc = s_cval[j0 * GL + lane];
+        for (int u = j0 + 1; u < g; ++u) {
+            const double2 c = s_cval[u * GL + lane];
+            acc.x += c.x;
+            acc.y += c.y;
+        }
+        acc.x += pval.x;
+        acc.y += pval.y;
+        write_row(prow, acc);
+    }
+    if (g == NG - 1 && a.split[t + 1]) {
+        int j0 = NG - 1;
+        while (j0 > 0 && s_crow[j0 - 1] == nrows)
+            --j0;
+        double2 acc = s_cval[j0 * GL + lane];
+        for (int u = j0 + 1; u < NG; ++u) {
+            const double2 c = s_cval[u * GL + lane];
+            acc.x += c.x;
+            acc.y += c.y;
+        }
+        *reinterpret_cast<double2 *>(a.carry_val + (size_t)t * L + 2 * lane) = acc;
+        if (CG) {
+            const size_t off = (size_t)(r0 + nrows) * L + 2 * lane;
+            const double2 rr = *reinterpret_cast<const double2 *>(a.x + off);
+            const double2 po = *reinterpret_cast<const double2 *>(a.p_old + off);
+            dot.x += (rr.x + beta2.x * po.x) * acc.x;
+            dot.y += (rr.y + beta2.y * po.y) * acc.y;
+        }
+    }
+
+    if (CG) {
+        // Reduce the per-lane column partials over the groups (lanes with equal tid % GL).
+#pragma unroll
+        for (int off = 32; off >= GL; off >>= 1) {
+            dot.x += __shfl_xor(dot.x, off);
+            dot.y += __shfl_xor(dot.y, off);
+        }
+        if ((tid & 63) < GL)
+            s_red2[tid >> 6][lane] = dot;
+        __syncthreads();
+        if (tid < GL) {
+            double2 tsum = s_red2[0][tid];
+#pragma unroll
+            for (int w = 1; w < kBlock / 64; ++w) {
+                tsum.x += s_red2[w][tid].x;
+                tsum.y += s_red2[w][tid].y;
+            }
+            store_sc1(&a.partials[(size_t)t * L + 2 * tid], tsum.x);
+            store_sc1(&a.partials[(size_t)t * L + 2 * tid + 1], tsum.y);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const unsigned tk =
+                __hip_atomic_fetch_add(&a.ctrl->ticket_a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_last = (tk == gridDim.x - 1);
+        }
+        __syncthreads();
+        if (s_last) {
+            // column j = tid % L, tiles strided by kBlock / L -- fixed order per column
+            constexpr int TPC = kBlock / L;
+            const int j = tid % L;
+            const int q = tid / L;
+            double v = 0.0;
+            for (int i = q; i < a.num_tiles; i += TPC)
+                v += load_sc1(&a.partials[(size_t)i * L + j]);
+            __shared__ double s_colred[kBlock];
+            s_colred[tid] = v;
+            __syncthreads();
+            if (tid < L) {
+                double pAp = s_colred[tid];
+                for (int u = 1; u < TPC; ++u)
+                    pAp += s_colred[u * L + tid];
+                CgScalars &s = a.scal[tid];
+                s.pAp = pAp;
+                const bool cv = a.conv[tid];
+                const double alpha = cv ? 0.0 : s.rs_old / pAp;
+                s.alpha = alpha;
+                if (!cv && !(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
+                    a.ctrl->breakdown = 1;
+                    a.ctrl->done = 1;
+                    a.ctrl->iters_out = a.ctrl->iter + 1;
+                }
+            }
+            if (tid == 0)
+                __hip_atomic_store(&a.ctrl->ticket_a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+// Rows split between tiles: y[R] = (carry_a + carry_a+1 + ...) + y[R], carries in tile order.
+// One thread per (carry, column); the first carry of each row's run sums the run.
+__global__ void k_fixup(const int *__restrict__ carry_tiles, const int *__restrict__ carry_rows, int nc,
+                        const double *__restrict__ carry_val, double *__restrict__ Y, int L,
+                        const CgControl *ctrl)
+{
+    if (ctrl && ctrl->done)
+        return;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = idx / L, j = idx % L;
+    if (i >= nc)
+        return;
+    const int R = carry_rows[i];
+    if (i > 0 && carry_rows[i - 1] == R)
+        return;
+    double sum = carry_val[(size_t)carry_tiles[i] * L + j];
+    for (int u = i + 1; u < nc && carry_rows[u] == R; ++u)
+        sum += carry_val[(size_t)carry_tiles[u] * L + j];
+    Y[(size_t)R * L + j] = sum + Y[(size_t)R * L + j];
+}
+
+// ------------------------------------------------------------------------------------------
+// CG: init and the fused update (x += alpha p; r += (-alpha) Ap; r.r; stop test; beta)
+// ------------------------------------------------------------------------------------------
+// Column-pair partial sums of a grid-stride loop over n*L elements viewed as pairs.  Each
+// thread always meets the same column pair because the stride (in pairs) is a multiple of
+// L/2 (L/2 divides 256).  For L == 1 the "pair" is two consecutive rows of one column.
+template <int L>
+__device__ __forceinline__ void colpair_block_reduce(double2 v, double2 (*s_red2)[L > 1 ? L / 2 : 1],
+                                                     double *partials_row)
+{
+    constexpr int GL = L > 1 ? L / 2 : 1;
+    const int tid = threadIdx.x;
+    if (L == 1)
+        v.x += v.y;
+#pragma unroll
+    for (int off = 32; off >= GL; off >>= 1) {
+        v.x += __shfl_xor(v.x, off);
+        if (L > 1)
+            v.y += __shfl_xor(v.y, off);
+    }
+    if ((tid & 63) < GL)
+        s_red2[tid >> 6][tid & 63] = v;
+    __syncthreads();
+    if (tid < GL) {
+        double2 s = s_red2[0][tid];
+#pragma unroll
+        for (int w = 1; w < kBlock / 64; ++w) {
+            s.x += s_red2[w][tid].x;
+            s.y += s_red2[w][tid].y;
+        }
+        if (L == 1) {
+            store_sc1(&partials_row[0], s.x);
+        } else {
+            store_sc1(&partials_row[2 * tid], s.x);
+            store_sc1(&partials_row[2 * tid + 1], s.y);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
+// Last block: reduce partials[nblk][L] per column in block order into out[j].
+template <int L>
+__device__ __forceinline__ void reduce_partials_cols(const double *partials, int nblk, double *s_colred,
+                                                     double *out_cols)
+{
+    constexpr int TPC = kBlock / L;
+    const int tid = threadIdx.x;
+    const int j = tid % L, q = tid / L;
+    double v = 0.0;
+    for (int i = q; i < nblk; i += TPC)
+        v += load_sc1(&partials[(size_t)i * L + j]);
+    s_colred[tid] = v;
+    __syncthreads();
+    if (tid < L) {
+        double s = s_colred[tid];
+        for (int u = 1; u < TPC; ++u)
+            s += s_colred[u * L + tid];
+        out_cols[tid] = s;
+    }
+    __syncthreads();
+}
+
+struct CgVecArgs {
+    long long n_elems;       // n * L
+    double *x;
+    double *r;
+    const double *p;         // CG init: b.  update: p_new
+    double *p0;              // init: p0 = b
+    const double *ap;
+    CgScalars *scal;
+    CgControl *ctrl;
+    unsigned char *conv;
+    double *partials;
+    double *hist;
+    int hist_cap;
+    double tol;
+};
+
+// x = 0, r = p0 = b; rs_old_j = r_j.r_j, b_norm_j = sqrt(b_j.b_j) (no_pretreatment.hpp:61-79,
+// single_strategy.hpp:120-131).
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_cg_init(CgVecArgs a)
+{
+    constexpr int GL = L > 1 ? L / 2 : 1;
+    __shared__ double2 s_red2[kBlock / 64][GL];
+    __shared__ double s_colred[kBlock];
+    __shared__ double s_out[L];
+    __shared__ int s_last;
+    const int tid = threadIdx.x;
+    const long long npairs = a.n_elems / 2;
+    const long long stride = (long long)gridDim.x * kBlock;
+    double2 acc = make_double2(0.0, 0.0);
+    for (long long i = (long long)blockIdx.x * kBlock + tid; i < npairs; i += stride) {
+        const double2 b = reinterpret_cast<const double2 *>(a.p)[i];
+        reinterpret_cast<double2 *>(a.x)[i] = make_double2(0.0, 0.0);
+        reinterpret_cast<double2 *>(a.r)[i] = b;
+        reinterpret_cast<double2 *>(a.p0)[i] = b;
+        acc.x += b.x * b.x;
+        acc.y += b.y * b.y;
+    }
+    if ((a.n_elems & 1) && blockIdx.x == 0 && tid == 0) {  // L == 1 with odd n
+        const long long i = a.n_elems - 1;
+        const double b = a.p[i];
+        a.x[i] = 0.0;
+        a.r[i] = b;
+        a.p0[i] = b;
+        acc.x += b * b;
+    }
+    colpair_block_reduce<L>(acc, s_red2, a.partials + (size_t)blockIdx.x * L);
+    if (tid == 0) {
+        const unsigned tk = __hip_atomic_fetch_add(&a.ctrl->ticket_i, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (tk == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (s_last) {
+        reduce_partials_cols<L>(a.partials, gridDim.x, s_colred, s_out);
+        if (tid < L) {
+            CgScalars &s = a.scal[tid];
+            const double bb = s_out[tid];
+            s.rs_old = bb;
+            double bn = sqrt(bb);
+            s.b_norm = bn == 0.0 ? 1.0 : bn;
+            s.alpha = 0.0;
+            s.beta = 0.0;
+            s.pAp = 0.0;
+            s.rs_new = 0.0;
+            a.conv[tid] = 0;
+        }
+        if (tid == 0) {
+            __hip_atomic_store(&a.ctrl->ticket_i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a.ctrl->iter = 0;
+            a.ctrl->done = 0;
+            a.ctrl->iters_out = 0;
+            a.ctrl->breakdown = 0;
+        }
+    }
+}
+
+// x += alpha p (AxpySingle / axpy_multiple), r += (-alpha) Ap, rs_new = r.r, then on the last
+// block: convergence with the reference's masks, history, beta, rs_old
+// (single_strategy.hpp:143-163; no_pretreatment.hpp:122-182).
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_cg_update(CgVecArgs a)
+{
+    constexpr int GL = L > 1 ? L / 2 : 1;
+    __shared__ double2 s_red2[kBlock / 64][GL];
+    __shared__ double s_colred[kBlock];
+    __shared__ double s_out[L];
+    __shared__ int s_last;
+    const int tid = threadIdx.x;
+    if (a.ctrl->done)
+        return;
+    const long long npairs = a.n_elems / 2;
+    const long long stride = (long long)gridDim.x * kBlock;
+    const long long i0 = (long long)blockIdx.x * kBlock + tid;
+    double2 al;
+    if (L == 1) {
+        al.x = a.scal[0].alpha;
+        al.y = al.x;
+    } else {
+        const int cp = (int)(i0 % GL);
+        al.x = a.scal[2 * cp].alpha;
+        al.y = a.scal[2 * cp + 1].alpha;
+    }
+    const double2 nal = make_double2(-al.x, -al.y);
+    double2 acc = make_double2(0.0, 0.0);
+    for (long long i = i0; i < npairs; i += stride) {
+        const double2 p = reinterpret_cast<const double2 *>(a.p)[i];
+        const double2 q = reinterpret_cast<const double2 *>(a.ap)[i];
+        double2 x = reinterpret_cast<double2 *>(a.x)[i];
+        double2 r = reinterpret_cast<double2 *>(a.r)[i];
+        x.x = x.x + al.x * p.x;
+        x.y = x.y + al.y * p.y;
+        r.x = r.x + nal.x * q.x;
+        r.y = r.y + nal.y * q.y;
+        reinterpret_cast<double2 *>(a.x)[i] = x;
+        reinterpret_cast<double2 *>(a.r)[i] = r;
+        acc.x += r.x * r.x;
+        acc.y += r.y * r.y;
+    }
+    if ((a.n_elems & 1) && blockIdx.x == 0 && tid == 0) {
+        const long long i = a.n_elems - 1;
+        a.x[i] = a.x[i] + al.x * a.p[i];
+        const double r = a.r[i] + nal.x * a.ap[i];
+        a.r[i] = r;
+        acc.x += r * r;
+    }
+    colpair_block_reduce<L>(acc, s_red2, a.partials + (size_t)blockIdx.x * L);
+    if (tid == 0) {
+        const unsigned tk = __hip_atomic_fetch_add(&a.ctrl->ticket_b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (tk == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (s_last) {
+        reduce_partials_cols<L>(a.partials, gridDim.x, s_colred, s_out);
+        if (tid == 0) {
+            __hip_atomic_store(&a.ctrl->ticket_b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int iter = a.ctrl->iter;
+            int nconv = 0;
+            double maxrel = 0.0;
+            for (int j = 0; j < L; ++j) {
+                CgScalars &s = a.scal[j];
+                const double rs_new = s_out[j];
+                s.rs_new = rs_new;
+                const double rel = sqrt(rs_new) / s.b_norm;
+                maxrel = maxrel > rel ? maxrel : rel;  // std::max(max, rel): NaN rel is skipped
+                if (!a.conv[j] && rel < a.tol)
+                    a.conv[j] = 1;
+                nconv += a.conv[j];
+            }
+            if (a.hist && iter < a.hist_cap)
+                a.hist[iter] = maxrel;
+            if (nconv == L) {
+                a.ctrl->done = 1;
+                a.ctrl->iters_out = iter + 1;
+            } else {
+                for (int j = 0; j < L; ++j) {
+                    CgScalars &s = a.scal[j];
+                    s.beta = a.conv[j] ? 0.0 : s.rs_new / s.rs_old;
+                    s.rs_old = s.rs_new;
+                }
+            }
+            a.ctrl->iter = iter + 1;
+        }
+    }
+}
+
+__global__ void k_flush(double *p, long long n, double v)
+{
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        p[i] = v;
+}
+
+// ------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------
+constexpr int kIptSpmv = 8;   // 2048 merge items per SpMV tile
+constexpr int kIptgSpmm = 8;  // items per lane group for SpMM tiles
+
+int tile_items_for(int L)
+{
+    if (L == 1)
+        return kBlock * kIptSpmv;
+    return (kBlock / (L / 2)) * kIptgSpmm;
+}
+
+bool supported_L(int L) { return L == 1 || L == 2 || L == 4 || L == 8 || L == 16; }
+
+hipError_t launch_merge_coords(const int *d_row_offsets, int m, int nnz, long long diag_step, int num_parts,
+                               int2 *d_out, hipStream_t s)
+{
+    const int n = num_parts + 1;
+    hipLaunchKernelGGL(k_merge_coords, dim3((n + 255) / 256), dim3(256), 0, s, d_row_offsets, m, nnz, diag_step,
+                       num_parts, d_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_snap(const int *d_row_offsets, int m, int2 *d_bounds, unsigned char *d_split, int num_tiles,
+                       int snap, hipStream_t s)
+{
+    const int n = num_tiles + 1;
+    hipLaunchKernelGGL(k_snap, dim3((n + 255) / 256), dim3(256), 0, s, d_row_offsets, m, d_bounds, d_split,
+                       num_tiles, snap);
+    return hipGetLastError();
+}
+
+static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double *X, double *Y)
+{
+    TileArgs a{};
+    a.row_offsets = h->d_row_offsets;
+    a.cols = h->d_cols;
+    a.vals = h->d_vals;
+    a.x = X;
+    a.y = Y;
+    a.bounds = plan.d_bounds;
+    a.split = plan.d_split;
+    a.carry_val = plan.d_carry_val;
+    a.num_tiles = plan.num_tiles;
+    return a;
+}
+
+template <bool CG>
+static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s)
+{
+    const dim3 grid(a.num_tiles), block(kBlock);
+    switch (L) {
+    case 1: hipLaunchKernelGGL((k_spmv_tile<kIptSpmv, CG>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((k_spmm_tile<2, kIptgSpmm, CG>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((k_spmm_tile<4, kIptgSpmm, CG>), grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((k_spmm_tile<8, kIptgSpmm, CG>), grid, block, 0, s, a); break;
+    case 16: hipLaunchKernelGGL((k_spmm_tile<16, kIptgSpmm, CG>), grid, block, 0, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L)
+{
+    if (plan.num_tiles == 0)
+        return hipSuccess;
+    return launch_tile<false>(make_args(h, plan, d_X, d_Y), L, h->stream);
+}
+
+hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L)
+{
+    if (plan.num_carries == 0)
+        return hipSuccess;
+    const int n = plan.num_carries * L;
+    hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, h->stream, plan.d_carry_tiles,
+                       plan.d_carry_rows, plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_spmm(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
+                       int *kernels_launched)
+{
+    hipError_t e = launch_spmm_tile_only(h, plan, d_X, d_Y, L);
+    if (e != hipSuccess)
+        return e;
+    e = launch_fixup(h, plan, d_Y, L);
+    if (kernels_launched)
+        *kernels_launched = (plan.num_tiles ? 1 : 0) + (plan.num_carries ? 1 : 0);
+    return e;
+}
+
+int cg_update_blocks(long long elems)
+{
+    const long long pairs = (elems + 1) / 2;
+    long long b = (pairs + kBlock * 4 - 1) / (kBlock * 4);  // ~4 pairs per thread
+    if (b < 1)
+        b = 1;
+    if (b > 2048)
+        b = 2048;
+    return (int)b;
+}
+
+template <int L>
+static void launch_vec(bool init, const CgVecArgs &a, int nblk, hipStream_t s)
+{
+    if (init)
+        hipLaunchKernelGGL((k_cg_init<L>), dim3(nblk), dim3(kBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL((k_cg_update<L>), dim3(nblk), dim3(kBlock), 0, s, a);
+}
+
+static hipError_t dispatch_vec(bool init, const CgVecArgs &a, int L, int nblk, hipStream_t s)
+{
+    switch (L) {
+    case 1: launch_vec<1>(init, a, nblk, s); break;
+    case 2: launch_vec<2>(init, a, nblk, s); break;
+    case 4: launch_vec<4>(init, a, nblk, s); break;
+    case 8: launch_vec<8>(init, a, nblk, s); break;
+    case 16: launch_vec<16>(init, a, nblk, s); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_cg_init(mspmv_handle_s *h, const double *d_b, double *d_x, int L, double tol, int nblk)
+{
+    CgVecArgs a{};
+    a.n_elems = (long long)h->m * L;
+    a.x = d_x;
+    a.r = h->d_r;
+    a.p = d_b;
+    a.p0 = h->d_p0;
+    a.scal = h->d_scal;
+    a.ctrl = h->d_ctrl;
+    a.conv = h->d_conv;
+    a.partials = h->d_partials;
+    a.tol = tol;
+    return dispatch_vec(true, a, L, nblk, h->stream);
+}
+
+hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *d_x, int L, int parity, int nblk,
+                               double tol)
+{
+    double *p_old = parity ? h->d_p1 : h->d_p0;
+    double *p_new = parity ? h->d_p0 : h->d_p1;
+    TileArgs ta = make_args(h, plan, h->d_r, h->d_ap);
+    ta.p_old = p_old;
+    ta.p_new = p_new;
+    ta.scal = h->d_scal;
+    ta.ctrl = h->d_ctrl;
+    ta.conv = h->d_conv;
+    ta.partials = h->d_partials;
+    hipError_t e = launch_tile<true>(ta, L, h->stream);
+    if (e != hipSuccess)
+        return e;
+    if (plan.num_carries) {
+        const int n = plan.num_carries * L;
+        hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, h->stream, plan.d_carry_tiles,
+                           plan.d_carry_rows, plan.num_carries, plan.d_carry_val, h->d_ap, L,
+                           (const CgControl *)h->d_ctrl);
+        if ((e = hipGetLastError()) != hipSuccess)
+            return e;
+    }
+    CgVecArgs va{};
+    va.n_elems = (long long)h->m * L;
+    va.x = d_x;
+    va.r = h->d_r;
+    va.p = p_new;
+    va.ap = h->d_ap;
+    va.scal = h->d_scal;
+    va.ctrl = h->d_ctrl;
+    va.conv = h->d_conv;
+    va.partials = h->d_partials;
+    va.hist = h->d_hist;
+    va.hist_cap = h->hist_cap;
+    va.tol = tol;
+    return dispatch_vec(false, va, L, nblk, h->stream);
+}
+
+hipError_t launch_flush(void *p, size_t bytes, hipStream_t s)
+{
+    const long long n = (long long)(bytes / sizeof(double));
+    hipLaunchKernelGGL(k_flush, dim3(2048), dim3(256), 0, s, (double *)p, n, 1.0);
+    return hipGetLastError();
+}
+
+}  // namespace mspmv

@@ -1,0 +1,205 @@
+// mspmv_synth.cpp -- deterministic synthetic CSR of the benchmark shapes (include/mspmv_synth.h).
+// Host C++17 + OpenMP; every value is a pure function of (seed, index).
+#include <omp.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <vector>
+
+#include "mspmv_synth.h"
+
+namespace {
+
+inline uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+inline double u01(uint64_t seed, uint64_t idx)  // [0,1) with 53 random bits
+{
+    return (double)(splitmix64(seed * 0x2545F4914F6CDD1Dull + idx) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// ell unique sorted columns in [lo, hi] (hi-lo+1 >= ell): one uniform pick per equal bucket.
+inline void bucket_cols(int lo, int hi, int ell, uint64_t seed, uint64_t key, int *out)
+{
+    const long long span = (long long)hi - lo + 1;
+    for (int k = 0; k < ell; ++k) {
+        const long long b0 = lo + span * k / ell;
+        const long long b1 = lo + span * (k + 1) / ell;  // exclusive
+        const long long w = b1 - b0;
+        const long long pick = (long long)(u01(seed, key * 131 + k) * (double)w);
+        out[k] = (int)(b0 + (pick < w ? pick : w - 1));
+    }
+}
+
+void prefix_from_lengths(const std::vector<int> &len, int *row_offsets)
+{
+    long long acc = 0;
+    row_offsets[0] = 0;
+    for (size_t i = 0; i < len.size(); ++i) {
+        acc += len[i];
+        row_offsets[i + 1] = (int)acc;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+mspmv_status mspmv_synth_banded(int m, long long nnz, int half_band, unsigned long long seed, int *row_offsets,
+                                int *cols, double *vals)
+{
+    if (m <= 0 || nnz < 0 || nnz > 0x7fffffffLL || !row_offsets || (nnz && (!cols || !vals)))
+        return MSPMV_ERR_INVALID;
+    const long long maxlen = (nnz + m - 1) / m;
+    if (half_band < maxlen || half_band < 1)
+        return MSPMV_ERR_INVALID;
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i <= m; ++i)
+        row_offsets[i] = (int)((long long)i * nnz / m);
+#pragma omp parallel for schedule(dynamic, 1024)
+    for (int i = 0; i < m; ++i) {
+        const int s = row_offsets[i], ell = row_offsets[i + 1] - s;
+        const int lo = std::max(0, i - half_band), hi = std::min(m - 1, i + half_band);
+        bucket_cols(lo, hi, ell, seed, (uint64_t)i, cols + s);
+        for (int k = 0; k < ell; ++k)
+            vals[s + k] = 0.5 + u01(seed ^ 0x5bd1e995ull, (uint64_t)(s + k));
+    }
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_synth_powerlaw(int m, int n, long long nnz, double exponent, unsigned long long seed,
+                                  int *row_offsets, int *cols, double *vals)
+{
+    if (m <= 0 || n <= 0 || nnz < 0 || nnz > (long long)m * n || nnz > 0x7fffffffLL || !row_offsets ||
+        (nnz && (!cols || !vals)))
+        return MSPMV_ERR_INVALID;
+    std::vector<double> w(m);
+    for (int i = 0; i < m; ++i)
+        w[i] = std::pow(1.0 - u01(seed, (uint64_t)i), -exponent);  // Pareto-tailed weights
+    double W = 0.0;
+    for (double v : w)
+        W += v;
+    std::vector<int> len(m);
+    long long assigned = 0;
+    double cum = 0.0;
+    long long prev = 0;
+    for (int i = 0; i < m; ++i) {
+        cum += w[i];
+        long long upto = (long long)std::floor((double)nnz * (cum / W));
+        if (i == m - 1)
+            upto = nnz;
+        long long ell = std::max(0LL, upto - prev);
+        prev = std::max(prev, upto);
+        ell = std::min<long long>(ell, n);
+        len[i] = (int)ell;
+        assigned += ell;
+    }
+    for (int i = 0; assigned < nnz; i = (i + 1) % m)  // redistribute what the n-cap removed
+        if (len[i] < n) {
+            ++len[i];
+            ++assigned;
+        }
+    prefix_from_lengths(len, row_offsets);
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int i = 0; i < m; ++i) {
+        const int s = row_offsets[i], ell = len[i];
+        if (ell > 0)
+            bucket_cols(0, n - 1, ell, seed ^ 0x9e37ull, (uint64_t)i, cols + s);
+        for (int k = 0; k < ell; ++k)
+            vals[s + k] = 0.5 + u01(seed ^ 0x5bd1e995ull, (uint64_t)(s + k));
+    }
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_synth_stencil(int kind, int m, int dim0, int dim1, int dim2, unsigned long long seed,
+                                 int *row_offsets, int *cols, double *vals, long long *nnz_out)
+{
+    if (!row_offsets || (kind != 0 && kind != 1) || dim0 <= 0)
+        return MSPMV_ERR_INVALID;
+    if (kind == 1) {
+        if (dim1 <= 0 || dim2 <= 0)
+            return MSPMV_ERR_INVALID;
+        const long long mm = (long long)dim0 * dim1 * dim2;
+        if (mm != m)
+            return MSPMV_ERR_INVALID;
+    }
+    if (m <= 0)
+        return MSPMV_ERR_INVALID;
+    const int W = dim0;
+    // neighbour list of point p in increasing column order (self included)
+    auto neigh = [&](int p, int *out) -> int {
+        int k = 0;
+        if (kind == 0) {
+            const int r = p / W, c = p % W;
+            const int cand_r[7] = {r - 1, r - 1, r, r, r, r + 1, r + 1};
+            const int cand_c[7] = {c, c + 1, c - 1, c, c + 1, c - 1, c};
+            for (int t = 0; t < 7; ++t) {
+                const int rr = cand_r[t], cc = cand_c[t];
+                if (rr < 0 || cc < 0 || cc >= W)
+                    continue;
+                const long long q = (long long)rr * W + cc;
+                if (q >= m)
+                    continue;
+                out[k++] = (int)q;
+            }
+        } else {
+            const int nx = dim0, ny = dim1, nz = dim2;
+            const int kx = p % nx, jy = (p / nx) % ny, iz = p / (nx * ny);
+            for (int di = -1; di <= 1; ++di)
+                for (int dj = -1; dj <= 1; ++dj)
+                    for (int dk = -1; dk <= 1; ++dk) {
+                        const int i2 = iz + di, j2 = jy + dj, k2 = kx + dk;
+                        if (i2 < 0 || i2 >= nz || j2 < 0 || j2 >= ny || k2 < 0 || k2 >= nx)
+                            continue;
+                        out[k++] = (i2 * ny + j2) * nx + k2;
+                    }
+        }
+        return k;
+    };
+    std::vector<int> len(m);
+#pragma omp parallel for schedule(static)
+    for (int p = 0; p < m; ++p) {
+        int tmp[27];
+        len[p] = neigh(p, tmp);
+    }
+    long long total = 0;
+    for (int v : len)
+        total += v;
+    if (total > 0x7fffffffLL)
+        return MSPMV_ERR_INVALID;
+    prefix_from_lengths(len, row_offsets);
+    if (nnz_out)
+        *nnz_out = total;
+    if (!cols || !vals)
+        return MSPMV_OK;
+#pragma omp parallel for schedule(static)
+    for (int p = 0; p < m; ++p) {
+        int nb[27];
+        const int k = neigh(p, nb);
+        const int s = row_offsets[p];
+        double diag = 1.0;
+        int self = -1;
+        for (int t = 0; t < k; ++t) {
+            const int q = nb[t];
+            cols[s + t] = q;
+            if (q == p) {
+                self = t;
+                continue;
+            }
+            const uint64_t a = (uint64_t)std::min(p, q), b = (uint64_t)std::max(p, q);
+            const double off = -u01(seed, a * 0x100000001B3ull + b);  // symmetric in (p, q)
+            vals[s + t] = off;
+            diag += -off;
+        }
+        vals[s + self] = diag;
+    }
+    return MSPMV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,394 @@
+"""mspmv -- Python host mirror of the reference's hot-path interface, over libmspmv.so.
+
+The product is the C-ABI library next to this file (HIP kernels for gfx950 + C++ host code,
+include/mspmv.h).  This module is a thin ctypes layer so tests and bench.py can drive it:
+
+* ``CsrMatrix`` mirrors ``CsrMatrix<double,int>`` (sparse_matrix.h:633-653);
+* ``GpuCsr`` owns one uploaded matrix (``mspmv_csr_create``) and exposes SpMV/SpMM/CG;
+* ``OmpMergeCsrmv`` / ``OmpMergeCsrmm`` / ``CGSolveSingle`` / ``CGSolveMultiple`` keep the
+  reference's names, argument order and meaning (cpu_spmv.cpp:357-367,
+  work_2025/spmm/merge_based.hpp:46-57, work_2025/main/single_strategy.hpp:102-110,
+  work_2025/main/no_pretreatment.hpp:32-43); ``num_threads`` is accepted and ignored.
+
+There is no CPU fallback: importing this module fails loudly if libmspmv.so is missing,
+and every compute call goes through the HIP library.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmspmv.so")
+
+SIMPLE, MERGE, NONZERO_SPLIT = 0, 1, 2  # SpmmKernel, work_2025/types.hpp:11-16
+
+STATUS = {
+    0: "OK", 1: "INVALID", 2: "HIP", 3: "OOM", 4: "BREAKDOWN", 5: "RCCL", 6: "UNSUPPORTED", 7: "IO",
+}
+SUPPORTED_L = (1, 2, 4, 8, 16)
+
+
+class MspmvError(RuntimeError):
+    def __init__(self, status: int, where: str, msg: str):
+        super().__init__(f"{where}: {STATUS.get(status, status)}: {msg}")
+        self.status = status
+
+
+class Coord(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_int), ("y", ctypes.c_int)]
+
+
+class _CsrD(ctypes.Structure):
+    _fields_ = [
+        ("num_rows", ctypes.c_int),
+        ("num_cols", ctypes.c_int),
+        ("num_nonzeros", ctypes.c_int),
+        ("row_offsets", ctypes.c_void_p),
+        ("column_indices", ctypes.c_void_p),
+        ("values", ctypes.c_void_p),
+    ]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_D = ctypes.c_double
+_PI = ctypes.POINTER(ctypes.c_int)
+_PD = ctypes.POINTER(ctypes.c_double)
+_SZ = ctypes.c_size_t
+
+# name -> (restype, argtypes); the single source of truth for the ctypes declarations
+_SIGS = {
+    "mspmv_last_error": (ctypes.c_char_p, []),
+    "mspmv_version": (ctypes.c_char_p, []),
+    "mspmv_device_count": (_I, []),
+    "mspmv_csr_create": (_I, [ctypes.POINTER(_CsrD), _I, ctypes.POINTER(_P)]),
+    "mspmv_csr_create_dev": (_I, [ctypes.POINTER(_CsrD), _I, ctypes.POINTER(_P)]),
+    "mspmv_destroy": (_I, [_P]),
+    "mspmv_shape": (_I, [_P, _PI, _PI, _PI]),
+    "mspmv_setup_ms": (_D, [_P]),
+    "mspmv_sync": (_I, [_P]),
+    "mspmv_merge_coords": (_I, [_P, _I, ctypes.POINTER(Coord)]),
+    "mspmv_dspmv": (_I, [_P, _P, _P]),
+    "mspmv_dspmv_dev": (_I, [_P, _P, _P]),
+    "mspmv_dspmm": (_I, [_P, _P, _P, _I]),
+    "mspmv_dspmm_dev": (_I, [_P, _P, _P, _I]),
+    "mspmv_dcg_single": (_I, [_P, _P, _P, _I, _D, _PI, _P, _I]),
+    "mspmv_dcg_single_dev": (_I, [_P, _P, _P, _I, _D, _PI, _P, _I]),
+    "mspmv_dcg_multi": (_I, [_P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
+    "mspmv_dcg_multi_dev": (_I, [_P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
+    "mspmv_time_spmm_dev": (_I, [_P, _P, _P, _I, _I, _SZ, _PD]),
+    "mspmv_last_kernel_ms": (_I, [_P, _PD, _PI]),
+    "mspmv_time_spmm_batch_dev": (_I, [_I, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _I,
+                                       _PD, _PD, _PI]),
+    "mspmv_tile_plan": (_I, [_P, _I, _PI, _PI, _PI, ctypes.POINTER(Coord)]),
+    "mspmv_device_malloc": (_I, [_I, _SZ, ctypes.POINTER(_P)]),
+    "mspmv_device_free": (_I, [_P]),
+    "mspmv_memcpy_h2d": (_I, [_P, _P, _SZ]),
+    "mspmv_memcpy_d2h": (_I, [_P, _P, _SZ]),
+    "mspmv_memcpy_d2d": (_I, [_P, _P, _SZ]),
+    "mspmv_memset_dev": (_I, [_P, _I, _SZ]),
+    "mspmv_synth_banded": (_I, [_I, ctypes.c_longlong, _I, ctypes.c_ulonglong, _P, _P, _P]),
+    "mspmv_synth_powerlaw": (_I, [_I, _I, ctypes.c_longlong, _D, ctypes.c_ulonglong, _P, _P, _P]),
+    "mspmv_synth_stencil": (_I, [_I, _I, _I, _I, _I, ctypes.c_ulonglong, _P, _P, _P,
+                                 ctypes.POINTER(ctypes.c_longlong)]),
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C sparse-matrix-linear-equations_amd/csrc`")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def _check(status: int, where: str, allow=()):
+    if status != 0 and status not in allow:
+        raise MspmvError(status, where, lib.mspmv_last_error().decode(errors="replace"))
+    return status
+
+
+def device_count() -> int:
+    return int(lib.mspmv_device_count())
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+# ----------------------------------------------------------------------------------------
+# CsrMatrix mirror
+# ----------------------------------------------------------------------------------------
+@dataclass
+class CsrMatrix:
+    """Host CSR with the fields of CsrMatrix<double,int> (sparse_matrix.h:648-653)."""
+
+    num_rows: int
+    num_cols: int
+    num_nonzeros: int
+    row_offsets: np.ndarray      # int32[num_rows+1]
+    column_indices: np.ndarray   # int32[num_nonzeros]
+    values: np.ndarray           # float64[num_nonzeros]
+
+    @classmethod
+    def from_arrays(cls, num_cols: int, row_offsets, column_indices, values) -> "CsrMatrix":
+        ro = np.ascontiguousarray(row_offsets, dtype=np.int32)
+        ci = np.ascontiguousarray(column_indices, dtype=np.int32)
+        va = np.ascontiguousarray(values, dtype=np.float64)
+        return cls(len(ro) - 1, int(num_cols), int(ro[-1]) if len(ro) else 0, ro, ci, va)
+
+    def _c(self) -> _CsrD:
+        return _CsrD(self.num_rows, self.num_cols, self.num_nonzeros, _ptr(self.row_offsets),
+                     _ptr(self.column_indices), _ptr(self.values))
+
+    # --- synthetic shapes; generated natively in libmspmv.so -------------
+    @classmethod
+    def synth_banded(cls, m: int, nnz: int, half_band: int, seed: int = 1) -> "CsrMatrix":
+        ro = np.empty(m + 1, np.int32)
+        ci = np.empty(max(nnz, 1), np.int32)
+        va = np.empty(max(nnz, 1), np.float64)
+        _check(lib.mspmv_synth_banded(m, nnz, half_band, seed, _ptr(ro), _ptr(ci), _ptr(va)), "synth_banded")
+        return cls(m, m, nnz, ro, ci[:nnz], va[:nnz])
+
+    @classmethod
+    def synth_powerlaw(cls, m: int, n: int, nnz: int, exponent: float = 1.2, seed: int = 3) -> "CsrMatrix":
+        ro = np.empty(m + 1, np.int32)
+        ci = np.empty(max(nnz, 1), np.int32)
+        va = np.empty(max(nnz, 1), np.float64)
+        _check(lib.mspmv_synth_powerlaw(m, n, nnz, exponent, seed, _ptr(ro), _ptr(ci), _ptr(va)), "synth_powerlaw")
+        return cls(m, n, nnz, ro, ci[:nnz], va[:nnz])
+
+    @classmethod
+    def synth_stencil(cls, kind: int, m: int, dim0: int, dim1: int = 0, dim2: int = 0, seed: int = 7) -> "CsrMatrix":
+        """kind 0: 2-D 7-point triangular FEM stencil (parabolic_fem shape), kind 1: 3-D
+        27-point (nlpkkt120 size).  Symmetric, strictly diagonally dominant -> SPD."""
+        ro = np.empty(m + 1, np.int32)
+        nnz = ctypes.c_longlong(0)
+        _check(lib.mspmv_synth_stencil(kind, m, dim0, dim1, dim2, seed, _ptr(ro), None, None, ctypes.byref(nnz)),
+               "synth_stencil(size)")
+        ci = np.empty(max(nnz.value, 1), np.int32)
+        va = np.empty(max(nnz.value, 1), np.float64)
+        _check(lib.mspmv_synth_stencil(kind, m, dim0, dim1, dim2, seed, _ptr(ro), _ptr(ci), _ptr(va),
+                                       ctypes.byref(nnz)), "synth_stencil")
+        return cls(m, m, int(nnz.value), ro, ci[: nnz.value], va[: nnz.value])
+
+
+# ----------------------------------------------------------------------------------------
+# device memory
+# ----------------------------------------------------------------------------------------
+class DeviceBuffer:
+    """A raw HBM allocation (mspmv_device_malloc)."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        p = ctypes.c_void_p()
+        _check(lib.mspmv_device_malloc(device, nbytes, ctypes.byref(p)), "device_malloc")
+        self.ptr = p.value
+        self.nbytes = nbytes
+
+    @classmethod
+    def from_array(cls, a: np.ndarray, device: int = 0) -> "DeviceBuffer":
+        a = np.ascontiguousarray(a)
+        b = cls(a.nbytes, device)
+        b.upload(a)
+        return b
+
+    def upload(self, a: np.ndarray):
+        a = np.ascontiguousarray(a)
+        assert a.nbytes <= self.nbytes
+        _check(lib.mspmv_memcpy_h2d(self.ptr, _ptr(a), a.nbytes), "memcpy_h2d")
+
+    def download(self, shape, dtype=np.float64) -> np.ndarray:
+        out = np.empty(shape, dtype)
+        assert out.nbytes <= self.nbytes
+        _check(lib.mspmv_memcpy_d2h(_ptr(out), self.ptr, out.nbytes), "memcpy_d2h")
+        return out
+
+    def fill_bytes(self, value: int = 0):
+        _check(lib.mspmv_memset_dev(self.ptr, value, self.nbytes), "memset")
+
+    def free(self):
+        if self.ptr:
+            lib.mspmv_device_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+# ----------------------------------------------------------------------------------------
+# the uploaded matrix
+# ----------------------------------------------------------------------------------------
+class GpuCsr:
+    """One CSR matrix resident in HBM with its merge-path tile plans (mspmv_csr_create)."""
+
+    def __init__(self, a: CsrMatrix, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib.mspmv_csr_create(ctypes.byref(a._c()), device, ctypes.byref(h)), "csr_create")
+        self.h = h.value
+        self.num_rows, self.num_cols, self.num_nonzeros = a.num_rows, a.num_cols, a.num_nonzeros
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.mspmv_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def setup_ms(self) -> float:
+        return float(lib.mspmv_setup_ms(self.h))
+
+    def sync(self):
+        _check(lib.mspmv_sync(self.h), "sync")
+
+    def merge_coords(self, num_parts: int) -> np.ndarray:
+        out = (Coord * (num_parts + 1))()
+        _check(lib.mspmv_merge_coords(self.h, num_parts, out), "merge_coords")
+        return np.ctypeslib.as_array(out).view(np.int32).reshape(num_parts + 1, 2).copy()
+
+    def tile_plan(self, L: int = 1):
+        nt, ti, nc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(lib.mspmv_tile_plan(self.h, L, ctypes.byref(nt), ctypes.byref(ti), ctypes.byref(nc), None), "tile_plan")
+        b = (Coord * (nt.value + 1))()
+        _check(lib.mspmv_tile_plan(self.h, L, None, None, None, b), "tile_plan")
+        bounds = np.ctypeslib.as_array(b).view(np.int32).reshape(nt.value + 1, 2).copy()
+        return {"num_tiles": nt.value, "tile_items": ti.value, "num_carries": nc.value, "bounds": bounds}
+
+    def spmv(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, np.float64)
+        assert x.shape == (self.num_cols,)
+        y = np.empty(self.num_rows, np.float64)
+        _check(lib.mspmv_dspmv(self.h, _ptr(x), _ptr(y)), "dspmv")
+        return y
+
+    def spmm(self, X: np.ndarray) -> np.ndarray:
+        X = np.ascontiguousarray(X, np.float64)
+        L = X.shape[1]
+        assert X.shape == (self.num_cols, L)
+        Y = np.empty((self.num_rows, L), np.float64)
+        _check(lib.mspmv_dspmm(self.h, _ptr(X), _ptr(Y), L), "dspmm")
+        return Y
+
+    def spmm_dev(self, dX: DeviceBuffer, dY: DeviceBuffer, L: int = 1):
+        _check(lib.mspmv_dspmm_dev(self.h, dX.ptr, dY.ptr, L), "dspmm_dev")
+
+    def time_spmm(self, dX: DeviceBuffer, dY: DeviceBuffer, L: int, reps: int, flush_bytes: int = 0):
+        """(avg ms per call, avg ms of the tile kernel, kernels per call), HIP events."""
+        ms = ctypes.c_double()
+        _check(lib.mspmv_time_spmm_dev(self.h, dX.ptr, dY.ptr, L, reps, flush_bytes, ctypes.byref(ms)), "time")
+        kms, kpc = ctypes.c_double(), ctypes.c_int()
+        _check(lib.mspmv_last_kernel_ms(self.h, ctypes.byref(kms), ctypes.byref(kpc)), "last_kernel_ms")
+        return ms.value, kms.value, kpc.value
+
+    def cg_single(self, b: np.ndarray, max_iters: int, tolerance: float, hist_cap: int = 0):
+        b = np.ascontiguousarray(b, np.float64)
+        x = np.empty_like(b)
+        it = ctypes.c_int()
+        hist = np.zeros(max(hist_cap, 1), np.float64)
+        st = lib.mspmv_dcg_single(self.h, _ptr(b), _ptr(x), max_iters, tolerance, ctypes.byref(it),
+                                  _ptr(hist) if hist_cap else None, hist_cap)
+        _check(st, "dcg_single", allow=(4,))
+        return x, it.value, hist[: min(it.value, hist_cap)], st
+
+    def cg_multi(self, B: np.ndarray, max_iters: int, tolerance: float, kernel: int = MERGE, hist_cap: int = 0):
+        B = np.ascontiguousarray(B, np.float64)
+        L = B.shape[1]
+        X = np.empty_like(B)
+        it = ctypes.c_int()
+        hist = np.zeros(max(hist_cap, 1), np.float64)
+        st = lib.mspmv_dcg_multi(self.h, _ptr(B), _ptr(X), L, max_iters, tolerance, kernel, ctypes.byref(it),
+                                 _ptr(hist) if hist_cap else None, hist_cap)
+        _check(st, "dcg_multi", allow=(4,))
+        return X, it.value, hist[: min(it.value, hist_cap)], st
+
+    def cg_dev(self, dB: DeviceBuffer, dX: DeviceBuffer, L: int, max_iters: int, tolerance: float,
+               hist_cap: int = 0):
+        it = ctypes.c_int()
+        hist = np.zeros(max(hist_cap, 1), np.float64)
+        st = lib.mspmv_dcg_multi_dev(self.h, dB.ptr, dX.ptr, L, max_iters, tolerance, MERGE, ctypes.byref(it),
+                                     _ptr(hist) if hist_cap else None, hist_cap)
+        _check(st, "dcg_multi_dev", allow=(4,))
+        return it.value, hist[: min(it.value, hist_cap)], st
+
+
+def time_spmm_batch(gs, dXs, dYs, L: int, reps: int):
+    """Time `reps` steps of one SpMM launch per matrix, all on gs[0]'s stream.
+    Returns (ms per step, ms per merge-tile kernel launch, kernels per step)."""
+    n = len(gs)
+    H = (_P * n)(*[g.h for g in gs])
+    X = (_P * n)(*[b.ptr for b in dXs])
+    Y = (_P * n)(*[b.ptr for b in dYs])
+    step, kern, kps = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+    _check(lib.mspmv_time_spmm_batch_dev(n, H, X, Y, L, reps, ctypes.byref(step), ctypes.byref(kern),
+                                         ctypes.byref(kps)), "time_spmm_batch")
+    return step.value, kern.value, kps.value
+
+
+# ----------------------------------------------------------------------------------------
+# the reference's operator names (drop-in facade)
+# ----------------------------------------------------------------------------------------
+def _gpu(a: CsrMatrix) -> GpuCsr:
+    g = getattr(a, "_gpu", None)
+    if g is None or g.h is None:
+        g = GpuCsr(a)
+        object.__setattr__(a, "_gpu", g)
+    return g
+
+
+def OmpMergeCsrmv(num_threads, a: CsrMatrix, row_end_offsets, column_indices, values, vector_x, vector_y_out):
+    """cpu_spmv.cpp:357-421: vector_y_out[:] = A @ vector_x (num_threads ignored on the GPU)."""
+    vector_y_out[:] = _gpu(a).spmv(vector_x)
+
+
+def OmpMergeCsrmm(num_threads, a: CsrMatrix, row_end_offsets, column_indices, values, vector_x, vector_y_out,
+                  num_vectors):
+    """work_2025/spmm/merge_based.hpp:46-153 on flat row-major n x num_vectors panels."""
+    X = np.asarray(vector_x, np.float64).reshape(a.num_cols, num_vectors)
+    vector_y_out[:] = _gpu(a).spmm(X).reshape(-1)
+
+
+def CGSolveSingle(a: CsrMatrix, b, x, max_iters: int, tolerance: float) -> int:
+    """work_2025/main/single_strategy.hpp:102-170; returns the iteration count."""
+    xs, it, _, _ = _gpu(a).cg_single(b, max_iters, tolerance)
+    x[:] = xs
+    return it
+
+
+def CGSolveMultiple(a: CsrMatrix, B, X, num_vectors: int, max_iters: int, tolerance: float,
+                    kernel_type: int = MERGE, max_errors: Optional[list] = None) -> int:
+    """work_2025/main/no_pretreatment.hpp:32-197 on flat interleaved n x num_vectors panels."""
+    Bm = np.asarray(B, np.float64).reshape(a.num_rows, num_vectors)
+    cap = max_iters if max_errors is not None else 0
+    Xs, it, hist, _ = _gpu(a).cg_multi(Bm, max_iters, tolerance, kernel_type, hist_cap=cap)
+    X[:] = Xs.reshape(-1)
+    if max_errors is not None:
+        max_errors.clear()
+        max_errors.extend(hist.tolist())
+    return it

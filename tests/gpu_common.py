@@ -1,0 +1,66 @@
+"""Shared helpers for the GPU parity tests."""
+import numpy as np
+
+EPS = 2.0 ** -53
+
+
+def groups_per_tile(L):
+    """Merge walkers per 256-thread tile: one per thread (L == 1) or one per L/2 lanes."""
+    return 256 if L == 1 else 256 // (L // 2)
+
+
+def unsplit_rows(a, plan, L):
+    """Rows whose merge items (nonzeros + row end) fall in ONE walker of ONE tile.
+
+    Mirrors the kernel's partition exactly: tile t spans plan bounds t..t+1; its walkers take
+    ceil(items / groups) consecutive diagonals each.  Such rows are summed sequentially in CSR
+    order from 0.0, i.e. bit-identically to SpmvGold (cpu_spmv.cpp:241-265).
+    """
+    bounds = plan["bounds"]
+    ng = groups_per_tile(L)
+    ro = a.row_offsets.astype(np.int64)
+    mask = np.zeros(a.num_rows, bool)
+    for t in range(plan["num_tiles"]):
+        r0, n0 = (int(v) for v in bounds[t])
+        r1, n1 = (int(v) for v in bounds[t + 1])
+        nrows = r1 - r0
+        if nrows <= 0:
+            continue
+        items = nrows + (n1 - n0)
+        ipt = -(-items // ng)
+        r = np.arange(nrows)
+        rs = ro[r0 + r] - n0
+        re = ro[r0 + r + 1] - n0
+        ok = (rs >= 0) & ((r + rs) // ipt == (r + re) // ipt)
+        mask[r0 + r] = ok
+    return mask
+
+
+def abs_bound(a, X):
+    """Per-row (and column) |A| |X| and row lengths, for reordering-error bounds."""
+    X = np.asarray(X, np.float64)
+    if X.ndim == 1:
+        X = X[:, None]
+    lens = np.diff(a.row_offsets).astype(np.int64)
+    rows = np.repeat(np.arange(a.num_rows), lens)
+    acc = np.zeros((a.num_rows, X.shape[1]))
+    np.add.at(acc, rows, np.abs(a.values)[:, None] * np.abs(X[a.column_indices]))
+    return acc, lens
+
+
+def check_parity(a, y_gpu, y_seq, X, plan, L):
+    """Unsplit rows bit-identical to the sequential CSR-order sum; split rows within the
+    summation-reordering bound 2 (len+1) eps (|A||x|)_i.  Returns (#bit-exact, #rows)."""
+    y_gpu = np.asarray(y_gpu, np.float64).reshape(a.num_rows, -1)
+    y_seq = np.asarray(y_seq, np.float64).reshape(a.num_rows, -1)
+    mask = unsplit_rows(a, plan, L)
+    g, s = y_gpu[mask], y_seq[mask]
+    diff = np.flatnonzero(g.view(np.uint64) != s.view(np.uint64))
+    assert diff.size == 0, f"{diff.size} unsplit entries not bit-identical, e.g. {g.ravel()[diff[:3]]} vs {s.ravel()[diff[:3]]}"
+    bound, lens = abs_bound(a, X)
+    tol = 2.0 * (lens[:, None] + 1) * EPS * bound + 1e-300
+    err = np.abs(y_gpu - y_seq)
+    bad = np.argwhere(err > tol)
+    assert bad.size == 0, f"{len(bad)} entries exceed the reordering bound, e.g. row {bad[:3]}"
+    assert np.all(np.isfinite(y_gpu) == np.isfinite(y_seq))
+    return int(mask.sum()), a.num_rows
