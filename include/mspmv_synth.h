@@ -22,6 +22,17 @@ extern "C" {
 MSPMV_API mspmv_status mspmv_synth_banded(int m, long long nnz, int half_band, unsigned long long seed, int *row_offsets,
                                 int *cols, double *vals);
 
+/* Node-blocked FEM pattern (pwtk / cant / rma10 are FEM/CFD matrices with several unknowns
+ * per mesh node): rows are grouped in nodes of `block` consecutive rows; every row of node I
+ * couples to the same set of neighbour nodes, chosen one per equal slice of the node band
+ * [I - half_band_nodes, I + half_band_nodes] (own node always included), and takes all
+ * `block` columns of each neighbour, so columns come in runs of `block` consecutive indices.
+ * Exactly `nnz` nonzeros (row i holds floor((i+1)nnz/m) - floor(i nnz/m), the last
+ * neighbour block truncated); values U(0.5, 1.5).  Requires half_band_nodes*2+1 >= the
+ * number of blocks the longest row needs. */
+MSPMV_API mspmv_status mspmv_synth_fem_blocked(int m, long long nnz, int block, int half_band_nodes,
+                                               unsigned long long seed, int *row_offsets, int *cols, double *vals);
+
 /* Power-law row lengths with the same contract as mspmv_synth_banded: row lengths drawn
  * from a Zipf-like law (a handful of rows hold a large share of nnz), columns spread over
  * the whole matrix.  Exercises merge-path load balance and long-row carries. */

@@ -85,7 +85,7 @@ static void free_plan(TilePlan &p)
 }
 
 // Build (once) the tile plan for L right-hand sides, validating on the host every bound the
-// kernels rely on (monotone boundaries, <= 1.5 * tile_items merge items per tile) before any
+// kernels rely on (monotone boundaries, <= 1.25 * tile_items merge items per tile) before any
 // tile kernel can run on it.
 static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out)
 {
@@ -97,7 +97,7 @@ static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out)
     }
     TilePlan p;
     p.tile_items = tile;
-    p.snap = tile / 2;
+    p.snap = tile / kSnapDiv;
     const long long total = (long long)h->m + h->nnz;
     p.num_tiles = (int)((total + tile - 1) / tile);
     const int T = p.num_tiles;
@@ -128,7 +128,7 @@ static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out)
         set_error(std::string("tile plan: ") + hipGetErrorString(e));
         return fail(MSPMV_ERR_HIP);
     }
-    const int maxi = tile + tile / 2;
+    const int maxi = tile + tile / kSnapDiv;
     if (hb[0].x != 0 || hb[0].y != 0 || hb[T].x != h->m || hb[T].y != h->nnz) {
         set_error("tile plan: bad end boundaries");
         return fail(MSPMV_ERR_INVALID);
@@ -217,10 +217,17 @@ static mspmv_status create_common(const mspmv_csr_d *a, int device, bool from_de
         return fail(MSPMV_ERR_HIP);
     }
     mspmv_status st;
+    // Column / value arrays are padded (zero column index, zero value) so the kernels' aligned
+    // 16-byte group reads past the last nonzero stay inside the allocation.
+    const size_t padded = (size_t)h->nnz + kNnzPad;
     if ((st = dev_alloc(&h->d_row_offsets, (size_t)h->m + 1)) != MSPMV_OK ||
-        (st = dev_alloc(&h->d_cols, (size_t)h->nnz)) != MSPMV_OK ||
-        (st = dev_alloc(&h->d_vals, (size_t)h->nnz)) != MSPMV_OK)
+        (st = dev_alloc(&h->d_cols, padded)) != MSPMV_OK || (st = dev_alloc(&h->d_vals, padded)) != MSPMV_OK)
         return fail(st);
+    if (hipMemset(h->d_cols, 0, sizeof(int) * padded) != hipSuccess ||
+        hipMemset(h->d_vals, 0, sizeof(double) * padded) != hipSuccess) {
+        set_error("hipMemset of padded CSR arrays failed");
+        return fail(MSPMV_ERR_HIP);
+    }
     const hipMemcpyKind kind = from_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     std::vector<int> host_ro;
     const int *ro = a->row_offsets;

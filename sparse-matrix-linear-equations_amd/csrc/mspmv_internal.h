@@ -13,6 +13,8 @@
 namespace mspmv {
 
 constexpr int kBlock = 256;  // 4 x 64-lane waves per workgroup
+constexpr int kNnzPad = 16;  // padding elements after the last nonzero of the device arrays
+constexpr int kSnapDiv = 4;  // a boundary snaps to its row start if <= tile/kSnapDiv nonzeros deep
 
 // A merge-path tile plan for one nominal tile size (merge items per tile).
 //
@@ -21,7 +23,7 @@ constexpr int kBlock = 256;  // 4 x 64-lane waves per workgroup
 // snapped"): the row is then computed whole by the tile that completes it, so no carry
 // crosses that boundary.  Boundaries deeper inside a long row stay exact merge-path
 // coordinates ("split") and the tile before them writes a carry that a small fix-up
-// kernel adds in tile order.  Every tile holds at most tile_items + snap merge items.
+// kernel adds in tile order.  Every tile holds at most tile_items + tile_items/kSnapDiv items.
 struct TilePlan {
     int tile_items = 0;
     int snap = 0;

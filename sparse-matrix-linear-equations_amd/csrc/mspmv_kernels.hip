@@ -19,6 +19,7 @@
 #include "mspmv_internal.h"
 
 #include <cstdio>
+#include <cstdlib>
 
 namespace mspmv {
 
@@ -32,6 +33,35 @@ __device__ __forceinline__ int xcd_tile(int b, int T)
     const int q = T >> 3, r = T & 7;
     const int k = b & 7, i = b >> 3;
     return k * q + (k < r ? k : r) + i;
+}
+
+// Streamed-once matrix arrays: nontemporal loads (don't displace x / X from the caches).
+template <bool NT, typename T>
+__device__ __forceinline__ T ld_stream(const T *p)
+{
+    if (NT)
+        return __builtin_nontemporal_load(p);
+    return *p;
+}
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef double v2d_t __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ int4 ld_stream(const int4 *p)
+{
+    if (NT) {
+        const v4i_t t = __builtin_nontemporal_load(reinterpret_cast<const v4i_t *>(p));
+        return make_int4(t.x, t.y, t.z, t.w);
+    }
+    return *p;
+}
+template <bool NT>
+__device__ __forceinline__ double2 ld_stream(const double2 *p)
+{
+    if (NT) {
+        const v2d_t t = __builtin_nontemporal_load(reinterpret_cast<const v2d_t *>(p));
+        return make_double2(t.x, t.y);
+    }
+    return *p;
 }
 
 __device__ __forceinline__ void store_sc1(double *p, double v)
@@ -143,19 +173,62 @@ struct TileArgs {
     double *partials;                  // CG: per-tile partial dots [tile][L]
 };
 
-// Single right-hand side.  TILE = 256*IPT merge items nominal, up to 1.5*TILE after snapping.
+// LDS slot of tile-local product k: one pad double every 4, so the walkers' strided reads
+// (about 8 products apart) spread over the banks.
+__device__ __forceinline__ int pslot(int k) { return k + (k >> 2); }
+
+// Stage products val*x[col] (or val*(r + beta p)[col] for CG) of the tile's nonzeros
+// [n0, n0+nnzt) into LDS.  Striped: lane l of round j takes nonzero l + 256 j, so each
+// gather instruction reads x at 64 CONSECUTIVE nonzeros' columns (runs of neighbouring
+// columns share cache lines) -- measured 1.4x faster than 16-byte-per-lane blocked loads,
+// whose gathers scatter over 4x more lines.  Every round's loads and gathers are issued
+// before any is consumed (indices past the tile clamp to its last nonzero).
+template <int NJ, bool CG, bool NT>
+__device__ __forceinline__ void stage_products(const TileArgs &a, int n0, int nnzt, double beta, double *s_prod)
+{
+    int c[NJ];
+    double v[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int k = min((int)threadIdx.x + j * kBlock, nnzt - 1);
+        c[j] = ld_stream<NT>(a.cols + n0 + k);
+        v[j] = ld_stream<NT>(a.vals + n0 + k);
+    }
+    double xv[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+        xv[j] = a.x[c[j]];
+    if (CG) {
+        double pv[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+            pv[j] = a.p_old[c[j]];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+            xv[j] = xv[j] + beta * pv[j];
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int k = (int)threadIdx.x + j * kBlock;
+        if (k < nnzt)
+            s_prod[pslot(k)] = v[j] * xv[j];
+    }
+}
+
+// Single right-hand side.  TILE = 256*IPT merge items nominal, up to 1.25*TILE after snapping.
 // CG: gathers p = r + beta*p_old on the fly (UpdatePSingle, single_strategy.hpp:89-97, fused
 // into the SpMV), writes p for its rows, Ap, and p.Ap by linearity; the last tile reduces
 // the partials in tile order and sets alpha = rs_old / pAp (single_strategy.hpp:140-141).
-template <int IPT, bool CG>
+template <int IPT, bool CG, bool NT>
 __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
 {
     constexpr int TILE = kBlock * IPT;
-    constexpr int MAXI = TILE + TILE / 2;
-    constexpr int MAXJ = MAXI / kBlock;
+    constexpr int MAXI = TILE + TILE / kSnapDiv;
+    constexpr int MAXJ = (MAXI + kBlock - 1) / kBlock;
     __shared__ int s_rowend[MAXI];
-    __shared__ double s_prod[MAXI];
+    __shared__ double s_prod[MAXI + MAXI / 4 + 1];
     __shared__ int s_crow[kBlock];
+    __shared__ int s_ccol[kBlock];
     __shared__ double s_cval[kBlock];
     __shared__ double s_red[kBlock / 64];
     __shared__ int s_last;
@@ -172,40 +245,35 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
     const int items = nrows + nnzt;
     const double beta = CG ? a.scal[0].beta : 0.0;
 
+    if (nnzt > 0) {  // block-uniform; loads for every round are issued before any is used
+        if (nnzt <= TILE)  // the common case: no snapped-in extra nonzeros
+            stage_products<IPT, CG, NT>(a, n0, nnzt, beta, s_prod);
+        else
+            stage_products<MAXJ, CG, NT>(a, n0, nnzt, beta, s_prod);
+    }
     for (int i = tid; i < nrows; i += kBlock)
         s_rowend[i] = a.row_offsets[r0 + 1 + i] - n0;
-    {
-        int c[MAXJ];
-        double v[MAXJ];
-#pragma unroll
-        for (int j = 0; j < MAXJ; ++j) {
-            const int k = tid + j * kBlock;
-            if (k < nnzt) {
-                c[j] = __builtin_nontemporal_load(a.cols + n0 + k);
-                v[j] = __builtin_nontemporal_load(a.vals + n0 + k);
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < MAXJ; ++j) {
-            const int k = tid + j * kBlock;
-            if (k < nnzt) {
-                double xv = a.x[c[j]];
-                if (CG)
-                    xv = xv + beta * a.p_old[c[j]];
-                s_prod[k] = v[j] * xv;
-            }
-        }
-    }
     __syncthreads();
 
     const int ipt = (items + kBlock - 1) / kBlock;
     const int d0 = min(tid * ipt, items);
-    const int d1 = min(d0 + ipt, items);
-    int cx, cy, ex, ey;
+    int cx, cy;
     lds_search(d0, s_rowend, nrows, nnzt, cx, cy);
-    lds_search(d1, s_rowend, nrows, nnzt, ex, ey);
+    // The walker's end is the next walker's start: one search per thread, shared via LDS.
+    s_crow[tid] = cx;
+    s_ccol[tid] = cy;
+    __syncthreads();
+    const int ex = tid + 1 < kBlock ? s_crow[tid + 1] : nrows;
+    const int ey = tid + 1 < kBlock ? s_ccol[tid + 1] : nnzt;
     // Does this thread's first row hold nonzeros that earlier threads of the tile consumed?
     const bool need_cin = (cx < ex) && (cy > (cx == 0 ? 0 : s_rowend[cx - 1]));
+    // This walker's products, read from LDS up front (independent reads, no dependent chain).
+    double pr[MAXJ];
+    if (ey > cy) {
+#pragma unroll
+        for (int j = 0; j < MAXJ; ++j)
+            pr[j] = s_prod[pslot(min(cy + j, ey - 1))];
+    }
 
     double dot = 0.0;
     auto write_row = [&](int row, double val) {
@@ -222,20 +290,26 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
     bool first = true, pend = false;
     int prow = 0;
     double pval = 0.0;
-    for (int k = cy; k < ey; ++k) {
-        while (cx < ex && s_rowend[cx] <= k) {
-            if (first && need_cin) {
-                pend = true;
-                prow = cx;
-                pval = run;
-            } else {
-                write_row(cx, run);
+    int next_end = cx < ex ? s_rowend[cx] : 0x7fffffff;  // end of the row being accumulated
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+        const int k = cy + j;
+        if (k < ey) {
+            while (next_end <= k) {
+                if (first && need_cin) {
+                    pend = true;
+                    prow = cx;
+                    pval = run;
+                } else {
+                    write_row(cx, run);
+                }
+                first = false;
+                run = 0.0;
+                ++cx;
+                next_end = cx < ex ? s_rowend[cx] : 0x7fffffff;
             }
-            first = false;
-            run = 0.0;
-            ++cx;
+            run += pr[j];
         }
-        run += s_prod[k];
     }
     while (cx < ex) {
         if (first && need_cin) {
@@ -249,6 +323,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
         run = 0.0;
         ++cx;
     }
+    __syncthreads();  // every walker has read its neighbour's start from s_crow / s_ccol
     s_crow[tid] = ex;
     s_cval[tid] = run;
     __syncthreads();
@@ -317,7 +392,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
     constexpr int GL = L / 2;
     constexpr int NG = kBlock / GL;
     constexpr int TILE = NG * IPTG;
-    constexpr int MAXI = TILE + TILE / 2;
+    constexpr int MAXI = TILE + TILE / kSnapDiv;
     constexpr int MAXJ = (MAXI + NG - 1) / NG;
     constexpr int STG = (MAXI + kBlock - 1) / kBlock;
     __shared__ int s_rowend[MAXI];
@@ -350,8 +425,8 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
     for (int j = 0; j < STG; ++j) {
         const int k = tid + j * kBlock;
         if (k < nnzt) {
-            s_col[k] = __builtin_nontemporal_load(a.cols + n0 + k);
-            s_val[k] = __builtin_nontemporal_load(a.vals + n0 + k);
+            s_col[k] = ld_stream<!CG>(a.cols + n0 + k);
+            s_val[k] = ld_stream<!CG>(a.vals + n0 + k);
         }
     }
     __syncthreads();
@@ -367,20 +442,27 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
     // Gather this walk's panel rows up front (<= MAXJ independent 16-B loads in flight).
     double2 xr[MAXJ];
     double vv[MAXJ];
+    if (ey > cy) {  // branch-free gather of every panel row this walk needs (clamped)
+        int cc[MAXJ];
 #pragma unroll
-    for (int j = 0; j < MAXJ; ++j) {
-        const int k = cy + j;
-        if (k < ey) {
-            const int c = s_col[k];
+        for (int j = 0; j < MAXJ; ++j) {
+            const int k = min(cy + j, ey - 1);
+            cc[j] = s_col[k];
             vv[j] = s_val[k];
-            const size_t off = (size_t)c * L + 2 * lane;
-            double2 xv = *reinterpret_cast<const double2 *>(a.x + off);
-            if (CG) {
-                const double2 po = *reinterpret_cast<const double2 *>(a.p_old + off);
-                xv.x = xv.x + beta2.x * po.x;
-                xv.y = xv.y + beta2.y * po.y;
+        }
+#pragma unroll
+        for (int j = 0; j < MAXJ; ++j)
+            xr[j] = *reinterpret_cast<const double2 *>(a.x + (size_t)cc[j] * L + 2 * lane);
+        if (CG) {
+            double2 po[MAXJ];
+#pragma unroll
+            for (int j = 0; j < MAXJ; ++j)
+                po[j] = *reinterpret_cast<const double2 *>(a.p_old + (size_t)cc[j] * L + 2 * lane);
+#pragma unroll
+            for (int j = 0; j < MAXJ; ++j) {
+                xr[j].x = xr[j].x + beta2.x * po[j].x;
+                xr[j].y = xr[j].y + beta2.y * po[j].y;
             }
-            xr[j] = xv;
         }
     }
 
@@ -793,13 +875,34 @@ __global__ void k_flush(double *p, long long n, double v)
 // ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
-constexpr int kIptSpmv = 8;   // 2048 merge items per SpMV tile
 constexpr int kIptgSpmm = 8;  // items per lane group for SpMM tiles
+
+// SpMV tuning: items per thread (tile = 256 * ipt merge items) and nontemporal matrix loads.
+// Defaults are the measured best; MSPMV_SPMV_IPT / MSPMV_SPMV_NT override them for A/B runs.
+struct SpmvTuning {
+    int ipt = 8;
+    int nt = 1;
+};
+static const SpmvTuning &spmv_tuning()
+{
+    static SpmvTuning t = [] {
+        SpmvTuning v;
+        if (const char *e = getenv("MSPMV_SPMV_IPT")) {
+            const int i = atoi(e);
+            if (i == 2 || i == 4 || i == 8 || i == 16)
+                v.ipt = i;
+        }
+        if (const char *e = getenv("MSPMV_SPMV_NT"))
+            v.nt = atoi(e) != 0;
+        return v;
+    }();
+    return t;
+}
 
 int tile_items_for(int L)
 {
     if (L == 1)
-        return kBlock * kIptSpmv;
+        return kBlock * spmv_tuning().ipt;
     return (kBlock / (L / 2)) * kIptgSpmm;
 }
 
@@ -843,7 +946,26 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s)
 {
     const dim3 grid(a.num_tiles), block(kBlock);
     switch (L) {
-    case 1: hipLaunchKernelGGL((k_spmv_tile<kIptSpmv, CG>), grid, block, 0, s, a); break;
+    case 1: {
+        const SpmvTuning &tu = spmv_tuning();
+        const bool nt = !CG && tu.nt;  // CG re-reads A every iteration: keep default cache policy
+#define MSPMV_SPMV_CASE(I)                                                                          \
+    case I:                                                                                        \
+        if (nt)                                                                                    \
+            hipLaunchKernelGGL((k_spmv_tile<I, CG, true>), grid, block, 0, s, a);                   \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_spmv_tile<I, CG, false>), grid, block, 0, s, a);                  \
+        break;
+        switch (tu.ipt) {
+            MSPMV_SPMV_CASE(2)
+            MSPMV_SPMV_CASE(4)
+            MSPMV_SPMV_CASE(8)
+            MSPMV_SPMV_CASE(16)
+        default: return hipErrorInvalidValue;
+        }
+#undef MSPMV_SPMV_CASE
+        break;
+    }
     case 2: hipLaunchKernelGGL((k_spmm_tile<2, kIptgSpmm, CG>), grid, block, 0, s, a); break;
     case 4: hipLaunchKernelGGL((k_spmm_tile<4, kIptgSpmm, CG>), grid, block, 0, s, a); break;
     case 8: hipLaunchKernelGGL((k_spmm_tile<8, kIptgSpmm, CG>), grid, block, 0, s, a); break;

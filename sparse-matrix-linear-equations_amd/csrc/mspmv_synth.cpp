@@ -73,6 +73,63 @@ mspmv_status mspmv_synth_banded(int m, long long nnz, int half_band, unsigned lo
     return MSPMV_OK;
 }
 
+mspmv_status mspmv_synth_fem_blocked(int m, long long nnz, int block, int half_band_nodes,
+                                     unsigned long long seed, int *row_offsets, int *cols, double *vals)
+{
+    if (m <= 0 || block <= 0 || nnz < 0 || nnz > 0x7fffffffLL || !row_offsets || (nnz && (!cols || !vals)))
+        return MSPMV_ERR_INVALID;
+    const int nodes = (m + block - 1) / block;
+    const long long maxlen = (nnz + m - 1) / m;
+    const int maxblk = (int)((maxlen + block - 1) / block);
+    if (half_band_nodes < 0 || 2LL * half_band_nodes + 1 < maxblk || maxblk > nodes)
+        return MSPMV_ERR_INVALID;
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i <= m; ++i)
+        row_offsets[i] = (int)((long long)i * nnz / m);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int I = 0; I < nodes; ++I) {
+        // neighbour nodes of node I: maxblk picks, one per slice of the node band, own node forced
+        int nb[1024];
+        const int nblk = std::min(maxblk, 1024);
+        const int lo = std::max(0, I - half_band_nodes), hi = std::min(nodes - 1, I + half_band_nodes);
+        const int span = hi - lo + 1;
+        const int take = std::min(nblk, span);
+        bucket_cols(lo, hi, take, seed, (uint64_t)I, nb);
+        bool has_self = false;
+        for (int k = 0; k < take; ++k)
+            has_self |= nb[k] == I;
+        if (!has_self) {  // replace the pick in I's slice by I itself (keeps the list sorted)
+            int k = 0;
+            while (k + 1 < take && nb[k + 1] <= I)
+                ++k;
+            if (nb[k] > I)
+                k = 0;
+            nb[k] = I;
+            std::sort(nb, nb + take);
+            for (int q = 1; q < take; ++q)  // resolve a possible duplicate with a neighbour slot
+                if (nb[q] <= nb[q - 1])
+                    nb[q] = nb[q - 1] + 1;
+        }
+        const int r_end = std::min(m, (I + 1) * block);
+        for (int i = I * block; i < r_end; ++i) {
+            const int s = row_offsets[i], ell = row_offsets[i + 1] - s;
+            int k = 0;
+            for (int q = 0; q < take && k < ell; ++q)
+                for (int d = 0; d < block && k < ell; ++d) {
+                    const long long c = (long long)nb[q] * block + d;
+                    if (c >= m)
+                        break;
+                    cols[s + k++] = (int)c;
+                }
+            for (int extra = 0; k < ell; ++extra)  // only when the matrix edge cut a block short
+                cols[s + k++] = std::min(m - 1, (int)(((long long)nb[take - 1] + 1) * block + extra));
+            for (int q = 0; q < ell; ++q)
+                vals[s + q] = 0.5 + u01(seed ^ 0x5bd1e995ull, (uint64_t)(s + q));
+        }
+    }
+    return MSPMV_OK;
+}
+
 mspmv_status mspmv_synth_powerlaw(int m, int n, long long nnz, double exponent, unsigned long long seed,
                                   int *row_offsets, int *cols, double *vals)
 {

@@ -93,6 +93,7 @@ _SIGS = {
     "mspmv_memcpy_d2d": (_I, [_P, _P, _SZ]),
     "mspmv_memset_dev": (_I, [_P, _I, _SZ]),
     "mspmv_synth_banded": (_I, [_I, ctypes.c_longlong, _I, ctypes.c_ulonglong, _P, _P, _P]),
+    "mspmv_synth_fem_blocked": (_I, [_I, ctypes.c_longlong, _I, _I, ctypes.c_ulonglong, _P, _P, _P]),
     "mspmv_synth_powerlaw": (_I, [_I, _I, ctypes.c_longlong, _D, ctypes.c_ulonglong, _P, _P, _P]),
     "mspmv_synth_stencil": (_I, [_I, _I, _I, _I, _I, ctypes.c_ulonglong, _P, _P, _P,
                                  ctypes.POINTER(ctypes.c_longlong)]),
@@ -161,6 +162,16 @@ class CsrMatrix:
         ci = np.empty(max(nnz, 1), np.int32)
         va = np.empty(max(nnz, 1), np.float64)
         _check(lib.mspmv_synth_banded(m, nnz, half_band, seed, _ptr(ro), _ptr(ci), _ptr(va)), "synth_banded")
+        return cls(m, m, nnz, ro, ci[:nnz], va[:nnz])
+
+    @classmethod
+    def synth_fem_blocked(cls, m: int, nnz: int, block: int, half_band_nodes: int, seed: int = 1) -> "CsrMatrix":
+        """FEM-like pattern: nodes of `block` unknowns, runs of `block` consecutive columns."""
+        ro = np.empty(m + 1, np.int32)
+        ci = np.empty(max(nnz, 1), np.int32)
+        va = np.empty(max(nnz, 1), np.float64)
+        _check(lib.mspmv_synth_fem_blocked(m, nnz, block, half_band_nodes, seed, _ptr(ro), _ptr(ci), _ptr(va)),
+               "synth_fem_blocked")
         return cls(m, m, nnz, ro, ci[:nnz], va[:nnz])
 
     @classmethod

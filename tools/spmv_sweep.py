@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""A/B sweep of SpMV tile variants on the bench workload (pwtk-shaped batch, cold per launch).
+
+    python tools/spmv_sweep.py                 # parent: runs every variant in child processes
+    python tools/spmv_sweep.py --child         # child: one timing line for the env's variant
+
+Variants are selected with MSPMV_SPMV_IPT / MSPMV_SPMV_NT (read once per process), so each
+runs in its own process; rounds alternate variants to spread device drift.
+"""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "sparse-matrix-linear-equations_amd")]
+
+
+def child():
+    import numpy as np
+    import mspmv
+    B = int(os.environ.get("SWEEP_BATCH", "4"))
+    gs, dx, dy = [], [], []
+    for i in range(B):
+        if os.environ.get("SWEEP_SHAPE", "fem") == "fem":
+            a = mspmv.CsrMatrix.synth_fem_blocked(217918, 11524432, 6, 1700, seed=1 + i)
+        else:
+            a = mspmv.CsrMatrix.synth_banded(217918, 11524432, 10000, seed=1 + i)
+        gs.append(mspmv.GpuCsr(a))
+        dx.append(mspmv.DeviceBuffer.from_array(np.random.default_rng(i).uniform(0, 1, a.num_cols)))
+        dy.append(mspmv.DeviceBuffer(8 * a.num_rows))
+    mspmv.time_spmm_batch(gs, dx, dy, 1, 5)
+    step, kern, _ = mspmv.time_spmm_batch(gs, dx, dy, 1, 50)
+    hot_step, hot_kern, _ = mspmv.time_spmm_batch(gs[:1], dx[:1], dy[:1], 1, 200)
+    nbytes = 12 * 11524432 + 4 * 217919 + 16 * 217918
+    print(json.dumps({"ipt": os.environ.get("MSPMV_SPMV_IPT"), "nt": os.environ.get("MSPMV_SPMV_NT"),
+                      "cold_kernel_us": round(kern * 1e3, 2), "cold_GBps": round(nbytes / kern / 1e6, 1),
+                      "step_us": round(step * 1e3, 2), "hot_kernel_us": round(hot_kern * 1e3, 2),
+                      "hot_GBps": round(nbytes / hot_kern / 1e6, 1)}), flush=True)
+
+
+def parent():
+    spec = os.environ.get("SWEEP_VARIANTS", "2:0,2:1,4:0,4:1,8:0,8:1,16:0,16:1")
+    variants = [tuple(int(x) for x in v.split(":")) for v in spec.split(",")]
+    rounds = int(os.environ.get("SWEEP_ROUNDS", "2"))
+    for r in range(rounds):
+        for ipt, nt in variants:
+            env = dict(os.environ, MSPMV_SPMV_IPT=str(ipt), MSPMV_SPMV_NT=str(nt))
+            out = subprocess.run([sys.executable, __file__, "--child"], env=env, capture_output=True, text=True,
+                                 timeout=300)
+            if out.returncode != 0:
+                print(f"variant ipt={ipt} nt={nt} failed rc={out.returncode}: {out.stderr[-500:]}", flush=True)
+                sys.exit(out.returncode)
+            print(f"round {r} " + out.stdout.strip(), flush=True)
+
+
+if __name__ == "__main__":
+    child() if "--child" in sys.argv else parent()
