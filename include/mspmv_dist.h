@@ -1,0 +1,72 @@
+/*
+ * mspmv_dist.h -- row-block sharded SpMV/SpMM and block CG over several GPUs (one process per
+ * GPU), RCCL over xGMI.  Part of libmspmv.so.
+ *
+ * The reference is single-process OpenMP and has no multi-GPU code; this is the
+ * north-star's "matrices shard by row-block across the node's 8 GPUs with an RCCL all-reduce of
+ * the CG dot products over xGMI".  Per CG iteration (CGSolveMultiple's recurrence,
+ * no_pretreatment.hpp:32-197, unchanged):
+ *   p_own = r + beta p_own; pack the owned p rows other ranks reference; grouped
+ *   ncclSend/ncclRecv into this rank's halo rows; Ap = A_local [p_own | p_halo] with the
+ *   local p.Ap; ncclAllReduce(L doubles); x += alpha p, r -= alpha Ap with the local r.r;
+ *   ncclAllReduce(L doubles); one-block convergence / beta step.
+ * Everything is stream-ordered on the local handle's stream; the host only polls the
+ * convergence flag once per batch of iterations.
+ */
+#ifndef MSPMV_DIST_H
+#define MSPMV_DIST_H
+
+#include "mspmv.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSPMV_UNIQUE_ID_BYTES 128
+
+typedef struct mspmv_dist_s *mspmv_dist;
+
+/* ---- host planning (no GPU needed) ------------------------------------------------------ */
+/* Contiguous row blocks balanced by merge path: row_begin[g] (g = 0..nranks) is the row
+ * coordinate of diagonal min(ceil((m+nnz)/nranks) * g, m+nnz) (MergePathSearch,
+ * cpu_spmv.cpp:208-235, at GPU granularity), so every rank gets equal rows + nonzeros. */
+MSPMV_API mspmv_status mspmv_dist_partition(const int *row_offsets, int num_rows, int num_nonzeros, int nranks,
+                                            int *row_begin);
+
+/* Localize rank `rank`'s rows (CSR with GLOBAL column ids, local_row_offsets rebased to 0):
+ * columns in [row_begin[rank], row_begin[rank+1]) become 0..n_own-1, every other column
+ * n_own + its position among the sorted distinct halo columns.  The nonzero order is kept
+ * (so each row is summed in the reference's CSR order).  halo_global (capacity halo_cap;
+ * NULL to size) receives the halo columns in that order -- grouped by owner rank, since
+ * ranks own ascending row ranges -- and halo_counts[g] how many rank g owns.  Requires a
+ * square matrix (columns partitioned like rows). */
+MSPMV_API mspmv_status mspmv_dist_localize(const int *row_begin, int nranks, int rank, const int *local_row_offsets,
+                                           const int *global_cols, int *local_cols, int *n_halo, int *halo_global,
+                                           int halo_cap, int *halo_counts);
+
+/* ---- communicator and sharded matrix ------------------------------------------------------ */
+/* Rank 0 creates the RCCL id and the host broadcasts it (torch.distributed, MPI, ...). */
+MSPMV_API mspmv_status mspmv_comm_unique_id(unsigned char id[MSPMV_UNIQUE_ID_BYTES]);
+/* Collective over all ranks: RCCL communicator init, localization of this rank's row block
+ * (`local_rows`: num_rows = rows owned, num_cols = global columns, GLOBAL column ids), upload,
+ * and the halo-exchange plan (request lists exchanged once with RCCL). */
+MSPMV_API mspmv_status mspmv_dist_create(const unsigned char id[MSPMV_UNIQUE_ID_BYTES], int nranks, int rank,
+                                         int device, const int *row_begin, const mspmv_csr_d *local_rows,
+                                         mspmv_dist *out);
+MSPMV_API mspmv_status mspmv_dist_destroy(mspmv_dist d);
+/* n_own rows owned, n_halo remote rows referenced, n_send owned rows other ranks reference. */
+MSPMV_API mspmv_status mspmv_dist_info(mspmv_dist d, int *n_own, int *n_halo, int *n_send);
+/* Y_own = (A X)_own with the halo exchange (collective).  Row-major n_own x L panels on the
+ * device.  L in {1, 2, 4, 8, 16}. */
+MSPMV_API mspmv_status mspmv_dist_spmm_dev(mspmv_dist d, const double *d_X_own, double *d_Y_own, int L);
+/* Sharded CGSolveMultiple (collective): B_own / X_own are this rank's rows of the interleaved
+ * n x L panels.  Iteration count, history and breakdown semantics as mspmv_dcg_multi. */
+MSPMV_API mspmv_status mspmv_dist_cg_dev(mspmv_dist d, const double *d_B_own, double *d_X_own, int L,
+                                         int max_iters, double tolerance, int *iters, double *max_err_hist,
+                                         int hist_cap);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MSPMV_DIST_H */

@@ -212,6 +212,9 @@ static mspmv_status create_common(const mspmv_csr_d *a, int device, bool from_de
         mspmv_destroy(h);
         return s;
     };
+    if (hipDeviceGetAttribute(&h->num_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        h->num_cus < 1)
+        h->num_cus = 256;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         set_error("hipStreamCreate failed");
         return fail(MSPMV_ERR_HIP);

@@ -1,0 +1,563 @@
+// mspmv_dist.hip -- row-block sharded SpMM and block CG over several GPUs (include/mspmv_dist.h).
+// Host planning is plain C++ (testable without a GPU); the data path is HIP kernels on the
+// local handle's stream plus RCCL point-to-point halo exchange and all-reduces over xGMI.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "mspmv_dist.h"
+#include "mspmv_internal.h"
+
+using namespace mspmv;
+
+namespace {
+
+mspmv_status fail_msg(mspmv_status st, const std::string &msg)
+{
+    set_error(msg);
+    return st;
+}
+
+#define D_HIP(expr)                                                                                \
+    do {                                                                                           \
+        hipError_t _e = (expr);                                                                    \
+        if (_e != hipSuccess)                                                                      \
+            return fail_msg(_e == hipErrorOutOfMemory ? MSPMV_ERR_OOM : MSPMV_ERR_HIP,             \
+                            std::string(#expr) + ": " + hipGetErrorString(_e));                    \
+    } while (0)
+
+#define D_NCCL(expr)                                                                               \
+    do {                                                                                           \
+        ncclResult_t _r = (expr);                                                                  \
+        if (_r != ncclSuccess)                                                                     \
+            return fail_msg(MSPMV_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(_r));   \
+    } while (0)
+
+#define D_ST(expr)                                                                                 \
+    do {                                                                                           \
+        mspmv_status _s = (expr);                                                                  \
+        if (_s != MSPMV_OK)                                                                        \
+            return _s;                                                                             \
+    } while (0)
+
+template <typename T>
+mspmv_status dalloc(T **p, size_t n)
+{
+    *p = nullptr;
+    hipError_t e = hipMalloc((void **)p, std::max<size_t>(n, 1) * sizeof(T));
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return fail_msg(e == hipErrorOutOfMemory ? MSPMV_ERR_OOM : MSPMV_ERR_HIP,
+                        std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
+    return MSPMV_OK;
+}
+
+template <typename T>
+void dfree(T *&p)
+{
+    if (p)
+        (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+}  // namespace
+
+struct mspmv_dist_s {
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0, device = 0;
+    int row_lo = 0, n_own = 0, n_halo = 0, n_send = 0;
+    std::vector<int> row_begin;
+    mspmv_handle local = nullptr;  // n_own x (n_own + n_halo) local CSR, owns the stream
+    // exchange plan (element counts in rows; multiplied by L at run time)
+    std::vector<int> send_counts, send_displs, recv_counts, recv_displs;
+    int *d_send_idx = nullptr;  // owned row index of every row to send, grouped by peer
+    // buffers (grown to the largest L used)
+    int cap_L = 0;
+    double *d_pext = nullptr;   // (n_own + n_halo) x L : [p_own | p_halo]
+    double *d_send = nullptr;   // n_send x L
+    double *d_r = nullptr, *d_ap = nullptr;  // n_own x L
+    double *d_partials = nullptr;
+    size_t partials_cap = 0;
+    CgScalars *d_scal = nullptr;
+    unsigned char *d_conv = nullptr;
+    CgControl *d_ctrl = nullptr;
+    CgControl *h_ctrl = nullptr;  // pinned
+    double *d_red = nullptr;      // [2 L]: p.Ap, r.r
+    double *d_hist = nullptr;
+    int hist_cap = 0;
+};
+
+extern "C" {
+
+mspmv_status mspmv_dist_partition(const int *row_offsets, int num_rows, int num_nonzeros, int nranks, int *row_begin)
+{
+    if (!row_offsets || !row_begin || nranks < 1 || num_rows < 0 || num_nonzeros < 0)
+        return fail_msg(MSPMV_ERR_INVALID, "dist_partition: bad arguments");
+    const long long total = (long long)num_rows + num_nonzeros;
+    const long long step = (total + nranks - 1) / nranks;
+    const int *a = row_offsets + 1;
+    for (int g = 0; g <= nranks; ++g) {
+        const long long dl = std::min(step * g, total);
+        const int d = (int)dl;
+        int lo = std::max(d - num_nonzeros, 0), hi = std::min(d, num_rows);
+        while (lo < hi) {
+            const int pivot = (lo + hi) >> 1;
+            if (a[pivot] <= d - pivot - 1)
+                lo = pivot + 1;
+            else
+                hi = pivot;
+        }
+        row_begin[g] = std::min(lo, num_rows);
+    }
+    row_begin[0] = 0;
+    row_begin[nranks] = num_rows;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_dist_localize(const int *row_begin, int nranks, int rank, const int *local_row_offsets,
+                                 const int *global_cols, int *local_cols, int *n_halo, int *halo_global, int halo_cap,
+                                 int *halo_counts)
+{
+    if (!row_begin || nranks < 1 || rank < 0 || rank >= nranks || !local_row_offsets || !n_halo)
+        return fail_msg(MSPMV_ERR_INVALID, "dist_localize: bad arguments");
+    const int lo = row_begin[rank], hi = row_begin[rank + 1];
+    const int rows = hi - lo;
+    const int nnz = local_row_offsets[rows];
+    if (nnz > 0 && !global_cols)
+        return fail_msg(MSPMV_ERR_INVALID, "dist_localize: null columns");
+    std::vector<int> halo;
+    halo.reserve(1024);
+    for (int k = 0; k < nnz; ++k) {
+        const int c = global_cols[k];
+        if (c < lo || c >= hi)
+            halo.push_back(c);
+    }
+    std::sort(halo.begin(), halo.end());
+    halo.erase(std::unique(halo.begin(), halo.end()), halo.end());
+    *n_halo = (int)halo.size();
+    if (halo_counts) {
+        for (int g = 0; g < nranks; ++g) {
+            auto b = std::lower_bound(halo.begin(), halo.end(), row_begin[g]);
+            auto e = std::lower_bound(halo.begin(), halo.end(), row_begin[g + 1]);
+            halo_counts[g] = (int)(e - b);
+        }
+    }
+    if (halo_global) {
+        if (halo_cap < (int)halo.size())
+            return fail_msg(MSPMV_ERR_INVALID, "dist_localize: halo_cap too small");
+        std::copy(halo.begin(), halo.end(), halo_global);
+    }
+    if (local_cols) {
+        const int n_own = rows;
+#pragma omp parallel for schedule(static)
+        for (int k = 0; k < nnz; ++k) {
+            const int c = global_cols[k];
+            if (c >= lo && c < hi)
+                local_cols[k] = c - lo;
+            else
+                local_cols[k] = n_own + (int)(std::lower_bound(halo.begin(), halo.end(), c) - halo.begin());
+        }
+    }
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_comm_unique_id(unsigned char id[MSPMV_UNIQUE_ID_BYTES])
+{
+    static_assert(sizeof(ncclUniqueId) == MSPMV_UNIQUE_ID_BYTES, "RCCL unique id size");
+    if (!id)
+        return fail_msg(MSPMV_ERR_INVALID, "null id");
+    ncclUniqueId u;
+    D_NCCL(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, sizeof(u));
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_dist_destroy(mspmv_dist d)
+{
+    if (!d)
+        return MSPMV_OK;
+    (void)hipSetDevice(d->device);
+    if (d->local)
+        mspmv_sync(d->local);
+    dfree(d->d_send_idx);
+    dfree(d->d_pext);
+    dfree(d->d_send);
+    dfree(d->d_r);
+    dfree(d->d_ap);
+    dfree(d->d_partials);
+    dfree(d->d_scal);
+    dfree(d->d_conv);
+    dfree(d->d_ctrl);
+    dfree(d->d_red);
+    dfree(d->d_hist);
+    if (d->h_ctrl)
+        (void)hipHostFree(d->h_ctrl);
+    if (d->local)
+        mspmv_destroy(d->local);
+    if (d->comm)
+        ncclCommDestroy(d->comm);
+    delete d;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_dist_create(const unsigned char id[MSPMV_UNIQUE_ID_BYTES], int nranks, int rank, int device,
+                               const int *row_begin, const mspmv_csr_d *local_rows, mspmv_dist *out)
+{
+    if (!id || !row_begin || !local_rows || !out || nranks < 1 || rank < 0 || rank >= nranks)
+        return fail_msg(MSPMV_ERR_INVALID, "dist_create: bad arguments");
+    *out = nullptr;
+    const int lo = row_begin[rank], hi = row_begin[rank + 1];
+    if (local_rows->num_rows != hi - lo || local_rows->num_cols != row_begin[nranks])
+        return fail_msg(MSPMV_ERR_INVALID, "dist_create: local rows do not match row_begin (square matrix needed)");
+    D_HIP(hipSetDevice(device));
+    auto *d = new mspmv_dist_s();
+    d->nranks = nranks;
+    d->rank = rank;
+    d->device = device;
+    d->row_lo = lo;
+    d->n_own = hi - lo;
+    d->row_begin.assign(row_begin, row_begin + nranks + 1);
+    auto bail = [&](mspmv_status s) {
+        mspmv_dist_destroy(d);
+        return s;
+    };
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    ncclResult_t nr = ncclCommInitRank(&d->comm, nranks, u, rank);
+    if (nr != ncclSuccess) {
+        d->comm = nullptr;
+        return bail(fail_msg(MSPMV_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(nr)));
+    }
+    // localize this rank's rows
+    const int nnz = local_rows->num_nonzeros;
+    std::vector<int> lcols((size_t)std::max(nnz, 1));
+    std::vector<int> halo_counts(nranks);
+    int n_halo = 0;
+    mspmv_status st = mspmv_dist_localize(row_begin, nranks, rank, local_rows->row_offsets, local_rows->column_indices,
+                                          nullptr, &n_halo, nullptr, 0, nullptr);
+    if (st != MSPMV_OK)
+        return bail(st);
+    std::vector<int> halo((size_t)std::max(n_halo, 1));
+    st = mspmv_dist_localize(row_begin, nranks, rank, local_rows->row_offsets, local_rows->column_indices,
+                             lcols.data(), &n_halo, halo.data(), n_halo, halo_counts.data());
+    if (st != MSPMV_OK)
+        return bail(st);
+    d->n_halo = n_halo;
+    mspmv_csr_d lc = *local_rows;
+    lc.num_cols = d->n_own + n_halo;
+    lc.column_indices = lcols.data();
+    if ((st = mspmv_csr_create(&lc, device, &d->local)) != MSPMV_OK)
+        return bail(st);
+    hipStream_t s = d->local->stream;
+    // request lists: every rank learns the counts matrix, then sends each owner the global
+    // ids it needs; the owner keeps them (as local rows) as its send list to that rank
+    int *d_cnt = nullptr, *d_cnt_all = nullptr, *d_halo = nullptr, *d_req = nullptr;
+    auto cleanup = [&]() {
+        dfree(d_cnt);
+        dfree(d_cnt_all);
+        dfree(d_halo);
+        dfree(d_req);
+    };
+    if ((st = dalloc(&d_cnt, nranks)) != MSPMV_OK || (st = dalloc(&d_cnt_all, (size_t)nranks * nranks)) != MSPMV_OK ||
+        (st = dalloc(&d_halo, halo.size())) != MSPMV_OK) {
+        cleanup();
+        return bail(st);
+    }
+    std::vector<int> cnt_all((size_t)nranks * nranks);
+    hipError_t he = hipMemcpy(d_cnt, halo_counts.data(), sizeof(int) * nranks, hipMemcpyHostToDevice);
+    if (he == hipSuccess && n_halo)
+        he = hipMemcpy(d_halo, halo.data(), sizeof(int) * n_halo, hipMemcpyHostToDevice);
+    if (he != hipSuccess) {
+        cleanup();
+        return bail(fail_msg(MSPMV_ERR_HIP, "dist_create: upload"));
+    }
+    nr = ncclAllGather(d_cnt, d_cnt_all, nranks, ncclInt32, d->comm, s);
+    if (nr == ncclSuccess && hipStreamSynchronize(s) == hipSuccess &&
+        hipMemcpy(cnt_all.data(), d_cnt_all, sizeof(int) * nranks * nranks, hipMemcpyDeviceToHost) == hipSuccess) {
+    } else {
+        cleanup();
+        return bail(fail_msg(MSPMV_ERR_RCCL, "dist_create: count all-gather failed"));
+    }
+    d->send_counts.assign(nranks, 0);
+    d->send_displs.assign(nranks + 1, 0);
+    d->recv_counts.assign(halo_counts.begin(), halo_counts.end());
+    d->recv_displs.assign(nranks + 1, 0);
+    for (int g = 0; g < nranks; ++g) {
+        d->send_counts[g] = cnt_all[(size_t)g * nranks + rank];  // rows rank g needs from me
+        d->send_displs[g + 1] = d->send_displs[g] + d->send_counts[g];
+        d->recv_displs[g + 1] = d->recv_displs[g] + d->recv_counts[g];
+    }
+    d->n_send = d->send_displs[nranks];
+    if ((st = dalloc(&d_req, d->n_send)) != MSPMV_OK) {
+        cleanup();
+        return bail(st);
+    }
+    nr = ncclGroupStart();
+    for (int g = 0; g < nranks && nr == ncclSuccess; ++g) {
+        if (g == rank)
+            continue;
+        if (d->recv_counts[g])
+            nr = ncclSend(d_halo + d->recv_displs[g], d->recv_counts[g], ncclInt32, g, d->comm, s);
+        if (nr == ncclSuccess && d->send_counts[g])
+            nr = ncclRecv(d_req + d->send_displs[g], d->send_counts[g], ncclInt32, g, d->comm, s);
+    }
+    ncclResult_t nr2 = ncclGroupEnd();
+    if (nr != ncclSuccess || nr2 != ncclSuccess || hipStreamSynchronize(s) != hipSuccess) {
+        cleanup();
+        return bail(fail_msg(MSPMV_ERR_RCCL, "dist_create: request exchange failed"));
+    }
+    std::vector<int> req((size_t)std::max(d->n_send, 1));
+    if (d->n_send && hipMemcpy(req.data(), d_req, sizeof(int) * d->n_send, hipMemcpyDeviceToHost) != hipSuccess) {
+        cleanup();
+        return bail(fail_msg(MSPMV_ERR_HIP, "dist_create: request download"));
+    }
+    cleanup();
+    for (int k = 0; k < d->n_send; ++k) {
+        req[k] -= lo;
+        if (req[k] < 0 || req[k] >= d->n_own)
+            return bail(fail_msg(MSPMV_ERR_INVALID, "dist_create: a peer requested a row this rank does not own"));
+    }
+    if ((st = dalloc(&d->d_send_idx, d->n_send)) != MSPMV_OK)
+        return bail(st);
+    if (d->n_send &&
+        hipMemcpy(d->d_send_idx, req.data(), sizeof(int) * d->n_send, hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail_msg(MSPMV_ERR_HIP, "dist_create: send list upload"));
+    if ((st = dalloc(&d->d_ctrl, 1)) != MSPMV_OK)
+        return bail(st);
+    if (hipHostMalloc((void **)&d->h_ctrl, sizeof(CgControl) * 2, hipHostMallocDefault) != hipSuccess)
+        return bail(fail_msg(MSPMV_ERR_HIP, "hipHostMalloc failed"));
+    *out = d;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_dist_info(mspmv_dist d, int *n_own, int *n_halo, int *n_send)
+{
+    if (!d)
+        return fail_msg(MSPMV_ERR_INVALID, "null dist");
+    if (n_own)
+        *n_own = d->n_own;
+    if (n_halo)
+        *n_halo = d->n_halo;
+    if (n_send)
+        *n_send = d->n_send;
+    return MSPMV_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+mspmv_status ensure_buffers(mspmv_dist_s *d, int L, int nblk, int num_tiles, int hist_cap)
+{
+    if (L > d->cap_L) {
+        dfree(d->d_pext);
+        dfree(d->d_send);
+        dfree(d->d_r);
+        dfree(d->d_ap);
+        dfree(d->d_scal);
+        dfree(d->d_conv);
+        dfree(d->d_red);
+        d->cap_L = 0;
+        D_ST(dalloc(&d->d_pext, (size_t)(d->n_own + d->n_halo) * L));
+        D_ST(dalloc(&d->d_send, (size_t)d->n_send * L));
+        D_ST(dalloc(&d->d_r, (size_t)d->n_own * L));
+        D_ST(dalloc(&d->d_ap, (size_t)d->n_own * L));
+        D_ST(dalloc(&d->d_scal, (size_t)L));
+        D_ST(dalloc(&d->d_conv, (size_t)L));
+        D_ST(dalloc(&d->d_red, (size_t)2 * L));
+        d->cap_L = L;
+    }
+    const size_t pc = (size_t)std::max(nblk, num_tiles) * L;
+    if (pc > d->partials_cap) {
+        dfree(d->d_partials);
+        d->partials_cap = 0;
+        D_ST(dalloc(&d->d_partials, pc));
+        d->partials_cap = pc;
+    }
+    if (hist_cap > d->hist_cap) {
+        dfree(d->d_hist);
+        d->hist_cap = 0;
+        D_ST(dalloc(&d->d_hist, (size_t)hist_cap));
+        d->hist_cap = hist_cap;
+    }
+    return MSPMV_OK;
+}
+
+// Pack the owned rows peers need and exchange them into the halo rows of d_pext.
+mspmv_status halo_exchange(mspmv_dist_s *d, int L, const CgControl *ctrl)
+{
+    hipStream_t s = d->local->stream;
+    D_HIP(launch_dist_pack(d->d_pext, d->d_send_idx, (long long)d->n_send * L, L, d->d_send, ctrl, s));
+    if (d->nranks == 1)
+        return MSPMV_OK;
+    D_NCCL(ncclGroupStart());
+    for (int g = 0; g < d->nranks; ++g) {
+        if (g == d->rank)
+            continue;
+        if (d->send_counts[g])
+            D_NCCL(ncclSend(d->d_send + (size_t)d->send_displs[g] * L, (size_t)d->send_counts[g] * L, ncclFloat64, g,
+                            d->comm, s));
+        if (d->recv_counts[g])
+            D_NCCL(ncclRecv(d->d_pext + (size_t)(d->n_own + d->recv_displs[g]) * L, (size_t)d->recv_counts[g] * L,
+                            ncclFloat64, g, d->comm, s));
+    }
+    D_NCCL(ncclGroupEnd());
+    return MSPMV_OK;
+}
+
+mspmv_status get_local_plan(mspmv_dist_s *d, int L, const TilePlan **plan)
+{
+    // mspmv_tile_plan builds (once) and returns the plan; the internal pointer comes from the map
+    int nt = 0;
+    D_ST(mspmv_tile_plan(d->local, L, &nt, nullptr, nullptr, nullptr));
+    auto it = d->local->plans.find(tile_items_for(L));
+    if (it == d->local->plans.end())
+        return fail_msg(MSPMV_ERR_INVALID, "local tile plan missing");
+    *plan = &it->second;
+    return MSPMV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+mspmv_status mspmv_dist_spmm_dev(mspmv_dist d, const double *d_X_own, double *d_Y_own, int L)
+{
+    if (!d)
+        return fail_msg(MSPMV_ERR_INVALID, "null dist");
+    if (!supported_L(L))
+        return fail_msg(MSPMV_ERR_UNSUPPORTED, "L must be one of 1, 2, 4, 8, 16");
+    D_HIP(hipSetDevice(d->device));
+    const TilePlan *plan = nullptr;
+    D_ST(get_local_plan(d, L, &plan));
+    D_ST(ensure_buffers(d, L, 1, plan->num_tiles, 0));
+    hipStream_t s = d->local->stream;
+    if (d->n_own)
+        D_HIP(hipMemcpyAsync(d->d_pext, d_X_own, sizeof(double) * (size_t)d->n_own * L, hipMemcpyDeviceToDevice, s));
+    D_ST(halo_exchange(d, L, nullptr));
+    return mspmv_dspmm_dev(d->local, d->d_pext, d_Y_own, L);
+}
+
+mspmv_status mspmv_dist_cg_dev(mspmv_dist d, const double *d_B_own, double *d_X_own, int L, int max_iters,
+                               double tolerance, int *iters, double *max_err_hist, int hist_cap)
+{
+    if (!d)
+        return fail_msg(MSPMV_ERR_INVALID, "null dist");
+    if (!supported_L(L))
+        return fail_msg(MSPMV_ERR_UNSUPPORTED, "L must be one of 1, 2, 4, 8, 16");
+    if (max_iters < 0)
+        return fail_msg(MSPMV_ERR_INVALID, "max_iters < 0");
+    D_HIP(hipSetDevice(d->device));
+    const TilePlan *plan = nullptr;
+    D_ST(get_local_plan(d, L, &plan));
+    const long long elems = (long long)d->n_own * L;
+    const int nblk = cg_update_blocks(std::max(elems, 2LL));
+    const int cap = max_err_hist ? std::max(hist_cap, 0) : 0;
+    D_ST(ensure_buffers(d, L, nblk, plan->num_tiles, cap));
+    hipStream_t s = d->local->stream;
+    DistVecArgs va{};
+    va.n_elems = elems;
+    va.x = d_X_own;
+    va.r = d->d_r;
+    va.p = d->d_pext;
+    va.p0 = d->d_pext;
+    va.ap = d->d_ap;
+    va.scal = d->d_scal;
+    va.ctrl = d->d_ctrl;
+    va.conv = d->d_conv;
+    va.partials = d->d_partials;
+    va.hist = cap ? d->d_hist : nullptr;
+    va.hist_cap = cap;
+    va.tol = tolerance;
+    double *pAp = d->d_red, *rr = d->d_red + L;
+    // init: x = 0, r = p = b; all-reduce b.b; scalars
+    D_HIP(hipMemsetAsync(d->d_ctrl, 0, sizeof(CgControl), s));
+    {
+        DistVecArgs a = va;
+        a.p = d_B_own;
+        a.red_out = rr;
+        D_HIP(launch_dist_vec_mirror(0, a, L, nblk, nullptr, s));
+        D_NCCL(ncclAllReduce(rr, rr, L, ncclFloat64, ncclSum, d->comm, s));
+        a.red_in = rr;
+        D_HIP(launch_dist_vec_mirror(1, a, L, 1, nullptr, s));
+    }
+    auto iteration = [&]() -> mspmv_status {
+        DistVecArgs a = va;
+        D_HIP(launch_dist_vec_mirror(2, a, L, nblk, d->d_pext, s));       // p = r + beta p
+        D_ST(halo_exchange(d, L, d->d_ctrl));                               // p halo rows
+        D_HIP(launch_spmm_dot(d->local, *plan, d->d_pext, d->d_ap, L, d->d_ctrl, d->d_partials, pAp));
+        D_NCCL(ncclAllReduce(pAp, pAp, L, ncclFloat64, ncclSum, d->comm, s));
+        a.red_in = pAp;
+        a.red_out = rr;
+        D_HIP(launch_dist_vec_mirror(3, a, L, nblk, nullptr, s));          // x, r, local r.r
+        D_NCCL(ncclAllReduce(rr, rr, L, ncclFloat64, ncclSum, d->comm, s));
+        D_HIP(launch_dist_vec_mirror(4, a, L, 1, nullptr, s));             // stop test, beta
+        return MSPMV_OK;
+    };
+    // batches of K iterations, the control word of batch b inspected while b+1 is queued
+    constexpr int K = 16;
+    hipEvent_t evs[2] = {nullptr, nullptr};
+    D_HIP(hipEventCreateWithFlags(&evs[0], hipEventDisableTiming));
+    D_HIP(hipEventCreateWithFlags(&evs[1], hipEventDisableTiming));
+    mspmv_status st = MSPMV_OK;
+    int launched = 0, pending = 0, oldest = 0, slot = 0;
+    while (st == MSPMV_OK) {
+        const int k = std::min(K, max_iters - launched);
+        if (k > 0) {
+            for (int i = 0; i < k && st == MSPMV_OK; ++i)
+                st = iteration();
+            if (st != MSPMV_OK)
+                break;
+            if (hipMemcpyAsync(&d->h_ctrl[slot], d->d_ctrl, sizeof(CgControl), hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipEventRecord(evs[slot], s) != hipSuccess) {
+                st = fail_msg(MSPMV_ERR_HIP, "dist CG: control copy failed");
+                break;
+            }
+            launched += k;
+            ++pending;
+            slot ^= 1;
+        }
+        if (pending == 0)
+            break;
+        if (pending == 2 || k <= 0) {
+            if (hipEventSynchronize(evs[oldest]) != hipSuccess) {
+                st = fail_msg(MSPMV_ERR_HIP, "dist CG: event sync failed");
+                break;
+            }
+            --pending;
+            const bool done = d->h_ctrl[oldest].done != 0;
+            oldest ^= 1;
+            if (done)
+                break;
+        }
+    }
+    // every rank reaches the same decision (the control word is a function of all-reduced
+    // values), so all ranks have enqueued the same collectives
+    hipError_t e = hipStreamSynchronize(s);
+    CgControl fin{};
+    if (e == hipSuccess)
+        e = hipMemcpy(&fin, d->d_ctrl, sizeof(CgControl), hipMemcpyDeviceToHost);
+    (void)hipEventDestroy(evs[0]);
+    (void)hipEventDestroy(evs[1]);
+    if (st != MSPMV_OK)
+        return st;
+    if (e != hipSuccess)
+        return fail_msg(MSPMV_ERR_HIP, std::string("dist CG finish: ") + hipGetErrorString(e));
+    const int it = fin.done ? fin.iters_out : fin.iter;
+    if (iters)
+        *iters = it;
+    if (cap > 0) {
+        const int nh = std::min(it, cap);
+        if (nh > 0)
+            D_HIP(hipMemcpy(max_err_hist, d->d_hist, sizeof(double) * nh, hipMemcpyDeviceToHost));
+    }
+    if (fin.breakdown)
+        return fail_msg(MSPMV_ERR_BREAKDOWN, "dist CG breakdown: non-finite alpha at iteration " + std::to_string(it));
+    return MSPMV_OK;
+}
+
+}  // extern "C"

@@ -62,6 +62,7 @@ struct CgControl {
 
 struct mspmv_handle_s {
     int device = 0;
+    int num_cus = 256;
     hipStream_t stream = nullptr;
     int m = 0, n = 0, nnz = 0;
     int *d_row_offsets = nullptr;
@@ -111,5 +112,33 @@ hipError_t launch_cg_init(mspmv_handle_s *h, const double *d_b, double *d_x, int
 hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *d_x, int L, int parity, int nblk,
                                double tol);
 int cg_update_blocks(long long elems);
+
+// Row-sharded CG (mspmv_dist.hip).  CgVecArgs lives in the kernels file; the dist code builds
+// it through this mirror.
+struct DistVecArgs {
+    long long n_elems;
+    double *x;
+    double *r;
+    const double *p;
+    double *p0;
+    const double *ap;
+    CgScalars *scal;
+    CgControl *ctrl;
+    unsigned char *conv;
+    double *partials;
+    double *hist;
+    int hist_cap;
+    double tol;
+    const double *red_in;
+    double *red_out;
+};
+// which: 0 init partial sums (b.b -> red_out), 1 init finish (red_in = all-reduced b.b),
+// 2 p update, 3 x/r update (alpha from red_in = all-reduced p.Ap; r.r -> red_out),
+// 4 finish (red_in = p.Ap, red_out = all-reduced r.r)
+hipError_t launch_dist_vec_mirror(int which, const DistVecArgs &a, int L, int nblk, double *p, hipStream_t s);
+hipError_t launch_dist_pack(const double *p, const int *idx, long long n_elems, int L, double *send,
+                            const CgControl *ctrl, hipStream_t s);
+hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
+                           CgControl *ctrl, double *partials, double *dot_out);
 
 }  // namespace mspmv

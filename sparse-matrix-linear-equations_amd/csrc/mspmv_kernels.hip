@@ -18,6 +18,7 @@
 //     sees one contiguous band of x / X.
 #include "mspmv_internal.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -171,7 +172,16 @@ struct TileArgs {
     CgControl *ctrl;                   // CG: iteration control
     const unsigned char *conv;         // CG: per-column converged flags
     double *partials;                  // CG: per-tile partial dots [tile][L]
+    double *dot_out;                   // MODE 2: the reduced x.(Ax) per column [L]
 };
+
+// Tile-kernel modes.
+//   0: y = A x.
+//   1: fused CG step: gather p = r + beta p_old, Ap = A p, write p for the tile's rows,
+//      p.Ap by linearity, last block sets alpha (single GPU).
+//   2: y = A x plus x.y over the rows (by linearity), last block writes dot_out (the
+//      row-sharded CG, whose x = [p_own | p_halo] was updated and exchanged beforehand).
+enum : int { kModeSpmv = 0, kModeCg = 1, kModeDot = 2 };
 
 // LDS slot of tile-local product k: one pad double every 4, so the walkers' strided reads
 // (about 8 products apart) spread over the banks.
@@ -215,82 +225,67 @@ __device__ __forceinline__ void stage_products(const TileArgs &a, int n0, int nn
     }
 }
 
-// Single right-hand side.  TILE = 256*IPT merge items nominal, up to 1.25*TILE after snapping.
-// CG: gathers p = r + beta*p_old on the fly (UpdatePSingle, single_strategy.hpp:89-97, fused
-// into the SpMV), writes p for its rows, Ap, and p.Ap by linearity; the last tile reduces
-// the partials in tile order and sets alpha = rs_old / pAp (single_strategy.hpp:140-141).
-template <int IPT, bool CG, bool NT>
-__global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
+// Per-tile LDS of the single-RHS kernels.
+template <int IPT>
+struct SpmvSmem {
+    static constexpr int TILE = kBlock * IPT;
+    static constexpr int MAXI = TILE + TILE / kSnapDiv;
+    static constexpr int MAXJ = (MAXI + kBlock - 1) / kBlock;
+    int rowend[MAXI];
+    double prod[MAXI + MAXI / 4 + 1];
+    int crow[kBlock];
+    int ccol[kBlock];
+    double cval[kBlock];
+    double red[kBlock / 64];
+    int last;
+};
+
+// Everything after staging, for one tile whose products and row ends are in LDS: one merge
+// search per walker, the register walk, in-tile carries, the cross-tile carry, the row
+// stores and (CG) the p.Ap contribution.  Called uniformly by all 256 threads; ends with the
+// LDS free for the next tile.
+template <int IPT, int MODE>
+__device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT> &sm, int t, int r0, int n0, int nrows,
+                                          int nnzt, double beta, double &dot)
 {
-    constexpr int TILE = kBlock * IPT;
-    constexpr int MAXI = TILE + TILE / kSnapDiv;
-    constexpr int MAXJ = (MAXI + kBlock - 1) / kBlock;
-    __shared__ int s_rowend[MAXI];
-    __shared__ double s_prod[MAXI + MAXI / 4 + 1];
-    __shared__ int s_crow[kBlock];
-    __shared__ int s_ccol[kBlock];
-    __shared__ double s_cval[kBlock];
-    __shared__ double s_red[kBlock / 64];
-    __shared__ int s_last;
-
+    constexpr int MAXJ = SpmvSmem<IPT>::MAXJ;
     const int tid = threadIdx.x;
-    if (CG && a.ctrl->done)
-        return;
-    const int t = xcd_tile(blockIdx.x, a.num_tiles);
-    const int2 b0 = a.bounds[t];
-    const int2 b1 = a.bounds[t + 1];
-    const int r0 = b0.x, n0 = b0.y;
-    const int nrows = b1.x - r0;
-    const int nnzt = b1.y - n0;
     const int items = nrows + nnzt;
-    const double beta = CG ? a.scal[0].beta : 0.0;
-
-    if (nnzt > 0) {  // block-uniform; loads for every round are issued before any is used
-        if (nnzt <= TILE)  // the common case: no snapped-in extra nonzeros
-            stage_products<IPT, CG, NT>(a, n0, nnzt, beta, s_prod);
-        else
-            stage_products<MAXJ, CG, NT>(a, n0, nnzt, beta, s_prod);
-    }
-    for (int i = tid; i < nrows; i += kBlock)
-        s_rowend[i] = a.row_offsets[r0 + 1 + i] - n0;
-    __syncthreads();
-
     const int ipt = (items + kBlock - 1) / kBlock;
     const int d0 = min(tid * ipt, items);
     int cx, cy;
-    lds_search(d0, s_rowend, nrows, nnzt, cx, cy);
+    lds_search(d0, sm.rowend, nrows, nnzt, cx, cy);
     // The walker's end is the next walker's start: one search per thread, shared via LDS.
-    s_crow[tid] = cx;
-    s_ccol[tid] = cy;
+    sm.crow[tid] = cx;
+    sm.ccol[tid] = cy;
     __syncthreads();
-    const int ex = tid + 1 < kBlock ? s_crow[tid + 1] : nrows;
-    const int ey = tid + 1 < kBlock ? s_ccol[tid + 1] : nnzt;
+    const int ex = tid + 1 < kBlock ? sm.crow[tid + 1] : nrows;
+    const int ey = tid + 1 < kBlock ? sm.ccol[tid + 1] : nnzt;
     // Does this thread's first row hold nonzeros that earlier threads of the tile consumed?
-    const bool need_cin = (cx < ex) && (cy > (cx == 0 ? 0 : s_rowend[cx - 1]));
+    const bool need_cin = (cx < ex) && (cy > (cx == 0 ? 0 : sm.rowend[cx - 1]));
     // This walker's products, read from LDS up front (independent reads, no dependent chain).
     double pr[MAXJ];
     if (ey > cy) {
 #pragma unroll
         for (int j = 0; j < MAXJ; ++j)
-            pr[j] = s_prod[pslot(min(cy + j, ey - 1))];
+            pr[j] = sm.prod[pslot(min(cy + j, ey - 1))];
     }
-
-    double dot = 0.0;
     auto write_row = [&](int row, double val) {
         const int R = r0 + row;
         a.y[R] = val;
-        if (CG) {
+        if (MODE == kModeCg) {
             const double pn = a.x[R] + beta * a.p_old[R];
             a.p_new[R] = pn;
             dot += pn * val;
+        } else if (MODE == kModeDot) {
+            dot += a.x[R] * val;
         }
     };
-
     double run = 0.0;
     bool first = true, pend = false;
     int prow = 0;
     double pval = 0.0;
-    int next_end = cx < ex ? s_rowend[cx] : 0x7fffffff;  // end of the row being accumulated
+    int next_end = cx < ex ? sm.rowend[cx] : 0x7fffffff;  // end of the row being accumulated
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) {
         const int k = cy + j;
@@ -306,7 +301,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
                 first = false;
                 run = 0.0;
                 ++cx;
-                next_end = cx < ex ? s_rowend[cx] : 0x7fffffff;
+                next_end = cx < ex ? sm.rowend[cx] : 0x7fffffff;
             }
             run += pr[j];
         }
@@ -323,72 +318,221 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
         run = 0.0;
         ++cx;
     }
-    __syncthreads();  // every walker has read its neighbour's start from s_crow / s_ccol
-    s_crow[tid] = ex;
-    s_cval[tid] = run;
+    __syncthreads();  // every walker has read its neighbour's start from crow / ccol
+    sm.crow[tid] = ex;
+    sm.cval[tid] = run;
     __syncthreads();
-
     if (pend) {  // close the row begun by earlier threads, summing their carries in thread order
         int j0 = tid - 1;
-        while (j0 > 0 && s_crow[j0 - 1] == prow)
+        while (j0 > 0 && sm.crow[j0 - 1] == prow)
             --j0;
-        double acc = s_cval[j0];
+        double acc = sm.cval[j0];
         for (int u = j0 + 1; u < tid; ++u)
-            acc += s_cval[u];
+            acc += sm.cval[u];
         write_row(prow, acc + pval);
     }
     if (tid == kBlock - 1 && a.split[t + 1]) {  // the tile's trailing partial row -> carry
         int j0 = kBlock - 1;
-        while (j0 > 0 && s_crow[j0 - 1] == nrows)
+        while (j0 > 0 && sm.crow[j0 - 1] == nrows)
             --j0;
-        double acc = s_cval[j0];
+        double acc = sm.cval[j0];
         for (int u = j0 + 1; u < kBlock; ++u)
-            acc += s_cval[u];
+            acc += sm.cval[u];
         a.carry_val[t] = acc;
-        if (CG) {
-            const int R = r0 + nrows;
-            const double pn = a.x[R] + beta * a.p_old[R];
-            dot += pn * acc;
-        }
+        const int R = r0 + nrows;
+        if (MODE == kModeCg)
+            dot += (a.x[R] + beta * a.p_old[R]) * acc;
+        else if (MODE == kModeDot)
+            dot += a.x[R] * acc;
     }
+    __syncthreads();  // LDS free for the next tile
+}
 
-    if (CG) {
-        const double tsum = block_sum(dot, s_red);
-        if (tid == 0) {
-            store_sc1(&a.partials[t], tsum);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const unsigned tk =
-                __hip_atomic_fetch_add(&a.ctrl->ticket_a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = (tk == gridDim.x - 1);
+// CG epilogue of the single-RHS tile kernels: this block's p.Ap partial -> partials[slot];
+// the last block to arrive reduces all partials in slot order and sets alpha = rs_old / pAp
+// (single_strategy.hpp:140-141).  Non-finite alpha (p.Ap == 0 or NaN) stops the solve.
+template <int IPT, int MODE>
+__device__ __forceinline__ void cg_alpha_epilogue(const TileArgs &a, SpmvSmem<IPT> &sm, int slot, int nslots,
+                                                  double dot)
+{
+    const int tid = threadIdx.x;
+    const double tsum = block_sum(dot, sm.red);
+    if (tid == 0) {
+        store_sc1(&a.partials[slot], tsum);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned tk = __hip_atomic_fetch_add(&a.ctrl->ticket_a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sm.last = (tk == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (sm.last) {
+        double v = 0.0;
+        for (int i = tid; i < nslots; i += kBlock)
+            v += load_sc1(&a.partials[i]);
+        const double pAp = block_sum(v, sm.red);
+        if (tid == 0 && MODE == kModeDot) {
+            __hip_atomic_store(&a.ctrl->ticket_a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a.dot_out[0] = pAp;
         }
-        __syncthreads();
-        if (s_last) {
-            double v = 0.0;
-            for (int i = tid; i < a.num_tiles; i += kBlock)
-                v += load_sc1(&a.partials[i]);
-            const double pAp = block_sum(v, s_red);
-            if (tid == 0) {
-                __hip_atomic_store(&a.ctrl->ticket_a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                CgScalars &s = a.scal[0];
-                s.pAp = pAp;
-                const double alpha = a.conv[0] ? 0.0 : s.rs_old / pAp;
-                s.alpha = alpha;
-                if (!a.conv[0] && !(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
-                    a.ctrl->breakdown = 1;
-                    a.ctrl->done = 1;
-                    a.ctrl->iters_out = a.ctrl->iter + 1;
-                }
+        if (tid == 0 && MODE == kModeCg) {
+            __hip_atomic_store(&a.ctrl->ticket_a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            CgScalars &s = a.scal[0];
+            s.pAp = pAp;
+            const double alpha = a.conv[0] ? 0.0 : s.rs_old / pAp;
+            s.alpha = alpha;
+            if (!a.conv[0] && !(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
+                a.ctrl->breakdown = 1;
+                a.ctrl->done = 1;
+                a.ctrl->iters_out = a.ctrl->iter + 1;
             }
         }
     }
 }
 
+// Single right-hand side, one tile per workgroup.  TILE = 256*IPT merge items nominal, up to
+// 1.25*TILE after snapping.  CG: gathers p = r + beta*p_old on the fly (UpdatePSingle,
+// single_strategy.hpp:89-97, fused into the SpMV), writes p for its rows, Ap, and p.Ap by
+// linearity.
+template <int IPT, int MODE, bool NT>
+__global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
+{
+    constexpr bool CG = MODE == kModeCg;
+    constexpr int TILE = SpmvSmem<IPT>::TILE;
+    constexpr int MAXJ = SpmvSmem<IPT>::MAXJ;
+    __shared__ SpmvSmem<IPT> sm;
+    const int tid = threadIdx.x;
+    if (MODE != kModeSpmv && a.ctrl->done)
+        return;
+    const int t = xcd_tile(blockIdx.x, a.num_tiles);
+    const int2 b0 = a.bounds[t];
+    const int2 b1 = a.bounds[t + 1];
+    const int r0 = b0.x, n0 = b0.y;
+    const int nrows = b1.x - r0;
+    const int nnzt = b1.y - n0;
+    const double beta = CG ? a.scal[0].beta : 0.0;
+    if (nnzt > 0) {  // block-uniform; loads for every round are issued before any is used
+        if (nnzt <= TILE)  // the common case: no snapped-in extra nonzeros
+            stage_products<IPT, CG, NT>(a, n0, nnzt, beta, sm.prod);
+        else
+            stage_products<MAXJ, CG, NT>(a, n0, nnzt, beta, sm.prod);
+    }
+    for (int i = tid; i < nrows; i += kBlock)
+        sm.rowend[i] = a.row_offsets[r0 + 1 + i] - n0;
+    __syncthreads();
+    double dot = 0.0;
+    walk_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, beta, dot);
+    if (MODE != kModeSpmv)
+        cg_alpha_epilogue<IPT, MODE>(a, sm, t, a.num_tiles, dot);
+}
+
+// Single right-hand side, persistent and software-pipelined: workgroup v (XCD-grouped) walks
+// the contiguous tile run [v*tpb, (v+1)*tpb).  The next tile's (col, val) loads are issued
+// right after the current tile's gathers, so HBM streaming overlaps the gather wait, the LDS
+// staging, the merge searches and the walk of the current tile (vmcnt ordering: the gathers
+// are older than the prefetch, so waiting for them does not wait for the prefetch).
+template <int IPT, int MODE, bool NT>
+__global__ __launch_bounds__(kBlock) void k_spmv_persist(TileArgs a, int tpb)
+{
+    constexpr bool CG = MODE == kModeCg;
+    constexpr int TILE = SpmvSmem<IPT>::TILE;
+    __shared__ SpmvSmem<IPT> sm;
+    const int tid = threadIdx.x;
+    if (MODE != kModeSpmv && a.ctrl->done)
+        return;
+    const int T = a.num_tiles;
+    const int v = xcd_tile(blockIdx.x, gridDim.x);
+    const int t_begin = min(v * tpb, T), t_end = min(t_begin + tpb, T);
+    const double beta = CG ? a.scal[0].beta : 0.0;
+    double dot = 0.0;
+    if (t_begin < t_end) {
+        int2 b0 = a.bounds[t_begin];
+        int2 b1 = a.bounds[t_begin + 1];
+        int c[IPT];
+        double vv[IPT];
+        {
+            const int nz = b1.y - b0.y;
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                const int k = max(min(tid + j * kBlock, nz - 1), 0);
+                c[j] = ld_stream<NT>(a.cols + b0.y + k);
+                vv[j] = ld_stream<NT>(a.vals + b0.y + k);
+            }
+        }
+        for (int t = t_begin; t < t_end; ++t) {
+            const int r0 = b0.x, n0 = b0.y;
+            const int nrows = b1.x - r0;
+            const int nnzt = b1.y - n0;
+            // (1) this tile's first round of row ends and its gathers (oldest loads first)
+            const int re0 = nrows > 0 ? a.row_offsets[r0 + 1 + min(tid, nrows - 1)] : 0;
+            double xv[IPT], pv[IPT];
+            if (nnzt > 0) {  // block-uniform (an all-empty tile may sit where x has no entries)
+#pragma unroll
+                for (int j = 0; j < IPT; ++j)
+                    xv[j] = a.x[c[j]];
+                if (CG) {
+#pragma unroll
+                    for (int j = 0; j < IPT; ++j)
+                        pv[j] = a.p_old[c[j]];
+                }
+            }
+            // (2) prefetch the next tile's (col, val) -- always issued (clamped) so the
+            //     compiler's vmcnt accounting stays exact on every path
+            const int2 b2 = a.bounds[min(t + 2, T)];
+            int cn[IPT];
+            double vn[IPT];
+            {
+                const int nz = b2.y - b1.y;
+#pragma unroll
+                for (int j = 0; j < IPT; ++j) {
+                    const int k = max(min(tid + j * kBlock, nz - 1), 0);
+                    cn[j] = ld_stream<NT>(a.cols + b1.y + k);
+                    vn[j] = ld_stream<NT>(a.vals + b1.y + k);
+                }
+            }
+            // (3) products and row ends to LDS
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                const int k = tid + j * kBlock;
+                double x = xv[j];
+                if (CG)
+                    x = x + beta * pv[j];
+                if (k < nnzt)
+                    sm.prod[pslot(k)] = vv[j] * x;
+            }
+            if (nnzt > TILE) {  // rare: a snapped-in tail beyond the prefetched rounds
+                for (int k = TILE + tid; k < nnzt; k += kBlock) {
+                    const int col = a.cols[n0 + k];
+                    double x = a.x[col];
+                    if (CG)
+                        x = x + beta * a.p_old[col];
+                    sm.prod[pslot(k)] = a.vals[n0 + k] * x;
+                }
+            }
+            if (tid < nrows)
+                sm.rowend[tid] = re0 - n0;
+            for (int i = kBlock + tid; i < nrows; i += kBlock)  // rare: > 256 rows in the tile
+                sm.rowend[i] = a.row_offsets[r0 + 1 + i] - n0;
+            __syncthreads();
+            walk_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, beta, dot);
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                c[j] = cn[j];
+                vv[j] = vn[j];
+            }
+            b0 = b1;
+            b1 = b2;
+        }
+    }
+    if (MODE != kModeSpmv)
+        cg_alpha_epilogue<IPT, MODE>(a, sm, blockIdx.x, gridDim.x, dot);
+}
+
 // Multi right-hand side (L = 2..16, row-major panels).  A group of L/2 lanes owns one merge
 // walk; each lane keeps a double2 of the L running totals (running_total[L],
 // merge_based.hpp:84-127).  TILE = (256/(L/2)) groups * IPTG items.
-template <int L, int IPTG, bool CG>
+template <int L, int IPTG, int MODE>
 __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
 {
+    constexpr bool CG = MODE == kModeCg;
     constexpr int GL = L / 2;
     constexpr int NG = kBlock / GL;
     constexpr int TILE = NG * IPTG;
@@ -406,7 +550,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
     const int tid = threadIdx.x;
     const int g = tid / GL;
     const int lane = tid % GL;
-    if (CG && a.ctrl->done)
+    if (MODE != kModeSpmv && a.ctrl->done)
         return;
     const int t = xcd_tile(blockIdx.x, a.num_tiles);
     const int2 b0 = a.bounds[t];
@@ -425,8 +569,8 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
     for (int j = 0; j < STG; ++j) {
         const int k = tid + j * kBlock;
         if (k < nnzt) {
-            s_col[k] = ld_stream<!CG>(a.cols + n0 + k);
-            s_val[k] = ld_stream<!CG>(a.vals + n0 + k);
+            s_col[k] = ld_stream<MODE == kModeSpmv>(a.cols + n0 + k);
+            s_val[k] = ld_stream<MODE == kModeSpmv>(a.vals + n0 + k);
         }
     }
     __syncthreads();
@@ -479,6 +623,10 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
             *reinterpret_cast<double2 *>(a.p_new + off) = pn;
             dot.x += pn.x * val.x;
             dot.y += pn.y * val.y;
+        } else if (MODE == kModeDot) {
+            const double2 xx = *reinterpret_cast<const double2 *>(a.x + off);
+            dot.x += xx.x * val.x;
+            dot.y += xx.y * val.y;
         }
     };
 
@@ -554,10 +702,15 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
             const double2 po = *reinterpret_cast<const double2 *>(a.p_old + off);
             dot.x += (rr.x + beta2.x * po.x) * acc.x;
             dot.y += (rr.y + beta2.y * po.y) * acc.y;
+        } else if (MODE == kModeDot) {
+            const size_t off = (size_t)(r0 + nrows) * L + 2 * lane;
+            const double2 xx = *reinterpret_cast<const double2 *>(a.x + off);
+            dot.x += xx.x * acc.x;
+            dot.y += xx.y * acc.y;
         }
     }
 
-    if (CG) {
+    if (MODE != kModeSpmv) {
         // Reduce the per-lane column partials over the groups (lanes with equal tid % GL).
 #pragma unroll
         for (int off = 32; off >= GL; off >>= 1) {
@@ -596,7 +749,13 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
             __shared__ double s_colred[kBlock];
             s_colred[tid] = v;
             __syncthreads();
-            if (tid < L) {
+            if (tid < L && MODE == kModeDot) {
+                double pAp = s_colred[tid];
+                for (int u = 1; u < TPC; ++u)
+                    pAp += s_colred[u * L + tid];
+                a.dot_out[tid] = pAp;
+            }
+            if (tid < L && CG) {
                 double pAp = s_colred[tid];
                 for (int u = 1; u < TPC; ++u)
                     pAp += s_colred[u * L + tid];
@@ -715,6 +874,11 @@ struct CgVecArgs {
     double *hist;
     int hist_cap;
     double tol;
+    // Row-sharded CG (mspmv_dist.hip): red_in = all-reduced p.Ap per column (alpha is formed
+    // from it in every block); red_out = where the last block leaves this rank's partial sums
+    // (b.b at init, r.r at update) for the all-reduce, instead of finishing the scalars.
+    const double *red_in;
+    double *red_out;
 };
 
 // x = 0, r = p0 = b; rs_old_j = r_j.r_j, b_norm_j = sqrt(b_j.b_j) (no_pretreatment.hpp:61-79,
@@ -753,7 +917,13 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CgVecArgs a)
         s_last = (tk == gridDim.x - 1);
     }
     __syncthreads();
-    if (s_last) {
+    if (s_last && a.red_out) {
+        reduce_partials_cols<L>(a.partials, gridDim.x, s_colred, s_out);
+        if (tid < L)
+            a.red_out[tid] = s_out[tid];
+        if (tid == 0)
+            __hip_atomic_store(&a.ctrl->ticket_i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (s_last) {
         reduce_partials_cols<L>(a.partials, gridDim.x, s_colred, s_out);
         if (tid < L) {
             CgScalars &s = a.scal[tid];
@@ -795,7 +965,11 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(CgVecArgs a)
     const long long stride = (long long)gridDim.x * kBlock;
     const long long i0 = (long long)blockIdx.x * kBlock + tid;
     double2 al;
-    if (L == 1) {
+    if (a.red_in) {  // sharded: alpha_j = rs_old_j / (all-reduced p.Ap)_j, masked (no_pretreatment.hpp:109-120)
+        const int j0 = L == 1 ? 0 : 2 * (int)(i0 % GL);
+        al.x = a.conv[j0] ? 0.0 : a.scal[j0].rs_old / a.red_in[j0];
+        al.y = L == 1 ? al.x : (a.conv[j0 + 1] ? 0.0 : a.scal[j0 + 1].rs_old / a.red_in[j0 + 1]);
+    } else if (L == 1) {
         al.x = a.scal[0].alpha;
         al.y = al.x;
     } else {
@@ -832,7 +1006,13 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(CgVecArgs a)
         s_last = (tk == gridDim.x - 1);
     }
     __syncthreads();
-    if (s_last) {
+    if (s_last && a.red_out) {
+        reduce_partials_cols<L>(a.partials, gridDim.x, s_colred, s_out);
+        if (tid < L)
+            a.red_out[tid] = s_out[tid];
+        if (tid == 0)
+            __hip_atomic_store(&a.ctrl->ticket_b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (s_last) {
         reduce_partials_cols<L>(a.partials, gridDim.x, s_colred, s_out);
         if (tid == 0) {
             __hip_atomic_store(&a.ctrl->ticket_b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -866,6 +1046,101 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(CgVecArgs a)
     }
 }
 
+// ---- row-sharded CG helpers ------------------------------------------------------------
+// After the all-reduce of b.b: rs_old_j = b_j.b_j, b_norm_j = sqrt (or 1), fresh control.
+template <int L>
+__global__ void k_dist_init_finish(CgVecArgs a)
+{
+    const int j = threadIdx.x;
+    if (j < L) {
+        CgScalars &s = a.scal[j];
+        const double bb = a.red_in[j];
+        s.rs_old = bb;
+        const double bn = sqrt(bb);
+        s.b_norm = bn == 0.0 ? 1.0 : bn;
+        s.alpha = s.beta = s.pAp = s.rs_new = 0.0;
+        a.conv[j] = 0;
+    }
+    if (j == 0) {
+        a.ctrl->iter = 0;
+        a.ctrl->done = 0;
+        a.ctrl->iters_out = 0;
+        a.ctrl->breakdown = 0;
+    }
+}
+
+// p_own = r + beta p_own  (update_p_multiple, utils_multiple.hpp:43-59; beta = 0 on the first
+// iteration gives p = r = b, the reference's P = B).
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_dist_pupdate(CgVecArgs a, double *p)
+{
+    if (a.ctrl->done)
+        return;
+    const long long n = a.n_elems;
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock) {
+        const int j = (int)(i % L);
+        p[i] = a.r[i] + a.scal[j].beta * p[i];
+    }
+}
+
+// Pack the owned entries other ranks need: send[e] = p[idx[e / L] * L + e % L].
+__global__ void k_dist_pack(const double *__restrict__ p, const int *__restrict__ idx, long long n_elems, int L,
+                            double *__restrict__ send, const CgControl *ctrl)
+{
+    if (ctrl && ctrl->done)
+        return;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n_elems;
+         e += (long long)gridDim.x * blockDim.x)
+        send[e] = p[(size_t)idx[e / L] * L + e % L];
+}
+
+// One block, after the all-reduces of p.Ap (red_in) and r.r (red_out): breakdown test,
+// convergence masks, max-residual history, beta, rs_old (no_pretreatment.hpp:109-182).
+template <int L>
+__global__ void k_dist_finish(CgVecArgs a)
+{
+    if (threadIdx.x != 0 || a.ctrl->done)
+        return;
+    const int iter = a.ctrl->iter;
+    for (int j = 0; j < L; ++j) {
+        if (a.conv[j])
+            continue;
+        const double alpha = a.scal[j].rs_old / a.red_in[j];
+        if (!(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
+            a.ctrl->breakdown = 1;
+            a.ctrl->done = 1;
+            a.ctrl->iters_out = iter + 1;
+            a.ctrl->iter = iter + 1;
+            return;
+        }
+    }
+    int nconv = 0;
+    double maxrel = 0.0;
+    for (int j = 0; j < L; ++j) {
+        CgScalars &s = a.scal[j];
+        const double rs_new = a.red_out[j];
+        s.rs_new = rs_new;
+        const double rel = sqrt(rs_new) / s.b_norm;
+        maxrel = maxrel > rel ? maxrel : rel;
+        if (!a.conv[j] && rel < a.tol)
+            a.conv[j] = 1;
+        nconv += a.conv[j];
+    }
+    if (a.hist && iter < a.hist_cap)
+        a.hist[iter] = maxrel;
+    if (nconv == L) {
+        a.ctrl->done = 1;
+        a.ctrl->iters_out = iter + 1;
+    } else {
+        for (int j = 0; j < L; ++j) {
+            CgScalars &s = a.scal[j];
+            s.beta = a.conv[j] ? 0.0 : s.rs_new / s.rs_old;
+            s.rs_old = s.rs_new;
+        }
+    }
+    a.ctrl->iter = iter + 1;
+}
+
 __global__ void k_flush(double *p, long long n, double v)
 {
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
@@ -882,6 +1157,8 @@ constexpr int kIptgSpmm = 8;  // items per lane group for SpMM tiles
 struct SpmvTuning {
     int ipt = 8;
     int nt = 1;
+    int persist = 1;  // persistent software-pipelined kernel
+    int bpc = 0;      // resident workgroups per CU for the persistent grid (0: occupancy query)
 };
 static const SpmvTuning &spmv_tuning()
 {
@@ -894,6 +1171,10 @@ static const SpmvTuning &spmv_tuning()
         }
         if (const char *e = getenv("MSPMV_SPMV_NT"))
             v.nt = atoi(e) != 0;
+        if (const char *e = getenv("MSPMV_SPMV_PERSIST"))
+            v.persist = atoi(e) != 0;
+        if (const char *e = getenv("MSPMV_SPMV_BPC"))
+            v.bpc = atoi(e);
         return v;
     }();
     return t;
@@ -941,20 +1222,49 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
     return a;
 }
 
-template <bool CG>
-static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s)
+// Persistent grid for the single-RHS kernel: min(tiles, CUs x resident workgroups), each
+// workgroup taking an equal contiguous run of tiles.
+template <typename K>
+static void persist_grid(K kernel, int num_tiles, int num_cus, int bpc, int *grid, int *tpb)
+{
+    if (bpc <= 0) {
+        int occ = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, kBlock, 0) != hipSuccess || occ < 1)
+            occ = 1;
+        bpc = occ;
+    }
+    const long long slots = (long long)std::max(num_cus, 1) * bpc;
+    int t = (int)((num_tiles + slots - 1) / slots);
+    t = std::max(t, 1);
+    *tpb = t;
+    *grid = (num_tiles + t - 1) / t;
+}
+
+template <int MODE>
+static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_cus)
 {
     const dim3 grid(a.num_tiles), block(kBlock);
     switch (L) {
     case 1: {
         const SpmvTuning &tu = spmv_tuning();
-        const bool nt = !CG && tu.nt;  // CG re-reads A every iteration: keep default cache policy
+        const bool nt = MODE == kModeSpmv && tu.nt;  // CG re-reads A every iteration: default policy
+#define MSPMV_LAUNCH_PERSIST(I, NTV)                                                               \
+    do {                                                                                           \
+        int g = 0, tpb = 0;                                                                        \
+        persist_grid(k_spmv_persist<I, MODE, NTV>, a.num_tiles, num_cus, tu.bpc, &g, &tpb);          \
+        hipLaunchKernelGGL((k_spmv_persist<I, MODE, NTV>), dim3(g), block, 0, s, a, tpb);            \
+    } while (0)
 #define MSPMV_SPMV_CASE(I)                                                                          \
     case I:                                                                                        \
-        if (nt)                                                                                    \
-            hipLaunchKernelGGL((k_spmv_tile<I, CG, true>), grid, block, 0, s, a);                   \
+        if (tu.persist) {                                                                          \
+            if (nt)                                                                                \
+                MSPMV_LAUNCH_PERSIST(I, true);                                                     \
+            else                                                                                   \
+                MSPMV_LAUNCH_PERSIST(I, false);                                                    \
+        } else if (nt)                                                                             \
+            hipLaunchKernelGGL((k_spmv_tile<I, MODE, true>), grid, block, 0, s, a);                   \
         else                                                                                       \
-            hipLaunchKernelGGL((k_spmv_tile<I, CG, false>), grid, block, 0, s, a);                  \
+            hipLaunchKernelGGL((k_spmv_tile<I, MODE, false>), grid, block, 0, s, a);                  \
         break;
         switch (tu.ipt) {
             MSPMV_SPMV_CASE(2)
@@ -964,12 +1274,13 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s)
         default: return hipErrorInvalidValue;
         }
 #undef MSPMV_SPMV_CASE
+#undef MSPMV_LAUNCH_PERSIST
         break;
     }
-    case 2: hipLaunchKernelGGL((k_spmm_tile<2, kIptgSpmm, CG>), grid, block, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((k_spmm_tile<4, kIptgSpmm, CG>), grid, block, 0, s, a); break;
-    case 8: hipLaunchKernelGGL((k_spmm_tile<8, kIptgSpmm, CG>), grid, block, 0, s, a); break;
-    case 16: hipLaunchKernelGGL((k_spmm_tile<16, kIptgSpmm, CG>), grid, block, 0, s, a); break;
+    case 2: hipLaunchKernelGGL((k_spmm_tile<2, kIptgSpmm, MODE>), grid, block, 0, s, a); break;
+    case 4: hipLaunchKernelGGL((k_spmm_tile<4, kIptgSpmm, MODE>), grid, block, 0, s, a); break;
+    case 8: hipLaunchKernelGGL((k_spmm_tile<8, kIptgSpmm, MODE>), grid, block, 0, s, a); break;
+    case 16: hipLaunchKernelGGL((k_spmm_tile<16, kIptgSpmm, MODE>), grid, block, 0, s, a); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -979,7 +1290,7 @@ hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const 
 {
     if (plan.num_tiles == 0)
         return hipSuccess;
-    return launch_tile<false>(make_args(h, plan, d_X, d_Y), L, h->stream);
+    return launch_tile<kModeSpmv>(make_args(h, plan, d_X, d_Y), L, h->stream, h->num_cus);
 }
 
 hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L)
@@ -1065,7 +1376,7 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *
     ta.ctrl = h->d_ctrl;
     ta.conv = h->d_conv;
     ta.partials = h->d_partials;
-    hipError_t e = launch_tile<true>(ta, L, h->stream);
+    hipError_t e = launch_tile<kModeCg>(ta, L, h->stream, h->num_cus);
     if (e != hipSuccess)
         return e;
     if (plan.num_carries) {
@@ -1092,6 +1403,62 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *
     return dispatch_vec(false, va, L, nblk, h->stream);
 }
 
+// ---- row-sharded CG launchers --------------------------------------------------------------
+template <int L>
+static hipError_t dist_launch_L(int which, const CgVecArgs &a, int nblk, double *p, hipStream_t s)
+{
+    switch (which) {
+    case 0: hipLaunchKernelGGL((k_cg_init<L>), dim3(nblk), dim3(kBlock), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((k_dist_init_finish<L>), dim3(1), dim3(64), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((k_dist_pupdate<L>), dim3(nblk), dim3(kBlock), 0, s, a, p); break;
+    case 3: hipLaunchKernelGGL((k_cg_update<L>), dim3(nblk), dim3(kBlock), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((k_dist_finish<L>), dim3(1), dim3(64), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_dist_vec(int which, const CgVecArgs &a, int L, int nblk, double *p, hipStream_t s)
+{
+    switch (L) {
+    case 1: return dist_launch_L<1>(which, a, nblk, p, s);
+    case 2: return dist_launch_L<2>(which, a, nblk, p, s);
+    case 4: return dist_launch_L<4>(which, a, nblk, p, s);
+    case 8: return dist_launch_L<8>(which, a, nblk, p, s);
+    case 16: return dist_launch_L<16>(which, a, nblk, p, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_dist_pack(const double *p, const int *idx, long long n_elems, int L, double *send,
+                            const CgControl *ctrl, hipStream_t s)
+{
+    if (n_elems <= 0)
+        return hipSuccess;
+    const long long nb = std::min<long long>((n_elems + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_dist_pack, dim3((unsigned)nb), dim3(256), 0, s, p, idx, n_elems, L, send, ctrl);
+    return hipGetLastError();
+}
+
+// Y = A X with x.(AX) per column reduced into dot_out (MODE 2), plus the carry fix-up.
+hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
+                           CgControl *ctrl, double *partials, double *dot_out)
+{
+    if (plan.num_tiles == 0)  // a rank without rows contributes 0 to the all-reduce
+        return hipMemsetAsync(dot_out, 0, sizeof(double) * L, h->stream);
+    TileArgs ta = make_args(h, plan, d_X, d_Y);
+    ta.ctrl = ctrl;
+    ta.partials = partials;
+    ta.dot_out = dot_out;
+    hipError_t e = launch_tile<kModeDot>(ta, L, h->stream, h->num_cus);
+    if (e != hipSuccess || plan.num_carries == 0)
+        return e;
+    const int n = plan.num_carries * L;
+    hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, h->stream, plan.d_carry_tiles,
+                       plan.d_carry_rows, plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)ctrl);
+    return hipGetLastError();
+}
+
 hipError_t launch_flush(void *p, size_t bytes, hipStream_t s)
 {
     const long long n = (long long)(bytes / sizeof(double));
@@ -1099,4 +1466,30 @@ hipError_t launch_flush(void *p, size_t bytes, hipStream_t s)
     return hipGetLastError();
 }
 
+}  // namespace mspmv
+
+namespace mspmv {
+hipError_t launch_dist_vec(int which, const CgVecArgs &a, int L, int nblk, double *p, hipStream_t s);
+
+hipError_t launch_dist_vec_mirror(int which, const DistVecArgs &d, int L, int nblk, double *p, hipStream_t s)
+{
+    static_assert(sizeof(DistVecArgs) == sizeof(CgVecArgs), "DistVecArgs must mirror CgVecArgs");
+    CgVecArgs a{};
+    a.n_elems = d.n_elems;
+    a.x = d.x;
+    a.r = d.r;
+    a.p = d.p;
+    a.p0 = d.p0;
+    a.ap = d.ap;
+    a.scal = d.scal;
+    a.ctrl = d.ctrl;
+    a.conv = d.conv;
+    a.partials = d.partials;
+    a.hist = d.hist;
+    a.hist_cap = d.hist_cap;
+    a.tol = d.tol;
+    a.red_in = d.red_in;
+    a.red_out = d.red_out;
+    return launch_dist_vec(which, a, L, nblk, p, s);
+}
 }  // namespace mspmv

@@ -93,6 +93,14 @@ _SIGS = {
     "mspmv_memcpy_d2d": (_I, [_P, _P, _SZ]),
     "mspmv_memset_dev": (_I, [_P, _I, _SZ]),
     "mspmv_synth_banded": (_I, [_I, ctypes.c_longlong, _I, ctypes.c_ulonglong, _P, _P, _P]),
+    "mspmv_dist_partition": (_I, [_P, _I, _I, _I, _P]),
+    "mspmv_dist_localize": (_I, [_P, _I, _I, _P, _P, _P, _PI, _P, _I, _P]),
+    "mspmv_comm_unique_id": (_I, [_P]),
+    "mspmv_dist_create": (_I, [_P, _I, _I, _I, _P, ctypes.POINTER(_CsrD), ctypes.POINTER(_P)]),
+    "mspmv_dist_destroy": (_I, [_P]),
+    "mspmv_dist_info": (_I, [_P, _PI, _PI, _PI]),
+    "mspmv_dist_spmm_dev": (_I, [_P, _P, _P, _I]),
+    "mspmv_dist_cg_dev": (_I, [_P, _P, _P, _I, _I, _D, _PI, _P, _I]),
     "mspmv_synth_fem_blocked": (_I, [_I, ctypes.c_longlong, _I, _I, ctypes.c_ulonglong, _P, _P, _P]),
     "mspmv_synth_powerlaw": (_I, [_I, _I, ctypes.c_longlong, _D, ctypes.c_ulonglong, _P, _P, _P]),
     "mspmv_synth_stencil": (_I, [_I, _I, _I, _I, _I, ctypes.c_ulonglong, _P, _P, _P,
@@ -403,3 +411,86 @@ def CGSolveMultiple(a: CsrMatrix, B, X, num_vectors: int, max_iters: int, tolera
         max_errors.clear()
         max_errors.extend(hist.tolist())
     return it
+
+
+# ----------------------------------------------------------------------------------------
+# row-block sharding over several GPUs (include/mspmv_dist.h)
+# ----------------------------------------------------------------------------------------
+def dist_partition(a: CsrMatrix, nranks: int) -> np.ndarray:
+    """Row blocks balanced by merge path (equal rows + nonzeros per rank)."""
+    rb = np.empty(nranks + 1, np.int32)
+    _check(lib.mspmv_dist_partition(_ptr(a.row_offsets), a.num_rows, a.num_nonzeros, nranks, _ptr(rb)),
+           "dist_partition")
+    return rb
+
+
+def local_rows(a: CsrMatrix, row_begin: np.ndarray, rank: int) -> CsrMatrix:
+    """This rank's rows with GLOBAL column ids (num_cols = global n)."""
+    lo, hi = int(row_begin[rank]), int(row_begin[rank + 1])
+    s, e = int(a.row_offsets[lo]), int(a.row_offsets[hi])
+    ro = np.ascontiguousarray(a.row_offsets[lo:hi + 1] - s, np.int32)
+    return CsrMatrix(hi - lo, a.num_cols, e - s, ro, np.ascontiguousarray(a.column_indices[s:e]),
+                     np.ascontiguousarray(a.values[s:e]))
+
+
+def dist_localize(row_begin: np.ndarray, rank: int, loc: CsrMatrix):
+    """(local column ids, sorted halo global ids, halo counts per owner rank)."""
+    nranks = len(row_begin) - 1
+    rb = np.ascontiguousarray(row_begin, np.int32)
+    nh = ctypes.c_int()
+    _check(lib.mspmv_dist_localize(_ptr(rb), nranks, rank, _ptr(loc.row_offsets), _ptr(loc.column_indices), None,
+                                   ctypes.byref(nh), None, 0, None), "dist_localize(size)")
+    lcols = np.empty(max(loc.num_nonzeros, 1), np.int32)
+    halo = np.empty(max(nh.value, 1), np.int32)
+    counts = np.empty(nranks, np.int32)
+    _check(lib.mspmv_dist_localize(_ptr(rb), nranks, rank, _ptr(loc.row_offsets), _ptr(loc.column_indices),
+                                   _ptr(lcols), ctypes.byref(nh), _ptr(halo), nh.value, _ptr(counts)),
+           "dist_localize")
+    return lcols[:loc.num_nonzeros], halo[:nh.value], counts
+
+
+def comm_unique_id() -> bytes:
+    buf = (ctypes.c_ubyte * 128)()
+    _check(lib.mspmv_comm_unique_id(buf), "comm_unique_id")
+    return bytes(buf)
+
+
+class DistCsr:
+    """This rank's row block of a matrix sharded over `nranks` GPUs (collective create)."""
+
+    def __init__(self, uid: bytes, nranks: int, rank: int, device: int, row_begin: np.ndarray, loc: CsrMatrix):
+        self.row_begin = np.ascontiguousarray(row_begin, np.int32)
+        idb = (ctypes.c_ubyte * 128).from_buffer_copy(uid)
+        h = ctypes.c_void_p()
+        _check(lib.mspmv_dist_create(idb, nranks, rank, device, _ptr(self.row_begin), ctypes.byref(loc._c()),
+                                     ctypes.byref(h)), "dist_create")
+        self.h = h.value
+        self.n_own = loc.num_rows
+
+    def info(self):
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(lib.mspmv_dist_info(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "dist_info")
+        return {"n_own": a.value, "n_halo": b.value, "n_send": c.value}
+
+    def spmm_dev(self, dX: DeviceBuffer, dY: DeviceBuffer, L: int):
+        _check(lib.mspmv_dist_spmm_dev(self.h, dX.ptr, dY.ptr, L), "dist_spmm_dev")
+
+    def cg_dev(self, dB: DeviceBuffer, dX: DeviceBuffer, L: int, max_iters: int, tolerance: float,
+               hist_cap: int = 0):
+        it = ctypes.c_int()
+        hist = np.zeros(max(hist_cap, 1))
+        st = lib.mspmv_dist_cg_dev(self.h, dB.ptr, dX.ptr, L, max_iters, tolerance, ctypes.byref(it),
+                                   _ptr(hist) if hist_cap else None, hist_cap)
+        _check(st, "dist_cg_dev", allow=(4,))
+        return it.value, hist[: min(it.value, hist_cap)], st
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.mspmv_dist_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,192 @@
+"""Row-block sharding on CPU with torch.distributed/gloo, world_size 2 (no GPU).
+
+Exercises the PRODUCT's host planning (mspmv_dist_partition / mspmv_dist_localize in
+libmspmv.so) and the sharded protocol the RCCL path runs (mspmv_dist.hip): request-list
+exchange (all-gather of halo counts, point-to-point request lists), pack + halo exchange of
+p, local SpMM on [p_own | p_halo], all-reduce of p.Ap and r.r, and the one-block stop/beta
+step.  The per-rank arithmetic here is numpy standing in for the HIP kernels, so this checks
+the partition, localization and communication schedule; the kernels themselves are covered
+by the -m gpu tests.  Results are compared with the oracle's single-process CGSolveMultiple.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _matrix(kind):
+    import mspmv
+    if kind == "fem2d":
+        return mspmv.CsrMatrix.synth_stencil(0, 2500, 50)
+    if kind == "stencil27":
+        return mspmv.CsrMatrix.synth_stencil(1, 10 * 11 * 12, 10, 11, 12)
+    return mspmv.CsrMatrix.synth_fem_blocked(3000, 60000, 3, 60, seed=4)
+
+
+def _local_matvec(ro, cols, vals, X):
+    lens = np.diff(ro)
+    rows = np.repeat(np.arange(len(lens)), lens)
+    Y = np.zeros((len(lens), X.shape[1]))
+    np.add.at(Y, rows, vals[:, None] * X[cols])
+    return Y
+
+
+def _worker(rank, world, port, kind, L, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    for p in (ROOT, os.path.join(ROOT, "sparse-matrix-linear-equations_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as td
+    import mspmv
+    td.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        a = _matrix(kind)
+        rb = mspmv.dist_partition(a, world)
+        lo, hi = int(rb[rank]), int(rb[rank + 1])
+        loc = mspmv.local_rows(a, rb, rank)
+        lcols, halo, counts = mspmv.dist_localize(rb, rank, loc)
+        n_own, n_halo = hi - lo, len(halo)
+        # --- request lists (mspmv_dist_create): all-gather counts, then point-to-point lists
+        cnt = torch.tensor(counts, dtype=torch.int32)
+        allc = [torch.zeros(world, dtype=torch.int32) for _ in range(world)]
+        td.all_gather(allc, cnt)
+        send_counts = [int(allc[g][rank]) for g in range(world)]
+        recv_displ = np.concatenate([[0], np.cumsum(counts)])
+        reqs, send_idx = [], []
+        for g in range(world):
+            if g == rank:
+                continue
+            if counts[g]:
+                reqs.append(td.isend(torch.from_numpy(halo[recv_displ[g]:recv_displ[g + 1]].copy()), g))
+        for g in range(world):
+            if g != rank and send_counts[g]:
+                buf = torch.zeros(send_counts[g], dtype=torch.int32)
+                td.recv(buf, g)
+                send_idx.append((g, buf.numpy() - lo))
+        for r in reqs:
+            r.wait()
+        for g, idx in send_idx:
+            assert idx.min() >= 0 and idx.max() < n_own
+
+        def exchange(p_own):
+            pext = np.zeros((n_own + n_halo, L))
+            pext[:n_own] = p_own
+            ops = []
+            for g, idx in send_idx:
+                ops.append(td.isend(torch.from_numpy(np.ascontiguousarray(p_own[idx])), g))
+            for g in range(world):
+                if g != rank and counts[g]:
+                    buf = torch.zeros((int(counts[g]), L), dtype=torch.float64)
+                    td.recv(buf, g)
+                    pext[n_own + recv_displ[g]:n_own + recv_displ[g + 1]] = buf.numpy()
+            for o in ops:
+                o.wait()
+            return pext
+
+        def allreduce(v):
+            t = torch.from_numpy(np.ascontiguousarray(v))
+            td.all_reduce(t)
+            return t.numpy()
+
+        # --- sharded SpMM vs the global product
+        rng = np.random.default_rng(11)
+        X = rng.uniform(-1, 1, (a.num_rows, L))
+        Y_own = _local_matvec(loc.row_offsets, lcols, loc.values, exchange(X[lo:hi]))
+        np.save(os.path.join(out_dir, f"spmm_{rank}.npy"), Y_own)
+        # --- sharded CG (mspmv_dist_cg_dev's schedule)
+        B = rng.uniform(0, 1, (a.num_rows, L))
+        b = B[lo:hi]
+        x = np.zeros_like(b)
+        r = b.copy()
+        p = b.copy()
+        rs_old = allreduce((b * b).sum(axis=0))
+        b_norm = np.sqrt(rs_old)
+        b_norm[b_norm == 0] = 1.0
+        conv = np.zeros(L, bool)
+        beta = np.zeros(L)
+        hist, it, tol = [], 0, 1e-9
+        for it in range(1, 3001):
+            p = r + beta * p
+            Ap = _local_matvec(loc.row_offsets, lcols, loc.values, exchange(p))
+            pAp = allreduce((p * Ap).sum(axis=0))
+            alpha = np.where(conv, 0.0, rs_old / pAp)
+            x = x + alpha * p
+            r = r + (-alpha) * Ap
+            rs_new = allreduce((r * r).sum(axis=0))
+            rel = np.sqrt(rs_new) / b_norm
+            hist.append(rel.max())
+            conv |= rel < tol
+            if conv.all():
+                break
+            beta = np.where(conv, 0.0, rs_new / rs_old)
+            rs_old = rs_new
+        np.save(os.path.join(out_dir, f"cg_x_{rank}.npy"), x)
+        np.save(os.path.join(out_dir, f"cg_h_{rank}.npy"), np.array(hist))
+        np.save(os.path.join(out_dir, f"meta_{rank}.npy"), np.array([lo, hi, it, n_halo]))
+    finally:
+        td.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,L", [("fem2d", 2), ("stencil27", 1), ("fem_blocked", 4)])
+def test_sharded_protocol_world2(tmp_path, orc, kind, L):
+    import torch.multiprocessing as mp
+    import mspmv
+    world = 2
+    mp.start_processes(_worker, args=(world, _free_port(), kind, L, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    a = _matrix(kind)
+    rb = mspmv.dist_partition(a, world)
+    assert rb[0] == 0 and rb[-1] == a.num_rows and np.all(np.diff(rb) > 0)
+    # merge-path balance: rows + nonzeros per rank within one row's worth of each other
+    work = [int(rb[g + 1] - rb[g]) + int(a.row_offsets[rb[g + 1]] - a.row_offsets[rb[g]]) for g in range(world)]
+    assert max(work) - min(work) <= 2 * np.diff(a.row_offsets).max() + 2
+    rng = np.random.default_rng(11)
+    X = rng.uniform(-1, 1, (a.num_rows, L))
+    Y = np.concatenate([np.load(tmp_path / f"spmm_{g}.npy") for g in range(world)])
+    np.testing.assert_allclose(Y, orc.csr_spmm_t(a, X), rtol=1e-13, atol=1e-13)
+    B = rng.uniform(0, 1, (a.num_rows, L))
+    if kind == "fem_blocked":  # not symmetric: the SpMM check above is the point
+        return
+    x = np.concatenate([np.load(tmp_path / f"cg_x_{g}.npy") for g in range(world)])
+    h0 = np.load(tmp_path / "cg_h_0.npy")
+    h1 = np.load(tmp_path / "cg_h_1.npy")
+    assert h0.tobytes() == h1.tobytes()  # every rank sees the same all-reduced scalars
+    Xo, it_o, ho = orc.cg_multi(a, B, 3000, 1e-9, kernel=1, P=8, hist_cap=3000)
+    assert abs(len(h0) - it_o) <= 1
+    k = min(len(h0), len(ho))
+    np.testing.assert_allclose(h0[:k], ho[:k], rtol=0, atol=1e-10)
+    assert np.linalg.norm(x - Xo) <= 1e-8 * np.linalg.norm(Xo)
+
+
+def test_partition_matches_merge_coords(orc):
+    import mspmv
+    a = _matrix("fem_blocked")
+    for world in (1, 2, 3, 8):
+        rb = mspmv.dist_partition(a, world)
+        np.testing.assert_array_equal(rb, orc.merge_coords(a, world)[:, 0])
+
+
+def test_localize_roundtrip():
+    import mspmv
+    a = _matrix("stencil27")
+    rb = mspmv.dist_partition(a, 4)
+    for rank in range(4):
+        loc = mspmv.local_rows(a, rb, rank)
+        lcols, halo, counts = mspmv.dist_localize(rb, rank, loc)
+        lo, hi = rb[rank], rb[rank + 1]
+        back = np.where(lcols < hi - lo, lcols + lo, halo[np.maximum(lcols - (hi - lo), 0)])
+        np.testing.assert_array_equal(back, loc.column_indices)
+        assert np.all(np.diff(halo) > 0) and counts.sum() == len(halo) and counts[rank] == 0
+        assert not np.any((halo >= lo) & (halo < hi))

@@ -34,22 +34,24 @@ def child():
     hot_step, hot_kern, _ = mspmv.time_spmm_batch(gs[:1], dx[:1], dy[:1], 1, 200)
     nbytes = 12 * 11524432 + 4 * 217919 + 16 * 217918
     print(json.dumps({"ipt": os.environ.get("MSPMV_SPMV_IPT"), "nt": os.environ.get("MSPMV_SPMV_NT"),
+                      "persist": os.environ.get("MSPMV_SPMV_PERSIST"), "bpc": os.environ.get("MSPMV_SPMV_BPC"),
                       "cold_kernel_us": round(kern * 1e3, 2), "cold_GBps": round(nbytes / kern / 1e6, 1),
                       "step_us": round(step * 1e3, 2), "hot_kernel_us": round(hot_kern * 1e3, 2),
                       "hot_GBps": round(nbytes / hot_kern / 1e6, 1)}), flush=True)
 
 
 def parent():
-    spec = os.environ.get("SWEEP_VARIANTS", "2:0,2:1,4:0,4:1,8:0,8:1,16:0,16:1")
+    spec = os.environ.get("SWEEP_VARIANTS", "4:1:0:0,8:1:0:0,4:1:1:0,8:1:1:0")   # ipt:nt:persist:bpc
     variants = [tuple(int(x) for x in v.split(":")) for v in spec.split(",")]
     rounds = int(os.environ.get("SWEEP_ROUNDS", "2"))
     for r in range(rounds):
-        for ipt, nt in variants:
-            env = dict(os.environ, MSPMV_SPMV_IPT=str(ipt), MSPMV_SPMV_NT=str(nt))
+        for ipt, nt, persist, bpc in variants:
+            env = dict(os.environ, MSPMV_SPMV_IPT=str(ipt), MSPMV_SPMV_NT=str(nt), MSPMV_SPMV_PERSIST=str(persist),
+                       MSPMV_SPMV_BPC=str(bpc))
             out = subprocess.run([sys.executable, __file__, "--child"], env=env, capture_output=True, text=True,
                                  timeout=300)
             if out.returncode != 0:
-                print(f"variant ipt={ipt} nt={nt} failed rc={out.returncode}: {out.stderr[-500:]}", flush=True)
+                print(f"variant ipt={ipt} nt={nt} persist={persist} failed rc={out.returncode}: {out.stderr[-500:]}", flush=True)
                 sys.exit(out.returncode)
             print(f"round {r} " + out.stdout.strip(), flush=True)
 
