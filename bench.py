@@ -1,24 +1,29 @@
 #!/usr/bin/env python3
 """bench.py -- MI355X merge-path fp64 SpMV (+ CG) benchmark; prints ONE JSON line on rank 0.
 
-Workload (BASELINE.json configs[1], "merge-based CSR SpMV fp64, 1 RHS, pwtk/rma10 on
+Headline workload (BASELINE.json configs[1], "merge-based CSR SpMV fp64, 1 RHS, pwtk/rma10 on
 1xMI355X"): a STEP is one SpMV over each matrix of a batch of 4 distinct synthetic
-pwtk-shaped matrices (m = 217,918, nnz = 11,524,432, band +-10,000; SuiteSparse files are
-not available offline).  The batch (571 MB) exceeds the 256 MiB Infinity Cache, so every
-launch streams its matrix from HBM -- the regime the >= 70 %-of-HBM target is about.
-All inputs are resident in HBM before the timed region.
+pwtk-shaped matrices -- m = 217,918, nnz = 11,524,432 (52.9 per row), 6 unknowns per mesh node
+with every row of a node coupling to the same neighbour nodes within +-1,700 nodes (pwtk is a
+6-DOF structural FEM matrix; SuiteSparse files are not available offline).  The batch (571 MB)
+exceeds the 256 MiB Infinity Cache, so every launch streams its matrix from HBM.  All inputs
+are resident in HBM before the timed region.
 
-  value      = 2 * nnz * batch * steps * n_gpus / max-over-ranks(time)   [GFLOP/s, whole job]
-  roofline   = algorithmic bytes per SpMV launch (12 nnz + 4 (m+1) + 8 n + 8 m)
-               / average duration of the merge-tile kernel, HIP events on its stream,
-               recorded inside the timed region; peak 8 TB/s (MI355X HBM3E)
-  cpu_baseline = the reference's own OmpMergeCsrmm(num_vectors = 1) (== cpu_spmv.cpp
-               OmpMergeCsrmv) compiled from /root/reference (oracle/_ref), else the oracle
-               port, timed on the host cores for ~10 s on matrix #0 (rank 0, N = 1 only).
+  value        = 2 * nnz * batch * steps * n_gpus / max-over-ranks(time)  [GFLOP/s, whole job]
+  roofline     = algorithmic bytes per SpMV launch, 12 nnz + 4 (m+1) + 8 n + 8 m,
+                 / the merge-tile kernel's average duration from HIP events recorded around
+                 every launch on its stream inside the timed region; peak 8 TB/s HBM3E
+  cpu_baseline = the reference's own merge CsrMV (work_2025 OmpMergeCsrmm with num_vectors = 1,
+                 == cpu_spmv.cpp OmpMergeCsrmv) compiled from /root/reference into oracle/_ref,
+                 else the oracle port; host cores, ~10 s on matrix #0 (rank 0, N = 1 only)
 
-Multi-GPU (--gpus N via torch.distributed.run): every rank runs its own batch on its own
-GPU (weak scaling; SpMV on row blocks needs no data-path collective); gloo carries only the
-barrier and the max-over-ranks time.
+Extra fields: the scattered-band stress shape, CG iterations/s for configs[3] (single CG,
+parabolic_fem shape) and configs[4] (8-RHS block CG, nlpkkt120 size; at N > 1 row-sharded over
+all ranks with RCCL halo exchange + dot all-reduces).
+
+Multi-GPU (--gpus N via torch.distributed.run): every rank runs its own SpMV batch on its own
+GPU (weak scaling; no data-path collective); gloo carries the barrier and the max-over-ranks
+time, and the RCCL id of the sharded CG.
 """
 import argparse
 import ctypes
@@ -36,9 +41,9 @@ import mspmv  # noqa: E402
 
 METRIC = "fp64 SpMV GFLOP/s + achieved HBM GB/s vs roofline; CG iters/sec"
 HBM_PEAK_GBS = 8000.0
-PWTK = dict(m=217918, nnz=11524432, half_band=10000)
-PARABOLIC_FEM = dict(m=525825, width=725)
-NLPKKT120 = dict(dims=(160, 135, 164))
+PWTK = dict(m=217918, nnz=11524432, block=6, half_band_nodes=1700)
+PARABOLIC_FEM = dict(m=525825, width=725, shift=1e-4)
+NLPKKT120 = dict(dims=(160, 135, 164), shift=1e-2, L=8)
 
 
 def spmv_bytes(m, n, nnz):
@@ -55,8 +60,7 @@ def glibc_rhs(seed, n):
     libc.srand(ctypes.c_uint(seed))
     r = libc.rand
     r.restype = ctypes.c_int
-    vals = np.fromiter((r() for _ in range(n)), dtype=np.float64, count=n)
-    return vals / 2147483647.0
+    return np.fromiter((r() for _ in range(n)), dtype=np.float64, count=n) / 2147483647.0
 
 
 class Dist:
@@ -83,6 +87,13 @@ class Dist:
         t = torch.tensor([v], dtype=torch.float64)
         self.td.all_reduce(t, op=self.td.ReduceOp.MAX)
         return float(t.item())
+
+    def bcast_bytes(self, b):
+        if not self.td:
+            return b
+        obj = [b]
+        self.td.broadcast_object_list(obj, src=0)
+        return obj[0]
 
 
 def cpu_baseline(a, x, seconds):
@@ -116,57 +127,79 @@ def cpu_baseline(a, x, seconds):
                          f"{calls} calls in {el:.1f} s"}
 
 
-def run_cg(dev, seconds_cpu, do_cpu):
-    """parabolic_fem-shaped single CG and nlpkkt120-shaped 8-RHS CG on one GPU."""
-    out = {}
-    pf = mspmv.CsrMatrix.synth_stencil(0, PARABOLIC_FEM["m"], PARABOLIC_FEM["width"])
+def run_cg_single(dev, cpu_seconds, do_cpu):
+    """configs[3]: CGSolveSingle on a parabolic_fem-shaped SPD matrix."""
+    pf = mspmv.CsrMatrix.synth_stencil(0, PARABOLIC_FEM["m"], PARABOLIC_FEM["width"],
+                                       diag_shift=PARABOLIC_FEM["shift"])
     n = pf.num_rows
     b = glibc_rhs(42, n)
     thr = float(np.sqrt(np.sum(b * b)) * 1e-5)  # calculate_threshold quirk, cpu_singlecg.cpp:92
     with mspmv.GpuCsr(pf, device=dev) as g:
         db, dx = mspmv.DeviceBuffer.from_array(b, dev), mspmv.DeviceBuffer(8 * n, dev)
-        g.cg_dev(db, dx, 1, 10000, thr)                     # warm (graph, workspace)
+        g.cg_dev(db, dx, 1, 10000, thr)  # warm (graph, workspace)
         t0 = time.perf_counter()
         it, _, st = g.cg_dev(db, dx, 1, 10000, thr)
         el = time.perf_counter() - t0
     ips = it / el
-    out["cg_single"] = {
-        "workload": f"CGSolveSingle, parabolic_fem-shaped SPD m={n} nnz={pf.num_nonzeros}, srand(42) RHS, "
-                    f"tol quirk 1e-5*||b||",
-        "iterations": it, "seconds": round(el, 5), "iters_per_s": round(ips, 1),
-        "achieved_GBps": round(cg_iter_bytes(n, pf.num_nonzeros) * ips / 1e9, 1), "status": st}
+    out = {"workload": f"CGSolveSingle, parabolic_fem-shaped SPD (7-pt FEM, diag shift {PARABOLIC_FEM['shift']}) "
+                       f"m={n} nnz={pf.num_nonzeros}, srand(42) RHS, tol = 1e-5*||b|| (cpu_singlecg quirk)",
+           "iterations": it, "seconds": round(el, 5), "iters_per_s": round(ips, 1),
+           "us_per_iter": round(el / max(it, 1) * 1e6, 2),
+           "achieved_GBps": round(cg_iter_bytes(n, pf.num_nonzeros) * ips / 1e9, 1), "status": st}
     if do_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from _oracle import Oracle
         orc = Oracle()
-        k = 0
-        t0 = time.perf_counter()
-        while time.perf_counter() - t0 < seconds_cpu:
-            orc.cg_single(pf, b, 100, thr)
-            k += 100
+        k, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < cpu_seconds:
+            _, its, _ = orc.cg_single(pf, b, 200, thr)
+            k += its
         el = time.perf_counter() - t0
-        out["cg_single"]["cpu_baseline"] = {
-            "iters_per_s": round(k / el, 1), "cores": orc.lib.orc_max_threads(), "kind": "port",
-            "sample": f"oracle CGSolveSingle restatement (reference CG needs <mkl.h>), {k} iterations"}
+        out["cpu_baseline"] = {"iters_per_s": round(k / el, 1), "cores": orc.lib.orc_max_threads(), "kind": "port",
+                               "sample": f"oracle CGSolveSingle restatement (the reference's CG headers need "
+                                         f"<mkl.h>), {k} iterations in {el:.1f} s"}
+    return out
+
+
+def run_cg_multi(d, dev):
+    """configs[4]: CGSolveMultiple, 8 RHS, nlpkkt120-sized 27-point SPD; row-sharded at N > 1."""
     nx, ny, nz = NLPKKT120["dims"]
-    nk = mspmv.CsrMatrix.synth_stencil(1, nx * ny * nz, nx, ny, nz)
-    L = 8
+    L = NLPKKT120["L"]
+    nk = mspmv.CsrMatrix.synth_stencil(1, nx * ny * nz, nx, ny, nz, diag_shift=NLPKKT120["shift"])
     n = nk.num_rows
     B = np.random.default_rng(42).uniform(0, 1, (n, L))
-    flat = B.reshape(-1)
-    thr = float(np.sqrt(np.sum(flat[:n] ** 2)) * 1e-5)  # calculate_threshold(b, num_rows) on the flat buffer, cpu_multicg.cpp:168
-    with mspmv.GpuCsr(nk, device=dev) as g:
-        dB, dX = mspmv.DeviceBuffer.from_array(B, dev), mspmv.DeviceBuffer(8 * n * L, dev)
-        g.cg_dev(dB, dX, L, 50000, thr)
+    thr = float(np.sqrt(np.sum(B.reshape(-1)[:n] ** 2)) * 1e-5)  # calculate_threshold on the flat buffer
+    if d.world == 1:
+        with mspmv.GpuCsr(nk, device=dev) as g:
+            dB, dX = mspmv.DeviceBuffer.from_array(B, dev), mspmv.DeviceBuffer(8 * n * L, dev)
+            g.cg_dev(dB, dX, L, 50000, thr)
+            t0 = time.perf_counter()
+            it, _, st = g.cg_dev(dB, dX, L, 50000, thr)
+            el = time.perf_counter() - t0
+        mode = "1 GPU"
+    else:
+        uid = d.bcast_bytes(mspmv.comm_unique_id() if d.rank == 0 else None)
+        rb = mspmv.dist_partition(nk, d.world)
+        loc = mspmv.local_rows(nk, rb, d.rank)
+        dc = mspmv.DistCsr(uid, d.world, d.rank, dev, rb, loc)
+        lo, hi = int(rb[d.rank]), int(rb[d.rank + 1])
+        dB = mspmv.DeviceBuffer.from_array(np.ascontiguousarray(B[lo:hi]), dev)
+        dX = mspmv.DeviceBuffer(8 * max(hi - lo, 1) * L, dev)
+        dc.cg_dev(dB, dX, L, 50000, thr)
+        d.barrier()
         t0 = time.perf_counter()
-        it, _, st = g.cg_dev(dB, dX, L, 50000, thr)
+        it, _, st = dc.cg_dev(dB, dX, L, 50000, thr)
         el = time.perf_counter() - t0
+        d.barrier()
+        el = d.max(el)
+        dc.close()
+        mode = f"row-sharded over {d.world} GPUs (RCCL halo exchange + 2 all-reduces per iteration)"
     ips = it / el
-    out["cg_multi"] = {
-        "workload": f"CGSolveMultiple L={L}, nlpkkt120-sized 27-pt SPD m={n} nnz={nk.num_nonzeros}, 1 GPU",
-        "iterations": it, "seconds": round(el, 4), "iters_per_s": round(ips, 1),
-        "achieved_GBps": round(cg_iter_bytes(n, nk.num_nonzeros, L) * ips / 1e9, 1), "status": st}
-    return out
+    return {"workload": f"CGSolveMultiple L={L}, nlpkkt120-sized 27-pt SPD (diag shift {NLPKKT120['shift']}) "
+                        f"m={n} nnz={nk.num_nonzeros}, {mode}",
+            "iterations": it, "seconds": round(el, 4), "iters_per_s": round(ips, 1),
+            "ms_per_iter": round(el / max(it, 1) * 1e3, 3),
+            "achieved_GBps": round(cg_iter_bytes(n, nk.num_nonzeros, L) * ips / 1e9, 1), "status": st}
 
 
 def main():
@@ -187,11 +220,11 @@ def main():
 
     mats, gs, dxs, dys, xs = [], [], [], [], []
     for i in range(args.batch):
-        a = mspmv.CsrMatrix.synth_banded(PWTK["m"], PWTK["nnz"], PWTK["half_band"], seed=1 + i + 1000 * d.rank)
+        a = mspmv.CsrMatrix.synth_fem_blocked(PWTK["m"], PWTK["nnz"], PWTK["block"], PWTK["half_band_nodes"],
+                                              seed=1 + i + 1000 * d.rank)
         x = np.random.default_rng(2 + i + 1000 * d.rank).uniform(0.0, 1.0, a.num_cols)
-        g = mspmv.GpuCsr(a, device=dev)
         mats.append(a)
-        gs.append(g)
+        gs.append(mspmv.GpuCsr(a, device=dev))
         xs.append(x)
         dxs.append(mspmv.DeviceBuffer.from_array(x, dev))
         dys.append(mspmv.DeviceBuffer(8 * a.num_rows, dev))
@@ -214,7 +247,6 @@ def main():
     value = flops / el / 1e9
     bytes_launch = spmv_bytes(a0.num_rows, a0.num_cols, a0.num_nonzeros)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    # hot: one matrix back to back (MALL-resident: 143 MB < 256 MiB Infinity Cache)
     hot_ms, hot_kern, _ = mspmv.time_spmm_batch(gs[:1], dxs[:1], dys[:1], 1, 200)
     ref_eff = (a0.num_nonzeros * 20 + a0.num_rows * 12) / (kern_ms * 1e-3) / 1e9  # cpu_spmv.cpp:722-726
 
@@ -222,38 +254,51 @@ def main():
         "metric": METRIC, "value": round(value, 2), "unit": "GFLOP/s", "n_gpus": d.world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (pwtk-shaped banded CSR, splitmix64 values; SuiteSparse unavailable offline)",
+        "data": "synthetic (pwtk-shaped 6-DOF FEM-blocked CSR, splitmix64 values; SuiteSparse unavailable offline)",
         "config": {"workload": f"merge-path CSR SpMV fp64, 1 RHS, batch of {args.batch} pwtk-shaped matrices "
                                f"per step per GPU (configs[1])",
                    "m": a0.num_rows, "nnz": a0.num_nonzeros, "batch": args.batch,
-                   "parallelism": f"independent row-block batches, {d.world} GPU(s)"},
+                   "parallelism": f"independent SpMV batches, {d.world} GPU(s)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "k_spmv_tile<8,false>", "bytes_per_launch": bytes_launch,
+                     "kernel": "k_spmv_persist<8,0,true>", "bytes_per_launch": bytes_launch,
                      "kernel_ms": round(kern_ms, 5), "kernels_per_step": kps},
         "spmv_gflops_per_launch": round(2.0 * a0.num_nonzeros / (kern_ms * 1e-3) / 1e9, 2),
         "reference_effective_GBps": round(ref_eff, 1),
         "hot_single_matrix": {"ms_per_call": round(hot_ms, 5), "kernel_ms": round(hot_kern, 5),
                               "GBps_vs_algorithmic": round(bytes_launch / (hot_kern * 1e-3) / 1e9, 1),
-                              "note": "one 143 MB matrix back to back: Infinity-Cache resident, not HBM-bound"},
+                              "note": "one 143 MB matrix back to back: Infinity-Cache resident"},
         "setup_ms": round(gs[0].setup_ms, 2),
     }
+    for g in gs:
+        g.close()
+
+    if d.rank == 0:  # stress shape: columns scattered one per band slice (x gathers hit a new line each)
+        sc = mspmv.CsrMatrix.synth_banded(PWTK["m"], PWTK["nnz"], 10000, seed=77)
+        with mspmv.GpuCsr(sc, device=dev) as g:
+            bx = mspmv.DeviceBuffer.from_array(np.random.default_rng(3).uniform(0, 1, sc.num_cols), dev)
+            by = mspmv.DeviceBuffer(8 * sc.num_rows, dev)
+            _, sk, _ = mspmv.time_spmm_batch([g], [bx], [by], 1, 100)
+        result["scatter_band_stress"] = {"kernel_ms": round(sk, 5),
+                                         "GBps_vs_algorithmic": round(bytes_launch / (sk * 1e-3) / 1e9, 1),
+                                         "note": "pwtk size, 53 columns per row scattered over +-10,000"}
 
     if d.rank == 0 and d.world == 1 and not args.no_cpu:
         y_cpu, cb = cpu_baseline(a0, xs[0], args.cpu_seconds)
         result["cpu_baseline"] = cb
-        y_gpu = dys[0].download(a0.num_rows)
+        with mspmv.GpuCsr(a0, device=dev) as g:
+            y_gpu = g.spmv(xs[0])
         rel = float(np.max(np.abs(y_gpu - y_cpu) / np.maximum(np.abs(y_cpu), 1e-300)))
         result["cpu_baseline"]["gpu_vs_cpu_max_rel_diff"] = rel
         result["speedup_vs_cpu"] = round(value / cb["value"], 1)
-    if d.rank == 0 and d.world == 1 and not args.no_cg:
+    if not args.no_cg:
         try:
-            result.update(run_cg(dev, min(args.cpu_seconds, 10.0), not args.no_cpu))
+            if d.world == 1:
+                result["cg_single"] = run_cg_single(dev, min(args.cpu_seconds, 10.0), not args.no_cpu)
+            result["cg_multi"] = run_cg_multi(d, dev)
         except Exception as e:  # the headline line must still print
-            result["cg_error"] = repr(e)
+            result["cg_error"] = repr(e)[:300]
 
-    for g in gs:
-        g.close()
     if d.rank == 0:
         print(json.dumps(result), flush=True)
     if d.td:

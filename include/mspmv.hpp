@@ -1,0 +1,110 @@
+// mspmv.hpp -- header-only C++ facade with the reference's own names and signatures, over the
+// C-ABI in mspmv.h.  A reference caller replaces
+//     #include "work_2025/spmm/merge_based.hpp" / single_strategy.hpp / no_pretreatment.hpp
+// by this header and links libmspmv.so; call sites stay as they are:
+//     OmpMergeCsrmv(g_omp_threads, a, a.row_offsets + 1, a.column_indices, a.values, x, y);   // cpu_spmv.cpp:448
+//     OmpMergeCsrmm(g_omp_threads, a, a.row_offsets + 1, a.column_indices, a.values, X, Y, L); // merge_based.hpp:46
+//     int it = CGSolveSingle(a, b, x, max_iters, threshold);                                   // single_strategy.hpp:102
+//     int it = CGSolveMultiple(a, B, X, L, max_iters, threshold, NONZERO_SPLIT, &errs);        // no_pretreatment.hpp:32
+// `Csr` is any type with the CsrMatrix<double,int> fields (sparse_matrix.h:648-653).  The matrix is
+// uploaded to HBM on first use and cached per (values pointer, nnz); call mspmv_facade_release(a)
+// before freeing or mutating a matrix.  num_threads is accepted and ignored (the GPU decides).
+// Errors throw std::runtime_error with mspmv_last_error() (the reference exit()s instead).
+#pragma once
+
+#include <algorithm>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "mspmv.h"
+
+namespace mspmv_facade {
+
+inline void check(mspmv_status s, const char *where)
+{
+    if (s != MSPMV_OK && s != MSPMV_ERR_BREAKDOWN)
+        throw std::runtime_error(std::string(where) + ": " + mspmv_last_error());
+}
+
+inline std::map<std::pair<const void *, int>, mspmv_handle> &cache()
+{
+    static std::map<std::pair<const void *, int>, mspmv_handle> c;
+    return c;
+}
+
+template <typename Csr>
+mspmv_handle handle_for(const Csr &a, int device = 0)
+{
+    auto key = std::make_pair((const void *)a.values, (int)a.num_nonzeros);
+    auto it = cache().find(key);
+    if (it != cache().end())
+        return it->second;
+    mspmv_csr_d d{a.num_rows, a.num_cols, a.num_nonzeros, a.row_offsets, a.column_indices, a.values};
+    mspmv_handle h = nullptr;
+    check(mspmv_csr_create(&d, device, &h), "mspmv_csr_create");
+    cache().emplace(key, h);
+    return h;
+}
+
+}  // namespace mspmv_facade
+
+template <typename Csr>
+void mspmv_facade_release(const Csr &a)
+{
+    auto key = std::make_pair((const void *)a.values, (int)a.num_nonzeros);
+    auto it = mspmv_facade::cache().find(key);
+    if (it != mspmv_facade::cache().end()) {
+        mspmv_destroy(it->second);
+        mspmv_facade::cache().erase(it);
+    }
+}
+
+// cpu_spmv.cpp:357-421
+template <typename Csr, typename OffsetT, typename ValueT>
+void OmpMergeCsrmv(int /*num_threads*/, Csr &a, OffsetT * /*row_end_offsets*/, OffsetT * /*column_indices*/,
+                   ValueT * /*values*/, ValueT *vector_x, ValueT *vector_y_out)
+{
+    static_assert(sizeof(ValueT) == 8 && sizeof(OffsetT) == 4, "mspmv: CsrMatrix<double,int> only");
+    mspmv_facade::check(mspmv_dspmv(mspmv_facade::handle_for(a), vector_x, vector_y_out), "mspmv_dspmv");
+}
+
+// work_2025/spmm/merge_based.hpp:46-153 (row-major n x num_vectors panels)
+template <typename Csr, typename OffsetT, typename ValueT>
+void OmpMergeCsrmm(int /*num_threads*/, Csr &a, OffsetT * /*row_end_offsets*/, OffsetT * /*column_indices*/,
+                   ValueT * /*values*/, ValueT *vector_x, ValueT *vector_y_out, int num_vectors)
+{
+    static_assert(sizeof(ValueT) == 8 && sizeof(OffsetT) == 4, "mspmv: CsrMatrix<double,int> only");
+    mspmv_facade::check(mspmv_dspmm(mspmv_facade::handle_for(a), vector_x, vector_y_out, num_vectors),
+                        "mspmv_dspmm");
+}
+
+// work_2025/main/single_strategy.hpp:102-170
+template <typename Csr, typename ValueT>
+int CGSolveSingle(Csr &a, const ValueT *b, ValueT *x, int max_iters, ValueT tolerance)
+{
+    int iters = 0;
+    mspmv_facade::check(
+        mspmv_dcg_single(mspmv_facade::handle_for(a), b, x, max_iters, tolerance, &iters, nullptr, 0),
+        "mspmv_dcg_single");
+    return iters;
+}
+
+// work_2025/main/no_pretreatment.hpp:32-197.  kernel_type is any value convertible to int
+// (the reference's SpmmKernel enum, work_2025/types.hpp:11-16).
+template <typename Csr, typename ValueT, typename KernelT>
+int CGSolveMultiple(Csr &a, const ValueT *B, ValueT *X, int num_vectors, int max_iters, ValueT tolerance,
+                    KernelT kernel_type, std::vector<double> *max_errors = nullptr)
+{
+    int iters = 0;
+    std::vector<double> hist(max_errors ? (size_t)max_iters : 0);
+    mspmv_facade::check(mspmv_dcg_multi(mspmv_facade::handle_for(a), B, X, num_vectors, max_iters, tolerance,
+                                        (mspmv_spmm_kernel)(int)kernel_type, &iters,
+                                        max_errors ? hist.data() : nullptr, max_errors ? max_iters : 0),
+                        "mspmv_dcg_multi");
+    if (max_errors)
+        max_errors->assign(hist.begin(), hist.begin() + std::min<size_t>(hist.size(), (size_t)iters));
+    return iters;
+}

@@ -40,13 +40,15 @@ MSPMV_API mspmv_status mspmv_synth_powerlaw(int m, int n, long long nnz, double 
                                   int *row_offsets, int *cols, double *vals);
 
 /* SPD stencils (symmetric pattern, off-diagonals -U(0,1) symmetric in (i,j), diagonal =
- * sum|off| + 1 -> strictly diagonally dominant).
+ * sum|off| + diag_shift -> strictly diagonally dominant for diag_shift > 0; a small shift
+ * gives the FEM-like condition numbers (hundreds to thousands of CG iterations).
  *   kind 0: 2-D 7-point triangular-mesh stencil (P1 FEM; parabolic_fem shape) on a grid
  *           `dim0` wide with m points in row-major order (last grid row may be partial);
  *   kind 1: 3-D 27-point stencil on dim0 x dim1 x dim2 (nlpkkt120-sized, made SPD).
  * Call with row_offsets only (cols/vals NULL) to size: fills row_offsets and *nnz_out. */
 MSPMV_API mspmv_status mspmv_synth_stencil(int kind, int m, int dim0, int dim1, int dim2, unsigned long long seed,
-                                 int *row_offsets, int *cols, double *vals, long long *nnz_out);
+                                           double diag_shift, int *row_offsets, int *cols, double *vals,
+                                           long long *nnz_out);
 
 #ifdef __cplusplus
 }

@@ -175,9 +175,9 @@ mspmv_status mspmv_synth_powerlaw(int m, int n, long long nnz, double exponent, 
 }
 
 mspmv_status mspmv_synth_stencil(int kind, int m, int dim0, int dim1, int dim2, unsigned long long seed,
-                                 int *row_offsets, int *cols, double *vals, long long *nnz_out)
+                                 double diag_shift, int *row_offsets, int *cols, double *vals, long long *nnz_out)
 {
-    if (!row_offsets || (kind != 0 && kind != 1) || dim0 <= 0)
+    if (!row_offsets || (kind != 0 && kind != 1) || dim0 <= 0 || !(diag_shift > 0.0))
         return MSPMV_ERR_INVALID;
     if (kind == 1) {
         if (dim1 <= 0 || dim2 <= 0)
@@ -240,7 +240,7 @@ mspmv_status mspmv_synth_stencil(int kind, int m, int dim0, int dim1, int dim2, 
         int nb[27];
         const int k = neigh(p, nb);
         const int s = row_offsets[p];
-        double diag = 1.0;
+        double diag = diag_shift;
         int self = -1;
         for (int t = 0; t < k; ++t) {
             const int q = nb[t];

@@ -93,6 +93,10 @@ _SIGS = {
     "mspmv_memcpy_d2d": (_I, [_P, _P, _SZ]),
     "mspmv_memset_dev": (_I, [_P, _I, _SZ]),
     "mspmv_synth_banded": (_I, [_I, ctypes.c_longlong, _I, ctypes.c_ulonglong, _P, _P, _P]),
+    "mspmv_market_read": (_I, [ctypes.c_char_p, _D, _PI, _PI, _PI, ctypes.POINTER(_P), ctypes.POINTER(_P),
+                               ctypes.POINTER(_P)]),
+    "mspmv_generate": (_I, [_I, _I, _I, _D, _PI, _PI, _PI, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P)]),
+    "mspmv_host_free": (None, [_P]),
     "mspmv_dist_partition": (_I, [_P, _I, _I, _I, _P]),
     "mspmv_dist_localize": (_I, [_P, _I, _I, _P, _P, _P, _PI, _P, _I, _P]),
     "mspmv_comm_unique_id": (_I, [_P]),
@@ -103,7 +107,7 @@ _SIGS = {
     "mspmv_dist_cg_dev": (_I, [_P, _P, _P, _I, _I, _D, _PI, _P, _I]),
     "mspmv_synth_fem_blocked": (_I, [_I, ctypes.c_longlong, _I, _I, ctypes.c_ulonglong, _P, _P, _P]),
     "mspmv_synth_powerlaw": (_I, [_I, _I, ctypes.c_longlong, _D, ctypes.c_ulonglong, _P, _P, _P]),
-    "mspmv_synth_stencil": (_I, [_I, _I, _I, _I, _I, ctypes.c_ulonglong, _P, _P, _P,
+    "mspmv_synth_stencil": (_I, [_I, _I, _I, _I, _I, ctypes.c_ulonglong, _D, _P, _P, _P,
                                  ctypes.POINTER(ctypes.c_longlong)]),
 }
 
@@ -163,6 +167,39 @@ class CsrMatrix:
         return _CsrD(self.num_rows, self.num_cols, self.num_nonzeros, _ptr(self.row_offsets),
                      _ptr(self.column_indices), _ptr(self.values))
 
+    # --- the reference's constructors (sparse_matrix.h), natively in libmspmv.so --------
+    @classmethod
+    def _from_c(cls, m, n, nnz, ro, ci, va) -> "CsrMatrix":
+        try:
+            r = np.ctypeslib.as_array(ctypes.cast(ro, ctypes.POINTER(ctypes.c_int)), (m.value + 1,)).copy()
+            k = nnz.value
+            c = np.ctypeslib.as_array(ctypes.cast(ci, ctypes.POINTER(ctypes.c_int)), (max(k, 1),))[:k].copy()
+            v = np.ctypeslib.as_array(ctypes.cast(va, ctypes.POINTER(ctypes.c_double)), (max(k, 1),))[:k].copy()
+        finally:
+            for p in (ro, ci, va):
+                lib.mspmv_host_free(p)
+        return cls(m.value, n.value, k, r, c, v)
+
+    @classmethod
+    def from_market(cls, path: str, default_value: float = 1.0) -> "CsrMatrix":
+        """CooMatrix::InitMarket + CsrMatrix::Init (sparse_matrix.h:211-380, 668-733)."""
+        m, n, nnz = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        ro, ci, va = _P(), _P(), _P()
+        _check(lib.mspmv_market_read(path.encode(), default_value, ctypes.byref(m), ctypes.byref(n),
+                                     ctypes.byref(nnz), ctypes.byref(ro), ctypes.byref(ci), ctypes.byref(va)),
+               f"market_read({path})")
+        return cls._from_c(m, n, nnz, ro, ci, va)
+
+    @classmethod
+    def generate(cls, kind: str, p0: int, p1: int = 0) -> "CsrMatrix":
+        """The reference's grid2d / grid3d / wheel / dense generators (sparse_matrix.h:385-623)."""
+        k = {"grid2d": 0, "grid3d": 1, "wheel": 2, "dense": 3}[kind]
+        m, n, nnz = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        ro, ci, va = _P(), _P(), _P()
+        _check(lib.mspmv_generate(k, p0, p1, 1.0, ctypes.byref(m), ctypes.byref(n), ctypes.byref(nnz),
+                                  ctypes.byref(ro), ctypes.byref(ci), ctypes.byref(va)), f"generate({kind})")
+        return cls._from_c(m, n, nnz, ro, ci, va)
+
     # --- synthetic shapes (SURVEY 8(d)); generated natively in libmspmv.so -------------
     @classmethod
     def synth_banded(cls, m: int, nnz: int, half_band: int, seed: int = 1) -> "CsrMatrix":
@@ -191,16 +228,17 @@ class CsrMatrix:
         return cls(m, n, nnz, ro, ci[:nnz], va[:nnz])
 
     @classmethod
-    def synth_stencil(cls, kind: int, m: int, dim0: int, dim1: int = 0, dim2: int = 0, seed: int = 7) -> "CsrMatrix":
+    def synth_stencil(cls, kind: int, m: int, dim0: int, dim1: int = 0, dim2: int = 0, seed: int = 7,
+                      diag_shift: float = 1.0) -> "CsrMatrix":
         """kind 0: 2-D 7-point triangular FEM stencil (parabolic_fem shape), kind 1: 3-D
-        27-point (nlpkkt120 size).  Symmetric, strictly diagonally dominant -> SPD."""
+        27-point (nlpkkt120 size).  Symmetric, diagonal = sum|off| + diag_shift -> SPD."""
         ro = np.empty(m + 1, np.int32)
         nnz = ctypes.c_longlong(0)
-        _check(lib.mspmv_synth_stencil(kind, m, dim0, dim1, dim2, seed, _ptr(ro), None, None, ctypes.byref(nnz)),
-               "synth_stencil(size)")
+        _check(lib.mspmv_synth_stencil(kind, m, dim0, dim1, dim2, seed, diag_shift, _ptr(ro), None, None,
+                                       ctypes.byref(nnz)), "synth_stencil(size)")
         ci = np.empty(max(nnz.value, 1), np.int32)
         va = np.empty(max(nnz.value, 1), np.float64)
-        _check(lib.mspmv_synth_stencil(kind, m, dim0, dim1, dim2, seed, _ptr(ro), _ptr(ci), _ptr(va),
+        _check(lib.mspmv_synth_stencil(kind, m, dim0, dim1, dim2, seed, diag_shift, _ptr(ro), _ptr(ci), _ptr(va),
                                        ctypes.byref(nnz)), "synth_stencil")
         return cls(m, m, int(nnz.value), ro, ci[: nnz.value], va[: nnz.value])
 

@@ -1,0 +1,61 @@
+// facade_demo -- a reference-style C++ caller using include/mspmv.hpp unchanged call sites:
+// the CsrMatrix<double,int> field layout (sparse_matrix.h:648-653), OmpMergeCsrmv /
+// OmpMergeCsrmm / CGSolveSingle / CGSolveMultiple with the reference's argument lists.
+// Prints one line per call; exit code 0 when every result checks out against a host loop.
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#include "mspmv.hpp"
+#include "mspmv_synth.h"
+
+template <typename ValueT, typename OffsetT>
+struct CsrMatrix {  // the reference's field names and order
+    OffsetT num_rows, num_cols, num_nonzeros;
+    OffsetT *row_offsets, *column_indices;
+    ValueT *values;
+};
+enum SpmmKernel { SIMPLE, MERGE, NONZERO_SPLIT };  // work_2025/types.hpp:11-16
+
+int main()
+{
+    const int m = 4000;
+    std::vector<int> ro(m + 1);
+    long long nnz = 0;
+    if (mspmv_synth_stencil(0, m, 64, 0, 0, 7, 1e-2, ro.data(), nullptr, nullptr, &nnz) != MSPMV_OK)
+        return 1;
+    std::vector<int> ci(nnz);
+    std::vector<double> va(nnz);
+    mspmv_synth_stencil(0, m, 64, 0, 0, 7, 1e-2, ro.data(), ci.data(), va.data(), &nnz);
+    CsrMatrix<double, int> a{m, m, (int)nnz, ro.data(), ci.data(), va.data()};
+    std::vector<double> x(m), y(m), b(m), sol(m);
+    for (int i = 0; i < m; ++i)
+        x[i] = b[i] = 1.0 + (i % 7) * 0.125;
+    try {
+        OmpMergeCsrmv(8, a, a.row_offsets + 1, a.column_indices, a.values, x.data(), y.data());
+        double err = 0;
+        for (int r = 0; r < m; ++r) {
+            double s = 0;
+            for (int k = ro[r]; k < ro[r + 1]; ++k)
+                s += va[k] * x[ci[k]];
+            err = std::max(err, std::fabs(s - y[r]) / std::max(std::fabs(s), 1e-300));
+        }
+        printf("OmpMergeCsrmv max rel err %.3g\n", err);
+        const int L = 4;
+        std::vector<double> X((size_t)m * L, 1.0), Y((size_t)m * L), B((size_t)m * L), XS((size_t)m * L);
+        OmpMergeCsrmm(8, a, a.row_offsets + 1, a.column_indices, a.values, X.data(), Y.data(), L);
+        printf("OmpMergeCsrmm Y[0] %.6f\n", Y[0]);
+        const int it1 = CGSolveSingle(a, b.data(), sol.data(), 5000, 1e-10);
+        for (size_t i = 0; i < B.size(); ++i)
+            B[i] = b[i / L] * (1 + (int)(i % L));
+        std::vector<double> errs;
+        const int itm = CGSolveMultiple(a, B.data(), XS.data(), L, 5000, 1e-10, NONZERO_SPLIT, &errs);
+        printf("CGSolveSingle %d iters, CGSolveMultiple %d iters (last max err %.3g)\n", it1, itm,
+               errs.empty() ? -1.0 : errs.back());
+        mspmv_facade_release(a);
+        return (err < 1e-12 && it1 > 0 && itm > 0 && !errs.empty() && errs.back() < 1e-10) ? 0 : 2;
+    } catch (const std::exception &e) {
+        printf("error: %s\n", e.what());
+        return 3;
+    }
+}

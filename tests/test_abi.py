@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("mspmv.h", "mspmv_synth.h", "mspmv_dist.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("mspmv.h", "mspmv_synth.h", "mspmv_dist.h", "mspmv_io.h")]
 
 
 def declared():
