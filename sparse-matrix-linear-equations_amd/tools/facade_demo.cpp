@@ -35,12 +35,14 @@ int main()
         OmpMergeCsrmv(8, a, a.row_offsets + 1, a.column_indices, a.values, x.data(), y.data());
         double err = 0;
         for (int r = 0; r < m; ++r) {
-            double s = 0;
-            for (int k = ro[r]; k < ro[r + 1]; ++k)
+            double s = 0, ab = 0;  // error measured against sum |a_k x_k| (reordered-sum bound)
+            for (int k = ro[r]; k < ro[r + 1]; ++k) {
                 s += va[k] * x[ci[k]];
-            err = std::max(err, std::fabs(s - y[r]) / std::max(std::fabs(s), 1e-300));
+                ab += std::fabs(va[k] * x[ci[k]]);
+            }
+            err = std::max(err, std::fabs(s - y[r]) / std::max(ab, 1e-300));
         }
-        printf("OmpMergeCsrmv max rel err %.3g\n", err);
+        printf("OmpMergeCsrmv max err relative to |A||x| %.3g\n", err);
         const int L = 4;
         std::vector<double> X((size_t)m * L, 1.0), Y((size_t)m * L), B((size_t)m * L), XS((size_t)m * L);
         OmpMergeCsrmm(8, a, a.row_offsets + 1, a.column_indices, a.values, X.data(), Y.data(), L);
