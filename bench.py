@@ -261,7 +261,7 @@ def main():
                    "parallelism": f"independent SpMV batches, {d.world} GPU(s)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "k_spmv_persist<8,0,true>", "bytes_per_launch": bytes_launch,
+                     "kernel": mspmv.lib.mspmv_spmv_kernel_name().decode(), "bytes_per_launch": bytes_launch,
                      "kernel_ms": round(kern_ms, 5), "kernels_per_step": kps},
         "spmv_gflops_per_launch": round(2.0 * a0.num_nonzeros / (kern_ms * 1e-3) / 1e9, 2),
         "reference_effective_GBps": round(ref_eff, 1),

@@ -158,6 +158,13 @@ MSPMV_API mspmv_status mspmv_last_kernel_ms(mspmv_handle h, double *tile_kernel_
  * bit-identical to SpmvGold). */
 MSPMV_API mspmv_status mspmv_tile_plan(mspmv_handle h, int L, int *num_tiles, int *tile_items, int *num_carries,
                                        mspmv_coord *bounds);
+/* Each tile's in-tile reduction (num_tiles entries): 0 = per-thread merge walk, g > 0 = row
+ * groups of 2^(g-1) lanes (g = 1: one row per thread, summed in CSR order -> bit-identical to
+ * SpmvGold for rows the tile holds whole).  Always 0 for L > 1. */
+MSPMV_API mspmv_status mspmv_tile_modes(mspmv_handle h, int L, unsigned char *modes);
+/* The single-RHS SpMV kernel instantiation this process launches (tuning read once from the
+ * MSPMV_SPMV_* environment), e.g. "k_spmv_tile<8,0,true>" -- the name rocprofv3 reports. */
+MSPMV_API const char *mspmv_spmv_kernel_name(void);
 
 /* ---- device memory helpers (so hosts need no HIP headers) ---------------------------- */
 MSPMV_API mspmv_status mspmv_device_malloc(int device, size_t bytes, void **d_ptr);

@@ -79,6 +79,7 @@ static void free_plan(TilePlan &p)
 {
     dev_free(p.d_bounds);
     dev_free(p.d_split);
+    dev_free(p.d_modes);
     dev_free(p.d_carry_tiles);
     dev_free(p.d_carry_rows);
     dev_free(p.d_carry_val);
@@ -104,6 +105,7 @@ static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out)
     mspmv_status st;
     if ((st = dev_alloc(&p.d_bounds, (size_t)T + 1)) != MSPMV_OK ||
         (st = dev_alloc(&p.d_split, (size_t)T + 1)) != MSPMV_OK ||
+        (st = dev_alloc(&p.d_modes, (size_t)std::max(T, 1))) != MSPMV_OK ||
         (st = dev_alloc(&p.d_carry_val, (size_t)std::max(T, 1) * 16)) != MSPMV_OK) {
         free_plan(p);
         return st;
@@ -116,6 +118,8 @@ static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out)
     hipError_t e = launch_merge_coords(h->d_row_offsets, h->m, h->nnz, tile, T, p.d_bounds, h->stream);
     if (e == hipSuccess)
         e = launch_snap(h->d_row_offsets, h->m, p.d_bounds, p.d_split, T, p.snap, h->stream);
+    if (e == hipSuccess)
+        e = launch_tile_modes(h->d_row_offsets, p.d_bounds, p.d_split, T, p.d_modes, h->stream);
     std::vector<int2> hb((size_t)T + 1);
     std::vector<unsigned char> hs((size_t)T + 1);
     if (e == hipSuccess)
@@ -302,6 +306,8 @@ static bool aligned16(const void *p) { return ((uintptr_t)p & 15u) == 0; }
 extern "C" {
 
 const char *mspmv_last_error(void) { return g_err.c_str(); }
+
+const char *mspmv_spmv_kernel_name(void) { return spmv_kernel_name(); }
 
 const char *mspmv_version(void) { return "mspmv 0.1.0 (gfx950, merge-path fp64)"; }
 
@@ -853,6 +859,22 @@ mspmv_status mspmv_tile_plan(mspmv_handle h, int L, int *num_tiles, int *tile_it
         *num_carries = plan->num_carries;
     if (bounds)
         HIP_TRY(hipMemcpy(bounds, plan->d_bounds, sizeof(int2) * (plan->num_tiles + 1), hipMemcpyDeviceToHost));
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_tile_modes(mspmv_handle h, int L, unsigned char *modes)
+{
+    ST_TRY(check_handle(h));
+    if (!supported_L(L))
+        return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
+    if (!modes)
+        return invalid("null modes");
+    const TilePlan *plan = nullptr;
+    ST_TRY(get_plan(h, L, &plan));
+    if (L > 1)  // the SpMM kernels always walk
+        memset(modes, 0, (size_t)plan->num_tiles);
+    else if (plan->num_tiles)
+        HIP_TRY(hipMemcpy(modes, plan->d_modes, plan->num_tiles, hipMemcpyDeviceToHost));
     return MSPMV_OK;
 }
 

@@ -14,7 +14,7 @@ namespace mspmv {
 
 constexpr int kBlock = 256;  // 4 x 64-lane waves per workgroup
 constexpr int kNnzPad = 16;  // padding elements after the last nonzero of the device arrays
-constexpr int kSnapDiv = 4;  // a boundary snaps to its row start if <= tile/kSnapDiv nonzeros deep
+constexpr int kSnapDiv = 8;  // a boundary snaps to its row start if <= tile/kSnapDiv nonzeros deep
 
 // A merge-path tile plan for one nominal tile size (merge items per tile).
 //
@@ -30,6 +30,7 @@ struct TilePlan {
     int num_tiles = 0;
     int2 *d_bounds = nullptr;           // [num_tiles+1] (row, nnz) boundary coordinates
     unsigned char *d_split = nullptr;   // [num_tiles+1] 1 = split boundary (carry crosses it)
+    unsigned char *d_modes = nullptr;   // [num_tiles] in-tile reduction: 0 walk, lg+1 row groups of 2^lg
     int num_carries = 0;                // tiles whose trailing boundary is split
     int *d_carry_tiles = nullptr;       // [num_carries] tile ids, ascending
     int *d_carry_rows = nullptr;        // [num_carries] row each carry belongs to
@@ -96,6 +97,8 @@ namespace mspmv {
 void set_error(const std::string &msg);
 hipError_t launch_merge_coords(const int *d_row_offsets, int m, int nnz, long long diag_step, int num_parts,
                                int2 *d_out, hipStream_t s);
+hipError_t launch_tile_modes(const int *d_row_offsets, const int2 *d_bounds, const unsigned char *d_split,
+                             int num_tiles, unsigned char *d_modes, hipStream_t s);
 hipError_t launch_snap(const int *d_row_offsets, int m, int2 *d_bounds, unsigned char *d_split, int num_tiles,
                        int snap, hipStream_t s);
 // y = A x (L == 1) or Y = A X (row-major panels), tile kernel + optional carry fix-up.
@@ -105,6 +108,7 @@ hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const 
 hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L);
 // Nominal tile size (merge items per tile) used for L right-hand sides.
 int tile_items_for(int L);
+const char *spmv_kernel_name();
 bool supported_L(int L);
 
 // CG pieces

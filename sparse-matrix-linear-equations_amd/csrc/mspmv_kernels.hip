@@ -153,6 +153,44 @@ __global__ void k_snap(const int *__restrict__ row_offsets, int m, int2 *__restr
     split[t] = s;
 }
 
+// Per-tile choice of the in-tile reduction of the single-RHS kernels (one thread per tile, at
+// plan time).  The tile's row segments -- its complete rows plus the trailing partial row of a
+// split boundary -- are either summed by row groups of G = 2^lg lanes (mode lg + 1) or, when
+// segment lengths are too uneven for that, by the per-thread merge walk (mode 0).  Cost model
+// in LDS-read steps of the slowest group: ceil(segments / groups) rounds of ceil(longest / G)
+// reads plus a log2(G)-step shuffle fold; the cheapest G wins if its cost is within max_cost
+// (the walk costs about IPT reads plus an 11-step search and two more barriers).
+__global__ void k_tile_modes(const int *__restrict__ row_offsets, const int2 *__restrict__ bounds,
+                             const unsigned char *__restrict__ split, int num_tiles, int max_cost,
+                             unsigned char *__restrict__ modes)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= num_tiles)
+        return;
+    const int2 b0 = bounds[t], b1 = bounds[t + 1];
+    const int nrows = b1.x - b0.x;
+    const bool tail = split[t + 1] != 0;
+    const int nseg = nrows + (tail ? 1 : 0);
+    int longest = 0, prev = b0.y;
+    for (int r = 0; r < nrows; ++r) {
+        const int e = row_offsets[b0.x + 1 + r];
+        longest = max(longest, e - prev);
+        prev = e;
+    }
+    if (tail)
+        longest = max(longest, b1.y - prev);
+    int best = 0, best_cost = max_cost + 1;
+    for (int lg = 0; lg <= 6; ++lg) {
+        const int groups = kBlock >> lg, G = 1 << lg;
+        const int cost = ((nseg + groups - 1) / groups) * ((longest + G - 1) / G + 3 * lg);
+        if (cost < best_cost) {
+            best_cost = cost;
+            best = lg + 1;
+        }
+    }
+    modes[t] = best_cost <= max_cost ? (unsigned char)best : (unsigned char)0;
+}
+
 // ------------------------------------------------------------------------------------------
 // tile kernels
 // ------------------------------------------------------------------------------------------
@@ -166,6 +204,7 @@ struct TileArgs {
     double *__restrict__ y;            // SpMV/SpMM: y / Y.   CG: Ap
     const int2 *__restrict__ bounds;
     const unsigned char *__restrict__ split;
+    const unsigned char *__restrict__ rmode;  // per-tile in-tile reduction (k_tile_modes)
     double *__restrict__ carry_val;
     int num_tiles;
     CgScalars *scal;                   // CG: per-column scalars
@@ -183,9 +222,10 @@ struct TileArgs {
 //      row-sharded CG, whose x = [p_own | p_halo] was updated and exchanged beforehand).
 enum : int { kModeSpmv = 0, kModeCg = 1, kModeDot = 2 };
 
-// LDS slot of tile-local product k: one pad double every 4, so the walkers' strided reads
-// (about 8 products apart) spread over the banks.
-__device__ __forceinline__ int pslot(int k) { return k + (k >> 2); }
+// LDS slot of tile-local product k: an XOR swizzle inside each aligned group of 8 doubles,
+// so walkers 8 products apart hit different banks, while staging writes and row-group reads
+// (consecutive k) stay conflict-free -- no padding, so the tile fits a smaller LDS footprint.
+__device__ __forceinline__ int pslot(int k) { return k ^ ((k >> 3) & 7); }
 
 // Stage products val*x[col] (or val*(r + beta p)[col] for CG) of the tile's nonzeros
 // [n0, n0+nnzt) into LDS.  Striped: lane l of round j takes nonzero l + 256 j, so each
@@ -225,19 +265,21 @@ __device__ __forceinline__ void stage_products(const TileArgs &a, int n0, int nn
     }
 }
 
-// Per-tile LDS of the single-RHS kernels.
+// Per-tile LDS of the single-RHS kernels.  Products and row ends share one buffer: a tile
+// holds nrows + nnzt <= MAXI items, so the nnzt products (slots [0, nnzt) rounded up to the
+// swizzle group) followed by the nrows int row ends always fit in MAXI + 8 doubles.
 template <int IPT>
 struct SpmvSmem {
     static constexpr int TILE = kBlock * IPT;
     static constexpr int MAXI = TILE + TILE / kSnapDiv;
     static constexpr int MAXJ = (MAXI + kBlock - 1) / kBlock;
-    int rowend[MAXI];
-    double prod[MAXI + MAXI / 4 + 1];
+    double prod[MAXI + 8];
     int crow[kBlock];
     int ccol[kBlock];
     double cval[kBlock];
     double red[kBlock / 64];
     int last;
+    __device__ __forceinline__ int *rowend(int nnzt) { return reinterpret_cast<int *>(prod + ((nnzt + 7) & ~7)); }
 };
 
 // Everything after staging, for one tile whose products and row ends are in LDS: one merge
@@ -250,11 +292,12 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT> &sm, 
 {
     constexpr int MAXJ = SpmvSmem<IPT>::MAXJ;
     const int tid = threadIdx.x;
+    const int *rend = sm.rowend(nnzt);
     const int items = nrows + nnzt;
     const int ipt = (items + kBlock - 1) / kBlock;
     const int d0 = min(tid * ipt, items);
     int cx, cy;
-    lds_search(d0, sm.rowend, nrows, nnzt, cx, cy);
+    lds_search(d0, rend, nrows, nnzt, cx, cy);
     // The walker's end is the next walker's start: one search per thread, shared via LDS.
     sm.crow[tid] = cx;
     sm.ccol[tid] = cy;
@@ -262,7 +305,7 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT> &sm, 
     const int ex = tid + 1 < kBlock ? sm.crow[tid + 1] : nrows;
     const int ey = tid + 1 < kBlock ? sm.ccol[tid + 1] : nnzt;
     // Does this thread's first row hold nonzeros that earlier threads of the tile consumed?
-    const bool need_cin = (cx < ex) && (cy > (cx == 0 ? 0 : sm.rowend[cx - 1]));
+    const bool need_cin = (cx < ex) && (cy > (cx == 0 ? 0 : rend[cx - 1]));
     // This walker's products, read from LDS up front (independent reads, no dependent chain).
     double pr[MAXJ];
     if (ey > cy) {
@@ -285,7 +328,7 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT> &sm, 
     bool first = true, pend = false;
     int prow = 0;
     double pval = 0.0;
-    int next_end = cx < ex ? sm.rowend[cx] : 0x7fffffff;  // end of the row being accumulated
+    int next_end = cx < ex ? rend[cx] : 0x7fffffff;  // end of the row being accumulated
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) {
         const int k = cy + j;
@@ -301,7 +344,7 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT> &sm, 
                 first = false;
                 run = 0.0;
                 ++cx;
-                next_end = cx < ex ? sm.rowend[cx] : 0x7fffffff;
+                next_end = cx < ex ? rend[cx] : 0x7fffffff;
             }
             run += pr[j];
         }
@@ -346,6 +389,74 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT> &sm, 
             dot += a.x[R] * acc;
     }
     __syncthreads();  // LDS free for the next tile
+}
+
+// Row-group reduction of one tile whose products and row ends are in LDS (mode lg + 1 of
+// k_tile_modes): groups of G = 2^lg lanes take the tile's row segments round-robin; lane j of
+// a group sums products j, j+G, ... of the segment in order from 0.0, then a fixed xor
+// butterfly folds the group and its lane 0 writes the row.  G = 1 is the sequential CSR-order
+// sum of SpmvGold (cpu_spmv.cpp:241-265), bit for bit.  A few instructions per product,
+// against the walk's merge search and per-item row-end test, for tiles whose rows are alike.
+template <int IPT, int MODE>
+__device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT> &sm, int t, int r0, int nrows,
+                                           int nnzt, double beta, double &dot, int lg)
+{
+    const int G = 1 << lg;
+    const int tid = threadIdx.x;
+    const int *rend = sm.rowend(nnzt);
+    const int lane = tid & (G - 1);
+    const bool tail = a.split[t + 1] != 0;
+    const int nseg = nrows + (tail ? 1 : 0);
+    for (int r = tid >> lg; r < nseg; r += kBlock >> lg) {  // uniform within a group
+        const int s0 = r == 0 ? 0 : rend[r - 1];
+        const int e = r < nrows ? rend[r] : nnzt;
+        double v = 0.0;
+        int k = s0 + lane;
+        for (; k + 3 * G < e; k += 4 * G) {  // four independent LDS reads in flight
+            const double p0 = sm.prod[pslot(k)], p1 = sm.prod[pslot(k + G)];
+            const double p2 = sm.prod[pslot(k + 2 * G)], p3 = sm.prod[pslot(k + 3 * G)];
+            v += p0;
+            v += p1;
+            v += p2;
+            v += p3;
+        }
+        for (; k < e; k += G)
+            v += sm.prod[pslot(k)];
+        for (int off = G >> 1; off > 0; off >>= 1)
+            v += __shfl_xor(v, off);
+        if (lane == 0) {
+            const int R = r0 + r;
+            if (r < nrows) {
+                a.y[R] = v;
+                if (MODE == kModeCg) {
+                    const double pn = a.x[R] + beta * a.p_old[R];
+                    a.p_new[R] = pn;
+                    dot += pn * v;
+                } else if (MODE == kModeDot) {
+                    dot += a.x[R] * v;
+                }
+            } else {  // the trailing partial row -> carry (k_fixup adds it in tile order)
+                a.carry_val[t] = v;
+                if (MODE == kModeCg)
+                    dot += (a.x[R] + beta * a.p_old[R]) * v;
+                else if (MODE == kModeDot)
+                    dot += a.x[R] * v;
+            }
+        }
+    }
+    __syncthreads();  // LDS free for the next tile
+}
+
+// One tile's reduction, by its plan-time mode.
+template <int IPT, int MODE>
+__device__ __forceinline__ void reduce_tile(const TileArgs &a, SpmvSmem<IPT> &sm, int t, int r0, int n0, int nrows,
+                                            int nnzt, double beta, double &dot)
+{
+    const int mode = a.rmode[t];
+    if (mode == 0)
+        walk_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, beta, dot);
+    else
+        group_tile<IPT, MODE>(a, sm, t, r0, nrows, nnzt, beta, dot, mode - 1);
 }
 
 // CG epilogue of the single-RHS tile kernels: this block's p.Ap partial -> partials[slot];
@@ -415,11 +526,12 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
         else
             stage_products<MAXJ, CG, NT>(a, n0, nnzt, beta, sm.prod);
     }
+    int *rend = sm.rowend(nnzt);
     for (int i = tid; i < nrows; i += kBlock)
-        sm.rowend[i] = a.row_offsets[r0 + 1 + i] - n0;
+        rend[i] = a.row_offsets[r0 + 1 + i] - n0;
     __syncthreads();
     double dot = 0.0;
-    walk_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, beta, dot);
+    reduce_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, beta, dot);
     if (MODE != kModeSpmv)
         cg_alpha_epilogue<IPT, MODE>(a, sm, t, a.num_tiles, dot);
 }
@@ -507,12 +619,13 @@ __global__ __launch_bounds__(kBlock) void k_spmv_persist(TileArgs a, int tpb)
                     sm.prod[pslot(k)] = a.vals[n0 + k] * x;
                 }
             }
+            int *rend = sm.rowend(nnzt);
             if (tid < nrows)
-                sm.rowend[tid] = re0 - n0;
+                rend[tid] = re0 - n0;
             for (int i = kBlock + tid; i < nrows; i += kBlock)  // rare: > 256 rows in the tile
-                sm.rowend[i] = a.row_offsets[r0 + 1 + i] - n0;
+                rend[i] = a.row_offsets[r0 + 1 + i] - n0;
             __syncthreads();
-            walk_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, beta, dot);
+            reduce_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, beta, dot);
 #pragma unroll
             for (int j = 0; j < IPT; ++j) {
                 c[j] = cn[j];
@@ -1157,8 +1270,9 @@ constexpr int kIptgSpmm = 8;  // items per lane group for SpMM tiles
 struct SpmvTuning {
     int ipt = 8;
     int nt = 1;
-    int persist = 1;  // persistent software-pipelined kernel
+    int persist = 0;  // persistent software-pipelined kernel (VGPR-bound at 4 waves/SIMD: slower)
     int bpc = 0;      // resident workgroups per CU for the persistent grid (0: occupancy query)
+    int rg_cost = 48; // k_tile_modes budget for row-group tiles (0: merge walk everywhere)
 };
 static const SpmvTuning &spmv_tuning()
 {
@@ -1175,9 +1289,21 @@ static const SpmvTuning &spmv_tuning()
             v.persist = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMV_BPC"))
             v.bpc = atoi(e);
+        if (const char *e = getenv("MSPMV_SPMV_RG_COST"))
+            v.rg_cost = atoi(e);
         return v;
     }();
     return t;
+}
+
+const char *spmv_kernel_name()
+{
+    static std::string name = [] {
+        const SpmvTuning &t = spmv_tuning();
+        return std::string(t.persist ? "k_spmv_persist<" : "k_spmv_tile<") + std::to_string(t.ipt) + ",0," +
+               (t.nt ? "true>" : "false>");
+    }();
+    return name.c_str();
 }
 
 int tile_items_for(int L)
@@ -1207,6 +1333,19 @@ hipError_t launch_snap(const int *d_row_offsets, int m, int2 *d_bounds, unsigned
     return hipGetLastError();
 }
 
+hipError_t launch_tile_modes(const int *d_row_offsets, const int2 *d_bounds, const unsigned char *d_split,
+                             int num_tiles, unsigned char *d_modes, hipStream_t s)
+{
+    if (num_tiles == 0)
+        return hipSuccess;
+    // Plans are shared by tile size across L; only the single-RHS kernels read the modes
+    // (SpMM tiles always walk), so they are always priced for those.
+    const int cost = spmv_tuning().rg_cost;
+    hipLaunchKernelGGL(k_tile_modes, dim3((num_tiles + 255) / 256), dim3(256), 0, s, d_row_offsets, d_bounds, d_split,
+                       num_tiles, cost, d_modes);
+    return hipGetLastError();
+}
+
 static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double *X, double *Y)
 {
     TileArgs a{};
@@ -1217,6 +1356,7 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
     a.y = Y;
     a.bounds = plan.d_bounds;
     a.split = plan.d_split;
+    a.rmode = plan.d_modes;
     a.carry_val = plan.d_carry_val;
     a.num_tiles = plan.num_tiles;
     return a;

@@ -86,6 +86,8 @@ _SIGS = {
     "mspmv_time_spmm_batch_dev": (_I, [_I, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _I,
                                        _PD, _PD, _PI]),
     "mspmv_tile_plan": (_I, [_P, _I, _PI, _PI, _PI, ctypes.POINTER(Coord)]),
+    "mspmv_tile_modes": (_I, [_P, _I, _P]),
+    "mspmv_spmv_kernel_name": (ctypes.c_char_p, []),
     "mspmv_device_malloc": (_I, [_I, _SZ, ctypes.POINTER(_P)]),
     "mspmv_device_free": (_I, [_P]),
     "mspmv_memcpy_h2d": (_I, [_P, _P, _SZ]),
@@ -336,7 +338,10 @@ class GpuCsr:
         b = (Coord * (nt.value + 1))()
         _check(lib.mspmv_tile_plan(self.h, L, None, None, None, b), "tile_plan")
         bounds = np.ctypeslib.as_array(b).view(np.int32).reshape(nt.value + 1, 2).copy()
-        return {"num_tiles": nt.value, "tile_items": ti.value, "num_carries": nc.value, "bounds": bounds}
+        modes = np.zeros(max(nt.value, 1), np.uint8)
+        _check(lib.mspmv_tile_modes(self.h, L, _ptr(modes)), "tile_modes")
+        return {"num_tiles": nt.value, "tile_items": ti.value, "num_carries": nc.value, "bounds": bounds,
+                "modes": modes[: nt.value]}
 
     def spmv(self, x: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(x, np.float64)

@@ -10,13 +10,16 @@ def groups_per_tile(L):
 
 
 def unsplit_rows(a, plan, L):
-    """Rows whose merge items (nonzeros + row end) fall in ONE walker of ONE tile.
+    """Rows the kernel sums sequentially in CSR order from 0.0, i.e. bit-identically to
+    SpmvGold (cpu_spmv.cpp:241-265).
 
-    Mirrors the kernel's partition exactly: tile t spans plan bounds t..t+1; its walkers take
-    ceil(items / groups) consecutive diagonals each.  Such rows are summed sequentially in CSR
-    order from 0.0, i.e. bit-identically to SpmvGold (cpu_spmv.cpp:241-265).
+    Mirrors the kernel's partition exactly: tile t spans plan bounds t..t+1.  A merge-walk tile
+    (mode 0) gives its walkers ceil(items / groups) consecutive diagonals each, and a row is
+    sequential when all its items fall in one walker.  A row-group tile (mode g > 0, groups of
+    2^(g-1) lanes) is sequential for its whole rows only when g == 1 (one row per thread).
     """
     bounds = plan["bounds"]
+    modes = plan.get("modes")
     ng = groups_per_tile(L)
     ro = a.row_offsets.astype(np.int64)
     mask = np.zeros(a.num_rows, bool)
@@ -26,12 +29,16 @@ def unsplit_rows(a, plan, L):
         nrows = r1 - r0
         if nrows <= 0:
             continue
-        items = nrows + (n1 - n0)
-        ipt = -(-items // ng)
         r = np.arange(nrows)
         rs = ro[r0 + r] - n0
         re = ro[r0 + r + 1] - n0
-        ok = (rs >= 0) & ((r + rs) // ipt == (r + re) // ipt)
+        mode = int(modes[t]) if modes is not None and len(modes) else 0
+        if mode == 0:
+            items = nrows + (n1 - n0)
+            ipt = -(-items // ng)
+            ok = (rs >= 0) & ((r + rs) // ipt == (r + re) // ipt)
+        else:
+            ok = (rs >= 0) & (mode == 1)
         mask[r0 + r] = ok
     return mask
 

@@ -92,6 +92,30 @@ def test_spmv_synthetic(orc, name):
         assert nb > 0.3 * n
 
 
+def test_tile_modes_cover_both_reductions(orc):
+    """k_tile_modes: short uniform rows -> one row per thread (mode 1, bit-exact whole rows);
+    long uniform rows -> wider row groups; skewed tiles -> the merge walk (mode 0); SpMM
+    plans always walk.  Parity holds on every mix."""
+    fem = mspmv.CsrMatrix.synth_stencil(0, 40000, 200, 0, 0, seed=3)
+    blk = mspmv.CsrMatrix.synth_fem_blocked(20000, 1000000, 6, 300, seed=2)
+    skew = mspmv.CsrMatrix.synth_powerlaw(50000, 50000, 1500000, exponent=1.8, seed=4)
+    for a, want in ((fem, {1}), (blk, None), (skew, None)):
+        x = np.random.default_rng(8).uniform(-1, 1, a.num_cols)
+        with mspmv.GpuCsr(a) as g:
+            plan = g.tile_plan(1)
+            modes = set(np.unique(plan["modes"]).tolist())
+            if want is not None:
+                assert modes == want, modes
+            if a is blk:
+                assert min(modes) >= 3, modes     # ~50 nnz rows: groups of >= 4 lanes
+            if a is skew:
+                assert 0 in modes, modes          # hub rows: merge walk
+            assert not np.any(g.tile_plan(4)["modes"])
+            nb, n = check_parity(a, g.spmv(x), orc.spmv_gold(a, x), x, plan, 1)
+            if a is fem:
+                assert nb >= n - 2 * plan["num_tiles"]   # all rows held whole by a tile
+
+
 @pytest.mark.parametrize("name", ["cant_small", "powerlaw", "fem2d", "powerlaw_rect"])
 @pytest.mark.parametrize("L", [1, 2, 4, 8, 16])
 def test_spmm_synthetic(orc, name, L):

@@ -4,7 +4,7 @@
     python tools/spmv_sweep.py                 # parent: runs every variant in child processes
     python tools/spmv_sweep.py --child         # child: one timing line for the env's variant
 
-Variants are selected with MSPMV_SPMV_IPT / MSPMV_SPMV_NT (read once per process), so each
+Variants are selected with MSPMV_SPMV_IPT / _NT / _PERSIST / _BPC / _RG_COST (read once per process), so each
 runs in its own process; rounds alternate variants to spread device drift.
 """
 import json
@@ -22,8 +22,11 @@ def child():
     B = int(os.environ.get("SWEEP_BATCH", "4"))
     gs, dx, dy = [], [], []
     for i in range(B):
-        if os.environ.get("SWEEP_SHAPE", "fem") == "fem":
+        shape = os.environ.get("SWEEP_SHAPE", "fem")
+        if shape == "fem":
             a = mspmv.CsrMatrix.synth_fem_blocked(217918, 11524432, 6, 1700, seed=1 + i)
+        elif shape == "powerlaw":
+            a = mspmv.CsrMatrix.synth_powerlaw(1 << 20, 1 << 20, 11524432, 1.8, seed=1 + i)
         else:
             a = mspmv.CsrMatrix.synth_banded(217918, 11524432, 10000, seed=1 + i)
         gs.append(mspmv.GpuCsr(a))
@@ -32,22 +35,25 @@ def child():
     mspmv.time_spmm_batch(gs, dx, dy, 1, 5)
     step, kern, _ = mspmv.time_spmm_batch(gs, dx, dy, 1, 50)
     hot_step, hot_kern, _ = mspmv.time_spmm_batch(gs[:1], dx[:1], dy[:1], 1, 200)
-    nbytes = 12 * 11524432 + 4 * 217919 + 16 * 217918
+    a0 = gs[0]
+    nbytes = 12 * a0.num_nonzeros + 4 * (a0.num_rows + 1) + 8 * (a0.num_rows + a0.num_cols)
+    modes = np.bincount(a0.tile_plan(1)["modes"], minlength=8).tolist()
     print(json.dumps({"ipt": os.environ.get("MSPMV_SPMV_IPT"), "nt": os.environ.get("MSPMV_SPMV_NT"),
                       "persist": os.environ.get("MSPMV_SPMV_PERSIST"), "bpc": os.environ.get("MSPMV_SPMV_BPC"),
+                      "rg": os.environ.get("MSPMV_SPMV_RG_COST"), "modes": modes,
                       "cold_kernel_us": round(kern * 1e3, 2), "cold_GBps": round(nbytes / kern / 1e6, 1),
                       "step_us": round(step * 1e3, 2), "hot_kernel_us": round(hot_kern * 1e3, 2),
                       "hot_GBps": round(nbytes / hot_kern / 1e6, 1)}), flush=True)
 
 
 def parent():
-    spec = os.environ.get("SWEEP_VARIANTS", "4:1:0:0,8:1:0:0,4:1:1:0,8:1:1:0")   # ipt:nt:persist:bpc
-    variants = [tuple(int(x) for x in v.split(":")) for v in spec.split(",")]
+    spec = os.environ.get("SWEEP_VARIANTS", "8:1:1:0:0,8:1:1:0:48")   # ipt:nt:persist:bpc[:rg_cost]
+    variants = [tuple(int(x) for x in (v + ":48").split(":")[:5]) for v in spec.split(",")]
     rounds = int(os.environ.get("SWEEP_ROUNDS", "2"))
     for r in range(rounds):
-        for ipt, nt, persist, bpc in variants:
+        for ipt, nt, persist, bpc, rg in variants:
             env = dict(os.environ, MSPMV_SPMV_IPT=str(ipt), MSPMV_SPMV_NT=str(nt), MSPMV_SPMV_PERSIST=str(persist),
-                       MSPMV_SPMV_BPC=str(bpc))
+                       MSPMV_SPMV_BPC=str(bpc), MSPMV_SPMV_RG_COST=str(rg))
             out = subprocess.run([sys.executable, __file__, "--child"], env=env, capture_output=True, text=True,
                                  timeout=300)
             if out.returncode != 0:
