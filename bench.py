@@ -41,6 +41,26 @@ import mspmv  # noqa: E402
 
 METRIC = "fp64 SpMV GFLOP/s + achieved HBM GB/s vs roofline; CG iters/sec"
 HBM_PEAK_GBS = 8000.0
+
+
+def pmc_traffic(kernel, bytes_launch):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from separate rocprofv3
+    --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command), or None when no summary
+    matches this kernel instantiation and workload size."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if d.get("bench_bytes_per_launch") != bytes_launch:
+            continue
+        for name, v in d.get("kernels", {}).items():
+            short = name.replace("void mspmv::", "").split("(")[0].replace(" ", "")
+            if short == kernel:
+                return v["traffic_bytes"], os.path.basename(path)
+    return None, None
 PWTK = dict(m=217918, nnz=11524432, block=6, half_band_nodes=1700)
 PARABOLIC_FEM = dict(m=525825, width=725, shift=1e-4)
 NLPKKT120 = dict(dims=(160, 135, 164), shift=1e-2, L=8)
@@ -248,6 +268,8 @@ def main():
     bytes_launch = spmv_bytes(a0.num_rows, a0.num_cols, a0.num_nonzeros)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     hot_ms, hot_kern, _ = mspmv.time_spmm_batch(gs[:1], dxs[:1], dys[:1], 1, 200)
+    kname = mspmv.lib.mspmv_spmv_kernel_name().decode()
+    traffic, traffic_src = pmc_traffic(kname, bytes_launch)
     ref_eff = (a0.num_nonzeros * 20 + a0.num_rows * 12) / (kern_ms * 1e-3) / 1e9  # cpu_spmv.cpp:722-726
 
     result = {
@@ -260,8 +282,9 @@ def main():
                    "m": a0.num_rows, "nnz": a0.num_nonzeros, "batch": args.batch,
                    "parallelism": f"independent SpMV batches, {d.world} GPU(s)"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": mspmv.lib.mspmv_spmv_kernel_name().decode(), "bytes_per_launch": bytes_launch,
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
+                     "kernel": kname, "bytes_per_launch": bytes_launch,
                      "kernel_ms": round(kern_ms, 5), "kernels_per_step": kps},
         "spmv_gflops_per_launch": round(2.0 * a0.num_nonzeros / (kern_ms * 1e-3) / 1e9, 2),
         "reference_effective_GBps": round(ref_eff, 1),
