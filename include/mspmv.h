@@ -158,9 +158,10 @@ MSPMV_API mspmv_status mspmv_last_kernel_ms(mspmv_handle h, double *tile_kernel_
  * bit-identical to SpmvGold). */
 MSPMV_API mspmv_status mspmv_tile_plan(mspmv_handle h, int L, int *num_tiles, int *tile_items, int *num_carries,
                                        mspmv_coord *bounds);
-/* Each tile's in-tile reduction (num_tiles entries): 0 = per-thread merge walk, g > 0 = row
- * groups of 2^(g-1) lanes (g = 1: one row per thread, summed in CSR order -> bit-identical to
- * SpmvGold for rows the tile holds whole).  Always 0 for L > 1. */
+/* Each tile's in-tile reduction for L right-hand sides (num_tiles entries): 0 = merge walk
+ * (one walker per thread, or per L/2 lanes), g > 0 = row groups with 2^(g-1) nonzero-parallel
+ * lanes per row (times L/2 column-pair lanes for L > 1).  g = 1 sums each row sequentially in
+ * CSR order -> bit-identical to SpmvGold / the row-split SpMM for rows the tile holds whole. */
 MSPMV_API mspmv_status mspmv_tile_modes(mspmv_handle h, int L, unsigned char *modes);
 /* The single-RHS SpMV kernel instantiation this process launches (tuning read once from the
  * MSPMV_SPMV_* environment), e.g. "k_spmv_tile<8,0,true>" -- the name rocprofv3 reports. */

@@ -79,7 +79,8 @@ static void free_plan(TilePlan &p)
 {
     dev_free(p.d_bounds);
     dev_free(p.d_split);
-    dev_free(p.d_modes);
+    for (auto &m : p.d_modes)
+        dev_free(m);
     dev_free(p.d_carry_tiles);
     dev_free(p.d_carry_rows);
     dev_free(p.d_carry_val);
@@ -88,14 +89,50 @@ static void free_plan(TilePlan &p)
 // Build (once) the tile plan for L right-hand sides, validating on the host every bound the
 // kernels rely on (monotone boundaries, <= 1.25 * tile_items merge items per tile) before any
 // tile kernel can run on it.
+static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out);
+
+// The in-tile reduction modes of a plan for L right-hand sides, built on first use.
+static mspmv_status ensure_modes(mspmv_handle_s *h, TilePlan &p, int L)
+{
+    unsigned char *&m = p.d_modes[l_index(L)];
+    if (m)
+        return MSPMV_OK;
+    mspmv_status st = dev_alloc(&m, (size_t)std::max(p.num_tiles, 1));
+    if (st != MSPMV_OK)
+        return st;
+    hipError_t e = launch_tile_modes(h->d_row_offsets, p.d_bounds, p.d_split, p.num_tiles, L, m, h->stream);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) {
+        set_error(std::string("tile modes: ") + hipGetErrorString(e));
+        dev_free(m);
+        m = nullptr;
+        return MSPMV_ERR_HIP;
+    }
+    return MSPMV_OK;
+}
+
 static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out)
 {
     const int tile = tile_items_for(L);
     auto it = h->plans.find(tile);
-    if (it != h->plans.end()) {
-        *out = &it->second;
-        return MSPMV_OK;
+    if (it == h->plans.end()) {
+        const TilePlan *np = nullptr;
+        mspmv_status st = build_plan(h, L, &np);
+        if (st != MSPMV_OK)
+            return st;
+        it = h->plans.find(tile);
     }
+    mspmv_status st = ensure_modes(h, it->second, L);
+    if (st != MSPMV_OK)
+        return st;
+    *out = &it->second;
+    return MSPMV_OK;
+}
+
+static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
+{
+    const int tile = tile_items_for(L);
     TilePlan p;
     p.tile_items = tile;
     p.snap = tile / kSnapDiv;
@@ -105,7 +142,6 @@ static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out)
     mspmv_status st;
     if ((st = dev_alloc(&p.d_bounds, (size_t)T + 1)) != MSPMV_OK ||
         (st = dev_alloc(&p.d_split, (size_t)T + 1)) != MSPMV_OK ||
-        (st = dev_alloc(&p.d_modes, (size_t)std::max(T, 1))) != MSPMV_OK ||
         (st = dev_alloc(&p.d_carry_val, (size_t)std::max(T, 1) * 16)) != MSPMV_OK) {
         free_plan(p);
         return st;
@@ -118,8 +154,6 @@ static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out)
     hipError_t e = launch_merge_coords(h->d_row_offsets, h->m, h->nnz, tile, T, p.d_bounds, h->stream);
     if (e == hipSuccess)
         e = launch_snap(h->d_row_offsets, h->m, p.d_bounds, p.d_split, T, p.snap, h->stream);
-    if (e == hipSuccess)
-        e = launch_tile_modes(h->d_row_offsets, p.d_bounds, p.d_split, T, p.d_modes, h->stream);
     std::vector<int2> hb((size_t)T + 1);
     std::vector<unsigned char> hs((size_t)T + 1);
     if (e == hipSuccess)
@@ -871,10 +905,8 @@ mspmv_status mspmv_tile_modes(mspmv_handle h, int L, unsigned char *modes)
         return invalid("null modes");
     const TilePlan *plan = nullptr;
     ST_TRY(get_plan(h, L, &plan));
-    if (L > 1)  // the SpMM kernels always walk
-        memset(modes, 0, (size_t)plan->num_tiles);
-    else if (plan->num_tiles)
-        HIP_TRY(hipMemcpy(modes, plan->d_modes, plan->num_tiles, hipMemcpyDeviceToHost));
+    if (plan->num_tiles)
+        HIP_TRY(hipMemcpy(modes, plan->d_modes[l_index(L)], plan->num_tiles, hipMemcpyDeviceToHost));
     return MSPMV_OK;
 }
 

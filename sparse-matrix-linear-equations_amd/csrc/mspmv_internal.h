@@ -30,7 +30,9 @@ struct TilePlan {
     int num_tiles = 0;
     int2 *d_bounds = nullptr;           // [num_tiles+1] (row, nnz) boundary coordinates
     unsigned char *d_split = nullptr;   // [num_tiles+1] 1 = split boundary (carry crosses it)
-    unsigned char *d_modes = nullptr;   // [num_tiles] in-tile reduction: 0 walk, lg+1 row groups of 2^lg
+    // [log2 L][num_tiles] in-tile reduction per right-hand-side count (plans are shared by
+    // tile size across L): 0 merge walk, lg+1 row groups of 2^lg nonzero lanes (k_tile_modes)
+    unsigned char *d_modes[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     int num_carries = 0;                // tiles whose trailing boundary is split
     int *d_carry_tiles = nullptr;       // [num_carries] tile ids, ascending
     int *d_carry_rows = nullptr;        // [num_carries] row each carry belongs to
@@ -98,7 +100,8 @@ void set_error(const std::string &msg);
 hipError_t launch_merge_coords(const int *d_row_offsets, int m, int nnz, long long diag_step, int num_parts,
                                int2 *d_out, hipStream_t s);
 hipError_t launch_tile_modes(const int *d_row_offsets, const int2 *d_bounds, const unsigned char *d_split,
-                             int num_tiles, unsigned char *d_modes, hipStream_t s);
+                             int num_tiles, int L, unsigned char *d_modes, hipStream_t s);
+inline int l_index(int L) { return L == 1 ? 0 : L == 2 ? 1 : L == 4 ? 2 : L == 8 ? 3 : 4; }
 hipError_t launch_snap(const int *d_row_offsets, int m, int2 *d_bounds, unsigned char *d_split, int num_tiles,
                        int snap, hipStream_t s);
 // y = A x (L == 1) or Y = A X (row-major panels), tile kernel + optional carry fix-up.

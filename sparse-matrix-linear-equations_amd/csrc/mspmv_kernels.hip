@@ -153,15 +153,15 @@ __global__ void k_snap(const int *__restrict__ row_offsets, int m, int2 *__restr
     split[t] = s;
 }
 
-// Per-tile choice of the in-tile reduction of the single-RHS kernels (one thread per tile, at
-// plan time).  The tile's row segments -- its complete rows plus the trailing partial row of a
+// Per-tile choice of the in-tile reduction (one thread per tile, at plan time; gl = lanes per
+// nonzero: 1 for SpMV, L/2 column-pair lanes for SpMM).  The tile's row segments -- its complete rows plus the trailing partial row of a
 // split boundary -- are either summed by row groups of G = 2^lg lanes (mode lg + 1) or, when
 // segment lengths are too uneven for that, by the per-thread merge walk (mode 0).  Cost model
 // in LDS-read steps of the slowest group: ceil(segments / groups) rounds of ceil(longest / G)
 // reads plus a log2(G)-step shuffle fold; the cheapest G wins if its cost is within max_cost
 // (the walk costs about IPT reads plus an 11-step search and two more barriers).
 __global__ void k_tile_modes(const int *__restrict__ row_offsets, const int2 *__restrict__ bounds,
-                             const unsigned char *__restrict__ split, int num_tiles, int max_cost,
+                             const unsigned char *__restrict__ split, int num_tiles, int gl, int max_cost,
                              unsigned char *__restrict__ modes)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -180,8 +180,8 @@ __global__ void k_tile_modes(const int *__restrict__ row_offsets, const int2 *__
     if (tail)
         longest = max(longest, b1.y - prev);
     int best = 0, best_cost = max_cost + 1;
-    for (int lg = 0; lg <= 6; ++lg) {
-        const int groups = kBlock >> lg, G = 1 << lg;
+    for (int lg = 0; (gl << lg) <= 64; ++lg) {  // a row group stays inside one wave
+        const int groups = kBlock / (gl << lg), G = 1 << lg;
         const int cost = ((nseg + groups - 1) / groups) * ((longest + G - 1) / G + 3 * lg);
         if (cost < best_cost) {
             best_cost = cost;
@@ -639,6 +639,87 @@ __global__ __launch_bounds__(kBlock) void k_spmv_persist(TileArgs a, int tpb)
         cg_alpha_epilogue<IPT, MODE>(a, sm, blockIdx.x, gridDim.x, dot);
 }
 
+// Row-group reduction of one multi-RHS tile (mode lgp + 1): a row group is GL column-pair
+// lanes x Gp = 2^lgp nonzero lanes.  Lane (c, j) of a group sums, for its columns 2c, 2c+1,
+// the products of nonzeros j, j+Gp, ... of the row in order from 0.0 (four panel-row gathers
+// in flight), a fixed xor butterfly over j folds the group, and j = 0 writes the row.
+// Gp = 1 is the row-by-row CSR-order sum of the reference's row-split SpMM, bit for bit.
+template <int L, int MODE>
+__device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_col, const double *s_val,
+                                                const int *rend, int t, int r0, int nrows, int nnzt,
+                                                double2 beta2, double2 &dot, int lgp)
+{
+    constexpr bool CG = MODE == kModeCg;
+    constexpr int GL = L / 2;
+    const int Gp = 1 << lgp;
+    const int tid = threadIdx.x;
+    const int lane = tid % GL;
+    const int sub = (tid / GL) & (Gp - 1);
+    const int W = GL << lgp;
+    const bool tail = a.split[t + 1] != 0;
+    const int nseg = nrows + (tail ? 1 : 0);
+    auto panel = [&](int c) {
+        double2 xv = *reinterpret_cast<const double2 *>(a.x + (size_t)c * L + 2 * lane);
+        if (CG) {
+            const double2 po = *reinterpret_cast<const double2 *>(a.p_old + (size_t)c * L + 2 * lane);
+            xv.x = xv.x + beta2.x * po.x;
+            xv.y = xv.y + beta2.y * po.y;
+        }
+        return xv;
+    };
+    for (int r = tid / W; r < nseg; r += kBlock / W) {  // uniform within a group
+        const int s0 = r == 0 ? 0 : rend[r - 1];
+        const int e = r < nrows ? rend[r] : nnzt;
+        double2 acc = make_double2(0.0, 0.0);
+        int k = s0 + sub;
+        for (; k + 3 * Gp < e; k += 4 * Gp) {
+            const int c0 = s_col[k], c1 = s_col[k + Gp], c2 = s_col[k + 2 * Gp], c3 = s_col[k + 3 * Gp];
+            const double v0 = s_val[k], v1 = s_val[k + Gp], v2 = s_val[k + 2 * Gp], v3 = s_val[k + 3 * Gp];
+            const double2 x0 = panel(c0), x1 = panel(c1), x2 = panel(c2), x3 = panel(c3);
+            acc.x += v0 * x0.x;
+            acc.y += v0 * x0.y;
+            acc.x += v1 * x1.x;
+            acc.y += v1 * x1.y;
+            acc.x += v2 * x2.x;
+            acc.y += v2 * x2.y;
+            acc.x += v3 * x3.x;
+            acc.y += v3 * x3.y;
+        }
+        for (; k < e; k += Gp) {
+            const double v = s_val[k];
+            const double2 xv = panel(s_col[k]);
+            acc.x += v * xv.x;
+            acc.y += v * xv.y;
+        }
+        for (int off = Gp >> 1; off > 0; off >>= 1) {
+            acc.x += __shfl_xor(acc.x, off * GL);
+            acc.y += __shfl_xor(acc.y, off * GL);
+        }
+        if (sub == 0) {
+            const size_t off = (size_t)(r0 + r) * L + 2 * lane;
+            if (r < nrows)
+                *reinterpret_cast<double2 *>(a.y + off) = acc;
+            else  // the trailing partial row -> carry (k_fixup adds it in tile order)
+                *reinterpret_cast<double2 *>(a.carry_val + (size_t)t * L + 2 * lane) = acc;
+            if (CG) {
+                const double2 rr = *reinterpret_cast<const double2 *>(a.x + off);
+                const double2 po = *reinterpret_cast<const double2 *>(a.p_old + off);
+                double2 pn;
+                pn.x = rr.x + beta2.x * po.x;
+                pn.y = rr.y + beta2.y * po.y;
+                if (r < nrows)
+                    *reinterpret_cast<double2 *>(a.p_new + off) = pn;
+                dot.x += pn.x * acc.x;
+                dot.y += pn.y * acc.y;
+            } else if (MODE == kModeDot) {
+                const double2 xx = *reinterpret_cast<const double2 *>(a.x + off);
+                dot.x += xx.x * acc.x;
+                dot.y += xx.y * acc.y;
+            }
+        }
+    }
+}
+
 // Multi right-hand side (L = 2..16, row-major panels).  A group of L/2 lanes owns one merge
 // walk; each lane keeps a double2 of the L running totals (running_total[L],
 // merge_based.hpp:84-127).  TILE = (256/(L/2)) groups * IPTG items.
@@ -688,6 +769,11 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
     }
     __syncthreads();
 
+    double2 dot = make_double2(0.0, 0.0);
+    const int rmode = a.rmode[t];
+    if (rmode != 0) {
+        spmm_group_rows<L, MODE>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, beta2, dot, rmode - 1);
+    } else {
     const int ipt = (items + NG - 1) / NG;
     const int d0 = min(g * ipt, items);
     const int d1 = min(d0 + ipt, items);
@@ -696,34 +782,6 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
     lds_search(d1, s_rowend, nrows, nnzt, ex, ey);
     const bool need_cin = (cx < ex) && (cy > (cx == 0 ? 0 : s_rowend[cx - 1]));
 
-    // Gather this walk's panel rows up front (<= MAXJ independent 16-B loads in flight).
-    double2 xr[MAXJ];
-    double vv[MAXJ];
-    if (ey > cy) {  // branch-free gather of every panel row this walk needs (clamped)
-        int cc[MAXJ];
-#pragma unroll
-        for (int j = 0; j < MAXJ; ++j) {
-            const int k = min(cy + j, ey - 1);
-            cc[j] = s_col[k];
-            vv[j] = s_val[k];
-        }
-#pragma unroll
-        for (int j = 0; j < MAXJ; ++j)
-            xr[j] = *reinterpret_cast<const double2 *>(a.x + (size_t)cc[j] * L + 2 * lane);
-        if (CG) {
-            double2 po[MAXJ];
-#pragma unroll
-            for (int j = 0; j < MAXJ; ++j)
-                po[j] = *reinterpret_cast<const double2 *>(a.p_old + (size_t)cc[j] * L + 2 * lane);
-#pragma unroll
-            for (int j = 0; j < MAXJ; ++j) {
-                xr[j].x = xr[j].x + beta2.x * po[j].x;
-                xr[j].y = xr[j].y + beta2.y * po[j].y;
-            }
-        }
-    }
-
-    double2 dot = make_double2(0.0, 0.0);
     auto write_row = [&](int row, double2 val) {
         const size_t off = (size_t)(r0 + row) * L + 2 * lane;
         *reinterpret_cast<double2 *>(a.y + off) = val;
@@ -747,24 +805,53 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
     bool first = true, pend = false;
     int prow = 0;
     double2 pval = make_double2(0.0, 0.0);
+    // The walk in chunks of WJ items: each chunk's panel rows are gathered together (WJ
+    // independent 16-B loads in flight, indices clamped so every load is issued), then walked.
+    constexpr int WJ = 4;
 #pragma unroll
-    for (int j = 0; j < MAXJ; ++j) {
-        const int k = cy + j;
-        if (k < ey) {
-            while (cx < ex && s_rowend[cx] <= k) {
-                if (first && need_cin) {
-                    pend = true;
-                    prow = cx;
-                    pval = run;
-                } else {
-                    write_row(cx, run);
-                }
-                first = false;
-                run = make_double2(0.0, 0.0);
-                ++cx;
+    for (int j0 = 0; j0 < MAXJ; j0 += WJ) {
+        if (cy + j0 >= ey)
+            break;
+        double2 xr[WJ];
+        double vv[WJ];
+#pragma unroll
+        for (int jj = 0; jj < WJ; ++jj) {
+            const int k = min(cy + j0 + jj, ey - 1);
+            vv[jj] = s_val[k];
+            xr[jj] = *reinterpret_cast<const double2 *>(a.x + (size_t)s_col[k] * L + 2 * lane);
+        }
+        if (CG) {
+            double2 po[WJ];
+#pragma unroll
+            for (int jj = 0; jj < WJ; ++jj) {
+                const int k = min(cy + j0 + jj, ey - 1);
+                po[jj] = *reinterpret_cast<const double2 *>(a.p_old + (size_t)s_col[k] * L + 2 * lane);
             }
-            run.x += vv[j] * xr[j].x;
-            run.y += vv[j] * xr[j].y;
+#pragma unroll
+            for (int jj = 0; jj < WJ; ++jj) {
+                xr[jj].x = xr[jj].x + beta2.x * po[jj].x;
+                xr[jj].y = xr[jj].y + beta2.y * po[jj].y;
+            }
+        }
+#pragma unroll
+        for (int jj = 0; jj < WJ; ++jj) {
+            const int k = cy + j0 + jj;
+            if (j0 + jj < MAXJ && k < ey) {
+                while (cx < ex && s_rowend[cx] <= k) {
+                    if (first && need_cin) {
+                        pend = true;
+                        prow = cx;
+                        pval = run;
+                    } else {
+                        write_row(cx, run);
+                    }
+                    first = false;
+                    run = make_double2(0.0, 0.0);
+                    ++cx;
+                }
+                run.x += vv[jj] * xr[jj].x;
+                run.y += vv[jj] * xr[jj].y;
+            }
         }
     }
     while (cx < ex) {
@@ -822,6 +909,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
             dot.y += xx.y * acc.y;
         }
     }
+    }  // merge walk
 
     if (MODE != kModeSpmv) {
         // Reduce the per-lane column partials over the groups (lanes with equal tid % GL).
@@ -1273,6 +1361,7 @@ struct SpmvTuning {
     int persist = 0;  // persistent software-pipelined kernel (VGPR-bound at 4 waves/SIMD: slower)
     int bpc = 0;      // resident workgroups per CU for the persistent grid (0: occupancy query)
     int rg_cost = 48; // k_tile_modes budget for row-group tiles (0: merge walk everywhere)
+    int spmm_rg_cost = 48;  // the same for the multi-RHS kernels
 };
 static const SpmvTuning &spmv_tuning()
 {
@@ -1291,6 +1380,8 @@ static const SpmvTuning &spmv_tuning()
             v.bpc = atoi(e);
         if (const char *e = getenv("MSPMV_SPMV_RG_COST"))
             v.rg_cost = atoi(e);
+        if (const char *e = getenv("MSPMV_SPMM_RG_COST"))
+            v.spmm_rg_cost = atoi(e);
         return v;
     }();
     return t;
@@ -1334,19 +1425,17 @@ hipError_t launch_snap(const int *d_row_offsets, int m, int2 *d_bounds, unsigned
 }
 
 hipError_t launch_tile_modes(const int *d_row_offsets, const int2 *d_bounds, const unsigned char *d_split,
-                             int num_tiles, unsigned char *d_modes, hipStream_t s)
+                             int num_tiles, int L, unsigned char *d_modes, hipStream_t s)
 {
     if (num_tiles == 0)
         return hipSuccess;
-    // Plans are shared by tile size across L; only the single-RHS kernels read the modes
-    // (SpMM tiles always walk), so they are always priced for those.
-    const int cost = spmv_tuning().rg_cost;
+    const int cost = L == 1 ? spmv_tuning().rg_cost : spmv_tuning().spmm_rg_cost;
     hipLaunchKernelGGL(k_tile_modes, dim3((num_tiles + 255) / 256), dim3(256), 0, s, d_row_offsets, d_bounds, d_split,
-                       num_tiles, cost, d_modes);
+                       num_tiles, L == 1 ? 1 : L / 2, cost, d_modes);
     return hipGetLastError();
 }
 
-static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double *X, double *Y)
+static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double *X, double *Y, int L)
 {
     TileArgs a{};
     a.row_offsets = h->d_row_offsets;
@@ -1356,7 +1445,7 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
     a.y = Y;
     a.bounds = plan.d_bounds;
     a.split = plan.d_split;
-    a.rmode = plan.d_modes;
+    a.rmode = plan.d_modes[l_index(L)];
     a.carry_val = plan.d_carry_val;
     a.num_tiles = plan.num_tiles;
     return a;
@@ -1430,7 +1519,7 @@ hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const 
 {
     if (plan.num_tiles == 0)
         return hipSuccess;
-    return launch_tile<kModeSpmv>(make_args(h, plan, d_X, d_Y), L, h->stream, h->num_cus);
+    return launch_tile<kModeSpmv>(make_args(h, plan, d_X, d_Y, L), L, h->stream, h->num_cus);
 }
 
 hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L)
@@ -1509,7 +1598,7 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *
 {
     double *p_old = parity ? h->d_p1 : h->d_p0;
     double *p_new = parity ? h->d_p0 : h->d_p1;
-    TileArgs ta = make_args(h, plan, h->d_r, h->d_ap);
+    TileArgs ta = make_args(h, plan, h->d_r, h->d_ap, L);
     ta.p_old = p_old;
     ta.p_new = p_new;
     ta.scal = h->d_scal;
@@ -1586,7 +1675,7 @@ hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double
 {
     if (plan.num_tiles == 0)  // a rank without rows contributes 0 to the all-reduce
         return hipMemsetAsync(dot_out, 0, sizeof(double) * L, h->stream);
-    TileArgs ta = make_args(h, plan, d_X, d_Y);
+    TileArgs ta = make_args(h, plan, d_X, d_Y, L);
     ta.ctrl = ctrl;
     ta.partials = partials;
     ta.dot_out = dot_out;

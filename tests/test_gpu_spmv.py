@@ -110,7 +110,13 @@ def test_tile_modes_cover_both_reductions(orc):
                 assert min(modes) >= 3, modes     # ~50 nnz rows: groups of >= 4 lanes
             if a is skew:
                 assert 0 in modes, modes          # hub rows: merge walk
-            assert not np.any(g.tile_plan(4)["modes"])
+            m4 = g.tile_plan(4)["modes"]
+            if a is skew:
+                assert 0 in set(m4.tolist())
+            if a is blk:
+                assert m4.min() >= 2          # SpMM row groups: 2 column-pair lanes x >= 2
+            X = np.random.default_rng(9).uniform(-1, 1, (a.num_cols, 4))
+            check_parity(a, g.spmm(X), orc.csr_spmm_t(a, X), X, g.tile_plan(4), 4)
             nb, n = check_parity(a, g.spmv(x), orc.spmv_gold(a, x), x, plan, 1)
             if a is fem:
                 assert nb >= n - 2 * plan["num_tiles"]   # all rows held whole by a tile

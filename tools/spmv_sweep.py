@@ -20,27 +20,30 @@ def child():
     import numpy as np
     import mspmv
     B = int(os.environ.get("SWEEP_BATCH", "4"))
+    L = int(os.environ.get("SWEEP_L", "1"))
     gs, dx, dy = [], [], []
     for i in range(B):
         shape = os.environ.get("SWEEP_SHAPE", "fem")
         if shape == "fem":
             a = mspmv.CsrMatrix.synth_fem_blocked(217918, 11524432, 6, 1700, seed=1 + i)
+        elif shape == "nlpkkt":   # nlpkkt120-sized 27-point stencil (the cg_multi workload)
+            a = mspmv.CsrMatrix.synth_stencil(1, 160 * 135 * 164, 160, 135, 164, seed=1 + i, diag_shift=1e-2)
         elif shape == "powerlaw":
             a = mspmv.CsrMatrix.synth_powerlaw(1 << 20, 1 << 20, 11524432, 1.8, seed=1 + i)
         else:
             a = mspmv.CsrMatrix.synth_banded(217918, 11524432, 10000, seed=1 + i)
         gs.append(mspmv.GpuCsr(a))
-        dx.append(mspmv.DeviceBuffer.from_array(np.random.default_rng(i).uniform(0, 1, a.num_cols)))
-        dy.append(mspmv.DeviceBuffer(8 * a.num_rows))
-    mspmv.time_spmm_batch(gs, dx, dy, 1, 5)
-    step, kern, _ = mspmv.time_spmm_batch(gs, dx, dy, 1, 50)
-    hot_step, hot_kern, _ = mspmv.time_spmm_batch(gs[:1], dx[:1], dy[:1], 1, 200)
+        dx.append(mspmv.DeviceBuffer.from_array(np.random.default_rng(i).uniform(0, 1, a.num_cols * L)))
+        dy.append(mspmv.DeviceBuffer(8 * a.num_rows * L))
+    mspmv.time_spmm_batch(gs, dx, dy, L, 5)
+    step, kern, _ = mspmv.time_spmm_batch(gs, dx, dy, L, 50)
+    hot_step, hot_kern, _ = mspmv.time_spmm_batch(gs[:1], dx[:1], dy[:1], L, 200)
     a0 = gs[0]
-    nbytes = 12 * a0.num_nonzeros + 4 * (a0.num_rows + 1) + 8 * (a0.num_rows + a0.num_cols)
-    modes = np.bincount(a0.tile_plan(1)["modes"], minlength=8).tolist()
+    nbytes = 12 * a0.num_nonzeros + 4 * (a0.num_rows + 1) + 8 * L * (a0.num_rows + a0.num_cols)
+    modes = np.bincount(a0.tile_plan(L)["modes"], minlength=8).tolist()
     print(json.dumps({"ipt": os.environ.get("MSPMV_SPMV_IPT"), "nt": os.environ.get("MSPMV_SPMV_NT"),
                       "persist": os.environ.get("MSPMV_SPMV_PERSIST"), "bpc": os.environ.get("MSPMV_SPMV_BPC"),
-                      "rg": os.environ.get("MSPMV_SPMV_RG_COST"), "modes": modes,
+                      "rg": os.environ.get("MSPMV_SPMV_RG_COST"), "L": L, "shape": shape, "modes": modes,
                       "cold_kernel_us": round(kern * 1e3, 2), "cold_GBps": round(nbytes / kern / 1e6, 1),
                       "step_us": round(step * 1e3, 2), "hot_kernel_us": round(hot_kern * 1e3, 2),
                       "hot_GBps": round(nbytes / hot_kern / 1e6, 1)}), flush=True)
@@ -53,7 +56,7 @@ def parent():
     for r in range(rounds):
         for ipt, nt, persist, bpc, rg in variants:
             env = dict(os.environ, MSPMV_SPMV_IPT=str(ipt), MSPMV_SPMV_NT=str(nt), MSPMV_SPMV_PERSIST=str(persist),
-                       MSPMV_SPMV_BPC=str(bpc), MSPMV_SPMV_RG_COST=str(rg))
+                       MSPMV_SPMV_BPC=str(bpc), MSPMV_SPMV_RG_COST=str(rg), MSPMV_SPMM_RG_COST=str(rg))
             out = subprocess.run([sys.executable, __file__, "--child"], env=env, capture_output=True, text=True,
                                  timeout=300)
             if out.returncode != 0:
