@@ -380,6 +380,7 @@ mspmv_status mspmv_destroy(mspmv_handle h)
     dev_free(h->d_p1);
     dev_free(h->d_ap);
     dev_free(h->d_partials);
+    dev_free(h->d_gtickets);
     dev_free(h->d_scal);
     dev_free(h->d_conv);
     dev_free(h->d_ctrl);
@@ -518,12 +519,20 @@ static mspmv_status ensure_cg_workspace(mspmv_handle_s *h, int L, int nblk, int 
         ST_TRY(dev_alloc(&h->d_ap, elems));
         h->cg_cap_elems = elems;
     }
-    const size_t pcap = (size_t)std::max(nblk, num_tiles) * L;
+    const size_t slots = (size_t)std::max(nblk, num_tiles);
+    const size_t pcap = partials_capacity(slots, L);
     if (pcap > h->partials_cap) {
         dev_free(h->d_partials);
         h->partials_cap = 0;
         ST_TRY(dev_alloc(&h->d_partials, pcap));
         h->partials_cap = pcap;
+    }
+    if (gtickets_capacity(slots) > h->gtickets_cap) {
+        dev_free(h->d_gtickets);
+        h->gtickets_cap = 0;
+        ST_TRY(dev_alloc(&h->d_gtickets, gtickets_capacity(slots)));
+        HIP_TRY(hipMemset(h->d_gtickets, 0, sizeof(unsigned) * gtickets_capacity(slots)));
+        h->gtickets_cap = gtickets_capacity(slots);
     }
     if (L > h->scal_cap) {
         dev_free(h->d_scal);

@@ -82,6 +82,8 @@ struct mspmv_dist_s {
     double *d_r = nullptr, *d_ap = nullptr;  // n_own x L
     double *d_partials = nullptr;
     size_t partials_cap = 0;
+    unsigned *d_gtickets = nullptr;
+    size_t gtickets_cap = 0;
     CgScalars *d_scal = nullptr;
     unsigned char *d_conv = nullptr;
     CgControl *d_ctrl = nullptr;
@@ -189,6 +191,7 @@ mspmv_status mspmv_dist_destroy(mspmv_dist d)
     dfree(d->d_r);
     dfree(d->d_ap);
     dfree(d->d_partials);
+    dfree(d->d_gtickets);
     dfree(d->d_scal);
     dfree(d->d_conv);
     dfree(d->d_ctrl);
@@ -371,12 +374,20 @@ mspmv_status ensure_buffers(mspmv_dist_s *d, int L, int nblk, int num_tiles, int
         D_ST(dalloc(&d->d_red, (size_t)2 * L));
         d->cap_L = L;
     }
-    const size_t pc = (size_t)std::max(nblk, num_tiles) * L;
+    const size_t slots = (size_t)std::max(nblk, num_tiles);
+    const size_t pc = partials_capacity(slots, L);
     if (pc > d->partials_cap) {
         dfree(d->d_partials);
         d->partials_cap = 0;
         D_ST(dalloc(&d->d_partials, pc));
         d->partials_cap = pc;
+    }
+    if (gtickets_capacity(slots) > d->gtickets_cap) {
+        dfree(d->d_gtickets);
+        d->gtickets_cap = 0;
+        D_ST(dalloc(&d->d_gtickets, gtickets_capacity(slots)));
+        D_HIP(hipMemset(d->d_gtickets, 0, sizeof(unsigned) * gtickets_capacity(slots)));
+        d->gtickets_cap = gtickets_capacity(slots);
     }
     if (hist_cap > d->hist_cap) {
         dfree(d->d_hist);
@@ -489,7 +500,7 @@ mspmv_status mspmv_dist_cg_dev(mspmv_dist d, const double *d_B_own, double *d_X_
         DistVecArgs a = va;
         D_HIP(launch_dist_vec_mirror(2, a, L, nblk, d->d_pext, s));       // p = r + beta p
         D_ST(halo_exchange(d, L, d->d_ctrl));                               // p halo rows
-        D_HIP(launch_spmm_dot(d->local, *plan, d->d_pext, d->d_ap, L, d->d_ctrl, d->d_partials, pAp));
+        D_HIP(launch_spmm_dot(d->local, *plan, d->d_pext, d->d_ap, L, d->d_ctrl, d->d_partials, d->d_gtickets, pAp));
         D_NCCL(ncclAllReduce(pAp, pAp, L, ncclFloat64, ncclSum, d->comm, s));
         a.red_in = pAp;
         a.red_out = rr;

@@ -14,7 +14,8 @@ namespace mspmv {
 
 constexpr int kBlock = 256;  // 4 x 64-lane waves per workgroup
 constexpr int kNnzPad = 16;  // padding elements after the last nonzero of the device arrays
-constexpr int kSnapDiv = 8;  // a boundary snaps to its row start if <= tile/kSnapDiv nonzeros deep
+constexpr int kSnapDiv = 8;
+constexpr int kSlotGroup = 256;  // CG partial slots folded together at the first reduction level  // a boundary snaps to its row start if <= tile/kSnapDiv nonzeros deep
 
 // A merge-path tile plan for one nominal tile size (merge items per tile).
 //
@@ -78,6 +79,8 @@ struct mspmv_handle_s {
     double *d_r = nullptr, *d_p0 = nullptr, *d_p1 = nullptr, *d_ap = nullptr;
     double *d_partials = nullptr;
     size_t partials_cap = 0;
+    unsigned *d_gtickets = nullptr;  // reduce_slots group tickets (zeroed once, self-resetting)
+    size_t gtickets_cap = 0;
     mspmv::CgScalars *d_scal = nullptr;
     unsigned char *d_conv = nullptr;   // per-column converged flags
     mspmv::CgControl *d_ctrl = nullptr;
@@ -146,6 +149,9 @@ hipError_t launch_dist_vec_mirror(int which, const DistVecArgs &a, int L, int nb
 hipError_t launch_dist_pack(const double *p, const int *idx, long long n_elems, int L, double *send,
                             const CgControl *ctrl, hipStream_t s);
 hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
-                           CgControl *ctrl, double *partials, double *dot_out);
+                           CgControl *ctrl, double *partials, unsigned *gtickets, double *dot_out);
+// Partials capacity (doubles) and group-ticket count for `slots` partial slots of L columns.
+inline size_t partials_capacity(size_t slots, int L) { return (slots + (slots + kSlotGroup - 1) / kSlotGroup) * L; }
+inline size_t gtickets_capacity(size_t slots) { return (slots + kSlotGroup - 1) / kSlotGroup + 1; }
 
 }  // namespace mspmv

@@ -109,6 +109,88 @@ __device__ __forceinline__ double block_sum(double v, double *s_red)
     return t;
 }
 
+// Sum of column j over rows q, q + kBlock/L, ... < count of a [count][L] array written by
+// other workgroups (agent-scope loads), in row order; eight loads in flight per batch.
+template <int L>
+__device__ __forceinline__ double fold_col_strided(const double *base, int count, int j, int q)
+{
+    constexpr int TPC = kBlock / L;
+    double v = 0.0;
+    int i = q;
+    for (; i + 7 * TPC < count; i += 8 * TPC) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            t[u] = load_sc1(&base[(size_t)(i + u * TPC) * L + j]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            v += t[u];
+    }
+    for (; i < count; i += TPC)
+        v += load_sc1(&base[(size_t)i * L + j]);
+    return v;
+}
+
+// Column totals of a [count][L] partials array in a fixed order (per-thread strided rows,
+// then threads in order) -> s_out[0..L).  Call uniformly from every thread.
+template <int L>
+__device__ __forceinline__ void fold_cols(const double *base, int count, double *s_tmp, double *s_out)
+{
+    constexpr int TPC = kBlock / L;
+    const int tid = threadIdx.x;
+    s_tmp[tid] = fold_col_strided<L>(base, count, tid % L, tid / L);
+    __syncthreads();
+    if (tid < L) {
+        double w = s_tmp[tid];
+        for (int u = 1; u < TPC; ++u)
+            w += s_tmp[u * L + tid];
+        s_out[tid] = w;
+    }
+    __syncthreads();
+}
+
+// Deterministic two-level "last block done" reduction of per-slot column partials.  The
+// caller has stored partials[slot][0..L) (agent scope, vmcnt drained) and synchronised.  The
+// last slot of each group of kSlotGroup to arrive folds its group (slot order) into level 2
+// at partials[nslots + g][..]; the last group to finish folds level 2 (group order) into
+// s_out.  Returns true in exactly that block.  Group tickets and *final_ticket reset
+// themselves, so the next launch starts from zero.  (A single level makes one block read
+// every partial: 1.5 M agent-scope loads for a 191 k-tile SpMM plan, ~2 ms.)
+template <int L>
+__device__ __forceinline__ bool reduce_slots(double *partials, unsigned *group_tickets, unsigned *final_ticket,
+                                             int slot, int nslots, double *s_tmp, double *s_out, int *s_flag)
+{
+    const int tid = threadIdx.x;
+    const int g = slot / kSlotGroup;
+    const int ngroups = (nslots + kSlotGroup - 1) / kSlotGroup;
+    const int gsize = min(kSlotGroup, nslots - g * kSlotGroup);
+    if (tid == 0) {
+        const unsigned tk = __hip_atomic_fetch_add(&group_tickets[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_flag = tk == (unsigned)gsize - 1;
+    }
+    __syncthreads();
+    if (!*s_flag)
+        return false;
+    fold_cols<L>(partials + (size_t)g * kSlotGroup * L, gsize, s_tmp, s_out);
+    if (tid < L) {
+        store_sc1(&partials[((size_t)nslots + g) * L + tid], s_out[tid]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (tid == 0) {
+        __hip_atomic_store(&group_tickets[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned tk = __hip_atomic_fetch_add(final_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_flag = tk == (unsigned)ngroups - 1;
+    }
+    __syncthreads();
+    if (!*s_flag)
+        return false;
+    fold_cols<L>(partials + (size_t)nslots * L, ngroups, s_tmp, s_out);
+    if (tid == 0)
+        __hip_atomic_store(final_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
 // ------------------------------------------------------------------------------------------
 // partition: the reference's partition coordinates and the tile plan boundaries
 // ------------------------------------------------------------------------------------------
@@ -210,7 +292,8 @@ struct TileArgs {
     CgScalars *scal;                   // CG: per-column scalars
     CgControl *ctrl;                   // CG: iteration control
     const unsigned char *conv;         // CG: per-column converged flags
-    double *partials;                  // CG: per-tile partial dots [tile][L]
+    double *partials;                  // CG: per-slot partial dots [slot][L], then level 2 [group][L]
+    unsigned *gtickets;                // CG: per-group tickets of reduce_slots (self-resetting)
     double *dot_out;                   // MODE 2: the reduced x.(Ax) per column [L]
 };
 
@@ -460,8 +543,9 @@ __device__ __forceinline__ void reduce_tile(const TileArgs &a, SpmvSmem<IPT> &sm
 }
 
 // CG epilogue of the single-RHS tile kernels: this block's p.Ap partial -> partials[slot];
-// the last block to arrive reduces all partials in slot order and sets alpha = rs_old / pAp
-// (single_strategy.hpp:140-141).  Non-finite alpha (p.Ap == 0 or NaN) stops the solve.
+// the two-level reduce_slots folds all partials in a fixed order and its last block sets
+// alpha = rs_old / pAp (single_strategy.hpp:140-141).  Non-finite alpha (p.Ap == 0 or NaN)
+// stops the solve.
 template <int IPT, int MODE>
 __device__ __forceinline__ void cg_alpha_epilogue(const TileArgs &a, SpmvSmem<IPT> &sm, int slot, int nslots,
                                                   double dot)
@@ -471,21 +555,15 @@ __device__ __forceinline__ void cg_alpha_epilogue(const TileArgs &a, SpmvSmem<IP
     if (tid == 0) {
         store_sc1(&a.partials[slot], tsum);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned tk = __hip_atomic_fetch_add(&a.ctrl->ticket_a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sm.last = (tk == gridDim.x - 1);
     }
     __syncthreads();
-    if (sm.last) {
-        double v = 0.0;
-        for (int i = tid; i < nslots; i += kBlock)
-            v += load_sc1(&a.partials[i]);
-        const double pAp = block_sum(v, sm.red);
-        if (tid == 0 && MODE == kModeDot) {
-            __hip_atomic_store(&a.ctrl->ticket_a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!reduce_slots<1>(a.partials, a.gtickets, &a.ctrl->ticket_a, slot, nslots, sm.cval, sm.red, &sm.last))
+        return;
+    if (tid == 0) {
+        const double pAp = sm.red[0];
+        if (MODE == kModeDot) {
             a.dot_out[0] = pAp;
-        }
-        if (tid == 0 && MODE == kModeCg) {
-            __hip_atomic_store(&a.ctrl->ticket_a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
             CgScalars &s = a.scal[0];
             s.pAp = pAp;
             const double alpha = a.conv[0] ? 0.0 : s.rs_old / pAp;
@@ -933,46 +1011,24 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __syncthreads();
-        if (tid == 0) {
-            const unsigned tk =
-                __hip_atomic_fetch_add(&a.ctrl->ticket_a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_last = (tk == gridDim.x - 1);
-        }
-        __syncthreads();
-        if (s_last) {
-            // column j = tid % L, tiles strided by kBlock / L -- fixed order per column
-            constexpr int TPC = kBlock / L;
-            const int j = tid % L;
-            const int q = tid / L;
-            double v = 0.0;
-            for (int i = q; i < a.num_tiles; i += TPC)
-                v += load_sc1(&a.partials[(size_t)i * L + j]);
-            __shared__ double s_colred[kBlock];
-            s_colred[tid] = v;
-            __syncthreads();
-            if (tid < L && MODE == kModeDot) {
-                double pAp = s_colred[tid];
-                for (int u = 1; u < TPC; ++u)
-                    pAp += s_colred[u * L + tid];
-                a.dot_out[tid] = pAp;
+        __shared__ double s_colred[kBlock];
+        __shared__ double s_tot[L];
+        if (!reduce_slots<L>(a.partials, a.gtickets, &a.ctrl->ticket_a, t, a.num_tiles, s_colred, s_tot, &s_last))
+            return;
+        if (tid < L && MODE == kModeDot)
+            a.dot_out[tid] = s_tot[tid];
+        if (tid < L && CG) {
+            const double pAp = s_tot[tid];
+            CgScalars &s = a.scal[tid];
+            s.pAp = pAp;
+            const bool cv = a.conv[tid];
+            const double alpha = cv ? 0.0 : s.rs_old / pAp;
+            s.alpha = alpha;
+            if (!cv && !(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
+                a.ctrl->breakdown = 1;
+                a.ctrl->done = 1;
+                a.ctrl->iters_out = a.ctrl->iter + 1;
             }
-            if (tid < L && CG) {
-                double pAp = s_colred[tid];
-                for (int u = 1; u < TPC; ++u)
-                    pAp += s_colred[u * L + tid];
-                CgScalars &s = a.scal[tid];
-                s.pAp = pAp;
-                const bool cv = a.conv[tid];
-                const double alpha = cv ? 0.0 : s.rs_old / pAp;
-                s.alpha = alpha;
-                if (!cv && !(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
-                    a.ctrl->breakdown = 1;
-                    a.ctrl->done = 1;
-                    a.ctrl->iters_out = a.ctrl->iter + 1;
-                }
-            }
-            if (tid == 0)
-                __hip_atomic_store(&a.ctrl->ticket_a, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -1046,10 +1102,7 @@ __device__ __forceinline__ void reduce_partials_cols(const double *partials, int
 {
     constexpr int TPC = kBlock / L;
     const int tid = threadIdx.x;
-    const int j = tid % L, q = tid / L;
-    double v = 0.0;
-    for (int i = q; i < nblk; i += TPC)
-        v += load_sc1(&partials[(size_t)i * L + j]);
+    const double v = fold_col_strided<L>(partials, nblk, tid % L, tid / L);
     s_colred[tid] = v;
     __syncthreads();
     if (tid < L) {
@@ -1605,6 +1658,7 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *
     ta.ctrl = h->d_ctrl;
     ta.conv = h->d_conv;
     ta.partials = h->d_partials;
+    ta.gtickets = h->d_gtickets;
     hipError_t e = launch_tile<kModeCg>(ta, L, h->stream, h->num_cus);
     if (e != hipSuccess)
         return e;
@@ -1671,13 +1725,14 @@ hipError_t launch_dist_pack(const double *p, const int *idx, long long n_elems, 
 
 // Y = A X with x.(AX) per column reduced into dot_out (MODE 2), plus the carry fix-up.
 hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
-                           CgControl *ctrl, double *partials, double *dot_out)
+                           CgControl *ctrl, double *partials, unsigned *gtickets, double *dot_out)
 {
     if (plan.num_tiles == 0)  // a rank without rows contributes 0 to the all-reduce
         return hipMemsetAsync(dot_out, 0, sizeof(double) * L, h->stream);
     TileArgs ta = make_args(h, plan, d_X, d_Y, L);
     ta.ctrl = ctrl;
     ta.partials = partials;
+    ta.gtickets = gtickets;
     ta.dot_out = dot_out;
     hipError_t e = launch_tile<kModeDot>(ta, L, h->stream, h->num_cus);
     if (e != hipSuccess || plan.num_carries == 0)
