@@ -481,6 +481,7 @@ mspmv_status mspmv_dist_cg_dev(mspmv_dist d, const double *d_B_own, double *d_X_
     va.ctrl = d->d_ctrl;
     va.conv = d->d_conv;
     va.partials = d->d_partials;
+    va.gtickets = d->d_gtickets;
     va.hist = cap ? d->d_hist : nullptr;
     va.hist_cap = cap;
     va.tol = tolerance;

@@ -15,7 +15,8 @@ namespace mspmv {
 constexpr int kBlock = 256;  // 4 x 64-lane waves per workgroup
 constexpr int kNnzPad = 16;  // padding elements after the last nonzero of the device arrays
 constexpr int kSnapDiv = 8;
-constexpr int kSlotGroup = 256;  // CG partial slots folded together at the first reduction level  // a boundary snaps to its row start if <= tile/kSnapDiv nonzeros deep
+constexpr int kSlotGroup = 32;     // fan-in of the CG partial-reduction tree (reduce_slots)
+constexpr int kTicketStride = 64;  // tickets 256 B apart: one per memory line  // a boundary snaps to its row start if <= tile/kSnapDiv nonzeros deep
 
 // A merge-path tile plan for one nominal tile size (merge items per tile).
 //
@@ -56,10 +57,7 @@ struct CgControl {
     int done;        // 1 once every column converged (or breakdown)
     int iters_out;   // iteration count to report (the reference's return value)
     int breakdown;   // 1 if p.Ap <= 0 or non-finite was met
-    unsigned ticket_a;
-    unsigned ticket_b;
-    unsigned ticket_i;
-    unsigned pad;
+    unsigned reserved[4];  // (formerly single-address tickets; see reduce_slots)
 };
 
 }  // namespace mspmv
@@ -141,6 +139,7 @@ struct DistVecArgs {
     double tol;
     const double *red_in;
     double *red_out;
+    unsigned *gtickets;
 };
 // which: 0 init partial sums (b.b -> red_out), 1 init finish (red_in = all-reduced b.b),
 // 2 p update, 3 x/r update (alpha from red_in = all-reduced p.Ap; r.r -> red_out),
@@ -151,7 +150,8 @@ hipError_t launch_dist_pack(const double *p, const int *idx, long long n_elems, 
 hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
                            CgControl *ctrl, double *partials, unsigned *gtickets, double *dot_out);
 // Partials capacity (doubles) and group-ticket count for `slots` partial slots of L columns.
-inline size_t partials_capacity(size_t slots, int L) { return (slots + (slots + kSlotGroup - 1) / kSlotGroup) * L; }
-inline size_t gtickets_capacity(size_t slots) { return (slots + kSlotGroup - 1) / kSlotGroup + 1; }
+// (every level of the tree: slots, slots/32, ... -> <= slots * 32/31 + one per level)
+inline size_t partials_capacity(size_t slots, int L) { return (slots + slots / (kSlotGroup - 1) + 8) * L; }
+inline size_t gtickets_capacity(size_t slots) { return (slots / (kSlotGroup - 1) + 8) * kTicketStride; }
 
 }  // namespace mspmv

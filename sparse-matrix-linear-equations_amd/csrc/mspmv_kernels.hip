@@ -149,46 +149,49 @@ __device__ __forceinline__ void fold_cols(const double *base, int count, double 
     __syncthreads();
 }
 
-// Deterministic two-level "last block done" reduction of per-slot column partials.  The
-// caller has stored partials[slot][0..L) (agent scope, vmcnt drained) and synchronised.  The
-// last slot of each group of kSlotGroup to arrive folds its group (slot order) into level 2
-// at partials[nslots + g][..]; the last group to finish folds level 2 (group order) into
-// s_out.  Returns true in exactly that block.  Group tickets and *final_ticket reset
-// themselves, so the next launch starts from zero.  (A single level makes one block read
-// every partial: 1.5 M agent-scope loads for a 191 k-tile SpMM plan, ~2 ms.)
+// Deterministic multi-level "last block done" reduction of per-slot column partials.  The
+// caller has stored partials[slot][0..L) (agent scope, vmcnt drained) and synchronised.  Slots
+// form groups of kSlotGroup; the last of a group to arrive (one agent-scope ticket per group)
+// folds the group in slot order into the next level, whose groups fold the same way, until
+// one group remains: its last arriver holds the totals in s_out and returns true (exactly one
+// block does).  Tickets reset themselves for the next launch.  Why a tree of small groups on
+// separate 256-B lines: agent-scope atomics on one address serialise at the memory side
+// (~10 ns each), so 2 k blocks on one ticket cost ~22 us; fan-in 32 keeps each chain short.
 template <int L>
-__device__ __forceinline__ bool reduce_slots(double *partials, unsigned *group_tickets, unsigned *final_ticket,
-                                             int slot, int nslots, double *s_tmp, double *s_out, int *s_flag)
+__device__ __forceinline__ bool reduce_slots(double *partials, unsigned *tickets, int slot, int nslots,
+                                             double *s_tmp, double *s_out, int *s_flag)
 {
     const int tid = threadIdx.x;
-    const int g = slot / kSlotGroup;
-    const int ngroups = (nslots + kSlotGroup - 1) / kSlotGroup;
-    const int gsize = min(kSlotGroup, nslots - g * kSlotGroup);
-    if (tid == 0) {
-        const unsigned tk = __hip_atomic_fetch_add(&group_tickets[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *s_flag = tk == (unsigned)gsize - 1;
+    double *lvl = partials;
+    int idx = slot, count = nslots;
+    for (;;) {
+        const int g = idx / kSlotGroup;
+        const int ngroups = (count + kSlotGroup - 1) / kSlotGroup;
+        const int gsize = min(kSlotGroup, count - g * kSlotGroup);
+        unsigned *tk = &tickets[(size_t)g * kTicketStride];
+        if (tid == 0) {
+            const unsigned v = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *s_flag = v == (unsigned)gsize - 1;
+        }
+        __syncthreads();
+        if (!*s_flag)
+            return false;
+        fold_cols<L>(lvl + (size_t)g * kSlotGroup * L, gsize, s_tmp, s_out);
+        if (tid == 0)
+            __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ngroups == 1)
+            return true;
+        double *next = lvl + (size_t)count * L;
+        if (tid < L) {
+            store_sc1(&next[(size_t)g * L + tid], s_out[tid]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        tickets += (size_t)ngroups * kTicketStride;
+        lvl = next;
+        idx = g;
+        count = ngroups;
     }
-    __syncthreads();
-    if (!*s_flag)
-        return false;
-    fold_cols<L>(partials + (size_t)g * kSlotGroup * L, gsize, s_tmp, s_out);
-    if (tid < L) {
-        store_sc1(&partials[((size_t)nslots + g) * L + tid], s_out[tid]);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    if (tid == 0) {
-        __hip_atomic_store(&group_tickets[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned tk = __hip_atomic_fetch_add(final_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *s_flag = tk == (unsigned)ngroups - 1;
-    }
-    __syncthreads();
-    if (!*s_flag)
-        return false;
-    fold_cols<L>(partials + (size_t)nslots * L, ngroups, s_tmp, s_out);
-    if (tid == 0)
-        __hip_atomic_store(final_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return true;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -557,7 +560,7 @@ __device__ __forceinline__ void cg_alpha_epilogue(const TileArgs &a, SpmvSmem<IP
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    if (!reduce_slots<1>(a.partials, a.gtickets, &a.ctrl->ticket_a, slot, nslots, sm.cval, sm.red, &sm.last))
+    if (!reduce_slots<1>(a.partials, a.gtickets, slot, nslots, sm.cval, sm.red, &sm.last))
         return;
     if (tid == 0) {
         const double pAp = sm.red[0];
@@ -1013,7 +1016,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
         __syncthreads();
         __shared__ double s_colred[kBlock];
         __shared__ double s_tot[L];
-        if (!reduce_slots<L>(a.partials, a.gtickets, &a.ctrl->ticket_a, t, a.num_tiles, s_colred, s_tot, &s_last))
+        if (!reduce_slots<L>(a.partials, a.gtickets, t, a.num_tiles, s_colred, s_tot, &s_last))
             return;
         if (tid < L && MODE == kModeDot)
             a.dot_out[tid] = s_tot[tid];
@@ -1095,24 +1098,6 @@ __device__ __forceinline__ void colpair_block_reduce(double2 v, double2 (*s_red2
     __syncthreads();
 }
 
-// Last block: reduce partials[nblk][L] per column in block order into out[j].
-template <int L>
-__device__ __forceinline__ void reduce_partials_cols(const double *partials, int nblk, double *s_colred,
-                                                     double *out_cols)
-{
-    constexpr int TPC = kBlock / L;
-    const int tid = threadIdx.x;
-    const double v = fold_col_strided<L>(partials, nblk, tid % L, tid / L);
-    s_colred[tid] = v;
-    __syncthreads();
-    if (tid < L) {
-        double s = s_colred[tid];
-        for (int u = 1; u < TPC; ++u)
-            s += s_colred[u * L + tid];
-        out_cols[tid] = s;
-    }
-    __syncthreads();
-}
 
 struct CgVecArgs {
     long long n_elems;       // n * L
@@ -1133,6 +1118,7 @@ struct CgVecArgs {
     // (b.b at init, r.r at update) for the all-reduce, instead of finishing the scalars.
     const double *red_in;
     double *red_out;
+    unsigned *gtickets;  // reduce_slots tickets
 };
 
 // x = 0, r = p0 = b; rs_old_j = r_j.r_j, b_norm_j = sqrt(b_j.b_j) (no_pretreatment.hpp:61-79,
@@ -1166,19 +1152,12 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CgVecArgs a)
         acc.x += b * b;
     }
     colpair_block_reduce<L>(acc, s_red2, a.partials + (size_t)blockIdx.x * L);
-    if (tid == 0) {
-        const unsigned tk = __hip_atomic_fetch_add(&a.ctrl->ticket_i, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (tk == gridDim.x - 1);
-    }
-    __syncthreads();
-    if (s_last && a.red_out) {
-        reduce_partials_cols<L>(a.partials, gridDim.x, s_colred, s_out);
+    if (!reduce_slots<L>(a.partials, a.gtickets, blockIdx.x, gridDim.x, s_colred, s_out, &s_last))
+        return;
+    if (a.red_out) {
         if (tid < L)
             a.red_out[tid] = s_out[tid];
-        if (tid == 0)
-            __hip_atomic_store(&a.ctrl->ticket_i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (s_last) {
-        reduce_partials_cols<L>(a.partials, gridDim.x, s_colred, s_out);
+    } else {
         if (tid < L) {
             CgScalars &s = a.scal[tid];
             const double bb = s_out[tid];
@@ -1192,7 +1171,6 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CgVecArgs a)
             a.conv[tid] = 0;
         }
         if (tid == 0) {
-            __hip_atomic_store(&a.ctrl->ticket_i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             a.ctrl->iter = 0;
             a.ctrl->done = 0;
             a.ctrl->iters_out = 0;
@@ -1255,21 +1233,13 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(CgVecArgs a)
         acc.x += r * r;
     }
     colpair_block_reduce<L>(acc, s_red2, a.partials + (size_t)blockIdx.x * L);
-    if (tid == 0) {
-        const unsigned tk = __hip_atomic_fetch_add(&a.ctrl->ticket_b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (tk == gridDim.x - 1);
-    }
-    __syncthreads();
-    if (s_last && a.red_out) {
-        reduce_partials_cols<L>(a.partials, gridDim.x, s_colred, s_out);
+    if (!reduce_slots<L>(a.partials, a.gtickets, blockIdx.x, gridDim.x, s_colred, s_out, &s_last))
+        return;
+    if (a.red_out) {
         if (tid < L)
             a.red_out[tid] = s_out[tid];
-        if (tid == 0)
-            __hip_atomic_store(&a.ctrl->ticket_b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (s_last) {
-        reduce_partials_cols<L>(a.partials, gridDim.x, s_colred, s_out);
+    } else {
         if (tid == 0) {
-            __hip_atomic_store(&a.ctrl->ticket_b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int iter = a.ctrl->iter;
             int nconv = 0;
             double maxrel = 0.0;
@@ -1642,6 +1612,7 @@ hipError_t launch_cg_init(mspmv_handle_s *h, const double *d_b, double *d_x, int
     a.ctrl = h->d_ctrl;
     a.conv = h->d_conv;
     a.partials = h->d_partials;
+    a.gtickets = h->d_gtickets;
     a.tol = tol;
     return dispatch_vec(true, a, L, nblk, h->stream);
 }
@@ -1680,6 +1651,7 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *
     va.ctrl = h->d_ctrl;
     va.conv = h->d_conv;
     va.partials = h->d_partials;
+    va.gtickets = h->d_gtickets;
     va.hist = h->d_hist;
     va.hist_cap = h->hist_cap;
     va.tol = tol;
@@ -1774,6 +1746,7 @@ hipError_t launch_dist_vec_mirror(int which, const DistVecArgs &d, int L, int nb
     a.tol = d.tol;
     a.red_in = d.red_in;
     a.red_out = d.red_out;
+    a.gtickets = d.gtickets;
     return launch_dist_vec(which, a, L, nblk, p, s);
 }
 }  // namespace mspmv
