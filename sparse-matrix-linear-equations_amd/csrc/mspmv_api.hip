@@ -382,6 +382,7 @@ mspmv_status mspmv_destroy(mspmv_handle h)
     dev_free(h->d_partials);
     dev_free(h->d_gtickets);
     dev_free(h->d_scal);
+    dev_free(h->d_red);
     dev_free(h->d_conv);
     dev_free(h->d_ctrl);
     dev_free(h->d_hist);
@@ -538,8 +539,10 @@ static mspmv_status ensure_cg_workspace(mspmv_handle_s *h, int L, int nblk, int 
         dev_free(h->d_scal);
         dev_free(h->d_conv);
         h->scal_cap = 0;
+        dev_free(h->d_red);
         ST_TRY(dev_alloc(&h->d_scal, (size_t)L));
         ST_TRY(dev_alloc(&h->d_conv, (size_t)L));
+        ST_TRY(dev_alloc(&h->d_red, (size_t)L));
         h->scal_cap = L;
     }
     if (!h->d_ctrl)

@@ -80,6 +80,7 @@ struct mspmv_handle_s {
     unsigned *d_gtickets = nullptr;  // reduce_slots group tickets (zeroed once, self-resetting)
     size_t gtickets_cap = 0;
     mspmv::CgScalars *d_scal = nullptr;
+    double *d_red = nullptr;  // [L] p.Ap of the split multi-RHS iteration (k_spmm_tile MODE 2 -> k_cg_update)
     unsigned char *d_conv = nullptr;   // per-column converged flags
     mspmv::CgControl *d_ctrl = nullptr;
     mspmv::CgControl *h_ctrl = nullptr;  // pinned mirror

@@ -1018,8 +1018,19 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
         __shared__ double s_tot[L];
         if (!reduce_slots<L>(a.partials, a.gtickets, t, a.num_tiles, s_colred, s_tot, &s_last))
             return;
-        if (tid < L && MODE == kModeDot)
+        if (tid < L && MODE == kModeDot) {
             a.dot_out[tid] = s_tot[tid];
+            // single-GPU split CG iteration (scal given): a non-finite alpha stops the solve
+            // before the update touches x and r, as the fused path does
+            if (a.scal && !a.conv[tid]) {
+                const double alpha = a.scal[tid].rs_old / s_tot[tid];
+                if (!(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
+                    a.ctrl->breakdown = 1;
+                    a.ctrl->done = 1;
+                    a.ctrl->iters_out = a.ctrl->iter + 1;
+                }
+            }
+        }
         if (tid < L && CG) {
             const double pAp = s_tot[tid];
             CgScalars &s = a.scal[tid];
@@ -1300,10 +1311,25 @@ __global__ __launch_bounds__(kBlock) void k_dist_pupdate(CgVecArgs a, double *p)
 {
     if (a.ctrl->done)
         return;
-    const long long n = a.n_elems;
-    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < n; i += (long long)gridDim.x * kBlock) {
-        const int j = (int)(i % L);
-        p[i] = a.r[i] + a.scal[j].beta * p[i];
+    const long long stride = (long long)gridDim.x * kBlock;
+    const long long i0 = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (L == 1) {
+        const double beta = a.scal[0].beta;
+        for (long long i = i0; i < a.n_elems; i += stride)
+            p[i] = a.r[i] + beta * p[i];
+        return;
+    }
+    // column pairs: the stride (in pairs) is a multiple of L/2, so a thread keeps its pair
+    constexpr int GL = L > 1 ? L / 2 : 1;
+    const int cp = (int)(i0 % GL);
+    const double2 beta = make_double2(a.scal[2 * cp].beta, a.scal[2 * cp + 1].beta);
+    const long long npairs = a.n_elems / 2;
+    for (long long i = i0; i < npairs; i += stride) {
+        const double2 r = reinterpret_cast<const double2 *>(a.r)[i];
+        double2 q = reinterpret_cast<double2 *>(p)[i];
+        q.x = r.x + beta.x * q.x;
+        q.y = r.y + beta.y * q.y;
+        reinterpret_cast<double2 *>(p)[i] = q;
     }
 }
 
@@ -1617,9 +1643,72 @@ hipError_t launch_cg_init(mspmv_handle_s *h, const double *d_b, double *d_x, int
     return dispatch_vec(true, a, L, nblk, h->stream);
 }
 
+hipError_t launch_dist_vec(int which, const CgVecArgs &a, int L, int nblk, double *p, hipStream_t s);
+
+static hipError_t launch_fixup_ctrl(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L)
+{
+    if (plan.num_carries == 0)
+        return hipSuccess;
+    const int n = plan.num_carries * L;
+    hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, h->stream, plan.d_carry_tiles, plan.d_carry_rows,
+                       plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)h->d_ctrl);
+    return hipGetLastError();
+}
+
+// Multi-RHS iteration, split: p = r + beta p (one streaming pass), then Y = A p with p.Ap by
+// linearity (MODE 2, which also stops on a non-finite alpha), then the update with alpha from
+// that p.Ap.  For L >= 2 the fused iteration would gather two L-wide panel rows (r and
+// p_old) per nonzero, and the SpMM is gather-bound: measured 1.33 ms vs 0.62 + 0.14 ms split
+// on the nlpkkt120-sized L = 8 case.
+static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &plan, double *d_x, int L, int nblk,
+                                            double tol)
+{
+    CgVecArgs va{};
+    va.n_elems = (long long)h->m * L;
+    va.x = d_x;
+    va.r = h->d_r;
+    va.p = h->d_p0;
+    va.ap = h->d_ap;
+    va.scal = h->d_scal;
+    va.ctrl = h->d_ctrl;
+    va.conv = h->d_conv;
+    va.partials = h->d_partials;
+    va.gtickets = h->d_gtickets;
+    va.hist = h->d_hist;
+    va.hist_cap = h->hist_cap;
+    va.tol = tol;
+    hipError_t e = launch_dist_vec(2, va, L, nblk, h->d_p0, h->stream);
+    if (e != hipSuccess)
+        return e;
+    TileArgs ta = make_args(h, plan, h->d_p0, h->d_ap, L);
+    ta.scal = h->d_scal;
+    ta.ctrl = h->d_ctrl;
+    ta.conv = h->d_conv;
+    ta.partials = h->d_partials;
+    ta.gtickets = h->d_gtickets;
+    ta.dot_out = h->d_red;
+    if ((e = launch_tile<kModeDot>(ta, L, h->stream, h->num_cus)) != hipSuccess)
+        return e;
+    if ((e = launch_fixup_ctrl(h, plan, h->d_ap, L)) != hipSuccess)
+        return e;
+    va.red_in = h->d_red;
+    return dispatch_vec(false, va, L, nblk, h->stream);
+}
+
+bool cg_split_iteration(int L)
+{
+    static const int mode = [] {
+        const char *e = getenv("MSPMV_CG_SPLIT");
+        return e ? atoi(e) : -1;
+    }();
+    return mode < 0 ? L >= 2 : mode != 0;
+}
+
 hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *d_x, int L, int parity, int nblk,
                                double tol)
 {
+    if (cg_split_iteration(L))
+        return launch_cg_iteration_split(h, plan, d_x, L, nblk, tol);
     double *p_old = parity ? h->d_p1 : h->d_p0;
     double *p_new = parity ? h->d_p0 : h->d_p1;
     TileArgs ta = make_args(h, plan, h->d_r, h->d_ap, L);

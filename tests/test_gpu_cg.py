@@ -148,3 +148,49 @@ def test_cg_facade_names(orc):
     errs = []
     it = mspmv.CGSolveMultiple(a, B, X, L, 5000, 1e-8, mspmv.NONZERO_SPLIT, errs)
     assert len(errs) == it and errs[-1] < 1e-8
+
+
+def test_cg_multi_breakdown_reported_split_path():
+    """L >= 2 runs the split iteration (p update pass, SpMM MODE 2, update): a zero RHS gives
+    p.Ap = 0 -> non-finite alpha, caught by the SpMM's last block before x and r change."""
+    a = spd_cases()["fem2d"]()
+    with mspmv.GpuCsr(a) as g:
+        X, it, _, st = g.cg_multi(np.zeros((a.num_rows, 4)), 100, 1e-8)
+    assert st == 4 and it == 1
+    assert np.all(X == 0.0)
+
+
+_FUSED_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import mspmv
+a = mspmv.CsrMatrix.synth_stencil(0, 4000, 64)
+B = np.random.default_rng(11).uniform(0, 1, (a.num_rows, 4))
+with mspmv.GpuCsr(a) as g:
+    X, it, h, st = g.cg_multi(B, 5000, 1e-9, hist_cap=5000)
+np.savez(sys.argv[2], X=X, it=it, h=h, st=st)
+"""
+
+
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_cg_multi_fused_and_split_iterations_match_oracle(orc, tmp_path, split):
+    """Both multi-RHS iteration forms (MSPMV_CG_SPLIT=0: gathers r and p_old per nonzero;
+    1: separate p update) reproduce the oracle; run in a child so the env is read fresh."""
+    import os
+    import subprocess
+    import sys
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "sparse-matrix-linear-equations_amd")
+    out = str(tmp_path / "r.npz")
+    env = dict(os.environ, MSPMV_CG_SPLIT=split)
+    r = subprocess.run([sys.executable, "-c", _FUSED_CHILD, pkg, out], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = np.load(out)
+    a = mspmv.CsrMatrix.synth_stencil(0, 4000, 64)
+    B = np.random.default_rng(11).uniform(0, 1, (a.num_rows, 4))
+    Xo, it_o, ho = orc.cg_multi(a, B, 5000, 1e-9, kernel=1, P=8, hist_cap=5000)
+    assert int(d["st"]) == 0 and iter_match(int(d["it"]), it_o, ho, 1e-9)
+    k = min(len(d["h"]), len(ho))
+    np.testing.assert_allclose(d["h"][:k], ho[:k], rtol=0, atol=1e-10)
+    assert np.linalg.norm(d["X"] - Xo) <= 1e-8 * np.linalg.norm(Xo)
