@@ -268,7 +268,7 @@ def main():
     bytes_launch = spmv_bytes(a0.num_rows, a0.num_cols, a0.num_nonzeros)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     hot_ms, hot_kern, _ = mspmv.time_spmm_batch(gs[:1], dxs[:1], dys[:1], 1, 200)
-    kname = mspmv.lib.mspmv_spmv_kernel_name().decode()
+    kname = gs[0].kernel_name()
     traffic, traffic_src = pmc_traffic(kname, bytes_launch)
     ref_eff = (a0.num_nonzeros * 20 + a0.num_rows * 12) / (kern_ms * 1e-3) / 1e9  # cpu_spmv.cpp:722-726
 

@@ -163,9 +163,11 @@ MSPMV_API mspmv_status mspmv_tile_plan(mspmv_handle h, int L, int *num_tiles, in
  * lanes per row (times L/2 column-pair lanes for L > 1).  g = 1 sums each row sequentially in
  * CSR order -> bit-identical to SpmvGold / the row-split SpMM for rows the tile holds whole. */
 MSPMV_API mspmv_status mspmv_tile_modes(mspmv_handle h, int L, unsigned char *modes);
-/* The single-RHS SpMV kernel instantiation this process launches (tuning read once from the
- * MSPMV_SPMV_* environment), e.g. "k_spmv_tile<8,0,true>" -- the name rocprofv3 reports. */
-MSPMV_API const char *mspmv_spmv_kernel_name(void);
+/* The single-RHS SpMV kernel instantiation launched for this matrix (tuning read once from
+ * the MSPMV_SPMV_* environment; nontemporal matrix loads above 128 MiB), e.g.
+ * "k_spmv_tile<8,0,true>" -- the name rocprofv3 reports.  Valid until the next call on this
+ * thread. */
+MSPMV_API const char *mspmv_spmv_kernel_name(mspmv_handle h);
 
 /* ---- device memory helpers (so hosts need no HIP headers) ---------------------------- */
 MSPMV_API mspmv_status mspmv_device_malloc(int device, size_t bytes, void **d_ptr);

@@ -341,7 +341,14 @@ extern "C" {
 
 const char *mspmv_last_error(void) { return g_err.c_str(); }
 
-const char *mspmv_spmv_kernel_name(void) { return spmv_kernel_name(); }
+const char *mspmv_spmv_kernel_name(mspmv_handle h)
+{
+    thread_local std::string name;
+    if (!h)
+        return "";
+    name = spmv_kernel_name(h);
+    return name.c_str();
+}
 
 const char *mspmv_version(void) { return "mspmv 0.1.0 (gfx950, merge-path fp64)"; }
 

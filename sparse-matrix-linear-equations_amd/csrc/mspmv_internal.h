@@ -113,7 +113,8 @@ hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const 
 hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L);
 // Nominal tile size (merge items per tile) used for L right-hand sides.
 int tile_items_for(int L);
-const char *spmv_kernel_name();
+std::string spmv_kernel_name(const mspmv_handle_s *h);
+bool stream_nt(const mspmv_handle_s *h);
 bool supported_L(int L);
 
 // CG pieces

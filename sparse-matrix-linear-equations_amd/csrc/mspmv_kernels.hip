@@ -242,9 +242,10 @@ __global__ void k_snap(const int *__restrict__ row_offsets, int m, int2 *__restr
 // nonzero: 1 for SpMV, L/2 column-pair lanes for SpMM).  The tile's row segments -- its complete rows plus the trailing partial row of a
 // split boundary -- are either summed by row groups of G = 2^lg lanes (mode lg + 1) or, when
 // segment lengths are too uneven for that, by the per-thread merge walk (mode 0).  Cost model
-// in LDS-read steps of the slowest group: ceil(segments / groups) rounds of ceil(longest / G)
-// reads plus a log2(G)-step shuffle fold; the cheapest G wins if its cost is within max_cost
-// (the walk costs about IPT reads plus an 11-step search and two more barriers).
+// in latency steps of the slowest group: ceil(segments / groups) rounds of the longest
+// segment's reads (SpMV: ceil(longest / G) LDS reads; SpMM: gather batches) plus the shuffle
+// fold; the cheapest G wins if its cost is within max_cost (about the walk it replaces: IPT
+// reads plus an 11-step search and two barriers for SpMV, IPTG/4 gather chunks for SpMM).
 __global__ void k_tile_modes(const int *__restrict__ row_offsets, const int2 *__restrict__ bounds,
                              const unsigned char *__restrict__ split, int num_tiles, int gl, int max_cost,
                              unsigned char *__restrict__ modes)
@@ -267,7 +268,11 @@ __global__ void k_tile_modes(const int *__restrict__ row_offsets, const int2 *__
     int best = 0, best_cost = max_cost + 1;
     for (int lg = 0; (gl << lg) <= 64; ++lg) {  // a row group stays inside one wave
         const int groups = kBlock / (gl << lg), G = 1 << lg;
-        const int cost = ((nseg + groups - 1) / groups) * ((longest + G - 1) / G + 3 * lg);
+        const int rounds = (nseg + groups - 1) / groups;
+        const int per_lane = (longest + G - 1) / G;
+        // SpMV: LDS product reads, one step each, plus a 3-step shuffle per fold level.
+        // SpMM: panel-row gathers in batches of 8 (about 4 steps of latency per batch).
+        const int cost = gl == 1 ? rounds * (per_lane + 3 * lg) : rounds * (4 * ((per_lane + 7) / 8) + lg);
         if (cost < best_cost) {
             best_cost = cost;
             best = lg + 1;
@@ -753,6 +758,22 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
         const int e = r < nrows ? rend[r] : nnzt;
         double2 acc = make_double2(0.0, 0.0);
         int k = s0 + sub;
+        // batches of 8 panel-row gathers in flight per lane (the SpMM is gather-latency bound:
+        // bytes in flight per CU set its rate), then 4, then singles; sums stay in order
+        for (; k + 7 * Gp < e; k += 8 * Gp) {
+            double v[8];
+            double2 xv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                v[u] = s_val[k + u * Gp];
+                xv[u] = panel(s_col[k + u * Gp]);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                acc.x += v[u] * xv[u].x;
+                acc.y += v[u] * xv[u].y;
+            }
+        }
         for (; k + 3 * Gp < e; k += 4 * Gp) {
             const int c0 = s_col[k], c1 = s_col[k + Gp], c2 = s_col[k + 2 * Gp], c3 = s_col[k + 3 * Gp];
             const double v0 = s_val[k], v1 = s_val[k + Gp], v2 = s_val[k + 2 * Gp], v3 = s_val[k + 3 * Gp];
@@ -804,7 +825,7 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
 // Multi right-hand side (L = 2..16, row-major panels).  A group of L/2 lanes owns one merge
 // walk; each lane keeps a double2 of the L running totals (running_total[L],
 // merge_based.hpp:84-127).  TILE = (256/(L/2)) groups * IPTG items.
-template <int L, int IPTG, int MODE>
+template <int L, int IPTG, int MODE, bool NT>
 __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
 {
     constexpr bool CG = MODE == kModeCg;
@@ -844,8 +865,8 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
     for (int j = 0; j < STG; ++j) {
         const int k = tid + j * kBlock;
         if (k < nnzt) {
-            s_col[k] = ld_stream<MODE == kModeSpmv>(a.cols + n0 + k);
-            s_val[k] = ld_stream<MODE == kModeSpmv>(a.vals + n0 + k);
+            s_col[k] = ld_stream<NT>(a.cols + n0 + k);
+            s_val[k] = ld_stream<NT>(a.vals + n0 + k);
         }
     }
     __syncthreads();
@@ -1400,17 +1421,17 @@ __global__ void k_flush(double *p, long long n, double v)
 // ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
-constexpr int kIptgSpmm = 8;  // items per lane group for SpMM tiles
 
 // SpMV tuning: items per thread (tile = 256 * ipt merge items) and nontemporal matrix loads.
 // Defaults are the measured best; MSPMV_SPMV_IPT / MSPMV_SPMV_NT override them for A/B runs.
 struct SpmvTuning {
     int ipt = 8;
-    int nt = 1;
+    int nt = -1;      // nontemporal matrix loads: -1 auto (matrix > kNtBytes), 0 never, 1 always
+    int spmm_iptg = 0;  // merge items per lane group of the SpMM tiles (8, 16, 32; 0: per L)
     int persist = 0;  // persistent software-pipelined kernel (VGPR-bound at 4 waves/SIMD: slower)
     int bpc = 0;      // resident workgroups per CU for the persistent grid (0: occupancy query)
     int rg_cost = 48; // k_tile_modes budget for row-group tiles (0: merge walk everywhere)
-    int spmm_rg_cost = 48;  // the same for the multi-RHS kernels
+    int spmm_rg_cost = -1;  // the same for the multi-RHS kernels (-1: scaled to the SpMM tile)
 };
 static const SpmvTuning &spmv_tuning()
 {
@@ -1422,7 +1443,12 @@ static const SpmvTuning &spmv_tuning()
                 v.ipt = i;
         }
         if (const char *e = getenv("MSPMV_SPMV_NT"))
-            v.nt = atoi(e) != 0;
+            v.nt = atoi(e) < 0 ? -1 : atoi(e) != 0;
+        if (const char *e = getenv("MSPMV_SPMM_IPTG")) {
+            const int i = atoi(e);
+            if (i == 8 || i == 16 || i == 32)
+                v.spmm_iptg = i;
+        }
         if (const char *e = getenv("MSPMV_SPMV_PERSIST"))
             v.persist = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMV_BPC"))
@@ -1436,21 +1462,37 @@ static const SpmvTuning &spmv_tuning()
     return t;
 }
 
-const char *spmv_kernel_name()
+// Nontemporal policy for the matrix stream: a matrix larger than kNtBytes cannot stay in the
+// 256 MiB Infinity Cache across calls anyway, so its lines are not allowed to evict x / X.
+constexpr double kNtBytes = 128.0 * 1024 * 1024;
+bool stream_nt(const mspmv_handle_s *h)
 {
-    static std::string name = [] {
-        const SpmvTuning &t = spmv_tuning();
-        return std::string(t.persist ? "k_spmv_persist<" : "k_spmv_tile<") + std::to_string(t.ipt) + ",0," +
-               (t.nt ? "true>" : "false>");
-    }();
-    return name.c_str();
+    const int nt = spmv_tuning().nt;
+    if (nt >= 0)
+        return nt != 0;
+    return 12.0 * (double)h->nnz + 4.0 * (double)h->m > kNtBytes;
+}
+
+std::string spmv_kernel_name(const mspmv_handle_s *h)
+{
+    const SpmvTuning &t = spmv_tuning();
+    return std::string(t.persist ? "k_spmv_persist<" : "k_spmv_tile<") + std::to_string(t.ipt) + ",0," +
+           (stream_nt(h) ? "true>" : "false>");
+}
+
+// SpMM tile depth: measured best 8 items per lane group for L <= 4 (fem-blocked pwtk shape,
+// L = 4: 55.6 vs 74.8 us at 16) and 16 for L >= 8 (nlpkkt120 shape, L = 8: 549 vs 741 us).
+int spmm_iptg_for(int L)
+{
+    const int i = spmv_tuning().spmm_iptg;
+    return i ? i : (L >= 8 ? 16 : 8);
 }
 
 int tile_items_for(int L)
 {
     if (L == 1)
         return kBlock * spmv_tuning().ipt;
-    return (kBlock / (L / 2)) * kIptgSpmm;
+    return (kBlock / (L / 2)) * spmm_iptg_for(L);
 }
 
 bool supported_L(int L) { return L == 1 || L == 2 || L == 4 || L == 8 || L == 16; }
@@ -1478,7 +1520,9 @@ hipError_t launch_tile_modes(const int *d_row_offsets, const int2 *d_bounds, con
 {
     if (num_tiles == 0)
         return hipSuccess;
-    const int cost = L == 1 ? spmv_tuning().rg_cost : spmv_tuning().spmm_rg_cost;
+    const SpmvTuning &tu = spmv_tuning();
+    // SpMM budget: twice the walk's gather chunks (4 steps each) plus its search
+    const int cost = L == 1 ? tu.rg_cost : tu.spmm_rg_cost >= 0 ? tu.spmm_rg_cost : 2 * (4 * (spmm_iptg_for(L) / 4) + 2);
     hipLaunchKernelGGL(k_tile_modes, dim3((num_tiles + 255) / 256), dim3(256), 0, s, d_row_offsets, d_bounds, d_split,
                        num_tiles, L == 1 ? 1 : L / 2, cost, d_modes);
     return hipGetLastError();
@@ -1519,13 +1563,12 @@ static void persist_grid(K kernel, int num_tiles, int num_cus, int bpc, int *gri
 }
 
 template <int MODE>
-static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_cus)
+static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_cus, bool nt)
 {
     const dim3 grid(a.num_tiles), block(kBlock);
+    const SpmvTuning &tu = spmv_tuning();
     switch (L) {
     case 1: {
-        const SpmvTuning &tu = spmv_tuning();
-        const bool nt = MODE == kModeSpmv && tu.nt;  // CG re-reads A every iteration: default policy
 #define MSPMV_LAUNCH_PERSIST(I, NTV)                                                               \
     do {                                                                                           \
         int g = 0, tpb = 0;                                                                        \
@@ -1555,10 +1598,27 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_c
 #undef MSPMV_LAUNCH_PERSIST
         break;
     }
-    case 2: hipLaunchKernelGGL((k_spmm_tile<2, kIptgSpmm, MODE>), grid, block, 0, s, a); break;
-    case 4: hipLaunchKernelGGL((k_spmm_tile<4, kIptgSpmm, MODE>), grid, block, 0, s, a); break;
-    case 8: hipLaunchKernelGGL((k_spmm_tile<8, kIptgSpmm, MODE>), grid, block, 0, s, a); break;
-    case 16: hipLaunchKernelGGL((k_spmm_tile<16, kIptgSpmm, MODE>), grid, block, 0, s, a); break;
+#define MSPMV_SPMM_NT(LL, I)                                                                       \
+    if (nt)                                                                                        \
+        hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, true>), grid, block, 0, s, a);                 \
+    else                                                                                           \
+        hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, false>), grid, block, 0, s, a);
+#define MSPMV_SPMM_CASE(LL)                                                                        \
+    case LL:                                                                                       \
+        if (spmm_iptg_for(LL) == 32) {                                                             \
+            MSPMV_SPMM_NT(LL, 32)                                                                  \
+        } else if (spmm_iptg_for(LL) == 16) {                                                      \
+            MSPMV_SPMM_NT(LL, 16)                                                                  \
+        } else {                                                                                   \
+            MSPMV_SPMM_NT(LL, 8)                                                                   \
+        }                                                                                          \
+        break;
+        MSPMV_SPMM_CASE(2)
+        MSPMV_SPMM_CASE(4)
+        MSPMV_SPMM_CASE(8)
+        MSPMV_SPMM_CASE(16)
+#undef MSPMV_SPMM_CASE
+#undef MSPMV_SPMM_NT
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1568,7 +1628,7 @@ hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const 
 {
     if (plan.num_tiles == 0)
         return hipSuccess;
-    return launch_tile<kModeSpmv>(make_args(h, plan, d_X, d_Y, L), L, h->stream, h->num_cus);
+    return launch_tile<kModeSpmv>(make_args(h, plan, d_X, d_Y, L), L, h->stream, h->num_cus, stream_nt(h));
 }
 
 hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L)
@@ -1687,7 +1747,7 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
     ta.partials = h->d_partials;
     ta.gtickets = h->d_gtickets;
     ta.dot_out = h->d_red;
-    if ((e = launch_tile<kModeDot>(ta, L, h->stream, h->num_cus)) != hipSuccess)
+    if ((e = launch_tile<kModeDot>(ta, L, h->stream, h->num_cus, stream_nt(h))) != hipSuccess)
         return e;
     if ((e = launch_fixup_ctrl(h, plan, h->d_ap, L)) != hipSuccess)
         return e;
@@ -1719,7 +1779,7 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *
     ta.conv = h->d_conv;
     ta.partials = h->d_partials;
     ta.gtickets = h->d_gtickets;
-    hipError_t e = launch_tile<kModeCg>(ta, L, h->stream, h->num_cus);
+    hipError_t e = launch_tile<kModeCg>(ta, L, h->stream, h->num_cus, stream_nt(h));
     if (e != hipSuccess)
         return e;
     if (plan.num_carries) {
@@ -1795,7 +1855,7 @@ hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double
     ta.partials = partials;
     ta.gtickets = gtickets;
     ta.dot_out = dot_out;
-    hipError_t e = launch_tile<kModeDot>(ta, L, h->stream, h->num_cus);
+    hipError_t e = launch_tile<kModeDot>(ta, L, h->stream, h->num_cus, stream_nt(h));
     if (e != hipSuccess || plan.num_carries == 0)
         return e;
     const int n = plan.num_carries * L;

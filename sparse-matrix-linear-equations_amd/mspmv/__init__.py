@@ -87,7 +87,7 @@ _SIGS = {
                                        _PD, _PD, _PI]),
     "mspmv_tile_plan": (_I, [_P, _I, _PI, _PI, _PI, ctypes.POINTER(Coord)]),
     "mspmv_tile_modes": (_I, [_P, _I, _P]),
-    "mspmv_spmv_kernel_name": (ctypes.c_char_p, []),
+    "mspmv_spmv_kernel_name": (ctypes.c_char_p, [_P]),
     "mspmv_device_malloc": (_I, [_I, _SZ, ctypes.POINTER(_P)]),
     "mspmv_device_free": (_I, [_P]),
     "mspmv_memcpy_h2d": (_I, [_P, _P, _SZ]),
@@ -342,6 +342,10 @@ class GpuCsr:
         _check(lib.mspmv_tile_modes(self.h, L, _ptr(modes)), "tile_modes")
         return {"num_tiles": nt.value, "tile_items": ti.value, "num_carries": nc.value, "bounds": bounds,
                 "modes": modes[: nt.value]}
+
+    def kernel_name(self) -> str:
+        """The single-RHS SpMV kernel instantiation used for this matrix (rocprofv3's name)."""
+        return lib.mspmv_spmv_kernel_name(self.h).decode()
 
     def spmv(self, x: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(x, np.float64)

@@ -29,7 +29,8 @@ def child():
         a = mspmv.CsrMatrix.synth_stencil(1, 160 * 135 * 164, 160, 135, 164, diag_shift=1e-2)
         L = 8
     n = a.num_rows
-    out = {"ipt": os.environ.get("MSPMV_SPMV_IPT"), "rg": os.environ.get("MSPMV_SPMV_RG_COST"), "shape": which, "L": L}
+    out = {"ipt": os.environ.get("MSPMV_SPMV_IPT"), "rg": os.environ.get("MSPMV_SPMV_RG_COST"),
+           "iptg": os.environ.get("MSPMV_SPMM_IPTG"), "shape": which, "L": L}
     with mspmv.GpuCsr(a) as g:
         dx = mspmv.DeviceBuffer.from_array(np.random.default_rng(1).uniform(0, 1, n * L))
         dy = mspmv.DeviceBuffer(8 * n * L)
@@ -49,10 +50,10 @@ def child():
 
 
 def parent():
-    spec = os.environ.get("PROBE_VARIANTS", "8:48,4:48,2:48")
+    spec = os.environ.get("PROBE_VARIANTS", "8:48,4:48,2:48")   # ipt:rg[:spmm_iptg]
     for v in spec.split(","):
-        ipt, rg = v.split(":")
-        env = dict(os.environ, MSPMV_SPMV_IPT=ipt, MSPMV_SPMV_RG_COST=rg)
+        f = v.split(":")
+        env = dict(os.environ, MSPMV_SPMV_IPT=f[0], MSPMV_SPMV_RG_COST=f[1], MSPMV_SPMM_IPTG=f[2] if len(f) > 2 else "0")
         r = subprocess.run([sys.executable, __file__, "--child"], env=env, capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
             print(f"variant {v} failed rc={r.returncode}: {r.stderr[-400:]}", flush=True)

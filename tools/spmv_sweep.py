@@ -43,20 +43,24 @@ def child():
     modes = np.bincount(a0.tile_plan(L)["modes"], minlength=8).tolist()
     print(json.dumps({"ipt": os.environ.get("MSPMV_SPMV_IPT"), "nt": os.environ.get("MSPMV_SPMV_NT"),
                       "persist": os.environ.get("MSPMV_SPMV_PERSIST"), "bpc": os.environ.get("MSPMV_SPMV_BPC"),
-                      "rg": os.environ.get("MSPMV_SPMV_RG_COST"), "L": L, "shape": shape, "modes": modes,
+                      "rg": os.environ.get("MSPMV_SPMV_RG_COST"), "iptg": os.environ.get("MSPMV_SPMM_IPTG"), "L": L, "shape": shape, "modes": modes,
                       "cold_kernel_us": round(kern * 1e3, 2), "cold_GBps": round(nbytes / kern / 1e6, 1),
                       "step_us": round(step * 1e3, 2), "hot_kernel_us": round(hot_kern * 1e3, 2),
                       "hot_GBps": round(nbytes / hot_kern / 1e6, 1)}), flush=True)
 
 
 def parent():
-    spec = os.environ.get("SWEEP_VARIANTS", "8:1:1:0:0,8:1:1:0:48")   # ipt:nt:persist:bpc[:rg_cost]
-    variants = [tuple(int(x) for x in (v + ":48").split(":")[:5]) for v in spec.split(",")]
+    spec = os.environ.get("SWEEP_VARIANTS", "8:1:0:0:0,8:1:0:0:48")   # ipt:nt:persist:bpc[:rg_cost[:spmm_iptg]]
+    variants = []
+    for v in spec.split(","):
+        f = [int(x) for x in v.split(":")]
+        variants.append(tuple(f + [48, 0][len(f) - 4:]) if len(f) < 6 else tuple(f[:6]))
     rounds = int(os.environ.get("SWEEP_ROUNDS", "2"))
     for r in range(rounds):
-        for ipt, nt, persist, bpc, rg in variants:
+        for ipt, nt, persist, bpc, rg, iptg in variants:
             env = dict(os.environ, MSPMV_SPMV_IPT=str(ipt), MSPMV_SPMV_NT=str(nt), MSPMV_SPMV_PERSIST=str(persist),
-                       MSPMV_SPMV_BPC=str(bpc), MSPMV_SPMV_RG_COST=str(rg), MSPMV_SPMM_RG_COST=str(rg))
+                       MSPMV_SPMV_BPC=str(bpc), MSPMV_SPMV_RG_COST=str(rg), MSPMV_SPMM_RG_COST=str(rg if rg <= 0 else -1),
+                       MSPMV_SPMM_IPTG=str(iptg))
             out = subprocess.run([sys.executable, __file__, "--child"], env=env, capture_output=True, text=True,
                                  timeout=300)
             if out.returncode != 0:
