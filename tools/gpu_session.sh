@@ -32,15 +32,15 @@ for s in $STEPS; do
         rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -5 "$OUT/bench.err"; stop_unless_ok $rc bench ;;
     prof)
         timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench \
-            -- python3 bench.py >"$OUT/prof_bench.json" 2>"$OUT/prof.err"
+            -- python3 bench.py --no-cpu --no-cg --no-extras >"$OUT/prof_bench.json" 2>"$OUT/prof.err"
         rc=$?; echo "prof rc=$rc"; find "$OUT/prof" -name "*kernel_stats.csv" | head -3
         stop_unless_ok $rc prof ;;
     pmc)
         timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o bench \
-            -- python3 bench.py --no-cpu --no-cg >"$OUT/pmc_fetch.json" 2>"$OUT/pmc_fetch.err"
+            -- python3 bench.py --no-cpu --no-cg --no-extras >"$OUT/pmc_fetch.json" 2>"$OUT/pmc_fetch.err"
         rc=$?; echo "pmc fetch rc=$rc"; stop_unless_ok $rc pmc_fetch
         timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o bench \
-            -- python3 bench.py --no-cpu --no-cg >"$OUT/pmc_write.json" 2>"$OUT/pmc_write.err"
+            -- python3 bench.py --no-cpu --no-cg --no-extras >"$OUT/pmc_write.json" 2>"$OUT/pmc_write.err"
         rc=$?; echo "pmc write rc=$rc"; stop_unless_ok $rc pmc_write ;;
     *)
         echo "unknown step $s"; exit 2 ;;
