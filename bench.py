@@ -11,8 +11,9 @@ are resident in HBM before the timed region.
 
   value        = 2 * nnz * batch * steps * n_gpus / max-over-ranks(time)  [GFLOP/s, whole job]
   roofline     = algorithmic bytes per SpMV launch, 12 nnz + 4 (m+1) + 8 n + 8 m,
-                 / the merge-tile kernel's average duration from HIP events recorded around
-                 every launch on its stream inside the timed region; peak 8 TB/s HBM3E
+                 / the merge-tile kernel's average duration: HIP events on its stream around
+                 the timed region / launches in it (every launch of a pwtk-shaped step is a
+                 tile kernel; the ~1.5 us launch boundary is included); peak 8 TB/s HBM3E
   cpu_baseline = the reference's own merge CsrMV (work_2025 OmpMergeCsrmm with num_vectors = 1,
                  == cpu_spmv.cpp OmpMergeCsrmv) compiled from /root/reference into oracle/_ref,
                  else the oracle port; host cores, ~10 s on matrix #0 (rank 0, N = 1 only)
@@ -225,8 +226,8 @@ def run_cg_multi(d, dev):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")

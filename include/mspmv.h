@@ -140,9 +140,11 @@ MSPMV_API mspmv_status mspmv_dcg_multi_dev(mspmv_handle h, const double *d_B, do
 MSPMV_API mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y, int L, int reps,
                                  size_t flush_bytes, double *avg_ms);
 /* Batch form for benchmarks: `reps` steps, each step one SpMM launch per handle (all handles
- * on one device), every launch enqueued on hs[0]'s stream and bracketed by HIP events.
- * *step_ms = average event time per step; *tile_kernel_ms = average duration of one merge
- * tile kernel launch; *kernels_per_step = launches per step (tile + fix-up kernels). */
+ * on one device), every launch enqueued back to back on hs[0]'s stream, HIP events only
+ * around the whole region.  *step_ms = average event time per step; *tile_kernel_ms =
+ * average duration of one merge tile kernel launch: region time / launches when a step holds
+ * only tile kernels (the launch boundary included), else from a second pass that brackets
+ * every tile launch with events; *kernels_per_step = launches per step (tile + fix-up). */
 MSPMV_API mspmv_status mspmv_time_spmm_batch_dev(int count, const mspmv_handle *hs, const double *const *d_X,
                                                  double *const *d_Y, int L, int reps, double *step_ms,
                                                  double *tile_kernel_ms, int *kernels_per_step);

@@ -839,38 +839,55 @@ mspmv_status mspmv_time_spmm_batch_dev(int count, const mspmv_handle *hs, const 
     hipStream_t s = hs[0]->stream;
     for (int i = 0; i < count; ++i)  // everything after this point is ordered on hs[0]'s stream
         HIP_TRY(hipStreamSynchronize(hs[i]->stream));
-    const size_t nev = (size_t)reps * count * 2 + 2;
+    // Pass 1 (the timed steps): launches back to back, events only around the whole region.
+    // Pass 2 (only when a step also holds fix-up kernels): events around every tile launch.
+    const bool has_fixups = kps > count;
+    const size_t nev = 2 + (has_fixups && tile_kernel_ms ? (size_t)reps * count * 2 : 0);
     std::vector<hipEvent_t> ev(nev, nullptr);
     for (auto &e : ev)
         HIP_TRY(hipEventCreate(&e));
-    hipError_t e = hipEventRecord(ev[nev - 2], s);
-    size_t k = 0;
+    hipError_t e = hipEventRecord(ev[0], s);
     for (int r = 0; r < reps && e == hipSuccess; ++r)
         for (int i = 0; i < count && e == hipSuccess; ++i) {
             hipStream_t own = hs[i]->stream;
             hs[i]->stream = s;
-            e = hipEventRecord(ev[k++], s);
-            if (e == hipSuccess)
-                e = launch_spmm_tile_only(hs[i], *plans[i], d_X[i], d_Y[i], L);
-            if (e == hipSuccess)
-                e = hipEventRecord(ev[k++], s);
+            e = launch_spmm_tile_only(hs[i], *plans[i], d_X[i], d_Y[i], L);
             if (e == hipSuccess)
                 e = launch_fixup(hs[i], *plans[i], d_Y[i], L);
             hs[i]->stream = own;
         }
     if (e == hipSuccess)
-        e = hipEventRecord(ev[nev - 1], s);
+        e = hipEventRecord(ev[1], s);
     if (e == hipSuccess)
-        e = hipEventSynchronize(ev[nev - 1]);
-    double sum = 0.0;
-    float ms = 0.f;
-    for (size_t j = 0; j + 1 < k && e == hipSuccess; j += 2) {
-        e = hipEventElapsedTime(&ms, ev[j], ev[j + 1]);
-        sum += ms;
-    }
+        e = hipEventSynchronize(ev[1]);
     float total = 0.f;
     if (e == hipSuccess)
-        e = hipEventElapsedTime(&total, ev[nev - 2], ev[nev - 1]);
+        e = hipEventElapsedTime(&total, ev[0], ev[1]);
+    double sum = (double)total;  // no fix-ups: every launch of the region is a tile kernel
+    size_t k = 2;
+    if (e == hipSuccess && nev > 2) {
+        for (int r = 0; r < reps && e == hipSuccess; ++r)
+            for (int i = 0; i < count && e == hipSuccess; ++i) {
+                hipStream_t own = hs[i]->stream;
+                hs[i]->stream = s;
+                e = hipEventRecord(ev[k++], s);
+                if (e == hipSuccess)
+                    e = launch_spmm_tile_only(hs[i], *plans[i], d_X[i], d_Y[i], L);
+                if (e == hipSuccess)
+                    e = hipEventRecord(ev[k++], s);
+                if (e == hipSuccess)
+                    e = launch_fixup(hs[i], *plans[i], d_Y[i], L);
+                hs[i]->stream = own;
+            }
+        if (e == hipSuccess)
+            e = hipEventSynchronize(ev[k - 1]);
+        sum = 0.0;
+        float ms = 0.f;
+        for (size_t j = 2; j + 1 < k && e == hipSuccess; j += 2) {
+            e = hipEventElapsedTime(&ms, ev[j], ev[j + 1]);
+            sum += ms;
+        }
+    }
     for (auto &x : ev)
         (void)hipEventDestroy(x);
     if (e != hipSuccess) {

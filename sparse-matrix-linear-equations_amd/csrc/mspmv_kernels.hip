@@ -18,6 +18,9 @@
 //     sees one contiguous band of x / X.
 #include "mspmv_internal.h"
 
+#ifndef MSPMV_LAB_ABLATE
+#define MSPMV_LAB_ABLATE 0
+#endif
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -303,6 +306,7 @@ struct TileArgs {
     double *partials;                  // CG: per-slot partial dots [slot][L], then level 2 [group][L]
     unsigned *gtickets;                // CG: per-group tickets of reduce_slots (self-resetting)
     double *dot_out;                   // MODE 2: the reduced x.(Ax) per column [L]
+    int m;                             // rows (row_offsets holds m + 1 entries)
 };
 
 // Tile-kernel modes.
@@ -338,7 +342,13 @@ __device__ __forceinline__ void stage_products(const TileArgs &a, int n0, int nn
     double xv[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
+#if MSPMV_LAB_ABLATE & 1
+        xv[j] = (double)c[j];
+#elif MSPMV_LAB_ABLATE & 8
+        xv[j] = a.x[c[j] & 1023];
+#else
         xv[j] = a.x[c[j]];
+#endif
     if (CG) {
         double pv[NJ];
 #pragma unroll
@@ -379,7 +389,7 @@ struct SpmvSmem {
 // LDS free for the next tile.
 template <int IPT, int MODE>
 __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT> &sm, int t, int r0, int n0, int nrows,
-                                          int nnzt, double beta, double &dot)
+                                          int nnzt, bool tail, double beta, double &dot)
 {
     constexpr int MAXJ = SpmvSmem<IPT>::MAXJ;
     const int tid = threadIdx.x;
@@ -465,7 +475,7 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT> &sm, 
             acc += sm.cval[u];
         write_row(prow, acc + pval);
     }
-    if (tid == kBlock - 1 && a.split[t + 1]) {  // the tile's trailing partial row -> carry
+    if (tid == kBlock - 1 && tail) {  // the tile's trailing partial row -> carry
         int j0 = kBlock - 1;
         while (j0 > 0 && sm.crow[j0 - 1] == nrows)
             --j0;
@@ -485,20 +495,25 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT> &sm, 
 // Row-group reduction of one tile whose products and row ends are in LDS (mode lg + 1 of
 // k_tile_modes): groups of G = 2^lg lanes take the tile's row segments round-robin; lane j of
 // a group sums products j, j+G, ... of the segment in order from 0.0, then a fixed xor
-// butterfly folds the group and its lane 0 writes the row.  G = 1 is the sequential CSR-order
-// sum of SpmvGold (cpu_spmv.cpp:241-265), bit for bit.  A few instructions per product,
-// against the walk's merge search and per-item row-end test, for tiles whose rows are alike.
+// butterfly folds the group.  G = 1 is the sequential CSR-order sum of SpmvGold
+// (cpu_spmv.cpp:241-265), bit for bit.  A few instructions per product, against the walk's
+// merge search and per-item row-end test, for tiles whose rows are alike.
+// Row results go through LDS (sm.cval) and are stored by one thread per row afterwards: one
+// coalesced store per tile, and no global memory operation inside the reduction loop (a loop
+// that only stores makes hipcc drain vmcnt before it, which would wait for the persistent
+// kernel's in-flight prefetch).  xr / pr: x[r0 + tid] and p_old[r0 + tid] (CG / dot modes),
+// loaded by the caller for tid <= nrows.
 template <int IPT, int MODE>
 __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT> &sm, int t, int r0, int nrows,
-                                           int nnzt, double beta, double &dot, int lg)
+                                           int nnzt, bool tail, double beta, double &dot, int lg, double xr,
+                                           double pr)
 {
     const int G = 1 << lg;
     const int tid = threadIdx.x;
     const int *rend = sm.rowend(nnzt);
     const int lane = tid & (G - 1);
-    const bool tail = a.split[t + 1] != 0;
     const int nseg = nrows + (tail ? 1 : 0);
-    for (int r = tid >> lg; r < nseg; r += kBlock >> lg) {  // uniform within a group
+    auto seg_sum = [&](int r) {
         const int s0 = r == 0 ? 0 : rend[r - 1];
         const int e = r < nrows ? rend[r] : nnzt;
         double v = 0.0;
@@ -515,6 +530,16 @@ __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT> &sm,
             v += sm.prod[pslot(k)];
         for (int off = G >> 1; off > 0; off >>= 1)
             v += __shfl_xor(v, off);
+        return v;
+    };
+    const int nfast = min(nseg, kBlock);
+    for (int r = tid >> lg; r < nfast; r += kBlock >> lg) {  // uniform within a group
+        const double v = seg_sum(r);
+        if (lane == 0)
+            sm.cval[r] = v;
+    }
+    for (int r = kBlock + (tid >> lg); r < nseg; r += kBlock >> lg) {  // rare: > kBlock segments
+        const double v = seg_sum(r);
         if (lane == 0) {
             const int R = r0 + r;
             if (r < nrows) {
@@ -526,7 +551,7 @@ __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT> &sm,
                 } else if (MODE == kModeDot) {
                     dot += a.x[R] * v;
                 }
-            } else {  // the trailing partial row -> carry (k_fixup adds it in tile order)
+            } else {
                 a.carry_val[t] = v;
                 if (MODE == kModeCg)
                     dot += (a.x[R] + beta * a.p_old[R]) * v;
@@ -535,19 +560,53 @@ __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT> &sm,
             }
         }
     }
+    __syncthreads();
+    if (tid < nfast) {
+        const double v = sm.cval[tid];
+        if (tid < nrows) {
+            const int R = r0 + tid;
+            a.y[R] = v;
+            if (MODE == kModeCg) {
+                const double pn = xr + beta * pr;
+                a.p_new[R] = pn;
+                dot += pn * v;
+            } else if (MODE == kModeDot) {
+                dot += xr * v;
+            }
+        } else {  // the trailing partial row -> carry (k_fixup adds it in tile order)
+            a.carry_val[t] = v;
+            if (MODE == kModeCg)
+                dot += (xr + beta * pr) * v;
+            else if (MODE == kModeDot)
+                dot += xr * v;
+        }
+    }
     __syncthreads();  // LDS free for the next tile
 }
 
-// One tile's reduction, by its plan-time mode.
+// One tile's reduction, by its plan-time mode (a.rmode[t]); tail = a.split[t + 1].
 template <int IPT, int MODE>
 __device__ __forceinline__ void reduce_tile(const TileArgs &a, SpmvSmem<IPT> &sm, int t, int r0, int n0, int nrows,
-                                            int nnzt, double beta, double &dot)
+                                            int nnzt, int mode, bool tail, double beta, double &dot, double xr,
+                                            double pr)
 {
-    const int mode = a.rmode[t];
     if (mode == 0)
-        walk_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, beta, dot);
+        walk_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, tail, beta, dot);
     else
-        group_tile<IPT, MODE>(a, sm, t, r0, nrows, nnzt, beta, dot, mode - 1);
+        group_tile<IPT, MODE>(a, sm, t, r0, nrows, nnzt, tail, beta, dot, mode - 1, xr, pr);
+}
+
+// x[r0 + tid] and p_old[r0 + tid] for the row-group epilogue (CG / dot modes), tid <= nrows.
+template <int MODE>
+__device__ __forceinline__ void row_operands(const TileArgs &a, int r0, int nrows, double &xr, double &pr)
+{
+    xr = pr = 0.0;
+    if (MODE != kModeSpmv && (int)threadIdx.x <= nrows) {
+        const int R = min(r0 + (int)threadIdx.x, a.m - 1);
+        xr = a.x[R];
+        if (MODE == kModeCg)
+            pr = a.p_old[R];
+    }
 }
 
 // CG epilogue of the single-RHS tile kernels: this block's p.Ap partial -> partials[slot];
@@ -600,8 +659,14 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
     if (MODE != kModeSpmv && a.ctrl->done)
         return;
     const int t = xcd_tile(blockIdx.x, a.num_tiles);
+#if MSPMV_LAB_ABLATE & 4
+    const long long M_ = 217918, NZ_ = 11524432;
+    const int2 b0 = make_int2((int)(t * M_ / a.num_tiles), (int)(t * NZ_ / a.num_tiles));
+    const int2 b1 = make_int2((int)((t + 1) * M_ / a.num_tiles), (int)((t + 1) * NZ_ / a.num_tiles));
+#else
     const int2 b0 = a.bounds[t];
     const int2 b1 = a.bounds[t + 1];
+#endif
     const int r0 = b0.x, n0 = b0.y;
     const int nrows = b1.x - r0;
     const int nnzt = b1.y - n0;
@@ -617,109 +682,138 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
         rend[i] = a.row_offsets[r0 + 1 + i] - n0;
     __syncthreads();
     double dot = 0.0;
-    reduce_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, beta, dot);
+#if MSPMV_LAB_ABLATE & 2
+    if (tid < nrows)
+        a.y[r0 + tid] = sm.prod[tid] + rend[tid];
+    return;
+#endif
+    double xr, pr;
+    row_operands<MODE>(a, r0, nrows, xr, pr);
+    reduce_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, a.rmode[t], a.split[t + 1] != 0, beta, dot, xr, pr);
     if (MODE != kModeSpmv)
         cg_alpha_epilogue<IPT, MODE>(a, sm, t, a.num_tiles, dot);
 }
 
-// Single right-hand side, persistent and software-pipelined: workgroup v (XCD-grouped) walks
-// the contiguous tile run [v*tpb, (v+1)*tpb).  The next tile's (col, val) loads are issued
-// right after the current tile's gathers, so HBM streaming overlaps the gather wait, the LDS
-// staging, the merge searches and the walk of the current tile (vmcnt ordering: the gathers
-// are older than the prefetch, so waiting for them does not wait for the prefetch).
+// Single right-hand side, persistent and software-pipelined.  Workgroup v (XCD-grouped) walks
+// the contiguous tile run [v*tpb, min((v+1)*tpb, T)); its bounds, reduction modes and tail
+// flags are staged in LDS once.  Two register stages (A, B) ping-pong, so no register copy of
+// an in-flight load ever forces a wait: while tile i's x gathers, products and in-tile
+// reduction run, the (col, val) stream and first row ends of tile i+1 are already in flight
+// (issued right after tile i's gathers, so waiting for the gathers -- the older loads -- never
+// waits for the prefetch).  The chain per tile is then gather latency + LDS reduction, with
+// the HBM stream of the next tile underneath it, instead of stream + gather + reduction.
+constexpr int kMaxTpb = 255;
+
+template <int IPT>
+struct PipeStage {
+    int c[IPT];
+    double v[IPT];
+    int re;  // this thread's row end (row tid of the tile), relative to nothing
+};
+
+// Issue one tile's stream: cols first (the gathers wait on them), then vals, then the first
+// round of row ends.  Always issued, clamped into the tile (an empty tile reads its start
+// element, which the kNnzPad padding keeps in bounds), so every path has the same count.
+template <int IPT, bool NT>
+__device__ __forceinline__ void pipe_issue(const TileArgs &a, int m, int2 b0, int2 b1, PipeStage<IPT> &st)
+{
+    const int nz = b1.y - b0.y, nr = b1.x - b0.x;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < IPT; ++j)
+        st.c[j] = ld_stream<NT>(a.cols + b0.y + max(min(tid + j * kBlock, nz - 1), 0));
+#pragma unroll
+    for (int j = 0; j < IPT; ++j)
+        st.v[j] = ld_stream<NT>(a.vals + b0.y + max(min(tid + j * kBlock, nz - 1), 0));
+    st.re = a.row_offsets[min(b0.x + 1 + max(min(tid, nr - 1), 0), m)];
+}
+
 template <int IPT, int MODE, bool NT>
-__global__ __launch_bounds__(kBlock) void k_spmv_persist(TileArgs a, int tpb)
+__device__ __forceinline__ void pipe_tile(const TileArgs &a, SpmvSmem<IPT> &sm, const int2 *s_b,
+                                          const unsigned char *s_mode, int m, int i, int ntl, int t,
+                                          PipeStage<IPT> &cur, PipeStage<IPT> &nxt, double beta, double &dot)
 {
     constexpr bool CG = MODE == kModeCg;
     constexpr int TILE = SpmvSmem<IPT>::TILE;
+    const int tid = threadIdx.x;
+    const int2 b0 = s_b[i], b1 = s_b[i + 1], b2 = s_b[min(i + 2, ntl)];
+    const int r0 = b0.x, n0 = b0.y;
+    const int nrows = b1.x - r0;
+    const int nnzt = b1.y - n0;
+    // (1) this tile's gathers (cur.c arrived: only loads issued before it are waited for)
+    double xv[IPT], pv[IPT];
+#pragma unroll
+    for (int j = 0; j < IPT; ++j)
+        xv[j] = a.x[cur.c[j]];
+    if (CG) {
+#pragma unroll
+        for (int j = 0; j < IPT; ++j)
+            pv[j] = a.p_old[cur.c[j]];
+    }
+    double xr, pr;  // CG / dot epilogue operands: issued before the prefetch, so waits stay counted
+    row_operands<MODE>(a, r0, nrows, xr, pr);
+    // (2) the next tile's stream, under this tile's gather wait and reduction
+    pipe_issue<IPT, NT>(a, m, b1, b2, nxt);
+    // (3) products and row ends to LDS
+#pragma unroll
+    for (int j = 0; j < IPT; ++j) {
+        const int k = tid + j * kBlock;
+        double x = xv[j];
+        if (CG)
+            x = x + beta * pv[j];
+        if (k < nnzt)
+            sm.prod[pslot(k)] = cur.v[j] * x;
+    }
+    if (nnzt > TILE) {  // rare: nonzeros snapped in beyond the nominal tile (direct loads)
+        for (int k = TILE + tid; k < nnzt; k += kBlock) {
+            const int col = a.cols[n0 + k];
+            double x = a.x[col];
+            if (CG)
+                x = x + beta * a.p_old[col];
+            sm.prod[pslot(k)] = a.vals[n0 + k] * x;
+        }
+    }
+    int *rend = sm.rowend(nnzt);
+    if (tid < nrows)
+        rend[tid] = cur.re - n0;
+    for (int r = kBlock + tid; r < nrows; r += kBlock)  // rare: > 256 rows in the tile
+        rend[r] = a.row_offsets[r0 + 1 + r] - n0;
+    __syncthreads();
+    const unsigned char mt = s_mode[i];
+    reduce_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, mt & 0x7f, (mt & 0x80) != 0, beta, dot, xr, pr);
+}
+
+template <int IPT, int MODE, bool NT>
+__global__ __launch_bounds__(kBlock) void k_spmv_persist(TileArgs a, int tpb)
+{
     __shared__ SpmvSmem<IPT> sm;
+    __shared__ int2 s_b[kMaxTpb + 1];
+    __shared__ unsigned char s_mode[kMaxTpb + 1];  // reduction mode | 0x80 when the tile has a tail
     const int tid = threadIdx.x;
     if (MODE != kModeSpmv && a.ctrl->done)
         return;
     const int T = a.num_tiles;
     const int v = xcd_tile(blockIdx.x, gridDim.x);
     const int t_begin = min(v * tpb, T), t_end = min(t_begin + tpb, T);
-    const double beta = CG ? a.scal[0].beta : 0.0;
+    const int ntl = t_end - t_begin;
+    const double beta = MODE == kModeCg ? a.scal[0].beta : 0.0;
+    if (tid <= ntl) {
+        s_b[tid] = a.bounds[t_begin + tid];
+        if (tid < ntl)
+            s_mode[tid] = (unsigned char)(a.rmode[t_begin + tid] | (a.split[t_begin + tid + 1] ? 0x80 : 0));
+    }
+    __syncthreads();
     double dot = 0.0;
-    if (t_begin < t_end) {
-        int2 b0 = a.bounds[t_begin];
-        int2 b1 = a.bounds[t_begin + 1];
-        int c[IPT];
-        double vv[IPT];
-        {
-            const int nz = b1.y - b0.y;
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                const int k = max(min(tid + j * kBlock, nz - 1), 0);
-                c[j] = ld_stream<NT>(a.cols + b0.y + k);
-                vv[j] = ld_stream<NT>(a.vals + b0.y + k);
-            }
+    if (ntl > 0) {
+        PipeStage<IPT> A, B;
+        pipe_issue<IPT, NT>(a, a.m, s_b[0], s_b[1], A);
+        int i = 0;
+        for (; i + 1 < ntl; i += 2) {
+            pipe_tile<IPT, MODE, NT>(a, sm, s_b, s_mode, a.m, i, ntl, t_begin + i, A, B, beta, dot);
+            pipe_tile<IPT, MODE, NT>(a, sm, s_b, s_mode, a.m, i + 1, ntl, t_begin + i + 1, B, A, beta, dot);
         }
-        for (int t = t_begin; t < t_end; ++t) {
-            const int r0 = b0.x, n0 = b0.y;
-            const int nrows = b1.x - r0;
-            const int nnzt = b1.y - n0;
-            // (1) this tile's first round of row ends and its gathers (oldest loads first)
-            const int re0 = nrows > 0 ? a.row_offsets[r0 + 1 + min(tid, nrows - 1)] : 0;
-            double xv[IPT], pv[IPT];
-            if (nnzt > 0) {  // block-uniform (an all-empty tile may sit where x has no entries)
-#pragma unroll
-                for (int j = 0; j < IPT; ++j)
-                    xv[j] = a.x[c[j]];
-                if (CG) {
-#pragma unroll
-                    for (int j = 0; j < IPT; ++j)
-                        pv[j] = a.p_old[c[j]];
-                }
-            }
-            // (2) prefetch the next tile's (col, val) -- always issued (clamped) so the
-            //     compiler's vmcnt accounting stays exact on every path
-            const int2 b2 = a.bounds[min(t + 2, T)];
-            int cn[IPT];
-            double vn[IPT];
-            {
-                const int nz = b2.y - b1.y;
-#pragma unroll
-                for (int j = 0; j < IPT; ++j) {
-                    const int k = max(min(tid + j * kBlock, nz - 1), 0);
-                    cn[j] = ld_stream<NT>(a.cols + b1.y + k);
-                    vn[j] = ld_stream<NT>(a.vals + b1.y + k);
-                }
-            }
-            // (3) products and row ends to LDS
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                const int k = tid + j * kBlock;
-                double x = xv[j];
-                if (CG)
-                    x = x + beta * pv[j];
-                if (k < nnzt)
-                    sm.prod[pslot(k)] = vv[j] * x;
-            }
-            if (nnzt > TILE) {  // rare: a snapped-in tail beyond the prefetched rounds
-                for (int k = TILE + tid; k < nnzt; k += kBlock) {
-                    const int col = a.cols[n0 + k];
-                    double x = a.x[col];
-                    if (CG)
-                        x = x + beta * a.p_old[col];
-                    sm.prod[pslot(k)] = a.vals[n0 + k] * x;
-                }
-            }
-            int *rend = sm.rowend(nnzt);
-            if (tid < nrows)
-                rend[tid] = re0 - n0;
-            for (int i = kBlock + tid; i < nrows; i += kBlock)  // rare: > 256 rows in the tile
-                rend[i] = a.row_offsets[r0 + 1 + i] - n0;
-            __syncthreads();
-            reduce_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, beta, dot);
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                c[j] = cn[j];
-                vv[j] = vn[j];
-            }
-            b0 = b1;
-            b1 = b2;
-        }
+        if (i < ntl)
+            pipe_tile<IPT, MODE, NT>(a, sm, s_b, s_mode, a.m, i, ntl, t_begin + i, A, B, beta, dot);
     }
     if (MODE != kModeSpmv)
         cg_alpha_epilogue<IPT, MODE>(a, sm, blockIdx.x, gridDim.x, dot);
@@ -1439,7 +1533,7 @@ static const SpmvTuning &spmv_tuning()
         SpmvTuning v;
         if (const char *e = getenv("MSPMV_SPMV_IPT")) {
             const int i = atoi(e);
-            if (i == 2 || i == 4 || i == 8 || i == 16)
+            if (i == 2 || i == 4 || i == 6 || i == 7 || i == 8 || i == 16)
                 v.ipt = i;
         }
         if (const char *e = getenv("MSPMV_SPMV_NT"))
@@ -1532,6 +1626,7 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
 {
     TileArgs a{};
     a.row_offsets = h->d_row_offsets;
+    a.m = h->m;
     a.cols = h->d_cols;
     a.vals = h->d_vals;
     a.x = X;
@@ -1557,7 +1652,7 @@ static void persist_grid(K kernel, int num_tiles, int num_cus, int bpc, int *gri
     }
     const long long slots = (long long)std::max(num_cus, 1) * bpc;
     int t = (int)((num_tiles + slots - 1) / slots);
-    t = std::max(t, 1);
+    t = std::min(std::max(t, 1), kMaxTpb);  // the kernel stages <= kMaxTpb + 1 bounds in LDS
     *tpb = t;
     *grid = (num_tiles + t - 1) / t;
 }
@@ -1590,6 +1685,8 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_c
         switch (tu.ipt) {
             MSPMV_SPMV_CASE(2)
             MSPMV_SPMV_CASE(4)
+            MSPMV_SPMV_CASE(6)
+            MSPMV_SPMV_CASE(7)
             MSPMV_SPMV_CASE(8)
             MSPMV_SPMV_CASE(16)
         default: return hipErrorInvalidValue;

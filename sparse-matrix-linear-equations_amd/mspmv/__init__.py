@@ -23,7 +23,7 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmspmv.so")
+LIB_PATH = os.environ.get("MSPMV_LIB") or os.path.join(_HERE, "libmspmv.so")  # MSPMV_LIB: A/B builds
 
 SIMPLE, MERGE, NONZERO_SPLIT = 0, 1, 2  # SpmmKernel, work_2025/types.hpp:11-16
 

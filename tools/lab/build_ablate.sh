@@ -1,0 +1,18 @@
+#!/bin/bash
+# Lab builds of libmspmv.so with compile-time ablations of the SpMV tile kernel (measurement only;
+# results are wrong by construction).  MSPMV_LIB=tools/lab/libmspmv_ablN.so selects one.
+#   bit 1: no x gather   bit 2: no in-tile reduction   bit 4: no bounds load (nominal tiles)
+set -e
+cd "$(dirname "$0")/../.."
+C=sparse-matrix-linear-equations_amd/csrc
+make -s -C $C -j8 >/dev/null
+for n in "$@"; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fvisibility=hidden -fopenmp \
+     -Iinclude -DMSPMV_LAB_ABLATE=$n -c $C/mspmv_kernels.hip -o /tmp/abl_$n.o &
+done
+wait
+for n in "$@"; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/lab/libmspmv_abl$n.so /tmp/abl_$n.o \
+     $C/build/mspmv_api.o $C/build/mspmv_dist.o $C/build/mspmv_synth.o $C/build/mspmv_io.o \
+     -fopenmp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+done
