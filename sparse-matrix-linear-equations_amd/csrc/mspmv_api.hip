@@ -387,6 +387,7 @@ mspmv_status mspmv_destroy(mspmv_handle h)
     dev_free(h->d_p1);
     dev_free(h->d_ap);
     dev_free(h->d_partials);
+    dev_free(h->d_partials_b);
     dev_free(h->d_gtickets);
     dev_free(h->d_scal);
     dev_free(h->d_red);
@@ -535,6 +536,8 @@ static mspmv_status ensure_cg_workspace(mspmv_handle_s *h, int L, int nblk, int 
         ST_TRY(dev_alloc(&h->d_partials, pcap));
         h->partials_cap = pcap;
     }
+    if (!h->d_partials_b)
+        ST_TRY(dev_alloc(&h->d_partials_b, (size_t)kUpdateMaxBlocks));
     if (gtickets_capacity(slots) > h->gtickets_cap) {
         dev_free(h->d_gtickets);
         h->gtickets_cap = 0;
@@ -584,14 +587,18 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
         return MSPMV_OK;
     const TilePlan *plan = nullptr;
     ST_TRY(get_plan(h, L, &plan));
-    const int nblk = cg_update_blocks((long long)h->m * L);
+    const bool pipelined = !cg_split_iteration(L);  // single RHS: consumer-side reductions
+    const int nblk = pipelined ? cg1_blocks(h->m) : cg_update_blocks((long long)h->m * L);
     const int cap = hist ? std::max(hist_cap, 0) : 0;
     ST_TRY(ensure_cg_workspace(h, L, nblk, plan->num_tiles, cap));
     const int use_cap = hist ? cap : 0;
     const int saved_cap = h->hist_cap;
     h->hist_cap = use_cap;  // kernels record only what the caller asked for
     HIP_TRY(hipMemsetAsync(h->d_ctrl, 0, sizeof(CgControl), h->stream));
-    HIP_TRY(launch_cg_init(h, d_b, d_x, L, tol, nblk));
+    if (pipelined)
+        HIP_TRY(launch_cg1_init(h, d_b, d_x, nblk));
+    else
+        HIP_TRY(launch_cg_init(h, d_b, d_x, L, tol, nblk));
 
     constexpr int K = 32;  // iterations per graph replay (even: p buffers alternate)
     hipGraph_t graph = nullptr;
@@ -656,6 +663,14 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
             oldest ^= 1;
             if (done)
                 break;
+        }
+    }
+    if (st == MSPMV_OK && pipelined && max_iters > 0) {
+        // the last iteration's stop test (a no-op once the solve has stopped)
+        hipError_t ef = launch_cg1_finish(h, max_iters & 1, nblk);
+        if (ef != hipSuccess) {
+            set_error(std::string("CG finish launch: ") + hipGetErrorString(ef));
+            st = MSPMV_ERR_HIP;
         }
     }
     hipError_t e = hipStreamSynchronize(h->stream);

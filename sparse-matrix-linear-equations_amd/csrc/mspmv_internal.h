@@ -16,7 +16,12 @@ constexpr int kBlock = 256;  // 4 x 64-lane waves per workgroup
 constexpr int kNnzPad = 16;  // padding elements after the last nonzero of the device arrays
 constexpr int kSnapDiv = 8;
 constexpr int kSlotGroup = 32;     // fan-in of the CG partial-reduction tree (reduce_slots)
-constexpr int kTicketStride = 64;  // tickets 256 B apart: one per memory line  // a boundary snaps to its row start if <= tile/kSnapDiv nonzeros deep
+constexpr int kTicketStride = 64;  // tickets 256 B apart: one per memory line
+// Single-RHS pipelined CG (consumer-side reductions): the update kernel sums at most
+// kConsumeTile of the SpMV's p.Ap partials (more are folded by group tickets first), the
+// SpMV sums the update's <= kUpdateMaxBlocks r.r partials.
+constexpr int kConsumeTile = 4096;
+constexpr int kUpdateMaxBlocks = 1024;
 
 // A merge-path tile plan for one nominal tile size (merge items per tile).
 //
@@ -50,6 +55,7 @@ struct CgScalars {
     double beta;
     double pAp;
     double rs_new;
+    double rs_par[2];  // single-RHS pipelined CG: r.r of iteration k at [k & 1] (k_spmv_tile MODE 1)
 };
 
 struct CgControl {
@@ -57,7 +63,8 @@ struct CgControl {
     int done;        // 1 once every column converged (or breakdown)
     int iters_out;   // iteration count to report (the reference's return value)
     int breakdown;   // 1 if p.Ap <= 0 or non-finite was met
-    unsigned reserved[4];  // (formerly single-address tickets; see reduce_slots)
+    int iter_par[2]; // single-RHS pipelined CG: iteration index handed to the next SpMV, by parity
+    unsigned reserved[2];
 };
 
 }  // namespace mspmv
@@ -77,6 +84,7 @@ struct mspmv_handle_s {
     double *d_r = nullptr, *d_p0 = nullptr, *d_p1 = nullptr, *d_ap = nullptr;
     double *d_partials = nullptr;
     size_t partials_cap = 0;
+    double *d_partials_b = nullptr;  // single-RHS pipelined CG: r.r partials of init / update (<= kUpdateMaxBlocks)
     unsigned *d_gtickets = nullptr;  // reduce_slots group tickets (zeroed once, self-resetting)
     size_t gtickets_cap = 0;
     mspmv::CgScalars *d_scal = nullptr;
@@ -122,6 +130,25 @@ hipError_t launch_cg_init(mspmv_handle_s *h, const double *d_b, double *d_x, int
 hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *d_x, int L, int parity, int nblk,
                                double tol);
 int cg_update_blocks(long long elems);
+// Pipelined single-RHS CG (L == 1 unless MSPMV_CG_SPLIT=1): init (x = 0, r = p0 = b, b.b
+// partials) and, after max_iters iterations, the last stop test; grid of cg1_blocks(m).
+bool cg_split_iteration(int L);
+int cg1_blocks(long long m);
+hipError_t launch_cg1_init(mspmv_handle_s *h, const double *d_b, double *d_x, int nblk);
+hipError_t launch_cg1_finish(mspmv_handle_s *h, int parity, int nblk);
+// Offset (doubles) and count of the partials level a consumer sums: levels of a fan-in
+// kSlotGroup tree are folded while more than `stop` partials would remain.
+inline void consumer_level(int nslots, int stop, int L, long long *off, int *count)
+{
+    long long o = 0;
+    int c = nslots;
+    while (c > stop) {
+        o += (long long)c * L;
+        c = (c + kSlotGroup - 1) / kSlotGroup;
+    }
+    *off = o;
+    *count = c;
+}
 
 // Row-sharded CG (mspmv_dist.hip).  CgVecArgs lives in the kernels file; the dist code builds
 // it through this mirror.

@@ -18,9 +18,6 @@
 //     sees one contiguous band of x / X.
 #include "mspmv_internal.h"
 
-#ifndef MSPMV_LAB_ABLATE
-#define MSPMV_LAB_ABLATE 0
-#endif
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -197,6 +194,73 @@ __device__ __forceinline__ bool reduce_slots(double *partials, unsigned *tickets
     }
 }
 
+// Consumer-side reduction (single-RHS pipelined CG).  A producer kernel leaves one partial per
+// workgroup; EVERY workgroup of the consumer kernel sums them itself, in one fixed order (thread
+// tid adds elements tid, tid + 256, ... ascending, then block_sum's fixed tree), so all agree
+// bit for bit and no ticket chain sits in the producer's tail.  The loads are issued early
+// (part_load) and summed late (part_sum), under the consumer's own streaming loads.
+template <int NR>
+struct PartRegs {
+    double v[NR];
+};
+template <int NR>
+__device__ __forceinline__ void part_load(const double *p, int n, PartRegs<NR> &r)
+{
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+        const int i = (int)threadIdx.x + j * kBlock;
+        r.v[j] = i < n ? p[i] : 0.0;
+    }
+}
+template <int NR>
+__device__ __forceinline__ double part_sum(const PartRegs<NR> &r, double *s_red)
+{
+    double v = r.v[0];
+#pragma unroll
+    for (int j = 1; j < NR; ++j)
+        v += r.v[j];
+    return block_sum(v, s_red);
+}
+
+// Publish this workgroup's partial (already stored at partials[slot], agent scope, vmcnt
+// drained, block synchronised) for a consumer kernel that sums at most `stop` of them: while
+// more would remain, groups of kSlotGroup are folded into the next level by their last arriver
+// (reduce_slots' tickets), down to the level consumer_level() names.
+template <int L>
+__device__ __forceinline__ void publish_partials(double *partials, unsigned *tickets, int slot, int nslots, int stop,
+                                                 double *s_tmp, double *s_out, int *s_flag)
+{
+    const int tid = threadIdx.x;
+    double *lvl = partials;
+    int idx = slot, count = nslots;
+    while (count > stop) {
+        const int g = idx / kSlotGroup;
+        const int ngroups = (count + kSlotGroup - 1) / kSlotGroup;
+        const int gsize = min(kSlotGroup, count - g * kSlotGroup);
+        unsigned *tk = &tickets[(size_t)g * kTicketStride];
+        if (tid == 0) {
+            const unsigned v = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *s_flag = v == (unsigned)gsize - 1;
+        }
+        __syncthreads();
+        if (!*s_flag)
+            return;
+        fold_cols<L>(lvl + (size_t)g * kSlotGroup * L, gsize, s_tmp, s_out);
+        if (tid == 0)
+            __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        double *next = lvl + (size_t)count * L;
+        if (tid < L) {
+            store_sc1(&next[(size_t)g * L + tid], s_out[tid]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        tickets += (size_t)ngroups * kTicketStride;
+        lvl = next;
+        idx = g;
+        count = ngroups;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // partition: the reference's partition coordinates and the tile plan boundaries
 // ------------------------------------------------------------------------------------------
@@ -307,6 +371,14 @@ struct TileArgs {
     unsigned *gtickets;                // CG: per-group tickets of reduce_slots (self-resetting)
     double *dot_out;                   // MODE 2: the reduced x.(Ax) per column [L]
     int m;                             // rows (row_offsets holds m + 1 entries)
+    // MODE 1 (single-RHS pipelined CG): the previous update's r.r partials (summed by every
+    // workgroup), the iteration parity, the stop test and the residual history
+    const double *part_in;
+    int n_part_in;
+    int parity;
+    double tol;
+    double *hist;
+    int hist_cap;
 };
 
 // Tile-kernel modes.
@@ -328,42 +400,50 @@ __device__ __forceinline__ int pslot(int k) { return k ^ ((k >> 3) & 7); }
 // columns share cache lines) -- measured 1.4x faster than 16-byte-per-lane blocked loads,
 // whose gathers scatter over 4x more lines.  Every round's loads and gathers are issued
 // before any is consumed (indices past the tile clamp to its last nonzero).
-template <int NJ, bool CG, bool NT>
-__device__ __forceinline__ void stage_products(const TileArgs &a, int n0, int nnzt, double beta, double *s_prod)
-{
+template <int NJ, bool CG>
+struct StageRegs {
     int c[NJ];
     double v[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        const int k = min((int)threadIdx.x + j * kBlock, nnzt - 1);
-        c[j] = ld_stream<NT>(a.cols + n0 + k);
-        v[j] = ld_stream<NT>(a.vals + n0 + k);
-    }
     double xv[NJ];
+    double pv[CG ? NJ : 1];
+};
+template <int NJ, bool CG, bool NT>
+__device__ __forceinline__ void stage_issue(const TileArgs &a, int n0, int nnzt, StageRegs<NJ, CG> &st)
+{
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
-#if MSPMV_LAB_ABLATE & 1
-        xv[j] = (double)c[j];
-#elif MSPMV_LAB_ABLATE & 8
-        xv[j] = a.x[c[j] & 1023];
-#else
-        xv[j] = a.x[c[j]];
-#endif
+        st.c[j] = ld_stream<NT>(a.cols + n0 + min((int)threadIdx.x + j * kBlock, nnzt - 1));
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+        st.v[j] = ld_stream<NT>(a.vals + n0 + min((int)threadIdx.x + j * kBlock, nnzt - 1));
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+        st.xv[j] = a.x[st.c[j]];
     if (CG) {
-        double pv[NJ];
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-            pv[j] = a.p_old[c[j]];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-            xv[j] = xv[j] + beta * pv[j];
+            st.pv[j] = a.p_old[st.c[j]];
     }
+}
+template <int NJ, bool CG>
+__device__ __forceinline__ void stage_store(const StageRegs<NJ, CG> &st, int nnzt, double beta, double *s_prod)
+{
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
         const int k = (int)threadIdx.x + j * kBlock;
+        double x = st.xv[j];
+        if (CG)
+            x = x + beta * st.pv[j];
         if (k < nnzt)
-            s_prod[pslot(k)] = v[j] * xv[j];
+            s_prod[pslot(k)] = st.v[j] * x;
     }
+}
+template <int NJ, bool CG, bool NT>
+__device__ __forceinline__ void stage_products(const TileArgs &a, int n0, int nnzt, double beta, double *s_prod)
+{
+    StageRegs<NJ, CG> st;
+    stage_issue<NJ, CG, NT>(a, n0, nnzt, st);
+    stage_store<NJ, CG>(st, nnzt, beta, s_prod);
 }
 
 // Per-tile LDS of the single-RHS kernels.  Products and row ends share one buffer: a tile
@@ -609,13 +689,11 @@ __device__ __forceinline__ void row_operands(const TileArgs &a, int r0, int nrow
     }
 }
 
-// CG epilogue of the single-RHS tile kernels: this block's p.Ap partial -> partials[slot];
-// the two-level reduce_slots folds all partials in a fixed order and its last block sets
-// alpha = rs_old / pAp (single_strategy.hpp:140-141).  Non-finite alpha (p.Ap == 0 or NaN)
-// stops the solve.
-template <int IPT, int MODE>
-__device__ __forceinline__ void cg_alpha_epilogue(const TileArgs &a, SpmvSmem<IPT> &sm, int slot, int nslots,
-                                                  double dot)
+// Dot-mode epilogue (split multi-RHS / row-sharded CG): this block's x.(Ax) partial ->
+// partials[slot]; reduce_slots folds all partials in a fixed order and its last block writes
+// dot_out (the sharded CG all-reduces it next).
+template <int IPT>
+__device__ __forceinline__ void dot_epilogue(const TileArgs &a, SpmvSmem<IPT> &sm, int slot, int nslots, double dot)
 {
     const int tid = threadIdx.x;
     const double tsum = block_sum(dot, sm.red);
@@ -626,21 +704,66 @@ __device__ __forceinline__ void cg_alpha_epilogue(const TileArgs &a, SpmvSmem<IP
     __syncthreads();
     if (!reduce_slots<1>(a.partials, a.gtickets, slot, nslots, sm.cval, sm.red, &sm.last))
         return;
-    if (tid == 0) {
-        const double pAp = sm.red[0];
-        if (MODE == kModeDot) {
-            a.dot_out[0] = pAp;
-        } else {
-            CgScalars &s = a.scal[0];
-            s.pAp = pAp;
-            const double alpha = a.conv[0] ? 0.0 : s.rs_old / pAp;
-            s.alpha = alpha;
-            if (!a.conv[0] && !(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
-                a.ctrl->breakdown = 1;
-                a.ctrl->done = 1;
-                a.ctrl->iters_out = a.ctrl->iter + 1;
-            }
+    if (tid == 0)
+        a.dot_out[0] = sm.red[0];
+}
+
+// Pipelined single-RHS CG, head of iteration k (MODE 1).  Every workgroup sums the previous
+// update's r.r partials itself (rs_k; at k = 0 the init's b.b), so the stop test and beta need
+// no ticket chain: the reference's check after iteration k-1 (single_strategy.hpp:150-156:
+// sqrt(rs_new)/||b|| < tol -> iterations = k) is taken here, then beta = rs_k / rs_{k-1}
+// (:158-160).  Workgroup 0 records the history and hands rs_k and k+1 on by parity.  Returns
+// false when the solve has stopped (converged): the caller returns at once.
+__device__ __forceinline__ bool cg1_head(const TileArgs &a, double rs, double &beta)
+{
+    CgScalars &s = a.scal[0];
+    CgControl *c = a.ctrl;
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    const int k = c->iter_par[a.parity];
+    if (k == 0) {  // r = p = b: no stop test before the first iteration
+        beta = 0.0;
+        if (lead) {
+            const double bn = sqrt(rs);
+            s.b_norm = bn == 0.0 ? 1.0 : bn;  // single_strategy.hpp:124-129
+            s.rs_par[0] = rs;
+            c->iter_par[1] = 1;
         }
+        return true;
+    }
+    const double rel = sqrt(rs) / s.b_norm;
+    if (lead) {
+        if (a.hist && k - 1 < a.hist_cap)
+            a.hist[k - 1] = rel;
+        c->iter = k;
+    }
+    if (rel < a.tol) {
+        if (lead) {
+            c->iters_out = k;
+            c->done = 1;
+        }
+        return false;
+    }
+    beta = rs / s.rs_par[a.parity ^ 1];
+    if (lead) {
+        s.rs_par[a.parity] = rs;
+        c->iter_par[a.parity ^ 1] = k + 1;
+    }
+    return true;
+}
+
+// Pipelined single-RHS CG tail of the SpMV: this tile's p.Ap partial, for the update kernel
+// to sum (folded by group tickets only beyond kConsumeTile tiles).
+template <int IPT>
+__device__ __forceinline__ void cg1_publish(const TileArgs &a, SpmvSmem<IPT> &sm, int slot, int nslots, double dot)
+{
+    const double tsum = block_sum(dot, sm.red);
+    if (threadIdx.x == 0) {
+        store_sc1(&a.partials[slot], tsum);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (nslots > kConsumeTile) {
+        __syncthreads();
+        publish_partials<1>(a.partials, a.gtickets, slot, nslots, kConsumeTile, sm.cval, sm.red, &sm.last);
     }
 }
 
@@ -659,39 +782,51 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
     if (MODE != kModeSpmv && a.ctrl->done)
         return;
     const int t = xcd_tile(blockIdx.x, a.num_tiles);
-#if MSPMV_LAB_ABLATE & 4
-    const long long M_ = 217918, NZ_ = 11524432;
-    const int2 b0 = make_int2((int)(t * M_ / a.num_tiles), (int)(t * NZ_ / a.num_tiles));
-    const int2 b1 = make_int2((int)((t + 1) * M_ / a.num_tiles), (int)((t + 1) * NZ_ / a.num_tiles));
-#else
     const int2 b0 = a.bounds[t];
     const int2 b1 = a.bounds[t + 1];
-#endif
     const int r0 = b0.x, n0 = b0.y;
     const int nrows = b1.x - r0;
     const int nnzt = b1.y - n0;
-    const double beta = CG ? a.scal[0].beta : 0.0;
-    if (nnzt > 0) {  // block-uniform; loads for every round are issued before any is used
-        if (nnzt <= TILE)  // the common case: no snapped-in extra nonzeros
-            stage_products<IPT, CG, NT>(a, n0, nnzt, beta, sm.prod);
-        else
-            stage_products<MAXJ, CG, NT>(a, n0, nnzt, beta, sm.prod);
+    double beta = 0.0;
+    bool go = true;
+    // CG: the update's r.r partials are loaded first; summed (-> stop test, beta) once this
+    // tile's stream and gathers are in flight.  Block-uniform, as is every branch on nnzt.
+    PartRegs<CG ? kUpdateMaxBlocks / kBlock : 1> pin;
+    if (CG)
+        part_load(a.part_in, a.n_part_in, pin);
+    auto head = [&]() {
+        if (CG)
+            go = cg1_head(a, part_sum(pin, sm.red), beta);
+    };
+    if (nnzt > 0 && nnzt <= TILE) {  // the common case: no snapped-in extra nonzeros
+        StageRegs<IPT, CG> st;
+        stage_issue<IPT, CG, NT>(a, n0, nnzt, st);
+        head();
+        if (go)
+            stage_store<IPT, CG>(st, nnzt, beta, sm.prod);
+    } else if (nnzt > TILE) {
+        StageRegs<MAXJ, CG> st;
+        stage_issue<MAXJ, CG, NT>(a, n0, nnzt, st);
+        head();
+        if (go)
+            stage_store<MAXJ, CG>(st, nnzt, beta, sm.prod);
+    } else {
+        head();
     }
+    if (CG && !go)
+        return;
     int *rend = sm.rowend(nnzt);
     for (int i = tid; i < nrows; i += kBlock)
         rend[i] = a.row_offsets[r0 + 1 + i] - n0;
     __syncthreads();
     double dot = 0.0;
-#if MSPMV_LAB_ABLATE & 2
-    if (tid < nrows)
-        a.y[r0 + tid] = sm.prod[tid] + rend[tid];
-    return;
-#endif
     double xr, pr;
     row_operands<MODE>(a, r0, nrows, xr, pr);
     reduce_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, a.rmode[t], a.split[t + 1] != 0, beta, dot, xr, pr);
-    if (MODE != kModeSpmv)
-        cg_alpha_epilogue<IPT, MODE>(a, sm, t, a.num_tiles, dot);
+    if (MODE == kModeCg)
+        cg1_publish<IPT>(a, sm, t, a.num_tiles, dot);
+    else if (MODE == kModeDot)
+        dot_epilogue<IPT>(a, sm, t, a.num_tiles, dot);
 }
 
 // Single right-hand side, persistent and software-pipelined.  Workgroup v (XCD-grouped) walks
@@ -786,6 +921,7 @@ __device__ __forceinline__ void pipe_tile(const TileArgs &a, SpmvSmem<IPT> &sm, 
 template <int IPT, int MODE, bool NT>
 __global__ __launch_bounds__(kBlock) void k_spmv_persist(TileArgs a, int tpb)
 {
+    static_assert(MODE != kModeCg, "the pipelined CG head runs in the one-tile kernel only");
     __shared__ SpmvSmem<IPT> sm;
     __shared__ int2 s_b[kMaxTpb + 1];
     __shared__ unsigned char s_mode[kMaxTpb + 1];  // reduction mode | 0x80 when the tile has a tail
@@ -815,8 +951,8 @@ __global__ __launch_bounds__(kBlock) void k_spmv_persist(TileArgs a, int tpb)
         if (i < ntl)
             pipe_tile<IPT, MODE, NT>(a, sm, s_b, s_mode, a.m, i, ntl, t_begin + i, A, B, beta, dot);
     }
-    if (MODE != kModeSpmv)
-        cg_alpha_epilogue<IPT, MODE>(a, sm, blockIdx.x, gridDim.x, dot);
+    if (MODE == kModeDot)
+        dot_epilogue<IPT>(a, sm, blockIdx.x, gridDim.x, dot);
 }
 
 // Row-group reduction of one multi-RHS tile (mode lgp + 1): a row group is GL column-pair
@@ -827,9 +963,8 @@ __global__ __launch_bounds__(kBlock) void k_spmv_persist(TileArgs a, int tpb)
 template <int L, int MODE>
 __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_col, const double *s_val,
                                                 const int *rend, int t, int r0, int nrows, int nnzt,
-                                                double2 beta2, double2 &dot, int lgp)
+                                                double2 &dot, int lgp)
 {
-    constexpr bool CG = MODE == kModeCg;
     constexpr int GL = L / 2;
     const int Gp = 1 << lgp;
     const int tid = threadIdx.x;
@@ -840,11 +975,6 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
     const int nseg = nrows + (tail ? 1 : 0);
     auto panel = [&](int c) {
         double2 xv = *reinterpret_cast<const double2 *>(a.x + (size_t)c * L + 2 * lane);
-        if (CG) {
-            const double2 po = *reinterpret_cast<const double2 *>(a.p_old + (size_t)c * L + 2 * lane);
-            xv.x = xv.x + beta2.x * po.x;
-            xv.y = xv.y + beta2.y * po.y;
-        }
         return xv;
     };
     for (int r = tid / W; r < nseg; r += kBlock / W) {  // uniform within a group
@@ -897,17 +1027,7 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
                 *reinterpret_cast<double2 *>(a.y + off) = acc;
             else  // the trailing partial row -> carry (k_fixup adds it in tile order)
                 *reinterpret_cast<double2 *>(a.carry_val + (size_t)t * L + 2 * lane) = acc;
-            if (CG) {
-                const double2 rr = *reinterpret_cast<const double2 *>(a.x + off);
-                const double2 po = *reinterpret_cast<const double2 *>(a.p_old + off);
-                double2 pn;
-                pn.x = rr.x + beta2.x * po.x;
-                pn.y = rr.y + beta2.y * po.y;
-                if (r < nrows)
-                    *reinterpret_cast<double2 *>(a.p_new + off) = pn;
-                dot.x += pn.x * acc.x;
-                dot.y += pn.y * acc.y;
-            } else if (MODE == kModeDot) {
+            if (MODE == kModeDot) {
                 const double2 xx = *reinterpret_cast<const double2 *>(a.x + off);
                 dot.x += xx.x * acc.x;
                 dot.y += xx.y * acc.y;
@@ -922,7 +1042,7 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
 template <int L, int IPTG, int MODE, bool NT>
 __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
 {
-    constexpr bool CG = MODE == kModeCg;
+    static_assert(MODE != kModeCg, "multi-RHS CG runs the split iteration (MODE 2)");
     constexpr int GL = L / 2;
     constexpr int NG = kBlock / GL;
     constexpr int TILE = NG * IPTG;
@@ -949,9 +1069,6 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
     const int nrows = b1.x - r0;
     const int nnzt = b1.y - n0;
     const int items = nrows + nnzt;
-    double2 beta2 = make_double2(0.0, 0.0);
-    if (CG)
-        beta2 = make_double2(a.scal[2 * lane].beta, a.scal[2 * lane + 1].beta);
 
     for (int i = tid; i < nrows; i += kBlock)
         s_rowend[i] = a.row_offsets[r0 + 1 + i] - n0;
@@ -968,7 +1085,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
     double2 dot = make_double2(0.0, 0.0);
     const int rmode = a.rmode[t];
     if (rmode != 0) {
-        spmm_group_rows<L, MODE>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, beta2, dot, rmode - 1);
+        spmm_group_rows<L, MODE>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, dot, rmode - 1);
     } else {
     const int ipt = (items + NG - 1) / NG;
     const int d0 = min(g * ipt, items);
@@ -981,16 +1098,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
     auto write_row = [&](int row, double2 val) {
         const size_t off = (size_t)(r0 + row) * L + 2 * lane;
         *reinterpret_cast<double2 *>(a.y + off) = val;
-        if (CG) {
-            const double2 rr = *reinterpret_cast<const double2 *>(a.x + off);
-            const double2 po = *reinterpret_cast<const double2 *>(a.p_old + off);
-            double2 pn;
-            pn.x = rr.x + beta2.x * po.x;
-            pn.y = rr.y + beta2.y * po.y;
-            *reinterpret_cast<double2 *>(a.p_new + off) = pn;
-            dot.x += pn.x * val.x;
-            dot.y += pn.y * val.y;
-        } else if (MODE == kModeDot) {
+        if (MODE == kModeDot) {
             const double2 xx = *reinterpret_cast<const double2 *>(a.x + off);
             dot.x += xx.x * val.x;
             dot.y += xx.y * val.y;
@@ -1015,19 +1123,6 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
             const int k = min(cy + j0 + jj, ey - 1);
             vv[jj] = s_val[k];
             xr[jj] = *reinterpret_cast<const double2 *>(a.x + (size_t)s_col[k] * L + 2 * lane);
-        }
-        if (CG) {
-            double2 po[WJ];
-#pragma unroll
-            for (int jj = 0; jj < WJ; ++jj) {
-                const int k = min(cy + j0 + jj, ey - 1);
-                po[jj] = *reinterpret_cast<const double2 *>(a.p_old + (size_t)s_col[k] * L + 2 * lane);
-            }
-#pragma unroll
-            for (int jj = 0; jj < WJ; ++jj) {
-                xr[jj].x = xr[jj].x + beta2.x * po[jj].x;
-                xr[jj].y = xr[jj].y + beta2.y * po[jj].y;
-            }
         }
 #pragma unroll
         for (int jj = 0; jj < WJ; ++jj) {
@@ -1092,13 +1187,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
             acc.y += c.y;
         }
         *reinterpret_cast<double2 *>(a.carry_val + (size_t)t * L + 2 * lane) = acc;
-        if (CG) {
-            const size_t off = (size_t)(r0 + nrows) * L + 2 * lane;
-            const double2 rr = *reinterpret_cast<const double2 *>(a.x + off);
-            const double2 po = *reinterpret_cast<const double2 *>(a.p_old + off);
-            dot.x += (rr.x + beta2.x * po.x) * acc.x;
-            dot.y += (rr.y + beta2.y * po.y) * acc.y;
-        } else if (MODE == kModeDot) {
+        if (MODE == kModeDot) {
             const size_t off = (size_t)(r0 + nrows) * L + 2 * lane;
             const double2 xx = *reinterpret_cast<const double2 *>(a.x + off);
             dot.x += xx.x * acc.x;
@@ -1144,19 +1233,6 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
                     a.ctrl->done = 1;
                     a.ctrl->iters_out = a.ctrl->iter + 1;
                 }
-            }
-        }
-        if (tid < L && CG) {
-            const double pAp = s_tot[tid];
-            CgScalars &s = a.scal[tid];
-            s.pAp = pAp;
-            const bool cv = a.conv[tid];
-            const double alpha = cv ? 0.0 : s.rs_old / pAp;
-            s.alpha = alpha;
-            if (!cv && !(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
-                a.ctrl->breakdown = 1;
-                a.ctrl->done = 1;
-                a.ctrl->iters_out = a.ctrl->iter + 1;
             }
         }
     }
@@ -1657,26 +1733,56 @@ static void persist_grid(K kernel, int num_tiles, int num_cus, int bpc, int *gri
     *grid = (num_tiles + t - 1) / t;
 }
 
+template <int I, int MODE, bool NTV>
+static void launch_spmv_persist(const TileArgs &a, hipStream_t s, int num_cus, int bpc)
+{
+    if constexpr (MODE != kModeCg) {
+        int g = 0, tpb = 0;
+        persist_grid(k_spmv_persist<I, MODE, NTV>, a.num_tiles, num_cus, bpc, &g, &tpb);
+        hipLaunchKernelGGL((k_spmv_persist<I, MODE, NTV>), dim3(g), dim3(kBlock), 0, s, a, tpb);
+    }
+}
+
+template <int LL, int I, int MODE>
+static void launch_spmm_nt(const TileArgs &a, hipStream_t s, bool nt)
+{
+    if constexpr (MODE != kModeCg) {
+        if (nt)
+            hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, true>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
+        else
+            hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, false>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
+    }
+}
+
+template <int LL, int MODE>
+static void launch_spmm_L(const TileArgs &a, hipStream_t s, bool nt)
+{
+    const int iptg = spmm_iptg_for(LL);
+    if (iptg == 32)
+        launch_spmm_nt<LL, 32, MODE>(a, s, nt);
+    else if (iptg == 16)
+        launch_spmm_nt<LL, 16, MODE>(a, s, nt);
+    else
+        launch_spmm_nt<LL, 8, MODE>(a, s, nt);
+}
+
+// MODE 1 (pipelined single-RHS CG) exists for L == 1 in the one-tile kernel only.
 template <int MODE>
 static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_cus, bool nt)
 {
     const dim3 grid(a.num_tiles), block(kBlock);
     const SpmvTuning &tu = spmv_tuning();
+    if (MODE == kModeCg && L != 1)
+        return hipErrorInvalidValue;
     switch (L) {
     case 1: {
-#define MSPMV_LAUNCH_PERSIST(I, NTV)                                                               \
-    do {                                                                                           \
-        int g = 0, tpb = 0;                                                                        \
-        persist_grid(k_spmv_persist<I, MODE, NTV>, a.num_tiles, num_cus, tu.bpc, &g, &tpb);          \
-        hipLaunchKernelGGL((k_spmv_persist<I, MODE, NTV>), dim3(g), block, 0, s, a, tpb);            \
-    } while (0)
 #define MSPMV_SPMV_CASE(I)                                                                          \
     case I:                                                                                        \
-        if (tu.persist) {                                                                          \
+        if (tu.persist && MODE != kModeCg) {                                                       \
             if (nt)                                                                                \
-                MSPMV_LAUNCH_PERSIST(I, true);                                                     \
+                launch_spmv_persist<I, MODE, true>(a, s, num_cus, tu.bpc);                         \
             else                                                                                   \
-                MSPMV_LAUNCH_PERSIST(I, false);                                                    \
+                launch_spmv_persist<I, MODE, false>(a, s, num_cus, tu.bpc);                        \
         } else if (nt)                                                                             \
             hipLaunchKernelGGL((k_spmv_tile<I, MODE, true>), grid, block, 0, s, a);                   \
         else                                                                                       \
@@ -1692,30 +1798,12 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_c
         default: return hipErrorInvalidValue;
         }
 #undef MSPMV_SPMV_CASE
-#undef MSPMV_LAUNCH_PERSIST
         break;
     }
-#define MSPMV_SPMM_NT(LL, I)                                                                       \
-    if (nt)                                                                                        \
-        hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, true>), grid, block, 0, s, a);                 \
-    else                                                                                           \
-        hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, false>), grid, block, 0, s, a);
-#define MSPMV_SPMM_CASE(LL)                                                                        \
-    case LL:                                                                                       \
-        if (spmm_iptg_for(LL) == 32) {                                                             \
-            MSPMV_SPMM_NT(LL, 32)                                                                  \
-        } else if (spmm_iptg_for(LL) == 16) {                                                      \
-            MSPMV_SPMM_NT(LL, 16)                                                                  \
-        } else {                                                                                   \
-            MSPMV_SPMM_NT(LL, 8)                                                                   \
-        }                                                                                          \
-        break;
-        MSPMV_SPMM_CASE(2)
-        MSPMV_SPMM_CASE(4)
-        MSPMV_SPMM_CASE(8)
-        MSPMV_SPMM_CASE(16)
-#undef MSPMV_SPMM_CASE
-#undef MSPMV_SPMM_NT
+    case 2: launch_spmm_L<2, MODE>(a, s, nt); break;
+    case 4: launch_spmm_L<4, MODE>(a, s, nt); break;
+    case 8: launch_spmm_L<8, MODE>(a, s, nt); break;
+    case 16: launch_spmm_L<16, MODE>(a, s, nt); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -1802,6 +1890,158 @@ hipError_t launch_cg_init(mspmv_handle_s *h, const double *d_b, double *d_x, int
 
 hipError_t launch_dist_vec(int which, const CgVecArgs &a, int L, int nblk, double *p, hipStream_t s);
 
+// ---- pipelined single-RHS CG (consumer-side reductions, no ticket chains) -------------------
+// Iteration k = [k_spmv_tile MODE 1: stop test + beta from the r.r partials, p = r + beta p_old
+// gathered, Ap, p.Ap partials] -> [k_cg1_update: alpha from the p.Ap partials, x, r, r.r
+// partials].  Each kernel sums its producer's partials itself (part_load / part_sum), so no
+// kernel ends on a chain of tickets and folds.
+struct Cg1Args {
+    long long m;
+    double *x;
+    double *r;
+    double *p0;            // init: p0 = b
+    const double *b;       // init
+    const double *p;       // update: p of this iteration
+    const double *ap;
+    CgScalars *scal;
+    CgControl *ctrl;
+    const double *part_in;  // producer partials (update: the SpMV's p.Ap; finish: the update's r.r)
+    int n_part_in;
+    double *part_out;       // this kernel's per-block partials (r.r, or b.b at init)
+    int parity;
+    double *hist;
+    int hist_cap;
+};
+
+// x = 0, r = p0 = b, and this block's b.b partial (the first SpMV sums them: rs_0, ||b||).
+__global__ __launch_bounds__(kBlock) void k_cg1_init(Cg1Args a)
+{
+    __shared__ double s_red[kBlock / 64];
+    double acc = 0.0;
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < a.m; i += (long long)gridDim.x * kBlock) {
+        const double b = a.b[i];
+        a.x[i] = 0.0;
+        a.r[i] = b;
+        a.p0[i] = b;
+        acc += b * b;
+    }
+    const double t = block_sum(acc, s_red);
+    if (threadIdx.x == 0)
+        a.part_out[blockIdx.x] = t;
+}
+
+// Tail of iteration k (single_strategy.hpp:140-148): alpha = rs_k / p.Ap (every block sums the
+// SpMV's partials in the same order), x += alpha p, r += (-alpha) Ap, r.r partial per block.  A
+// non-finite alpha stops the solve before x and r change (the reference keeps going on NaN).
+__global__ __launch_bounds__(kBlock) void k_cg1_update(Cg1Args a)
+{
+    __shared__ double s_red[kBlock / 64];
+    const int tid = threadIdx.x;
+    if (a.ctrl->done)
+        return;
+    PartRegs<kConsumeTile / kBlock> pin;
+    part_load(a.part_in, a.n_part_in, pin);
+    const long long stride = (long long)gridDim.x * kBlock;
+    const long long i0 = (long long)blockIdx.x * kBlock + tid;
+    double p = 0.0, q = 0.0, x = 0.0, r = 0.0;  // the first element's operands, in flight under the sum
+    if (i0 < a.m) {
+        p = a.p[i0];
+        q = a.ap[i0];
+        x = a.x[i0];
+        r = a.r[i0];
+    }
+    const double pAp = part_sum(pin, s_red);
+    const double alpha = a.scal[0].rs_par[a.parity] / pAp;
+    if (!(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
+        if (blockIdx.x == 0 && tid == 0) {
+            a.ctrl->breakdown = 1;
+            a.ctrl->iters_out = a.ctrl->iter_par[a.parity] + 1;
+            a.ctrl->done = 1;
+        }
+        return;
+    }
+    const double nal = -alpha;
+    double acc = 0.0;
+    for (long long i = i0; i < a.m; i += stride) {
+        if (i != i0) {
+            p = a.p[i];
+            q = a.ap[i];
+            x = a.x[i];
+            r = a.r[i];
+        }
+        x = x + alpha * p;
+        r = r + nal * q;
+        a.x[i] = x;
+        a.r[i] = r;
+        acc += r * r;
+    }
+    const double t = block_sum(acc, s_red);
+    if (tid == 0)
+        a.part_out[blockIdx.x] = t;
+}
+
+// After max_iters iterations: the last iteration's stop test and history entry (the SpMV that
+// would take it is not launched); iterations = max_iters either way (single_strategy.hpp:152-170).
+__global__ __launch_bounds__(kBlock) void k_cg1_finish(Cg1Args a)
+{
+    __shared__ double s_red[kBlock / 64];
+    if (a.ctrl->done)
+        return;
+    PartRegs<kUpdateMaxBlocks / kBlock> pin;
+    part_load(a.part_in, a.n_part_in, pin);
+    const double rs = part_sum(pin, s_red);
+    if (threadIdx.x == 0) {
+        CgControl *c = a.ctrl;
+        const int k = c->iter_par[a.parity];
+        if (a.hist && k >= 1 && k - 1 < a.hist_cap)
+            a.hist[k - 1] = sqrt(rs) / a.scal[0].b_norm;
+        c->iter = k;
+        c->iters_out = k;
+        c->done = 1;
+    }
+}
+
+int cg1_blocks(long long m)
+{
+    const long long b = (m + kBlock - 1) / kBlock;  // one element per thread up to the cap
+    return (int)std::max<long long>(1, std::min<long long>(b, kUpdateMaxBlocks));
+}
+
+static Cg1Args cg1_args(mspmv_handle_s *h, double *d_x)
+{
+    Cg1Args a{};
+    a.m = h->m;
+    a.x = d_x;
+    a.r = h->d_r;
+    a.p0 = h->d_p0;
+    a.ap = h->d_ap;
+    a.scal = h->d_scal;
+    a.ctrl = h->d_ctrl;
+    a.hist = h->d_hist;
+    a.hist_cap = h->hist_cap;
+    return a;
+}
+
+hipError_t launch_cg1_init(mspmv_handle_s *h, const double *d_b, double *d_x, int nblk)
+{
+    Cg1Args a = cg1_args(h, d_x);
+    a.b = d_b;
+    a.part_out = h->d_partials_b;
+    hipLaunchKernelGGL(k_cg1_init, dim3(nblk), dim3(kBlock), 0, h->stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_cg1_finish(mspmv_handle_s *h, int parity, int nblk)
+{
+    Cg1Args a = cg1_args(h, nullptr);
+    a.part_in = h->d_partials_b;
+    a.n_part_in = nblk;
+    a.parity = parity;
+    hipLaunchKernelGGL(k_cg1_finish, dim3(1), dim3(kBlock), 0, h->stream, a);
+    return hipGetLastError();
+}
+
+
 static hipError_t launch_fixup_ctrl(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L)
 {
     if (plan.num_carries == 0)
@@ -1852,13 +2092,15 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
     return dispatch_vec(false, va, L, nblk, h->stream);
 }
 
+// Multi-RHS CG always runs the split iteration; single-RHS the pipelined one unless
+// MSPMV_CG_SPLIT=1 asks for the split form (A/B runs, and its own parity test).
 bool cg_split_iteration(int L)
 {
     static const int mode = [] {
         const char *e = getenv("MSPMV_CG_SPLIT");
-        return e ? atoi(e) : -1;
+        return e ? atoi(e) : 0;
     }();
-    return mode < 0 ? L >= 2 : mode != 0;
+    return L >= 2 || mode != 0;
 }
 
 hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *d_x, int L, int parity, int nblk,
@@ -1868,40 +2110,35 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *
         return launch_cg_iteration_split(h, plan, d_x, L, nblk, tol);
     double *p_old = parity ? h->d_p1 : h->d_p0;
     double *p_new = parity ? h->d_p0 : h->d_p1;
-    TileArgs ta = make_args(h, plan, h->d_r, h->d_ap, L);
+    TileArgs ta = make_args(h, plan, h->d_r, h->d_ap, 1);
     ta.p_old = p_old;
     ta.p_new = p_new;
     ta.scal = h->d_scal;
     ta.ctrl = h->d_ctrl;
-    ta.conv = h->d_conv;
     ta.partials = h->d_partials;
     ta.gtickets = h->d_gtickets;
-    hipError_t e = launch_tile<kModeCg>(ta, L, h->stream, h->num_cus, stream_nt(h));
+    ta.part_in = h->d_partials_b;
+    ta.n_part_in = nblk;
+    ta.parity = parity;
+    ta.tol = tol;
+    ta.hist = h->d_hist;
+    ta.hist_cap = h->hist_cap;
+    hipError_t e = launch_tile<kModeCg>(ta, 1, h->stream, h->num_cus, stream_nt(h));
     if (e != hipSuccess)
         return e;
-    if (plan.num_carries) {
-        const int n = plan.num_carries * L;
-        hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, h->stream, plan.d_carry_tiles,
-                           plan.d_carry_rows, plan.num_carries, plan.d_carry_val, h->d_ap, L,
-                           (const CgControl *)h->d_ctrl);
-        if ((e = hipGetLastError()) != hipSuccess)
-            return e;
-    }
-    CgVecArgs va{};
-    va.n_elems = (long long)h->m * L;
-    va.x = d_x;
-    va.r = h->d_r;
-    va.p = p_new;
-    va.ap = h->d_ap;
-    va.scal = h->d_scal;
-    va.ctrl = h->d_ctrl;
-    va.conv = h->d_conv;
-    va.partials = h->d_partials;
-    va.gtickets = h->d_gtickets;
-    va.hist = h->d_hist;
-    va.hist_cap = h->hist_cap;
-    va.tol = tol;
-    return dispatch_vec(false, va, L, nblk, h->stream);
+    if ((e = launch_fixup_ctrl(h, plan, h->d_ap, 1)) != hipSuccess)
+        return e;
+    Cg1Args a = cg1_args(h, d_x);
+    a.p = p_new;
+    long long off = 0;
+    int count = 0;
+    consumer_level(plan.num_tiles, kConsumeTile, 1, &off, &count);
+    a.part_in = h->d_partials + off;
+    a.n_part_in = count;
+    a.part_out = h->d_partials_b;
+    a.parity = parity;
+    hipLaunchKernelGGL(k_cg1_update, dim3(nblk), dim3(kBlock), 0, h->stream, a);
+    return hipGetLastError();
 }
 
 // ---- row-sharded CG launchers --------------------------------------------------------------
@@ -1972,6 +2209,7 @@ hipError_t launch_flush(void *p, size_t bytes, hipStream_t s)
 
 namespace mspmv {
 hipError_t launch_dist_vec(int which, const CgVecArgs &a, int L, int nblk, double *p, hipStream_t s);
+
 
 hipError_t launch_dist_vec_mirror(int which, const DistVecArgs &d, int L, int nblk, double *p, hipStream_t s)
 {

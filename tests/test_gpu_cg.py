@@ -160,7 +160,7 @@ def test_cg_multi_breakdown_reported_split_path():
     assert np.all(X == 0.0)
 
 
-_FUSED_CHILD = r"""
+_SPLIT_CHILD = r"""
 import sys, numpy as np
 sys.path.insert(0, sys.argv[1])
 import mspmv
@@ -168,14 +168,17 @@ a = mspmv.CsrMatrix.synth_stencil(0, 4000, 64)
 B = np.random.default_rng(11).uniform(0, 1, (a.num_rows, 4))
 with mspmv.GpuCsr(a) as g:
     X, it, h, st = g.cg_multi(B, 5000, 1e-9, hist_cap=5000)
-np.savez(sys.argv[2], X=X, it=it, h=h, st=st)
+    x1, it1, h1, st1 = g.cg_single(B[:, 0].copy(), 5000, 1e-9, hist_cap=5000)
+np.savez(sys.argv[2], X=X, it=it, h=h, st=st, x1=x1, it1=it1, h1=h1, st1=st1)
 """
 
 
 @pytest.mark.parametrize("split", ["0", "1"])
-def test_cg_multi_fused_and_split_iterations_match_oracle(orc, tmp_path, split):
-    """Both multi-RHS iteration forms (MSPMV_CG_SPLIT=0: gathers r and p_old per nonzero;
-    1: separate p update) reproduce the oracle; run in a child so the env is read fresh."""
+def test_cg_pipelined_and_split_iterations_match_oracle(orc, tmp_path, split):
+    """Both iteration forms reproduce the oracle: single RHS pipelined (MSPMV_CG_SPLIT=0: stop
+    test and beta summed by every SpMV workgroup, alpha by every update workgroup) or split
+    (=1: p update pass, SpMV MODE 2, update); multi-RHS always split.  Run in a child so the
+    environment is read fresh."""
     import os
     import subprocess
     import sys
@@ -183,7 +186,7 @@ def test_cg_multi_fused_and_split_iterations_match_oracle(orc, tmp_path, split):
                        "sparse-matrix-linear-equations_amd")
     out = str(tmp_path / "r.npz")
     env = dict(os.environ, MSPMV_CG_SPLIT=split)
-    r = subprocess.run([sys.executable, "-c", _FUSED_CHILD, pkg, out], env=env, capture_output=True, text=True,
+    r = subprocess.run([sys.executable, "-c", _SPLIT_CHILD, pkg, out], env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     d = np.load(out)
@@ -194,3 +197,8 @@ def test_cg_multi_fused_and_split_iterations_match_oracle(orc, tmp_path, split):
     k = min(len(d["h"]), len(ho))
     np.testing.assert_allclose(d["h"][:k], ho[:k], rtol=0, atol=1e-10)
     assert np.linalg.norm(d["X"] - Xo) <= 1e-8 * np.linalg.norm(Xo)
+    xo, it1_o, h1o = orc.cg_single(a, B[:, 0].copy(), 5000, 1e-9, hist_cap=5000)
+    assert int(d["st1"]) == 0 and iter_match(int(d["it1"]), it1_o, h1o, 1e-9)
+    k = min(len(d["h1"]), len(h1o))
+    np.testing.assert_allclose(d["h1"][:k], h1o[:k], rtol=0, atol=1e-10)
+    assert np.linalg.norm(d["x1"] - xo) <= 1e-8 * np.linalg.norm(xo)

@@ -1,3 +1,2 @@
 set -o pipefail
-export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/cgprof -o cg -- python3 tools/cg_probe.py --child > gpurun_out/cgprof.txt 2>&1; rc=$?; tail -2 gpurun_out/cgprof.txt; exit $rc
+PROBE_VARIANTS=8:48,16:48,7:48,6:48,4:48 timeout -k 10 500 python tools/cg_probe.py > gpurun_out/cgprobe_ipt.txt 2>&1; rc=$?; cat gpurun_out/cgprobe_ipt.txt; exit $rc
