@@ -788,6 +788,12 @@ mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y,
         HIP_TRY(hipMalloc(&h->d_flush, flush_bytes));
         h->flush_cap = flush_bytes;
     }
+    // A/B lab hook: MSPMV_TIME_DOT=1 times the CG's MODE 2 SpMM (x.(AX) partials + fold) instead
+    static const bool time_dot = getenv("MSPMV_TIME_DOT") != nullptr;
+    if (time_dot) {
+        ST_TRY(ensure_cg_workspace(h, L, cg_update_blocks((long long)h->m * L), plan->num_tiles, 0));
+        HIP_TRY(hipMemsetAsync(h->d_ctrl, 0, sizeof(CgControl), h->stream));
+    }
     std::vector<hipEvent_t> ev((size_t)reps * 2 + 2, nullptr);
     for (auto &e : ev)
         HIP_TRY(hipEventCreate(&e));
@@ -797,7 +803,9 @@ mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y,
             e = launch_flush(h->d_flush, flush_bytes, h->stream);
         if (e == hipSuccess)
             e = hipEventRecord(ev[2 * i], h->stream);
-        if (e == hipSuccess)
+        if (e == hipSuccess && time_dot)
+            e = launch_spmm_dot(h, *plan, d_X, d_Y, L, h->d_ctrl, h->d_partials, h->d_gtickets, h->d_red);
+        else if (e == hipSuccess)
             e = launch_spmm_tile_only(h, *plan, d_X, d_Y, L);
         if (e == hipSuccess)
             e = hipEventRecord(ev[2 * i + 1], h->stream);

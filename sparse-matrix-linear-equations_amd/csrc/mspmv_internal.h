@@ -177,7 +177,8 @@ hipError_t launch_dist_vec_mirror(int which, const DistVecArgs &a, int L, int nb
 hipError_t launch_dist_pack(const double *p, const int *idx, long long n_elems, int L, double *send,
                             const CgControl *ctrl, hipStream_t s);
 hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
-                           CgControl *ctrl, double *partials, unsigned *gtickets, double *dot_out);
+                           CgControl *ctrl, double *partials, unsigned *gtickets, double *dot_out,
+                           const CgScalars *scal = nullptr, const unsigned char *conv = nullptr);
 // Partials capacity (doubles) and group-ticket count for `slots` partial slots of L columns.
 // (every level of the tree: slots, slots/32, ... -> <= slots * 32/31 + one per level)
 inline size_t partials_capacity(size_t slots, int L) { return (slots + slots / (kSlotGroup - 1) + 8) * L; }

@@ -690,22 +690,13 @@ __device__ __forceinline__ void row_operands(const TileArgs &a, int r0, int nrow
 }
 
 // Dot-mode epilogue (split multi-RHS / row-sharded CG): this block's x.(Ax) partial ->
-// partials[slot]; reduce_slots folds all partials in a fixed order and its last block writes
-// dot_out (the sharded CG all-reduces it next).
+// partials[slot], a plain store; k_fold_dot (a later launch) sums the partials in tile order.
 template <int IPT>
-__device__ __forceinline__ void dot_epilogue(const TileArgs &a, SpmvSmem<IPT> &sm, int slot, int nslots, double dot)
+__device__ __forceinline__ void dot_epilogue(const TileArgs &a, SpmvSmem<IPT> &sm, int slot, double dot)
 {
-    const int tid = threadIdx.x;
     const double tsum = block_sum(dot, sm.red);
-    if (tid == 0) {
-        store_sc1(&a.partials[slot], tsum);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    if (!reduce_slots<1>(a.partials, a.gtickets, slot, nslots, sm.cval, sm.red, &sm.last))
-        return;
-    if (tid == 0)
-        a.dot_out[0] = sm.red[0];
+    if (threadIdx.x == 0)
+        a.partials[slot] = tsum;
 }
 
 // Pipelined single-RHS CG, head of iteration k (MODE 1).  Every workgroup sums the previous
@@ -779,8 +770,8 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
     constexpr int MAXJ = SpmvSmem<IPT>::MAXJ;
     __shared__ SpmvSmem<IPT> sm;
     const int tid = threadIdx.x;
-    if (MODE != kModeSpmv && a.ctrl->done)
-        return;
+    // CG: stop flag loaded now, tested after the stream and gathers are issued (see k_spmm_tile)
+    const int stopped = MODE != kModeSpmv ? a.ctrl->done : 0;
     const int t = xcd_tile(blockIdx.x, a.num_tiles);
     const int2 b0 = a.bounds[t];
     const int2 b1 = a.bounds[t + 1];
@@ -794,8 +785,10 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
     PartRegs<CG ? kUpdateMaxBlocks / kBlock : 1> pin;
     if (CG)
         part_load(a.part_in, a.n_part_in, pin);
-    auto head = [&]() {
-        if (CG)
+    auto head = [&]() {  // the stop flag is tested before cg1_head records anything
+        if (stopped)
+            go = false;
+        else if (CG)
             go = cg1_head(a, part_sum(pin, sm.red), beta);
     };
     if (nnzt > 0 && nnzt <= TILE) {  // the common case: no snapped-in extra nonzeros
@@ -813,8 +806,10 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
     } else {
         head();
     }
-    if (CG && !go)
+    if (!go)
         return;
+    // Row ends after the staging: measured faster here than issuing them with the stream
+    // (+0.9 us on the pwtk shape), unlike the multi-RHS kernel.
     int *rend = sm.rowend(nnzt);
     for (int i = tid; i < nrows; i += kBlock)
         rend[i] = a.row_offsets[r0 + 1 + i] - n0;
@@ -826,7 +821,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
     if (MODE == kModeCg)
         cg1_publish<IPT>(a, sm, t, a.num_tiles, dot);
     else if (MODE == kModeDot)
-        dot_epilogue<IPT>(a, sm, t, a.num_tiles, dot);
+        dot_epilogue<IPT>(a, sm, t, dot);
 }
 
 // Single right-hand side, persistent and software-pipelined.  Workgroup v (XCD-grouped) walks
@@ -951,8 +946,11 @@ __global__ __launch_bounds__(kBlock) void k_spmv_persist(TileArgs a, int tpb)
         if (i < ntl)
             pipe_tile<IPT, MODE, NT>(a, sm, s_b, s_mode, a.m, i, ntl, t_begin + i, A, B, beta, dot);
     }
-    if (MODE == kModeDot)
-        dot_epilogue<IPT>(a, sm, blockIdx.x, gridDim.x, dot);
+    if (MODE == kModeDot) {  // one partial per tile: the run's sum at its first tile, zeros after
+        dot_epilogue<IPT>(a, sm, t_begin, dot);
+        for (int i = 1 + tid; i < ntl; i += kBlock)
+            a.partials[t_begin + i] = 0.0;
+    }
 }
 
 // Row-group reduction of one multi-RHS tile (mode lgp + 1): a row group is GL column-pair
@@ -980,6 +978,10 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
     for (int r = tid / W; r < nseg; r += kBlock / W) {  // uniform within a group
         const int s0 = r == 0 ? 0 : rend[r - 1];
         const int e = r < nrows ? rend[r] : nnzt;
+        // MODE 2: the row's own x, issued ahead of the row's gathers (used after them)
+        double2 xx = make_double2(0.0, 0.0);
+        if (MODE == kModeDot && sub == 0)
+            xx = *reinterpret_cast<const double2 *>(a.x + (size_t)(r0 + r) * L + 2 * lane);
         double2 acc = make_double2(0.0, 0.0);
         int k = s0 + sub;
         // batches of 8 panel-row gathers in flight per lane (the SpMM is gather-latency bound:
@@ -1028,7 +1030,6 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
             else  // the trailing partial row -> carry (k_fixup adds it in tile order)
                 *reinterpret_cast<double2 *>(a.carry_val + (size_t)t * L + 2 * lane) = acc;
             if (MODE == kModeDot) {
-                const double2 xx = *reinterpret_cast<const double2 *>(a.x + off);
                 dot.x += xx.x * acc.x;
                 dot.y += xx.y * acc.y;
             }
@@ -1040,7 +1041,7 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
 // walk; each lane keeps a double2 of the L running totals (running_total[L],
 // merge_based.hpp:84-127).  TILE = (256/(L/2)) groups * IPTG items.
 template <int L, int IPTG, int MODE, bool NT>
-__global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void k_spmm_tile(TileArgs a)
 {
     static_assert(MODE != kModeCg, "multi-RHS CG runs the split iteration (MODE 2)");
     constexpr int GL = L / 2;
@@ -1055,13 +1056,14 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
     __shared__ int s_crow[NG];
     __shared__ double2 s_cval[NG * GL];
     __shared__ double2 s_red2[kBlock / 64][GL];
-    __shared__ int s_last;
 
     const int tid = threadIdx.x;
     const int g = tid / GL;
     const int lane = tid % GL;
-    if (MODE != kModeSpmv && a.ctrl->done)
-        return;
+    // CG: the stop flag is loaded now and tested once the tile's stream is in flight, so the
+    // flag's round trip does not delay every workgroup's first load (MODE 2 writes only the
+    // scratch Ap and partials: a stopped solve only needs the work skipped, not fenced)
+    const int stopped = MODE != kModeSpmv ? a.ctrl->done : 0;
     const int t = xcd_tile(blockIdx.x, a.num_tiles);
     const int2 b0 = a.bounds[t];
     const int2 b1 = a.bounds[t + 1];
@@ -1070,17 +1072,34 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
     const int nnzt = b1.y - n0;
     const int items = nrows + nnzt;
 
-    for (int i = tid; i < nrows; i += kBlock)
-        s_rowend[i] = a.row_offsets[r0 + 1 + i] - n0;
+    // Every round's loads are issued before any is stored to LDS (indices clamped into the
+    // tile), the first round of row ends with them: one memory round trip per tile, not STG.
+    const int re0 = a.row_offsets[min(r0 + 1 + min(tid, max(nrows - 1, 0)), a.m)];  // clamped: always issued
+    if (nnzt > 0) {  // block-uniform
+        int cst[STG];
+        double vst[STG];
 #pragma unroll
-    for (int j = 0; j < STG; ++j) {
-        const int k = tid + j * kBlock;
-        if (k < nnzt) {
-            s_col[k] = ld_stream<NT>(a.cols + n0 + k);
-            s_val[k] = ld_stream<NT>(a.vals + n0 + k);
+        for (int j = 0; j < STG; ++j)
+            cst[j] = ld_stream<NT>(a.cols + n0 + min(tid + j * kBlock, nnzt - 1));
+#pragma unroll
+        for (int j = 0; j < STG; ++j)
+            vst[j] = ld_stream<NT>(a.vals + n0 + min(tid + j * kBlock, nnzt - 1));
+#pragma unroll
+        for (int j = 0; j < STG; ++j) {
+            const int k = tid + j * kBlock;
+            if (k < nnzt) {
+                s_col[k] = cst[j];
+                s_val[k] = vst[j];
+            }
         }
     }
+    if (tid < nrows)
+        s_rowend[tid] = re0 - n0;
+    for (int i = kBlock + tid; i < nrows; i += kBlock)  // rare: > 256 rows in the tile
+        s_rowend[i] = a.row_offsets[r0 + 1 + i] - n0;
     __syncthreads();
+    if (stopped)
+        return;
 
     double2 dot = make_double2(0.0, 0.0);
     const int rmode = a.rmode[t];
@@ -1213,26 +1232,46 @@ __global__ __launch_bounds__(kBlock) void k_spmm_tile(TileArgs a)
                 tsum.x += s_red2[w][tid].x;
                 tsum.y += s_red2[w][tid].y;
             }
-            store_sc1(&a.partials[(size_t)t * L + 2 * tid], tsum.x);
-            store_sc1(&a.partials[(size_t)t * L + 2 * tid + 1], tsum.y);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            // plain stores: k_fold_dot (a later launch) sums the tiles' partials
+            a.partials[(size_t)t * L + 2 * tid] = tsum.x;
+            a.partials[(size_t)t * L + 2 * tid + 1] = tsum.y;
         }
-        __syncthreads();
-        __shared__ double s_colred[kBlock];
-        __shared__ double s_tot[L];
-        if (!reduce_slots<L>(a.partials, a.gtickets, t, a.num_tiles, s_colred, s_tot, &s_last))
-            return;
-        if (tid < L && MODE == kModeDot) {
-            a.dot_out[tid] = s_tot[tid];
-            // single-GPU split CG iteration (scal given): a non-finite alpha stops the solve
-            // before the update touches x and r, as the fused path does
-            if (a.scal && !a.conv[tid]) {
-                const double alpha = a.scal[tid].rs_old / s_tot[tid];
-                if (!(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
-                    a.ctrl->breakdown = 1;
-                    a.ctrl->done = 1;
-                    a.ctrl->iters_out = a.ctrl->iter + 1;
-                }
+    }
+}
+
+// x.(A x) per column from the tile kernels' MODE 2 partials [T][L], in a fixed order: block g
+// folds tiles [g*q, g*q + q) (fold_cols), reduce_slots folds the block sums and its last block
+// writes dot_out.  The tile kernels thus end without any ticket or store drain (a ticket per
+// tile cost the L = 8 SpMM ~40 % on the nlpkkt120 shape).  scal given (single-GPU split CG): a
+// non-finite alpha = rs_old / dot stops the solve before the update touches x and r.
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_fold_dot(const double *part, int T, int q, double *lvl,
+                                                     unsigned *tickets, double *dot_out, const CgScalars *scal,
+                                                     const unsigned char *conv, CgControl *ctrl)
+{
+    __shared__ double s_tmp[kBlock];
+    __shared__ double s_out[L];
+    __shared__ int s_last;
+    const int tid = threadIdx.x;
+    if (ctrl && ctrl->done)
+        return;
+    const int t0 = min((int)blockIdx.x * q, T);
+    fold_cols<L>(part + (size_t)t0 * L, min(q, T - t0), s_tmp, s_out);
+    if (tid < L) {
+        store_sc1(&lvl[(size_t)blockIdx.x * L + tid], s_out[tid]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (!reduce_slots<L>(lvl, tickets, blockIdx.x, gridDim.x, s_tmp, s_out, &s_last))
+        return;
+    if (tid < L) {
+        dot_out[tid] = s_out[tid];
+        if (scal && !conv[tid]) {
+            const double alpha = scal[tid].rs_old / s_out[tid];
+            if (!(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
+                ctrl->breakdown = 1;
+                ctrl->done = 1;
+                ctrl->iters_out = ctrl->iter + 1;
             }
         }
     }
@@ -2077,16 +2116,8 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
     hipError_t e = launch_dist_vec(2, va, L, nblk, h->d_p0, h->stream);
     if (e != hipSuccess)
         return e;
-    TileArgs ta = make_args(h, plan, h->d_p0, h->d_ap, L);
-    ta.scal = h->d_scal;
-    ta.ctrl = h->d_ctrl;
-    ta.conv = h->d_conv;
-    ta.partials = h->d_partials;
-    ta.gtickets = h->d_gtickets;
-    ta.dot_out = h->d_red;
-    if ((e = launch_tile<kModeDot>(ta, L, h->stream, h->num_cus, stream_nt(h))) != hipSuccess)
-        return e;
-    if ((e = launch_fixup_ctrl(h, plan, h->d_ap, L)) != hipSuccess)
+    if ((e = launch_spmm_dot(h, plan, h->d_p0, h->d_ap, L, h->d_ctrl, h->d_partials, h->d_gtickets, h->d_red,
+                             h->d_scal, h->d_conv)) != hipSuccess)
         return e;
     va.red_in = h->d_red;
     return dispatch_vec(false, va, L, nblk, h->stream);
@@ -2178,9 +2209,11 @@ hipError_t launch_dist_pack(const double *p, const int *idx, long long n_elems, 
     return hipGetLastError();
 }
 
-// Y = A X with x.(AX) per column reduced into dot_out (MODE 2), plus the carry fix-up.
+// Y = A X with x.(AX) per column reduced into dot_out (MODE 2), plus the carry fix-up and the
+// partials fold.  scal / conv (single-GPU split CG) add the non-finite-alpha stop.
 hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
-                           CgControl *ctrl, double *partials, unsigned *gtickets, double *dot_out)
+                           CgControl *ctrl, double *partials, unsigned *gtickets, double *dot_out,
+                           const CgScalars *scal, const unsigned char *conv)
 {
     if (plan.num_tiles == 0)  // a rank without rows contributes 0 to the all-reduce
         return hipMemsetAsync(dot_out, 0, sizeof(double) * L, h->stream);
@@ -2190,11 +2223,33 @@ hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double
     ta.gtickets = gtickets;
     ta.dot_out = dot_out;
     hipError_t e = launch_tile<kModeDot>(ta, L, h->stream, h->num_cus, stream_nt(h));
-    if (e != hipSuccess || plan.num_carries == 0)
+    if (e != hipSuccess)
         return e;
-    const int n = plan.num_carries * L;
-    hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, h->stream, plan.d_carry_tiles,
-                       plan.d_carry_rows, plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)ctrl);
+    if (plan.num_carries) {
+        const int n = plan.num_carries * L;
+        hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, h->stream, plan.d_carry_tiles,
+                           plan.d_carry_rows, plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)ctrl);
+        if ((e = hipGetLastError()) != hipSuccess)
+            return e;
+    }
+    const int T = plan.num_tiles;
+    const int G = std::max(1, std::min(256, (T + 63) / 64));  // >= 64 tiles per fold block
+    const int q = (T + G - 1) / G;
+    double *lvl = partials + (size_t)T * L;  // partials_capacity() leaves room for these levels
+    switch (L) {
+#define MSPMV_FOLD(LL)                                                                             \
+    case LL:                                                                                       \
+        hipLaunchKernelGGL((k_fold_dot<LL>), dim3(G), dim3(kBlock), 0, h->stream, partials, T, q, lvl, gtickets, \
+                           dot_out, scal, conv, ctrl);                                             \
+        break;
+        MSPMV_FOLD(1)
+        MSPMV_FOLD(2)
+        MSPMV_FOLD(4)
+        MSPMV_FOLD(8)
+        MSPMV_FOLD(16)
+#undef MSPMV_FOLD
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Lab builds of libmspmv.so with compile-time ablations of the SpMV tile kernel (measurement only;
 # results are wrong by construction).  MSPMV_LIB=tools/lab/libmspmv_ablN.so selects one.
-#   bit 1: no x gather   bit 2: no in-tile reduction   bit 4: no bounds load (nominal tiles)
+#   (the MSPMV_LAB_ABLATE switches are added to the kernels by hand for an experiment and removed after)
 set -e
 cd "$(dirname "$0")/../.."
 C=sparse-matrix-linear-equations_amd/csrc
