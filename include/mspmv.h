@@ -131,6 +131,28 @@ MSPMV_API mspmv_status mspmv_dcg_multi_dev(mspmv_handle h, const double *d_B, do
                                  double tolerance, mspmv_spmm_kernel kernel, int *iters, double *max_err_hist,
                                  int hist_cap);
 
+/* ---- SPAI-preconditioned block CG ---------------------------------------------------- */
+/* SPAI preconditioner M with A's own pattern, SparseApproximateInversion
+ * (work_2025/cg/sparse_approximate_inversion.hpp:40-321): column k of M minimises
+ * ||A(I,J) m - e_k(I)||_2 (J = rows of A's column k, I = rows those columns touch; Householder
+ * QR where the reference calls LAPACKE_dgels; a rank-deficient column gives zeros, as the
+ * reference's info != 0 fallback), then M = (M + M^T)/2 over the pattern.  Host setup
+ * (OpenMP), like the reference's; m_values[num_nonzeros] receives M's values in A's CSR order,
+ * so M's CSR is (A.row_offsets, A.column_indices, m_values).  Square A only. */
+MSPMV_API mspmv_status mspmv_spai_values(const mspmv_csr_d *a, double *m_values);
+/* SPAISolveMultiple (work_2025/main/sparse_approximate_inverse.hpp:30-230) on the GPU: X = 0,
+ * R = B, Z = M R, P = Z, rs_old = R.Z; per iteration AP = A P, alpha = rs_old/P.AP (0 when
+ * converged or P.AP == 0), X += alpha P, R -= alpha AP, stop test on sqrt(R.R)/||B_j|| with the
+ * per-column masks and the max-over-columns history, Z = M R, beta = R.Z/rs_old (0 when converged
+ * or rs_old == 0), P = Z + beta P.  `m` is M's handle (same shape and device as `a`); both SpMMs
+ * are merge-path tile kernels.  L in {1, 2, 4, 8, 16}; interleaved n x L panels. */
+MSPMV_API mspmv_status mspmv_dpcg_spai_multi(mspmv_handle a, mspmv_handle m, const double *B, double *X, int L,
+                                             int max_iters, double tolerance, mspmv_spmm_kernel kernel, int *iters,
+                                             double *max_err_hist, int hist_cap);
+MSPMV_API mspmv_status mspmv_dpcg_spai_multi_dev(mspmv_handle a, mspmv_handle m, const double *d_B, double *d_X,
+                                                 int L, int max_iters, double tolerance, mspmv_spmm_kernel kernel,
+                                                 int *iters, double *max_err_hist, int hist_cap);
+
 /* ---- measurement helpers (HIP events on the handle's stream) ------------------------ */
 /* Enqueue `reps` back-to-back SpMV (L == 1) or SpMM launches on device buffers and return
  * the average milliseconds per call measured by hipEvents on the handle's stream.

@@ -490,6 +490,106 @@ ORC_EXPORT int orc_cg_multi(int num_rows, int num_nonzeros, const int *row_offse
     return iter;
 }
 
+/* SPAISolveMultiple: work_2025/main/sparse_approximate_inverse.hpp:30-230.  M shares A's
+ * pattern (SparseApproximateInversion's static pattern), so only its values m_vals are passed.
+ * Z = M R and A P run through the same SpmmKernel dispatch as the reference (:81-92, :114-125,
+ * :184-195). */
+static void spmm_dispatch(int kernel_type, int num_threads, int n, int nnz, const int *row_offsets, const int *cols,
+                          const double *vals, const double *X, double *Y, int L)
+{
+    switch (kernel_type) {
+    case ORC_SIMPLE:
+        orc_csr_spmm_t(n, row_offsets, cols, vals, X, Y, L);
+        break;
+    case ORC_MERGE:
+        orc_merge_csrmm(num_threads, n, nnz, row_offsets, cols, vals, X, Y, L);
+        break;
+    default:
+        orc_nonzero_split_csrmm(num_threads, n, nnz, row_offsets, cols, vals, X, Y, L);
+        break;
+    }
+}
+
+ORC_EXPORT int orc_pcg_spai_multi(int num_rows, int num_nonzeros, const int *row_offsets, const int *cols,
+                                  const double *vals, const double *m_vals, const double *B, double *X, int L,
+                                  int max_iters, double tolerance, int kernel_type, int num_threads,
+                                  double *max_err_hist, int hist_cap)
+{
+    int n = num_rows;
+    size_t nl = (size_t)n * L;
+    double *R = (double *)malloc(sizeof(double) * nl);
+    double *P = (double *)malloc(sizeof(double) * nl);
+    double *AP = (double *)malloc(sizeof(double) * nl);
+    double *Z = (double *)malloc(sizeof(double) * nl);
+    double *alpha = (double *)malloc(sizeof(double) * L);
+    double *beta = (double *)malloc(sizeof(double) * L);
+    double *rs_old = (double *)malloc(sizeof(double) * L);
+    double *rs_new = (double *)malloc(sizeof(double) * L);
+    double *pAp = (double *)malloc(sizeof(double) * L);
+    double *b_norms = (double *)malloc(sizeof(double) * L);
+    char *converged = (char *)malloc(L);
+
+    for (size_t i = 0; i < nl; ++i) { /* :59-67 */
+        X[i] = 0.0;
+        R[i] = B[i];
+        P[i] = 0.0;
+        Z[i] = 0.0;
+    }
+    dot_multiple(n, L, B, B, b_norms); /* :69-78 */
+    for (int i = 0; i < L; ++i) {
+        b_norms[i] = sqrt(b_norms[i]);
+        if (b_norms[i] == 0.0)
+            b_norms[i] = 1.0;
+        converged[i] = 0;
+    }
+    memset(Z, 0, sizeof(double) * nl);
+    spmm_dispatch(kernel_type, num_threads, n, num_nonzeros, row_offsets, cols, m_vals, R, Z, L); /* :80-92 */
+    for (size_t i = 0; i < nl; ++i)                                                              /* :94-97 */
+        P[i] = Z[i];
+    dot_multiple(n, L, R, Z, rs_old); /* :99-100 */
+
+    int iter;
+    for (iter = 0; iter < max_iters; ++iter) {
+        memset(AP, 0, sizeof(double) * nl);
+        spmm_dispatch(kernel_type, num_threads, n, num_nonzeros, row_offsets, cols, vals, P, AP, L); /* :111-125 */
+        dot_multiple(n, L, P, AP, pAp);                                                           /* :127-128 */
+        for (int i = 0; i < L; ++i)                                                               /* :130-138 */
+            alpha[i] = (!converged[i] && pAp[i] != 0.0) ? rs_old[i] / pAp[i] : 0.0;
+        axpy_multiple(n, L, alpha, P, X); /* :140-141 */
+        for (int i = 0; i < L; ++i)
+            alpha[i] = -alpha[i];
+        axpy_multiple(n, L, alpha, AP, R); /* :143-149 */
+        dot_multiple(n, L, R, R, pAp);     /* :151-153 */
+        int num_converged = 0;             /* :155-169 */
+        double max_relative_error = 0.0;
+        for (int i = 0; i < L; ++i) {
+            double rel_error = sqrt(pAp[i]) / b_norms[i];
+            max_relative_error = max_relative_error > rel_error ? max_relative_error : rel_error;
+            if (!converged[i] && rel_error < tolerance)
+                converged[i] = 1;
+            if (converged[i])
+                num_converged++;
+        }
+        if (max_err_hist && iter < hist_cap) /* :171-175 */
+            max_err_hist[iter] = max_relative_error;
+        if (num_converged == L) { /* :177-181 */
+            iter++;
+            break;
+        }
+        memset(Z, 0, sizeof(double) * nl);
+        spmm_dispatch(kernel_type, num_threads, n, num_nonzeros, row_offsets, cols, m_vals, R, Z, L); /* :183-195 */
+        dot_multiple(n, L, R, Z, rs_new);                                                            /* :197-198 */
+        for (int i = 0; i < L; ++i) {                                                                /* :200-210 */
+            beta[i] = (!converged[i] && rs_old[i] != 0.0) ? rs_new[i] / rs_old[i] : 0.0;
+            rs_old[i] = rs_new[i];
+        }
+        update_p_multiple(n, L, Z, beta, P); /* :212-214 */
+    }
+    free(R); free(P); free(AP); free(Z); free(alpha); free(beta);
+    free(rs_old); free(rs_new); free(pAp); free(b_norms); free(converged);
+    return iter;
+}
+
 /* calculate_threshold: cpu_singlecg.cpp:22-34 (dup cpu_multicg.cpp:49-61). */
 ORC_EXPORT double orc_calculate_threshold(const double *b, int num_rows, double tolerance)
 {

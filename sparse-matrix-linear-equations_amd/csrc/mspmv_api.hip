@@ -394,6 +394,10 @@ mspmv_status mspmv_destroy(mspmv_handle h)
     dev_free(h->d_conv);
     dev_free(h->d_ctrl);
     dev_free(h->d_hist);
+    if (h->cg_exec)
+        (void)hipGraphExecDestroy(h->cg_exec);
+    if (h->cg_graph)
+        (void)hipGraphDestroy(h->cg_graph);
     if (h->d_flush)
         (void)hipFree(h->d_flush);
     if (h->h_ctrl)
@@ -568,11 +572,14 @@ static mspmv_status ensure_cg_workspace(mspmv_handle_s *h, int L, int nblk, int 
     return MSPMV_OK;
 }
 
+// CG (hm == nullptr) or SPAI-preconditioned CG with the preconditioner's handle hm.
 static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d_x, int L, int max_iters,
-                                 double tol, int *iters, double *hist, int hist_cap)
+                                 double tol, int *iters, double *hist, int hist_cap, mspmv_handle_s *hm = nullptr)
 {
     if (h->m != h->n)
         return invalid("CG needs a square matrix");
+    if (hm && (hm->m != h->m || hm->n != h->n || hm->device != h->device))
+        return invalid("the preconditioner must match the matrix's shape and device");
     if (!supported_L(L))
         return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
     if (max_iters < 0)
@@ -585,38 +592,72 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
         *iters = 0;
     if (h->m == 0)
         return MSPMV_OK;
-    const TilePlan *plan = nullptr;
+    const TilePlan *plan = nullptr, *mplan = nullptr;
     ST_TRY(get_plan(h, L, &plan));
-    const bool pipelined = !cg_split_iteration(L);  // single RHS: consumer-side reductions
+    if (hm) {
+        ST_TRY(get_plan(hm, L, &mplan));
+        HIP_TRY(hipStreamSynchronize(hm->stream));  // hm's SpMMs are enqueued on h's stream
+    }
+    const bool pipelined = !hm && !cg_split_iteration(L);  // single RHS: consumer-side reductions
     const int nblk = pipelined ? cg1_blocks(h->m) : cg_update_blocks((long long)h->m * L);
     const int cap = hist ? std::max(hist_cap, 0) : 0;
-    ST_TRY(ensure_cg_workspace(h, L, nblk, plan->num_tiles, cap));
+    ST_TRY(ensure_cg_workspace(h, L, nblk, std::max(plan->num_tiles, mplan ? mplan->num_tiles : 0), cap));
     const int use_cap = hist ? cap : 0;
     const int saved_cap = h->hist_cap;
     h->hist_cap = use_cap;  // kernels record only what the caller asked for
     HIP_TRY(hipMemsetAsync(h->d_ctrl, 0, sizeof(CgControl), h->stream));
-    if (pipelined)
+    if (hm)
+        HIP_TRY(launch_pcg_init(h, hm, *mplan, d_b, d_x, L, tol, nblk));
+    else if (pipelined)
         HIP_TRY(launch_cg1_init(h, d_b, d_x, nblk));
     else
         HIP_TRY(launch_cg_init(h, d_b, d_x, L, tol, nblk));
+    auto iterate = [&](int i) -> hipError_t {
+        return hm ? launch_pcg_iteration(h, hm, *plan, *mplan, d_x, L, nblk, tol)
+                  : launch_cg_iteration(h, *plan, d_x, L, i & 1, nblk, tol);
+    };
 
     constexpr int K = 32;  // iterations per graph replay (even: p buffers alternate)
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t exec = nullptr;
     mspmv_status st = MSPMV_OK;
+    hipGraphExec_t exec = nullptr;
     if (max_iters >= K) {
-        hipError_t e = hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal);
-        for (int i = 0; i < K && e == hipSuccess; ++i)
-            e = launch_cg_iteration(h, *plan, d_x, L, i & 1, nblk, tol);
-        hipError_t e2 = hipStreamEndCapture(h->stream, &graph);
-        if (e == hipSuccess)
-            e = e2;
-        if (e == hipSuccess)
-            e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-        if (e != hipSuccess) {
-            set_error(std::string("CG graph capture: ") + hipGetErrorString(e));
-            st = MSPMV_ERR_HIP;
+        // The graph bakes in every buffer, the plan, L, the tolerance and the history size:
+        // reuse the handle's graph while all of them are unchanged (instantiation costs ms).
+        const void *tk = nullptr;
+        static_assert(sizeof(tk) == sizeof(tol), "tolerance bits as a key word");
+        std::memcpy(&tk, &tol, sizeof tk);
+        const std::vector<const void *> key = {
+            d_x, h->d_r, h->d_p0, h->d_p1, h->d_ap, h->d_partials, h->d_partials_b, h->d_gtickets, h->d_scal,
+            h->d_conv, h->d_red, h->d_ctrl, h->d_hist, h->stream, plan, tk,
+            reinterpret_cast<const void *>((intptr_t)L), reinterpret_cast<const void *>((intptr_t)nblk),
+            reinterpret_cast<const void *>((intptr_t)use_cap), hm, mplan,
+            hm ? (const void *)hm->d_vals : nullptr};
+        if (!h->cg_exec || h->cg_graph_key != key) {
+            if (h->cg_exec)
+                (void)hipGraphExecDestroy(h->cg_exec);
+            if (h->cg_graph)
+                (void)hipGraphDestroy(h->cg_graph);
+            h->cg_exec = nullptr;
+            h->cg_graph = nullptr;
+            h->cg_graph_key.clear();
+            hipError_t e = hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal);
+            for (int i = 0; i < K && e == hipSuccess; ++i)
+                e = iterate(i);
+            hipGraph_t graph = nullptr;
+            hipError_t e2 = hipStreamEndCapture(h->stream, &graph);
+            if (e == hipSuccess)
+                e = e2;
+            h->cg_graph = graph;
+            if (e == hipSuccess)
+                e = hipGraphInstantiate(&h->cg_exec, graph, nullptr, nullptr, 0);
+            if (e != hipSuccess) {
+                set_error(std::string("CG graph capture: ") + hipGetErrorString(e));
+                st = MSPMV_ERR_HIP;
+            } else {
+                h->cg_graph_key = key;
+            }
         }
+        exec = h->cg_exec;
     }
     hipEvent_t evs[2] = {nullptr, nullptr};
     if (st == MSPMV_OK && (hipEventCreateWithFlags(&evs[0], hipEventDisableTiming) != hipSuccess ||
@@ -636,7 +677,7 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
                 e = hipGraphLaunch(exec, h->stream);
             else
                 for (int i = 0; i < k && e == hipSuccess; ++i)
-                    e = launch_cg_iteration(h, *plan, d_x, L, i & 1, nblk, tol);
+                    e = iterate(i);
             if (e == hipSuccess)
                 e = hipMemcpyAsync(&h->h_ctrl[slot], h->d_ctrl, sizeof(CgControl), hipMemcpyDeviceToHost, h->stream);
             if (e == hipSuccess)
@@ -684,10 +725,6 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
     for (auto &ev : evs)
         if (ev)
             (void)hipEventDestroy(ev);
-    if (exec)
-        (void)hipGraphExecDestroy(exec);
-    if (graph)
-        (void)hipGraphDestroy(graph);
     h->hist_cap = saved_cap;
     if (st != MSPMV_OK)
         return st;
@@ -707,7 +744,7 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
 }
 
 static mspmv_status cg_solve_host(mspmv_handle h, const double *B, double *X, int L, int max_iters, double tol,
-                                  int *iters, double *hist, int hist_cap)
+                                  int *iters, double *hist, int hist_cap, mspmv_handle hm = nullptr)
 {
     ST_TRY(check_handle(h));
     if (h->m == 0) {
@@ -726,7 +763,7 @@ static mspmv_status cg_solve_host(mspmv_handle h, const double *B, double *X, in
         st = MSPMV_ERR_HIP;
     }
     if (st == MSPMV_OK)
-        st = cg_solve_dev(h, dB, dX, L, max_iters, tol, iters, hist, hist_cap);
+        st = cg_solve_dev(h, dB, dX, L, max_iters, tol, iters, hist, hist_cap, hm);
     if ((st == MSPMV_OK || st == MSPMV_ERR_BREAKDOWN) && hipMemcpy(X, dX, bytes, hipMemcpyDeviceToHost) != hipSuccess) {
         set_error("X download failed");
         st = MSPMV_ERR_HIP;
@@ -765,6 +802,27 @@ mspmv_status mspmv_dcg_multi(mspmv_handle h, const double *B, double *X, int L, 
     if (!supported_L(L))
         return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
     return cg_solve_host(h, B, X, L, max_iters, tolerance, iters, max_err_hist, hist_cap);
+}
+
+mspmv_status mspmv_dpcg_spai_multi_dev(mspmv_handle a, mspmv_handle m, const double *d_B, double *d_X, int L,
+                                       int max_iters, double tolerance, mspmv_spmm_kernel kernel, int *iters,
+                                       double *max_err_hist, int hist_cap)
+{
+    (void)kernel;  // the GPU always runs the merge-path SpMM
+    ST_TRY(check_handle(a));
+    ST_TRY(check_handle(m));
+    return cg_solve_dev(a, d_B, d_X, L, max_iters, tolerance, iters, max_err_hist, hist_cap, m);
+}
+
+mspmv_status mspmv_dpcg_spai_multi(mspmv_handle a, mspmv_handle m, const double *B, double *X, int L, int max_iters,
+                                   double tolerance, mspmv_spmm_kernel kernel, int *iters, double *max_err_hist,
+                                   int hist_cap)
+{
+    (void)kernel;
+    if (!supported_L(L))
+        return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
+    ST_TRY(check_handle(m));
+    return cg_solve_host(a, B, X, L, max_iters, tolerance, iters, max_err_hist, hist_cap, m);
 }
 
 // ---- measurement ---------------------------------------------------------------------------

@@ -95,6 +95,10 @@ struct mspmv_handle_s {
     double *d_hist = nullptr;
     int hist_cap = 0;
     int scal_cap = 0;
+    // CG iteration graph (K iterations), reused while everything it was captured with is unchanged
+    hipGraph_t cg_graph = nullptr;
+    hipGraphExec_t cg_exec = nullptr;
+    std::vector<const void *> cg_graph_key;
     // timing
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     double last_tile_kernel_ms = 0.0;
@@ -169,6 +173,7 @@ struct DistVecArgs {
     const double *red_in;
     double *red_out;
     unsigned *gtickets;
+    int pcg;
 };
 // which: 0 init partial sums (b.b -> red_out), 1 init finish (red_in = all-reduced b.b),
 // 2 p update, 3 x/r update (alpha from red_in = all-reduced p.Ap; r.r -> red_out),
@@ -178,7 +183,15 @@ hipError_t launch_dist_pack(const double *p, const int *idx, long long n_elems, 
                             const CgControl *ctrl, hipStream_t s);
 hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
                            CgControl *ctrl, double *partials, unsigned *gtickets, double *dot_out,
-                           const CgScalars *scal = nullptr, const unsigned char *conv = nullptr);
+                           CgScalars *scal = nullptr, const unsigned char *conv = nullptr, int fold_mode = -1);
+// SPAI-preconditioned block CG (SPAISolveMultiple, work_2025/main/sparse_approximate_inverse.hpp:
+// 30-230) on A's handle h with the preconditioner's handle hm (same shape and device): init
+// (X = 0, R = B, Z = M R, P = Z, rs_old = R.Z) and one iteration (AP = A P -> alpha; X, R update
+// and stop test; Z = M R -> beta; P = Z + beta P).  hm's SpMMs run on h's stream.
+hipError_t launch_pcg_init(mspmv_handle_s *h, mspmv_handle_s *hm, const TilePlan &mplan, const double *d_b,
+                           double *d_x, int L, double tol, int nblk);
+hipError_t launch_pcg_iteration(mspmv_handle_s *h, mspmv_handle_s *hm, const TilePlan &plan, const TilePlan &mplan,
+                                double *d_x, int L, int nblk, double tol);
 // Partials capacity (doubles) and group-ticket count for `slots` partial slots of L columns.
 // (every level of the tree: slots, slots/32, ... -> <= slots * 32/31 + one per level)
 inline size_t partials_capacity(size_t slots, int L) { return (slots + slots / (kSlotGroup - 1) + 8) * L; }

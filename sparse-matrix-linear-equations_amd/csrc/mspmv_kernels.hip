@@ -1040,8 +1040,19 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
 // Multi right-hand side (L = 2..16, row-major panels).  A group of L/2 lanes owns one merge
 // walk; each lane keeps a double2 of the L running totals (running_total[L],
 // merge_based.hpp:84-127).  TILE = (256/(L/2)) groups * IPTG items.
+// Workgroups per CU the multi-RHS tile's LDS allows, capped at 7: the register budget is pinned
+// to it (the dot mode would otherwise need 90 VGPRs and fall to 5 workgroups at L = 8).
+constexpr int spmm_waves_per_eu(int L, int IPTG)
+{
+    const int items = (kBlock / (L / 2)) * IPTG;
+    const int lds = 16 * (items + items / kSnapDiv) + 6144;  // + s_crow, s_cval, s_red2
+    const int w = 163840 / lds;
+    return w < 1 ? 1 : w > 7 ? 7 : w;
+}
+
 template <int L, int IPTG, int MODE, bool NT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) void k_spmm_tile(TileArgs a)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(spmm_waves_per_eu(L, IPTG)))) void
+k_spmm_tile(TileArgs a)
 {
     static_assert(MODE != kModeCg, "multi-RHS CG runs the split iteration (MODE 2)");
     constexpr int GL = L / 2;
@@ -1239,6 +1250,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
     }
 }
 
+// What the fold's last block derives from the totals (k_fold_dot `mode`).
+enum : int { kFoldDot = 0, kFoldCgAlpha = 1, kFoldPcgAlpha = 2, kFoldPcgBeta = 3, kFoldPcgInit = 4 };
+
 // x.(A x) per column from the tile kernels' MODE 2 partials [T][L], in a fixed order: block g
 // folds tiles [g*q, g*q + q) (fold_cols), reduce_slots folds the block sums and its last block
 // writes dot_out.  The tile kernels thus end without any ticket or store drain (a ticket per
@@ -1246,8 +1260,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(7))) voi
 // non-finite alpha = rs_old / dot stops the solve before the update touches x and r.
 template <int L>
 __global__ __launch_bounds__(kBlock) void k_fold_dot(const double *part, int T, int q, double *lvl,
-                                                     unsigned *tickets, double *dot_out, const CgScalars *scal,
-                                                     const unsigned char *conv, CgControl *ctrl)
+                                                     unsigned *tickets, double *dot_out, CgScalars *scal,
+                                                     const unsigned char *conv, CgControl *ctrl, int mode)
 {
     __shared__ double s_tmp[kBlock];
     __shared__ double s_out[L];
@@ -1265,14 +1279,25 @@ __global__ __launch_bounds__(kBlock) void k_fold_dot(const double *part, int T, 
     if (!reduce_slots<L>(lvl, tickets, blockIdx.x, gridDim.x, s_tmp, s_out, &s_last))
         return;
     if (tid < L) {
-        dot_out[tid] = s_out[tid];
-        if (scal && !conv[tid]) {
-            const double alpha = scal[tid].rs_old / s_out[tid];
+        const double d = s_out[tid];
+        dot_out[tid] = d;
+        if (mode == kFoldCgAlpha && !conv[tid]) {
+            const double alpha = scal[tid].rs_old / d;
             if (!(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
                 ctrl->breakdown = 1;
                 ctrl->done = 1;
                 ctrl->iters_out = ctrl->iter + 1;
             }
+        } else if (mode == kFoldPcgAlpha) {  // sparse_approximate_inverse.hpp:131-138
+            CgScalars &s = scal[tid];
+            s.pAp = d;
+            s.alpha = (!conv[tid] && d != 0.0) ? s.rs_old / d : 0.0;
+        } else if (mode == kFoldPcgBeta) {  // :200-210 (rs_old <- rs_new for every column)
+            CgScalars &s = scal[tid];
+            s.beta = (!conv[tid] && s.rs_old != 0.0) ? d / s.rs_old : 0.0;
+            s.rs_old = d;
+        } else if (mode == kFoldPcgInit) {  // :99-100
+            scal[tid].rs_old = d;
         }
     }
 }
@@ -1360,6 +1385,7 @@ struct CgVecArgs {
     const double *red_in;
     double *red_out;
     unsigned *gtickets;  // reduce_slots tickets
+    int pcg;             // k_cg_update: SPAI-PCG (beta and rs_old come from R.Z, k_fold_dot)
 };
 
 // x = 0, r = p0 = b; rs_old_j = r_j.r_j, b_norm_j = sqrt(b_j.b_j) (no_pretreatment.hpp:61-79,
@@ -1499,7 +1525,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(CgVecArgs a)
             if (nconv == L) {
                 a.ctrl->done = 1;
                 a.ctrl->iters_out = iter + 1;
-            } else {
+            } else if (!a.pcg) {  // PCG: beta and rs_old follow Z = M R (k_fold_dot kFoldPcgBeta)
                 for (int j = 0; j < L; ++j) {
                     CgScalars &s = a.scal[j];
                     s.beta = a.conv[j] ? 0.0 : s.rs_new / s.rs_old;
@@ -2213,8 +2239,9 @@ hipError_t launch_dist_pack(const double *p, const int *idx, long long n_elems, 
 // partials fold.  scal / conv (single-GPU split CG) add the non-finite-alpha stop.
 hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
                            CgControl *ctrl, double *partials, unsigned *gtickets, double *dot_out,
-                           const CgScalars *scal, const unsigned char *conv)
+                           CgScalars *scal, const unsigned char *conv, int fold_mode)
 {
+    const int mode = fold_mode >= 0 ? fold_mode : scal ? kFoldCgAlpha : kFoldDot;
     if (plan.num_tiles == 0)  // a rank without rows contributes 0 to the all-reduce
         return hipMemsetAsync(dot_out, 0, sizeof(double) * L, h->stream);
     TileArgs ta = make_args(h, plan, d_X, d_Y, L);
@@ -2240,7 +2267,7 @@ hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double
 #define MSPMV_FOLD(LL)                                                                             \
     case LL:                                                                                       \
         hipLaunchKernelGGL((k_fold_dot<LL>), dim3(G), dim3(kBlock), 0, h->stream, partials, T, q, lvl, gtickets, \
-                           dot_out, scal, conv, ctrl);                                             \
+                           dot_out, scal, conv, ctrl, mode);                                       \
         break;
         MSPMV_FOLD(1)
         MSPMV_FOLD(2)
@@ -2286,6 +2313,71 @@ hipError_t launch_dist_vec_mirror(int which, const DistVecArgs &d, int L, int nb
     a.red_in = d.red_in;
     a.red_out = d.red_out;
     a.gtickets = d.gtickets;
+    a.pcg = d.pcg;
     return launch_dist_vec(which, a, L, nblk, p, s);
+}
+
+// ---- SPAI-preconditioned block CG (SPAISolveMultiple) ------------------------------------------
+static CgVecArgs pcg_vec_args(mspmv_handle_s *h, double *d_x, int L, double tol)
+{
+    CgVecArgs va{};
+    va.n_elems = (long long)h->m * L;
+    va.x = d_x;
+    va.r = h->d_r;
+    va.p = h->d_p0;
+    va.p0 = h->d_p0;
+    va.ap = h->d_ap;
+    va.scal = h->d_scal;
+    va.ctrl = h->d_ctrl;
+    va.conv = h->d_conv;
+    va.partials = h->d_partials;
+    va.gtickets = h->d_gtickets;
+    va.hist = h->d_hist;
+    va.hist_cap = h->hist_cap;
+    va.tol = tol;
+    va.pcg = 1;
+    return va;
+}
+
+// X = 0, R = B, b_norms (sparse_approximate_inverse.hpp:59-78); Z = M R and rs_old = R.Z
+// (:80-92, :99-100); P = Z (:94-97).  Z lives in h->d_p1, P in h->d_p0.
+hipError_t launch_pcg_init(mspmv_handle_s *h, mspmv_handle_s *hm, const TilePlan &mplan, const double *d_b,
+                           double *d_x, int L, double tol, int nblk)
+{
+    hipError_t e = launch_cg_init(h, d_b, d_x, L, tol, nblk);
+    if (e != hipSuccess)
+        return e;
+    hipStream_t own = hm->stream;
+    hm->stream = h->stream;
+    e = launch_spmm_dot(hm, mplan, h->d_r, h->d_p1, L, h->d_ctrl, h->d_partials, h->d_gtickets, h->d_red,
+                        h->d_scal, h->d_conv, kFoldPcgInit);
+    hm->stream = own;
+    if (e != hipSuccess)
+        return e;
+    return hipMemcpyAsync(h->d_p0, h->d_p1, sizeof(double) * (size_t)h->m * L, hipMemcpyDeviceToDevice, h->stream);
+}
+
+// One PCG iteration, four launches plus two folds: AP = A P with P.AP -> alpha (:111-138);
+// X += alpha P, R -= alpha AP, R.R -> masks, max-residual history, stop (:140-181);
+// Z = M R with R.Z -> beta, rs_old (:183-210); P = Z + beta P (:212-214).
+hipError_t launch_pcg_iteration(mspmv_handle_s *h, mspmv_handle_s *hm, const TilePlan &plan, const TilePlan &mplan,
+                                double *d_x, int L, int nblk, double tol)
+{
+    CgVecArgs va = pcg_vec_args(h, d_x, L, tol);
+    hipError_t e = launch_spmm_dot(h, plan, h->d_p0, h->d_ap, L, h->d_ctrl, h->d_partials, h->d_gtickets, h->d_red,
+                                   h->d_scal, h->d_conv, kFoldPcgAlpha);
+    if (e != hipSuccess)
+        return e;
+    if ((e = dispatch_vec(false, va, L, nblk, h->stream)) != hipSuccess)
+        return e;
+    hipStream_t own = hm->stream;
+    hm->stream = h->stream;
+    e = launch_spmm_dot(hm, mplan, h->d_r, h->d_p1, L, h->d_ctrl, h->d_partials, h->d_gtickets, h->d_red,
+                        h->d_scal, h->d_conv, kFoldPcgBeta);
+    hm->stream = own;
+    if (e != hipSuccess)
+        return e;
+    va.r = h->d_p1;  // P = Z + beta P
+    return launch_dist_vec(2, va, L, nblk, h->d_p0, h->stream);
 }
 }  // namespace mspmv

@@ -81,6 +81,9 @@ _SIGS = {
     "mspmv_dcg_single_dev": (_I, [_P, _P, _P, _I, _D, _PI, _P, _I]),
     "mspmv_dcg_multi": (_I, [_P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
     "mspmv_dcg_multi_dev": (_I, [_P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
+    "mspmv_spai_values": (_I, [ctypes.POINTER(_CsrD), _P]),
+    "mspmv_dpcg_spai_multi": (_I, [_P, _P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
+    "mspmv_dpcg_spai_multi_dev": (_I, [_P, _P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
     "mspmv_time_spmm_dev": (_I, [_P, _P, _P, _I, _I, _SZ, _PD]),
     "mspmv_last_kernel_ms": (_I, [_P, _PD, _PI]),
     "mspmv_time_spmm_batch_dev": (_I, [_I, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _I,
@@ -403,6 +406,37 @@ class GpuCsr:
         _check(st, "dcg_multi_dev", allow=(4,))
         return it.value, hist[: min(it.value, hist_cap)], st
 
+    def pcg_spai(self, m: "GpuCsr", B: np.ndarray, max_iters: int, tolerance: float, hist_cap: int = 0):
+        """SPAISolveMultiple with the preconditioner M's handle `m` (mspmv_dpcg_spai_multi)."""
+        B = np.ascontiguousarray(B, np.float64)
+        if B.ndim == 1:
+            B = B[:, None]
+        L = B.shape[1]
+        X = np.empty_like(B)
+        it = ctypes.c_int()
+        hist = np.zeros(max(hist_cap, 1), np.float64)
+        st = lib.mspmv_dpcg_spai_multi(self.h, m.h, _ptr(B), _ptr(X), L, max_iters, tolerance, MERGE,
+                                       ctypes.byref(it), _ptr(hist) if hist_cap else None, hist_cap)
+        _check(st, "dpcg_spai_multi", allow=(4,))
+        return X, it.value, hist[: min(it.value, hist_cap)], st
+
+    def pcg_spai_dev(self, m: "GpuCsr", dB: DeviceBuffer, dX: DeviceBuffer, L: int, max_iters: int,
+                     tolerance: float, hist_cap: int = 0):
+        it = ctypes.c_int()
+        hist = np.zeros(max(hist_cap, 1), np.float64)
+        st = lib.mspmv_dpcg_spai_multi_dev(self.h, m.h, dB.ptr, dX.ptr, L, max_iters, tolerance, MERGE,
+                                           ctypes.byref(it), _ptr(hist) if hist_cap else None, hist_cap)
+        _check(st, "dpcg_spai_multi_dev", allow=(4,))
+        return it.value, hist[: min(it.value, hist_cap)], st
+
+
+def spai_values(a: CsrMatrix) -> np.ndarray:
+    """M's values on A's pattern (mspmv_spai_values; SparseApproximateInversion,
+    work_2025/cg/sparse_approximate_inversion.hpp:40-321).  Host setup, as in the reference."""
+    out = np.zeros(max(a.num_nonzeros, 1), np.float64)
+    _check(lib.mspmv_spai_values(ctypes.byref(a._c()), _ptr(out)), "spai_values")
+    return out[: a.num_nonzeros]
+
 
 def time_spmm_batch(gs, dXs, dYs, L: int, reps: int):
     """Time `reps` steps of one SpMM launch per matrix, all on gs[0]'s stream.
@@ -453,6 +487,25 @@ def CGSolveMultiple(a: CsrMatrix, B, X, num_vectors: int, max_iters: int, tolera
     Bm = np.asarray(B, np.float64).reshape(a.num_rows, num_vectors)
     cap = max_iters if max_errors is not None else 0
     Xs, it, hist, _ = _gpu(a).cg_multi(Bm, max_iters, tolerance, kernel_type, hist_cap=cap)
+    X[:] = Xs.reshape(-1)
+    if max_errors is not None:
+        max_errors.clear()
+        max_errors.extend(hist.tolist())
+    return it
+
+
+def SparseApproximateInversion(a: CsrMatrix) -> CsrMatrix:
+    """work_2025/cg/sparse_approximate_inversion.hpp:40-321: returns M (A's pattern, SPAI values).
+    The reference fills an output CsrMatrix argument and returns true; here M is returned."""
+    return CsrMatrix.from_arrays(a.num_cols, a.row_offsets, a.column_indices, spai_values(a))
+
+
+def SPAISolveMultiple(a: CsrMatrix, m: CsrMatrix, B, X, num_vectors: int, max_iters: int, tolerance: float,
+                      kernel_type: int = MERGE, max_errors: Optional[list] = None) -> int:
+    """work_2025/main/sparse_approximate_inverse.hpp:30-230 on flat interleaved n x num_vectors panels."""
+    Bm = np.asarray(B, np.float64).reshape(a.num_rows, num_vectors)
+    cap = max_iters if max_errors is not None else 0
+    Xs, it, hist, _ = _gpu(a).pcg_spai(_gpu(m), Bm, max_iters, tolerance, hist_cap=cap)
     X[:] = Xs.reshape(-1)
     if max_errors is not None:
         max_errors.clear()

@@ -38,6 +38,7 @@ class Oracle:
             "orc_nonzero_split_csrmm": (None, [_I, _I, _I, _P, _P, _P, _P, _P, _I]),
             "orc_cg_single": (_I, [_I, _P, _P, _P, _P, _P, _I, _D, _P, _I]),
             "orc_cg_multi": (_I, [_I, _I, _P, _P, _P, _P, _P, _I, _I, _D, _I, _I, _P, _I]),
+            "orc_pcg_spai_multi": (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _D, _I, _I, _P, _I]),
             "orc_calculate_threshold": (_D, [_P, _I, _D]),
             "orc_glibc_rand_fill": (None, [ctypes.c_uint, ctypes.c_longlong, _P]),
             "orc_coo_to_csr": (None, [_I, _I, _P, _P, _P, _P, _P, _P]),
@@ -128,6 +129,18 @@ class Oracle:
         it = self.lib.orc_cg_multi(a.num_rows, a.num_nonzeros, _p(a.row_offsets), _p(a.column_indices), _p(a.values),
                                    _p(B), _p(X), L, max_iters, tol, kernel, P, _p(hist) if hist_cap else None,
                                    hist_cap)
+        return X, it, hist[: min(it, hist_cap)]
+
+    def pcg_spai_multi(self, a, m_vals, B, max_iters, tol, kernel=1, P=8, hist_cap=0):
+        """SPAISolveMultiple (sparse_approximate_inverse.hpp:30-230); M = (A's pattern, m_vals)."""
+        B = np.ascontiguousarray(B, np.float64)
+        m_vals = np.ascontiguousarray(m_vals, np.float64)
+        L = B.shape[1]
+        X = np.empty_like(B)
+        hist = np.zeros(max(hist_cap, 1))
+        it = self.lib.orc_pcg_spai_multi(a.num_rows, a.num_nonzeros, _p(a.row_offsets), _p(a.column_indices),
+                                         _p(a.values), _p(m_vals), _p(B), _p(X), L, max_iters, tol, kernel, P,
+                                         _p(hist) if hist_cap else None, hist_cap)
         return X, it, hist[: min(it, hist_cap)]
 
     def calculate_threshold(self, b, n, tol):
