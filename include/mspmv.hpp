@@ -108,3 +108,38 @@ int CGSolveMultiple(Csr &a, const ValueT *B, ValueT *X, int num_vectors, int max
         max_errors->assign(hist.begin(), hist.begin() + std::min<size_t>(hist.size(), (size_t)iters));
     return iters;
 }
+
+// work_2025/cg/sparse_approximate_inversion.hpp:40-321: l receives A's pattern and the SPAI
+// values (arrays allocated with new[], the reference's own non-MKL branch, :68-72).
+template <typename Csr>
+bool SparseApproximateInversion(const Csr &a, Csr &l)
+{
+    l.num_rows = a.num_rows;
+    l.num_cols = a.num_cols;
+    l.num_nonzeros = a.num_nonzeros;
+    l.row_offsets = new int[(size_t)a.num_rows + 1];
+    l.column_indices = new int[(size_t)a.num_nonzeros];
+    l.values = new double[(size_t)a.num_nonzeros];
+    std::copy(a.row_offsets, a.row_offsets + a.num_rows + 1, l.row_offsets);
+    std::copy(a.column_indices, a.column_indices + a.num_nonzeros, l.column_indices);
+    mspmv_csr_d d{a.num_rows, a.num_cols, a.num_nonzeros, a.row_offsets, a.column_indices, a.values};
+    mspmv_facade::check(mspmv_spai_values(&d, l.values), "mspmv_spai_values");
+    return true;
+}
+
+// work_2025/main/sparse_approximate_inverse.hpp:30-230
+template <typename Csr, typename ValueT, typename KernelT>
+int SPAISolveMultiple(Csr &a, Csr &m, const ValueT *B, ValueT *X, int num_vectors, int max_iters,
+                      ValueT tolerance, KernelT kernel_type, std::vector<double> *max_errors = nullptr)
+{
+    int iters = 0;
+    std::vector<double> hist(max_errors ? (size_t)max_iters : 0);
+    mspmv_facade::check(mspmv_dpcg_spai_multi(mspmv_facade::handle_for(a), mspmv_facade::handle_for(m), B, X,
+                                              num_vectors, max_iters, tolerance,
+                                              (mspmv_spmm_kernel)(int)kernel_type, &iters,
+                                              max_errors ? hist.data() : nullptr, max_errors ? max_iters : 0),
+                        "mspmv_dpcg_spai_multi");
+    if (max_errors)
+        max_errors->assign(hist.begin(), hist.begin() + std::min<size_t>(hist.size(), (size_t)iters));
+    return iters;
+}
