@@ -84,6 +84,8 @@ static void free_plan(TilePlan &p)
     dev_free(p.d_carry_tiles);
     dev_free(p.d_carry_rows);
     dev_free(p.d_carry_val);
+    dev_free(p.d_colbase);
+    dev_free(p.d_cols16);
 }
 
 // Build (once) the tile plan for L right-hand sides, validating on the host every bound the
@@ -194,6 +196,31 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
         if (e != hipSuccess) {
             set_error(std::string("tile plan upload: ") + hipGetErrorString(e));
             return fail(MSPMV_ERR_HIP);
+        }
+    }
+    if (L == 1 && T > 0 && h->nnz > 0 && spmv_cols16_enabled()) {  // the single-RHS kernels' 16-bit stream
+        if ((st = dev_alloc(&p.d_colbase, (size_t)T)) != MSPMV_OK ||
+            (st = dev_alloc(&p.d_cols16, (size_t)h->nnz + kNnzPad)) != MSPMV_OK)
+            return fail(st);
+        e = hipMemsetAsync(p.d_cols16, 0, sizeof(unsigned short) * ((size_t)h->nnz + kNnzPad), h->stream);
+        if (e == hipSuccess)
+            e = launch_pack_cols16(h->d_cols, p.d_bounds, T, p.d_colbase, p.d_cols16, h->stream);
+        std::vector<int> hbase((size_t)T);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(hbase.data(), p.d_colbase, sizeof(int) * T, hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) {
+            set_error(std::string("16-bit columns: ") + hipGetErrorString(e));
+            return fail(MSPMV_ERR_HIP);
+        }
+        for (int b : hbase)
+            p.num_tiles16 += b >= 0;
+        if (p.num_tiles16 == 0) {  // nothing fits: keep the plan on int32 columns only
+            dev_free(p.d_colbase);
+            dev_free(p.d_cols16);
+            p.d_colbase = nullptr;
+            p.d_cols16 = nullptr;
         }
     }
     auto res = h->plans.emplace(tile, p);

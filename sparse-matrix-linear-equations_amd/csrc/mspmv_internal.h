@@ -45,6 +45,12 @@ struct TilePlan {
     int *d_carry_rows = nullptr;        // [num_carries] row each carry belongs to
     double *d_carry_val = nullptr;      // [num_tiles * L_max]
     int carry_L = 0;                    // capacity (columns) of d_carry_val
+    // Single-RHS plans: 16-bit column offsets.  A tile whose columns span < 65536 stores
+    // col - colbase[t] in cols16 (2 B per nonzero instead of 4 in the HBM stream); colbase[t]
+    // = -1 keeps the tile on the int32 columns.  Null when not built.
+    int *d_colbase = nullptr;           // [num_tiles]
+    unsigned short *d_cols16 = nullptr; // [nnz + kNnzPad]
+    int num_tiles16 = 0;                // tiles on the 16-bit stream
 };
 
 // Device-resident CG scalars (one set per right-hand side column).
@@ -118,6 +124,10 @@ hipError_t launch_tile_modes(const int *d_row_offsets, const int2 *d_bounds, con
 inline int l_index(int L) { return L == 1 ? 0 : L == 2 ? 1 : L == 4 ? 2 : L == 8 ? 3 : 4; }
 hipError_t launch_snap(const int *d_row_offsets, int m, int2 *d_bounds, unsigned char *d_split, int num_tiles,
                        int snap, hipStream_t s);
+// Per-tile 16-bit column offsets (TilePlan::d_colbase / d_cols16); whether plans get them.
+hipError_t launch_pack_cols16(const int *d_cols, const int2 *d_bounds, int num_tiles, int *d_colbase,
+                              unsigned short *d_cols16, hipStream_t s);
+bool spmv_cols16_enabled();
 // y = A x (L == 1) or Y = A X (row-major panels), tile kernel + optional carry fix-up.
 hipError_t launch_spmm(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
                        int *kernels_launched);

@@ -305,6 +305,43 @@ __global__ void k_snap(const int *__restrict__ row_offsets, int m, int2 *__restr
     split[t] = s;
 }
 
+// 16-bit column offsets, one workgroup per tile: the tile's column range (block min / max), and
+// when it spans < 65536 columns, cols16[k] = col[k] - colbase[t] for the tile's nonzeros.
+__global__ __launch_bounds__(kBlock) void k_pack_cols16(const int *__restrict__ cols, const int2 *__restrict__ bounds,
+                                                        int *__restrict__ colbase, unsigned short *__restrict__ cols16)
+{
+    __shared__ int s_min[kBlock / 64], s_max[kBlock / 64];
+    const int t = blockIdx.x, tid = threadIdx.x;
+    const int n0 = bounds[t].y, n1 = bounds[t + 1].y;
+    int lo = 0x7fffffff, hi = -1;
+    for (int k = n0 + tid; k < n1; k += kBlock) {
+        const int c = cols[k];
+        lo = min(lo, c);
+        hi = max(hi, c);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = min(lo, __shfl_xor(lo, off));
+        hi = max(hi, __shfl_xor(hi, off));
+    }
+    if ((tid & 63) == 0) {
+        s_min[tid >> 6] = lo;
+        s_max[tid >> 6] = hi;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) {
+        lo = min(lo, s_min[w]);
+        hi = max(hi, s_max[w]);
+    }
+    const int base = (n1 > n0 && hi - lo < 65536) ? lo : -1;
+    if (tid == 0)
+        colbase[t] = base;
+    if (base >= 0)
+        for (int k = n0 + tid; k < n1; k += kBlock)
+            cols16[k] = (unsigned short)(cols[k] - base);
+}
+
 // Per-tile choice of the in-tile reduction (one thread per tile, at plan time; gl = lanes per
 // nonzero: 1 for SpMV, L/2 column-pair lanes for SpMM).  The tile's row segments -- its complete rows plus the trailing partial row of a
 // split boundary -- are either summed by row groups of G = 2^lg lanes (mode lg + 1) or, when
@@ -379,6 +416,9 @@ struct TileArgs {
     double tol;
     double *hist;
     int hist_cap;
+    // single-RHS plans: per-tile 16-bit column offsets (TilePlan::d_colbase / d_cols16; null: off)
+    const int *colbase;
+    const unsigned short *cols16;
 };
 
 // Tile-kernel modes.
@@ -408,11 +448,17 @@ struct StageRegs {
     double pv[CG ? NJ : 1];
 };
 template <int NJ, bool CG, bool NT>
-__device__ __forceinline__ void stage_issue(const TileArgs &a, int n0, int nnzt, StageRegs<NJ, CG> &st)
+__device__ __forceinline__ void stage_issue(const TileArgs &a, int n0, int nnzt, int colbase, StageRegs<NJ, CG> &st)
 {
+    if (colbase >= 0) {  // block-uniform: the tile's 16-bit column offsets
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-        st.c[j] = ld_stream<NT>(a.cols + n0 + min((int)threadIdx.x + j * kBlock, nnzt - 1));
+        for (int j = 0; j < NJ; ++j)
+            st.c[j] = colbase + (int)ld_stream<NT>(a.cols16 + n0 + min((int)threadIdx.x + j * kBlock, nnzt - 1));
+    } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+            st.c[j] = ld_stream<NT>(a.cols + n0 + min((int)threadIdx.x + j * kBlock, nnzt - 1));
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
         st.v[j] = ld_stream<NT>(a.vals + n0 + min((int)threadIdx.x + j * kBlock, nnzt - 1));
@@ -442,7 +488,7 @@ template <int NJ, bool CG, bool NT>
 __device__ __forceinline__ void stage_products(const TileArgs &a, int n0, int nnzt, double beta, double *s_prod)
 {
     StageRegs<NJ, CG> st;
-    stage_issue<NJ, CG, NT>(a, n0, nnzt, st);
+    stage_issue<NJ, CG, NT>(a, n0, nnzt, -1, st);
     stage_store<NJ, CG>(st, nnzt, beta, s_prod);
 }
 
@@ -791,15 +837,16 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
         else if (CG)
             go = cg1_head(a, part_sum(pin, sm.red), beta);
     };
+    const int colbase = a.cols16 ? a.colbase[t] : -1;
     if (nnzt > 0 && nnzt <= TILE) {  // the common case: no snapped-in extra nonzeros
         StageRegs<IPT, CG> st;
-        stage_issue<IPT, CG, NT>(a, n0, nnzt, st);
+        stage_issue<IPT, CG, NT>(a, n0, nnzt, colbase, st);
         head();
         if (go)
             stage_store<IPT, CG>(st, nnzt, beta, sm.prod);
     } else if (nnzt > TILE) {
         StageRegs<MAXJ, CG> st;
-        stage_issue<MAXJ, CG, NT>(a, n0, nnzt, st);
+        stage_issue<MAXJ, CG, NT>(a, n0, nnzt, colbase, st);
         head();
         if (go)
             stage_store<MAXJ, CG>(st, nnzt, beta, sm.prod);
@@ -1667,6 +1714,7 @@ struct SpmvTuning {
     int bpc = 0;      // resident workgroups per CU for the persistent grid (0: occupancy query)
     int rg_cost = 48; // k_tile_modes budget for row-group tiles (0: merge walk everywhere)
     int spmm_rg_cost = -1;  // the same for the multi-RHS kernels (-1: scaled to the SpMM tile)
+    int cols16 = 1;   // single-RHS plans carry 16-bit column offsets where a tile's span allows
 };
 static const SpmvTuning &spmv_tuning()
 {
@@ -1692,6 +1740,8 @@ static const SpmvTuning &spmv_tuning()
             v.rg_cost = atoi(e);
         if (const char *e = getenv("MSPMV_SPMM_RG_COST"))
             v.spmm_rg_cost = atoi(e);
+        if (const char *e = getenv("MSPMV_SPMV_C16"))
+            v.cols16 = atoi(e) != 0;
         return v;
     }();
     return t;
@@ -1741,6 +1791,15 @@ hipError_t launch_merge_coords(const int *d_row_offsets, int m, int nnz, long lo
     return hipGetLastError();
 }
 
+hipError_t launch_pack_cols16(const int *d_cols, const int2 *d_bounds, int num_tiles, int *d_colbase,
+                              unsigned short *d_cols16, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_pack_cols16, dim3(num_tiles), dim3(kBlock), 0, s, d_cols, d_bounds, d_colbase, d_cols16);
+    return hipGetLastError();
+}
+
+bool spmv_cols16_enabled() { return spmv_tuning().cols16 != 0; }
+
 hipError_t launch_snap(const int *d_row_offsets, int m, int2 *d_bounds, unsigned char *d_split, int num_tiles,
                        int snap, hipStream_t s)
 {
@@ -1777,6 +1836,10 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
     a.rmode = plan.d_modes[l_index(L)];
     a.carry_val = plan.d_carry_val;
     a.num_tiles = plan.num_tiles;
+    if (L == 1) {
+        a.colbase = plan.d_colbase;
+        a.cols16 = plan.d_cols16;
+    }
     return a;
 }
 
