@@ -58,6 +58,8 @@ typedef struct mspmv_csr_d {
 } mspmv_csr_d;
 
 typedef struct mspmv_handle_s *mspmv_handle;
+/* An IC(0) factor resident on a device (mspmv_ic0_create). */
+typedef struct mspmv_ic0_s *mspmv_ic0;
 
 /* Merge-path coordinate (CUB CoordinateT / the reference's int2, types.hpp:3-7). */
 typedef struct mspmv_coord {
@@ -152,6 +154,29 @@ MSPMV_API mspmv_status mspmv_dpcg_spai_multi(mspmv_handle a, mspmv_handle m, con
 MSPMV_API mspmv_status mspmv_dpcg_spai_multi_dev(mspmv_handle a, mspmv_handle m, const double *d_B, double *d_X,
                                                  int L, int max_iters, double tolerance, mspmv_spmm_kernel kernel,
                                                  int *iters, double *max_err_hist, int hist_cap);
+
+/* ---- IC(0)-preconditioned block CG --------------------------------------------------- */
+/* IncompleteCholesky (work_2025/cg/incomplete_cholesky_decomp.hpp:84-201) on the host, as in the
+ * reference: L has A's lower-triangle pattern (diagonal included, A's CSR order); on a
+ * non-positive pivot the factorization restarts with the diagonal shifted by 1e-3, x10 per
+ * attempt, 20 attempts (MSPMV_ERR_BREAKDOWN after that).  mspmv_ic0_nnz gives L's nonzero count;
+ * l_row_offsets[n+1], l_cols / l_vals[nnz_l] receive L; *shift (nullable) the shift used. */
+MSPMV_API mspmv_status mspmv_ic0_nnz(const mspmv_csr_d *a, int *nnz_l);
+MSPMV_API mspmv_status mspmv_ic0_factor(const mspmv_csr_d *a, int *l_row_offsets, int *l_cols, double *l_vals,
+                                        double *shift);
+/* Upload L and its transpose (TransposeCsr, :11-78) for the GPU triangular solves. */
+MSPMV_API mspmv_status mspmv_ic0_create(const mspmv_csr_d *l, int device, mspmv_ic0 *out);
+MSPMV_API mspmv_status mspmv_ic0_destroy(mspmv_ic0 m);
+/* PCGSolveMultiple (work_2025/main/incomplete_cholesky.hpp:33-199) on the GPU: Z = L^-T L^-1 R by
+ * two sync-free triangular solves per application (one wave per row, per-row ready flags),
+ * merge-path SpMM for A P, the reference's masks and max-residual history.  A stalled solve
+ * (a dependency never ready) is reported as MSPMV_ERR_BREAKDOWN, never a hang. */
+MSPMV_API mspmv_status mspmv_dpcg_ic0_multi(mspmv_handle a, mspmv_ic0 m, const double *B, double *X, int L,
+                                            int max_iters, double tolerance, mspmv_spmm_kernel kernel, int *iters,
+                                            double *max_err_hist, int hist_cap);
+MSPMV_API mspmv_status mspmv_dpcg_ic0_multi_dev(mspmv_handle a, mspmv_ic0 m, const double *d_B, double *d_X, int L,
+                                                int max_iters, double tolerance, mspmv_spmm_kernel kernel,
+                                                int *iters, double *max_err_hist, int hist_cap);
 
 /* ---- measurement helpers (HIP events on the handle's stream) ------------------------ */
 /* Enqueue `reps` back-to-back SpMV (L == 1) or SpMM launches on device buffers and return

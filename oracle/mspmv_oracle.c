@@ -590,6 +590,226 @@ ORC_EXPORT int orc_pcg_spai_multi(int num_rows, int num_nonzeros, const int *row
     return iter;
 }
 
+/* ------------------------------------------------------------------------- */
+/* IC(0): work_2025/cg/incomplete_cholesky_decomp.hpp (the file includes      */
+/* <mkl.h>, so it is restated, not built) and PCGSolveMultiple,               */
+/* work_2025/main/incomplete_cholesky.hpp:33-199.                             */
+/* ------------------------------------------------------------------------- */
+/* IncompleteCholesky :84-201.  l_* receive L (A's lower triangle, A's order); returns 1 on
+ * success (after at most 20 shifted attempts), 0 on failure; *shift_out the shift used. */
+ORC_EXPORT int orc_ic0_factor(int n, const int *ro, const int *ci, const double *va, int *l_ro, int *l_ci,
+                              double *l_va, double *shift_out)
+{
+    int nz = 0;
+    l_ro[0] = 0;
+    for (int i = 0; i < n; ++i) { /* :91-148 */
+        for (int k = ro[i]; k < ro[i + 1]; ++k)
+            if (ci[k] <= i) {
+                l_ci[nz] = ci[k];
+                l_va[nz] = va[k];
+                ++nz;
+            }
+        l_ro[i + 1] = nz;
+    }
+    double *backup = (double *)malloc(sizeof(double) * (nz > 0 ? nz : 1));
+    memcpy(backup, l_va, sizeof(double) * nz);
+    double shift = 0.0;
+    for (int retry = 0; retry < 20; ++retry) { /* :150-225 */
+        int failed = 0;
+        if (retry > 0)
+            for (int idx = 0; idx < n; ++idx)
+                for (int off = l_ro[idx]; off < l_ro[idx + 1]; ++off) {
+                    l_va[off] = backup[off];
+                    if (l_ci[off] == idx)
+                        l_va[off] += shift;
+                }
+        for (int i = 0; i < n && !failed; ++i) {
+            for (int ko = l_ro[i]; ko < l_ro[i + 1]; ++ko) {
+                int k = l_ci[ko];
+                double sum = 0.0;
+                int jl = l_ro[i], jk = l_ro[k];
+                while (jl < ko && jk < l_ro[k + 1]) {
+                    if (l_ci[jl] == l_ci[jk]) {
+                        sum += l_va[jl] * l_va[jk];
+                        jl++;
+                        jk++;
+                    } else if (l_ci[jl] < l_ci[jk]) {
+                        jl++;
+                    } else {
+                        jk++;
+                    }
+                }
+                l_va[ko] -= sum;
+                if (k == i) {
+                    if (l_va[ko] <= 0) {
+                        failed = 1;
+                        break;
+                    }
+                    l_va[ko] = sqrt(l_va[ko]);
+                } else {
+                    l_va[ko] /= l_va[l_ro[k + 1] - 1];
+                }
+            }
+        }
+        if (!failed) {
+            free(backup);
+            if (shift_out)
+                *shift_out = shift;
+            return 1;
+        }
+        shift = shift == 0.0 ? 1e-3 : shift * 10.0;
+    }
+    free(backup);
+    return 0;
+}
+
+/* TransposeCsr :11-78 (counting sort by column; rows in order within each output row). */
+static void transpose_csr(int n, int nnz, const int *ro, const int *ci, const double *va, int *t_ro, int *t_ci,
+                          double *t_va)
+{
+    int *cnt = (int *)calloc((size_t)n + 1, sizeof(int));
+    for (int k = 0; k < nnz; ++k)
+        cnt[ci[k] + 1]++;
+    for (int c = 0; c < n; ++c)
+        cnt[c + 1] += cnt[c];
+    memcpy(t_ro, cnt, sizeof(int) * ((size_t)n + 1));
+    for (int r = 0; r < n; ++r)
+        for (int k = ro[r]; k < ro[r + 1]; ++k) {
+            int d = cnt[ci[k]]++;
+            t_ci[d] = r;
+            t_va[d] = va[k];
+        }
+    free(cnt);
+}
+
+/* ForwardSolveMultiple :231-271 and BackwardSolveMultiple :277-346 (sequential, CSR order). */
+static void forward_solve_multiple(int n, const int *ro, const int *ci, const double *va, const double *b, double *x,
+                                   int L, double *sum)
+{
+    for (int i = 0; i < n; ++i) {
+        for (int v = 0; v < L; ++v)
+            sum[v] = 0.0;
+        int diag_offset = 0;
+        for (int k = ro[i]; k < ro[i + 1]; ++k) {
+            int j = ci[k];
+            if (i == j) {
+                diag_offset = k;
+                continue;
+            }
+            for (int v = 0; v < L; ++v)
+                sum[v] += va[k] * x[(size_t)j * L + v];
+        }
+        double d = va[diag_offset];
+        for (int v = 0; v < L; ++v)
+            x[(size_t)i * L + v] = (b[(size_t)i * L + v] - sum[v]) / d;
+    }
+}
+
+static void backward_solve_multiple(int n, const int *ro, const int *ci, const double *va, const double *b, double *x,
+                                    int L, double *sum)
+{
+    for (int i = n - 1; i >= 0; --i) {
+        for (int v = 0; v < L; ++v)
+            sum[v] = 0.0;
+        double d = 0.0;
+        for (int k = ro[i]; k < ro[i + 1]; ++k) {
+            int j = ci[k];
+            if (i == j) {
+                d = va[k];
+                continue;
+            }
+            for (int v = 0; v < L; ++v)
+                sum[v] += va[k] * x[(size_t)j * L + v];
+        }
+        for (int v = 0; v < L; ++v)
+            x[(size_t)i * L + v] = d == 0.0 ? 0.0 : (b[(size_t)i * L + v] - sum[v]) / d;
+    }
+}
+
+/* PCGSolveMultiple :33-199 with the factor L (l_*); L^T is formed here as the driver does. */
+ORC_EXPORT int orc_pcg_ic0_multi(int num_rows, int num_nonzeros, const int *row_offsets, const int *cols,
+                                 const double *vals, int l_nnz, const int *l_ro, const int *l_ci, const double *l_va,
+                                 const double *B, double *X, int L, int max_iters, double tolerance, int kernel_type,
+                                 int num_threads, double *max_err_hist, int hist_cap)
+{
+    int n = num_rows;
+    size_t nl = (size_t)n * L;
+    int *t_ro = (int *)malloc(sizeof(int) * ((size_t)n + 1));
+    int *t_ci = (int *)malloc(sizeof(int) * (l_nnz > 0 ? l_nnz : 1));
+    double *t_va = (double *)malloc(sizeof(double) * (l_nnz > 0 ? l_nnz : 1));
+    transpose_csr(n, l_nnz, l_ro, l_ci, l_va, t_ro, t_ci, t_va);
+    double *R = (double *)malloc(sizeof(double) * nl);
+    double *P = (double *)malloc(sizeof(double) * nl);
+    double *AP = (double *)malloc(sizeof(double) * nl);
+    double *Z = (double *)malloc(sizeof(double) * nl);
+    double *Y = (double *)malloc(sizeof(double) * nl);
+    double *alpha = (double *)malloc(sizeof(double) * L);
+    double *beta = (double *)malloc(sizeof(double) * L);
+    double *rho_old = (double *)malloc(sizeof(double) * L);
+    double *rho_new = (double *)malloc(sizeof(double) * L);
+    double *pAp = (double *)malloc(sizeof(double) * L);
+    double *rn = (double *)malloc(sizeof(double) * L);
+    double *b_norms = (double *)malloc(sizeof(double) * L);
+    double *sum = (double *)malloc(sizeof(double) * L);
+    char *converged = (char *)malloc(L);
+
+    for (size_t i = 0; i < nl; ++i) /* :64-70 */
+        X[i] = 0.0;
+    memcpy(R, B, sizeof(double) * nl);
+    dot_multiple(n, L, B, B, b_norms); /* :72-81 */
+    for (int i = 0; i < L; ++i) {
+        b_norms[i] = sqrt(b_norms[i]);
+        if (b_norms[i] == 0.0)
+            b_norms[i] = 1.0;
+        converged[i] = 0;
+    }
+    forward_solve_multiple(n, l_ro, l_ci, l_va, R, Y, L, sum); /* :83-86 */
+    backward_solve_multiple(n, t_ro, t_ci, t_va, Y, Z, L, sum);
+    memcpy(P, Z, sizeof(double) * nl);  /* :88-89 */
+    dot_multiple(n, L, R, Z, rho_old); /* :91 */
+
+    int iter;
+    for (iter = 0; iter < max_iters; ++iter) {
+        memset(AP, 0, sizeof(double) * nl); /* :101-114 */
+        spmm_dispatch(kernel_type, num_threads, n, num_nonzeros, row_offsets, cols, vals, P, AP, L);
+        dot_multiple(n, L, P, AP, pAp); /* :116 */
+        for (int i = 0; i < L; ++i)     /* :118-125 */
+            alpha[i] = converged[i] ? 0.0 : rho_old[i] / pAp[i];
+        axpy_multiple(n, L, alpha, P, X); /* :127 */
+        for (int i = 0; i < L; ++i)
+            alpha[i] = -alpha[i];
+        axpy_multiple(n, L, alpha, AP, R); /* :129-132 */
+        dot_multiple(n, L, R, R, rn);      /* :134-135 */
+        int num_converged = 0;             /* :137-150 */
+        double max_relative_error = 0.0;
+        for (int i = 0; i < L; ++i) {
+            double rel_error = sqrt(rn[i]) / b_norms[i];
+            max_relative_error = max_relative_error > rel_error ? max_relative_error : rel_error;
+            if (!converged[i] && rel_error < tolerance)
+                converged[i] = 1;
+            if (converged[i])
+                num_converged++;
+        }
+        if (max_err_hist && iter < hist_cap) /* :153-157 */
+            max_err_hist[iter] = max_relative_error;
+        if (num_converged == L) { /* :159-163 */
+            iter++;
+            break;
+        }
+        forward_solve_multiple(n, l_ro, l_ci, l_va, R, Y, L, sum); /* :165-166 */
+        backward_solve_multiple(n, t_ro, t_ci, t_va, Y, Z, L, sum);
+        dot_multiple(n, L, R, Z, rho_new); /* :168 */
+        for (int i = 0; i < L; ++i)        /* :170-177 */
+            beta[i] = converged[i] ? 0.0 : rho_new[i] / rho_old[i];
+        update_p_multiple(n, L, Z, beta, P); /* :179 */
+        memcpy(rho_old, rho_new, sizeof(double) * L);
+    }
+    free(t_ro); free(t_ci); free(t_va); free(R); free(P); free(AP); free(Z); free(Y);
+    free(alpha); free(beta); free(rho_old); free(rho_new); free(pAp); free(rn); free(b_norms); free(sum);
+    free(converged);
+    return iter;
+}
+
 /* calculate_threshold: cpu_singlecg.cpp:22-34 (dup cpu_multicg.cpp:49-61). */
 ORC_EXPORT double orc_calculate_threshold(const double *b, int num_rows, double tolerance)
 {

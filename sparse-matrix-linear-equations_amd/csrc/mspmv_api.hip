@@ -599,14 +599,28 @@ static mspmv_status ensure_cg_workspace(mspmv_handle_s *h, int L, int nblk, int 
     return MSPMV_OK;
 }
 
-// CG (hm == nullptr) or SPAI-preconditioned CG with the preconditioner's handle hm.
+// CG; SPAI-preconditioned CG with the preconditioner's handle hm; or IC(0)-preconditioned CG
+// with the factor ic.
 static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d_x, int L, int max_iters,
-                                 double tol, int *iters, double *hist, int hist_cap, mspmv_handle_s *hm = nullptr)
+                                 double tol, int *iters, double *hist, int hist_cap, mspmv_handle_s *hm = nullptr,
+                                 mspmv_ic0_s *ic = nullptr)
 {
     if (h->m != h->n)
         return invalid("CG needs a square matrix");
     if (hm && (hm->m != h->m || hm->n != h->n || hm->device != h->device))
         return invalid("the preconditioner must match the matrix's shape and device");
+    if (ic && (ic->n != h->m || ic->device != h->device))
+        return invalid("the IC(0) factor must match the matrix's shape and device");
+    if (ic && (size_t)h->m * L > ic->y_cap) {
+        if (ic->d_y)
+            (void)hipFree(ic->d_y);
+        ic->d_y = nullptr;
+        ic->y_cap = 0;
+        HIP_TRY(hipSetDevice(h->device));
+        if (hipMalloc(&ic->d_y, sizeof(double) * (size_t)h->m * L) != hipSuccess)
+            return (set_error("IC(0) workspace allocation failed"), MSPMV_ERR_OOM);
+        ic->y_cap = (size_t)h->m * L;
+    }
     if (!supported_L(L))
         return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
     if (max_iters < 0)
@@ -625,7 +639,7 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
         ST_TRY(get_plan(hm, L, &mplan));
         HIP_TRY(hipStreamSynchronize(hm->stream));  // hm's SpMMs are enqueued on h's stream
     }
-    const bool pipelined = !hm && !cg_split_iteration(L);  // single RHS: consumer-side reductions
+    const bool pipelined = !hm && !ic && !cg_split_iteration(L);  // single RHS: consumer-side reductions
     const int nblk = pipelined ? cg1_blocks(h->m) : cg_update_blocks((long long)h->m * L);
     const int cap = hist ? std::max(hist_cap, 0) : 0;
     ST_TRY(ensure_cg_workspace(h, L, nblk, std::max(plan->num_tiles, mplan ? mplan->num_tiles : 0), cap));
@@ -635,13 +649,18 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
     HIP_TRY(hipMemsetAsync(h->d_ctrl, 0, sizeof(CgControl), h->stream));
     if (hm)
         HIP_TRY(launch_pcg_init(h, hm, *mplan, d_b, d_x, L, tol, nblk));
+    else if (ic)
+        HIP_TRY(launch_pcg_ic0_init(h, ic, d_b, d_x, L, tol, nblk));
     else if (pipelined)
         HIP_TRY(launch_cg1_init(h, d_b, d_x, nblk));
     else
         HIP_TRY(launch_cg_init(h, d_b, d_x, L, tol, nblk));
     auto iterate = [&](int i) -> hipError_t {
-        return hm ? launch_pcg_iteration(h, hm, *plan, *mplan, d_x, L, nblk, tol)
-                  : launch_cg_iteration(h, *plan, d_x, L, i & 1, nblk, tol);
+        if (hm)
+            return launch_pcg_iteration(h, hm, *plan, *mplan, d_x, L, nblk, tol);
+        if (ic)
+            return launch_pcg_ic0_iteration(h, ic, *plan, d_x, L, nblk, tol);
+        return launch_cg_iteration(h, *plan, d_x, L, i & 1, nblk, tol);
     };
 
     constexpr int K = 32;  // iterations per graph replay (even: p buffers alternate)
@@ -658,7 +677,8 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
             h->d_conv, h->d_red, h->d_ctrl, h->d_hist, h->stream, plan, tk,
             reinterpret_cast<const void *>((intptr_t)L), reinterpret_cast<const void *>((intptr_t)nblk),
             reinterpret_cast<const void *>((intptr_t)use_cap), hm, mplan,
-            hm ? (const void *)hm->d_vals : nullptr};
+            hm ? (const void *)hm->d_vals : nullptr, ic, ic ? (const void *)ic->d_y : nullptr,
+            ic ? (const void *)ic->d_lva : nullptr};
         if (!h->cg_exec || h->cg_graph_key != key) {
             if (h->cg_exec)
                 (void)hipGraphExecDestroy(h->cg_exec);
@@ -763,6 +783,10 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
         if (nh > 0)
             HIP_TRY(hipMemcpy(hist, h->d_hist, sizeof(double) * nh, hipMemcpyDeviceToHost));
     }
+    if (fin.breakdown == 2) {
+        set_error("IC(0) apply: a triangular-solve dependency never became ready (solve stalled)");
+        return MSPMV_ERR_BREAKDOWN;
+    }
     if (fin.breakdown) {
         set_error("CG breakdown: p.Ap gave a non-finite alpha at iteration " + std::to_string(it));
         return MSPMV_ERR_BREAKDOWN;
@@ -771,7 +795,8 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
 }
 
 static mspmv_status cg_solve_host(mspmv_handle h, const double *B, double *X, int L, int max_iters, double tol,
-                                  int *iters, double *hist, int hist_cap, mspmv_handle hm = nullptr)
+                                  int *iters, double *hist, int hist_cap, mspmv_handle hm = nullptr,
+                                  mspmv_ic0 ic = nullptr)
 {
     ST_TRY(check_handle(h));
     if (h->m == 0) {
@@ -790,7 +815,7 @@ static mspmv_status cg_solve_host(mspmv_handle h, const double *B, double *X, in
         st = MSPMV_ERR_HIP;
     }
     if (st == MSPMV_OK)
-        st = cg_solve_dev(h, dB, dX, L, max_iters, tol, iters, hist, hist_cap, hm);
+        st = cg_solve_dev(h, dB, dX, L, max_iters, tol, iters, hist, hist_cap, hm, ic);
     if ((st == MSPMV_OK || st == MSPMV_ERR_BREAKDOWN) && hipMemcpy(X, dX, bytes, hipMemcpyDeviceToHost) != hipSuccess) {
         set_error("X download failed");
         st = MSPMV_ERR_HIP;
@@ -850,6 +875,112 @@ mspmv_status mspmv_dpcg_spai_multi(mspmv_handle a, mspmv_handle m, const double 
         return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
     ST_TRY(check_handle(m));
     return cg_solve_host(a, B, X, L, max_iters, tolerance, iters, max_err_hist, hist_cap, m);
+}
+
+// ---- IC(0) factor on the device --------------------------------------------------------------
+mspmv_status mspmv_ic0_create(const mspmv_csr_d *l, int device, mspmv_ic0 *out)
+{
+    if (!out)
+        return invalid("null output");
+    *out = nullptr;
+    ST_TRY(validate_host_csr(l));
+    if (l->num_rows != l->num_cols)
+        return invalid("IC(0) factor must be square");
+    const int n = l->num_rows, nnz = l->num_nonzeros;
+    for (int r = 0; r < n; ++r)
+        if (l->row_offsets[r + 1] < l->row_offsets[r])
+            return invalid("row_offsets not monotone");
+    if (l->row_offsets[0] != 0 || l->row_offsets[n] != nnz)
+        return invalid("row_offsets inconsistent with num_nonzeros");
+    for (int k = 0; k < nnz; ++k)
+        if (l->column_indices[k] < 0 || l->column_indices[k] >= n)
+            return invalid("column index out of range");
+    // TransposeCsr (incomplete_cholesky_decomp.hpp:11-78): counting sort by column, rows in order
+    std::vector<int> uro((size_t)n + 1, 0), uci((size_t)std::max(nnz, 1));
+    std::vector<double> uva((size_t)std::max(nnz, 1));
+    for (int k = 0; k < nnz; ++k)
+        ++uro[(size_t)l->column_indices[k] + 1];
+    for (int c = 0; c < n; ++c)
+        uro[(size_t)c + 1] += uro[c];
+    {
+        std::vector<int> pos(uro.begin(), uro.end() - 1);
+        for (int r = 0; r < n; ++r)
+            for (int k = l->row_offsets[r]; k < l->row_offsets[r + 1]; ++k) {
+                const int d = pos[l->column_indices[k]]++;
+                uci[d] = r;
+                uva[d] = l->values[k];
+            }
+    }
+    HIP_TRY(hipSetDevice(device));
+    mspmv_ic0_s *m = new mspmv_ic0_s;
+    m->device = device;
+    m->n = n;
+    m->nnz = nnz;
+    mspmv_status st = MSPMV_OK;
+    auto up = [&](auto **d, const auto *src, size_t cnt) {
+        if (st != MSPMV_OK)
+            return;
+        st = dev_alloc(d, std::max<size_t>(cnt, 1));
+        if (st == MSPMV_OK && cnt && hipMemcpy(*d, src, sizeof(**d) * cnt, hipMemcpyHostToDevice) != hipSuccess) {
+            set_error("IC(0) upload failed");
+            st = MSPMV_ERR_HIP;
+        }
+    };
+    up(&m->d_lro, l->row_offsets, (size_t)n + 1);
+    up(&m->d_lci, l->column_indices, (size_t)nnz);
+    up(&m->d_lva, l->values, (size_t)nnz);
+    up(&m->d_uro, uro.data(), (size_t)n + 1);
+    up(&m->d_uci, uci.data(), (size_t)nnz);
+    up(&m->d_uva, uva.data(), (size_t)nnz);
+    if (st == MSPMV_OK)
+        st = dev_alloc(&m->d_ready, (size_t)std::max(n, 1));
+    if (st != MSPMV_OK) {
+        mspmv_ic0_destroy(m);
+        return st;
+    }
+    *out = m;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_ic0_destroy(mspmv_ic0 m)
+{
+    if (!m)
+        return MSPMV_OK;
+    (void)hipSetDevice(m->device);
+    dev_free(m->d_lro);
+    dev_free(m->d_lci);
+    dev_free(m->d_lva);
+    dev_free(m->d_uro);
+    dev_free(m->d_uci);
+    dev_free(m->d_uva);
+    dev_free(m->d_ready);
+    if (m->d_y)
+        (void)hipFree(m->d_y);
+    delete m;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_dpcg_ic0_multi_dev(mspmv_handle a, mspmv_ic0 m, const double *d_B, double *d_X, int L,
+                                      int max_iters, double tolerance, mspmv_spmm_kernel kernel, int *iters,
+                                      double *max_err_hist, int hist_cap)
+{
+    (void)kernel;
+    ST_TRY(check_handle(a));
+    if (!m)
+        return invalid("null IC(0) factor");
+    return cg_solve_dev(a, d_B, d_X, L, max_iters, tolerance, iters, max_err_hist, hist_cap, nullptr, m);
+}
+
+mspmv_status mspmv_dpcg_ic0_multi(mspmv_handle a, mspmv_ic0 m, const double *B, double *X, int L, int max_iters,
+                                  double tolerance, mspmv_spmm_kernel kernel, int *iters, double *max_err_hist,
+                                  int hist_cap)
+{
+    (void)kernel;
+    if (!supported_L(L))
+        return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
+    if (!m)
+        return invalid("null IC(0) factor");
+    return cg_solve_host(a, B, X, L, max_iters, tolerance, iters, max_err_hist, hist_cap, nullptr, m);
 }
 
 // ---- measurement ---------------------------------------------------------------------------

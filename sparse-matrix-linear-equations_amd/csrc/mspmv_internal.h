@@ -113,6 +113,20 @@ struct mspmv_handle_s {
     size_t flush_cap = 0;
 };
 
+// IC(0) factor on the device (mspmv_ic0_create): L and its transpose for the two sync-free
+// triangular solves of the preconditioner apply, their ready flags and the intermediate Y.
+struct mspmv_ic0_s {
+    int device = 0;
+    int n = 0, nnz = 0;
+    int *d_lro = nullptr, *d_lci = nullptr;  // L (lower, diagonal last in each row)
+    double *d_lva = nullptr;
+    int *d_uro = nullptr, *d_uci = nullptr;  // L^T (upper, diagonal first)
+    double *d_uva = nullptr;
+    int *d_ready = nullptr;                  // [n] per-row ready flags of the running solve
+    double *d_y = nullptr;                   // [n * L] forward-solve result
+    size_t y_cap = 0;
+};
+
 namespace mspmv {
 
 // ---- launchers (mspmv_kernels.hip) --------------------------------------------------
@@ -202,6 +216,12 @@ hipError_t launch_pcg_init(mspmv_handle_s *h, mspmv_handle_s *hm, const TilePlan
                            double *d_x, int L, double tol, int nblk);
 hipError_t launch_pcg_iteration(mspmv_handle_s *h, mspmv_handle_s *hm, const TilePlan &plan, const TilePlan &mplan,
                                 double *d_x, int L, int nblk, double tol);
+// IC(0)-preconditioned block CG (PCGSolveMultiple, work_2025/main/incomplete_cholesky.hpp:33-199):
+// Z = L^-T L^-1 R by two sync-free triangular solves (k_trsv); ic->d_y must hold m * L.
+hipError_t launch_pcg_ic0_init(mspmv_handle_s *h, mspmv_ic0_s *ic, const double *d_b, double *d_x, int L, double tol,
+                               int nblk);
+hipError_t launch_pcg_ic0_iteration(mspmv_handle_s *h, mspmv_ic0_s *ic, const TilePlan &plan, double *d_x, int L,
+                                    int nblk, double tol);
 // Partials capacity (doubles) and group-ticket count for `slots` partial slots of L columns.
 // (every level of the tree: slots, slots/32, ... -> <= slots * 32/31 + one per level)
 inline size_t partials_capacity(size_t slots, int L) { return (slots + slots / (kSlotGroup - 1) + 8) * L; }

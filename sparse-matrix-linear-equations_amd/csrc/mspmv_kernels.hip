@@ -1636,6 +1636,111 @@ __global__ __launch_bounds__(kBlock) void k_dist_pupdate(CgVecArgs a, double *p)
     }
 }
 
+// ---- IC(0) preconditioner apply: sync-free sparse triangular solves ---------------------------
+// Spin on a ready flag written by another wave (agent-scope relaxed loads, s_sleep between
+// polls).  Bounded: after ~2^20 polls the caller reports a stall instead of hanging the GPU.
+__device__ __forceinline__ bool wait_flag(const int *f)
+{
+    for (int it = 0; it < (1 << 20); ++it) {
+        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
+            return true;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return false;
+}
+
+// x = T^-1 b for a triangular CSR T, one wave per row: ForwardSolveMultiple (FWD, T = L lower,
+// rows ascending) and BackwardSolveMultiple (T = L^T upper, rows descending),
+// incomplete_cholesky_decomp.hpp:231-348.  Lane (q, v) takes nonzeros q, q + 64/L, ... of the
+// row for right-hand side v; a dependency j waits on ready[j], then x[j] is read (sc1 loads); a
+// fixed xor butterfly folds the row's partial sums; x[i] is stored write-through (sc1), drained,
+// and ready[i] raised.  Waves are dispatched in row order and wait only on earlier rows, so
+// every awaited row belongs to a wave already resident or finished: no deadlock.  The partial
+// sums are folded in a tree, not in CSR order (the reference's sequential sum): results agree to
+// rounding.  BackwardSolveMultiple's zero-diagonal rule (x = 0) is kept; a forward row takes
+// the diagonal as stored.
+template <int L, bool FWD>
+__global__ __launch_bounds__(kBlock) void k_trsv(const int *__restrict__ ro, const int *__restrict__ ci,
+                                                 const double *__restrict__ va, int n, const double *b, double *x,
+                                                 int *ready, CgControl *ctrl)
+{
+    constexpr int NZ = 64 / L;
+    const int w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (w >= n || ctrl->done)  // done is set only by earlier launches: uniform here
+        return;
+    const int i = FWD ? w : n - 1 - w;
+    const int lane = threadIdx.x & 63;
+    const int v = lane % L, q = lane / L;
+    const int k1 = ro[i + 1];
+    double sum = 0.0, diag = 0.0;
+    bool ok = true;
+    for (int k0 = ro[i]; k0 < k1; k0 += NZ) {
+        const int k = k0 + q;
+        if (k < k1) {
+            const int j = ci[k];
+            const double a = va[k];
+            if (j == i) {
+                diag = a;
+            } else {
+                ok = wait_flag(&ready[j]) && ok;
+                sum += a * load_sc1(&x[(size_t)j * L + v]);
+            }
+        }
+    }
+#pragma unroll
+    for (int off = L; off < 64; off <<= 1) {
+        sum += __shfl_xor(sum, off);
+        diag += __shfl_xor(diag, off);
+    }
+    if (q == 0) {
+        const double bi = b[(size_t)i * L + v];
+        const double xi = (!FWD && diag == 0.0) ? 0.0 : (bi - sum) / diag;
+        store_sc1(&x[(size_t)i * L + v], xi);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+        __hip_atomic_store(&ready[i], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!ok)
+            ctrl->breakdown = 2;  // a dependency never became ready (reported, never hung)
+    }
+}
+
+// R.Z per column and the PCG scalars after it (PCGSolveMultiple): mode 0 (init, :96-104)
+// rs_old = R.Z; mode 1 (:171-185) beta = converged ? 0 : R.Z / rs_old, rs_old = R.Z.
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_pcg_dot(CgVecArgs a, int mode)
+{
+    constexpr int GL = L > 1 ? L / 2 : 1;
+    __shared__ double2 s_red2[kBlock / 64][GL];
+    __shared__ double s_colred[kBlock];
+    __shared__ double s_out[L];
+    __shared__ int s_last;
+    const int tid = threadIdx.x;
+    if (a.ctrl->done)
+        return;
+    const long long npairs = a.n_elems / 2;
+    const long long stride = (long long)gridDim.x * kBlock;
+    double2 acc = make_double2(0.0, 0.0);
+    for (long long i = (long long)blockIdx.x * kBlock + tid; i < npairs; i += stride) {
+        const double2 r = reinterpret_cast<const double2 *>(a.r)[i];
+        const double2 z = reinterpret_cast<const double2 *>(a.p)[i];
+        acc.x += r.x * z.x;
+        acc.y += r.y * z.y;
+    }
+    if ((a.n_elems & 1) && blockIdx.x == 0 && tid == 0)
+        acc.x += a.r[a.n_elems - 1] * a.p[a.n_elems - 1];
+    colpair_block_reduce<L>(acc, s_red2, a.partials + (size_t)blockIdx.x * L);
+    if (!reduce_slots<L>(a.partials, a.gtickets, blockIdx.x, gridDim.x, s_colred, s_out, &s_last))
+        return;
+    if (tid < L) {
+        CgScalars &s = a.scal[tid];
+        const double d = s_out[tid];
+        if (mode == 1)
+            s.beta = a.conv[tid] ? 0.0 : d / s.rs_old;
+        s.rs_old = d;
+    }
+}
+
 // Pack the owned entries other ranks need: send[e] = p[idx[e / L] * L + e % L].
 __global__ void k_dist_pack(const double *__restrict__ p, const int *__restrict__ idx, long long n_elems, int L,
                             double *__restrict__ send, const CgControl *ctrl)
@@ -2443,4 +2548,98 @@ hipError_t launch_pcg_iteration(mspmv_handle_s *h, mspmv_handle_s *hm, const Til
     va.r = h->d_p1;  // P = Z + beta P
     return launch_dist_vec(2, va, L, nblk, h->d_p0, h->stream);
 }
+// ---- IC(0)-preconditioned block CG (PCGSolveMultiple) -------------------------------------------
+template <int L>
+static void trsv_L(const mspmv_ic0_s *ic, bool fwd, const double *b, double *x, CgControl *ctrl, hipStream_t s)
+{
+    const dim3 grid((ic->n + kBlock / 64 - 1) / (kBlock / 64)), block(kBlock);
+    if (fwd)
+        hipLaunchKernelGGL((k_trsv<L, true>), grid, block, 0, s, ic->d_lro, ic->d_lci, ic->d_lva, ic->n, b, x,
+                           ic->d_ready, ctrl);
+    else
+        hipLaunchKernelGGL((k_trsv<L, false>), grid, block, 0, s, ic->d_uro, ic->d_uci, ic->d_uva, ic->n, b, x,
+                           ic->d_ready, ctrl);
+}
+
+// Z = L^-T (L^-1 R): ForwardSolveMultiple into ic->d_y, then BackwardSolveMultiple
+// (incomplete_cholesky.hpp:89-92, :166-167); the ready flags are cleared before each solve.
+static hipError_t ic0_apply(mspmv_handle_s *h, mspmv_ic0_s *ic, int L, const double *r, double *z)
+{
+    if (ic->n == 0)
+        return hipSuccess;
+    for (int pass = 0; pass < 2; ++pass) {
+        hipError_t e = hipMemsetAsync(ic->d_ready, 0, sizeof(int) * (size_t)ic->n, h->stream);
+        if (e != hipSuccess)
+            return e;
+        const bool fwd = pass == 0;
+        const double *in = fwd ? r : ic->d_y;
+        double *out = fwd ? ic->d_y : z;
+        switch (L) {
+        case 1: trsv_L<1>(ic, fwd, in, out, h->d_ctrl, h->stream); break;
+        case 2: trsv_L<2>(ic, fwd, in, out, h->d_ctrl, h->stream); break;
+        case 4: trsv_L<4>(ic, fwd, in, out, h->d_ctrl, h->stream); break;
+        case 8: trsv_L<8>(ic, fwd, in, out, h->d_ctrl, h->stream); break;
+        case 16: trsv_L<16>(ic, fwd, in, out, h->d_ctrl, h->stream); break;
+        default: return hipErrorInvalidValue;
+        }
+        if ((e = hipGetLastError()) != hipSuccess)
+            return e;
+    }
+    return hipSuccess;
+}
+
+static hipError_t pcg_dot(const CgVecArgs &va, int L, int nblk, int mode, hipStream_t s)
+{
+    switch (L) {
+    case 1: hipLaunchKernelGGL((k_pcg_dot<1>), dim3(nblk), dim3(kBlock), 0, s, va, mode); break;
+    case 2: hipLaunchKernelGGL((k_pcg_dot<2>), dim3(nblk), dim3(kBlock), 0, s, va, mode); break;
+    case 4: hipLaunchKernelGGL((k_pcg_dot<4>), dim3(nblk), dim3(kBlock), 0, s, va, mode); break;
+    case 8: hipLaunchKernelGGL((k_pcg_dot<8>), dim3(nblk), dim3(kBlock), 0, s, va, mode); break;
+    case 16: hipLaunchKernelGGL((k_pcg_dot<16>), dim3(nblk), dim3(kBlock), 0, s, va, mode); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// X = 0, R = B, b_norms (incomplete_cholesky.hpp:66-85); Z = M^-1 R (:87-92); P = Z (:94-95);
+// rs_old = R.Z (:97).  Z lives in h->d_p1, P in h->d_p0.
+hipError_t launch_pcg_ic0_init(mspmv_handle_s *h, mspmv_ic0_s *ic, const double *d_b, double *d_x, int L, double tol,
+                               int nblk)
+{
+    hipError_t e = launch_cg_init(h, d_b, d_x, L, tol, nblk);
+    if (e == hipSuccess)
+        e = ic0_apply(h, ic, L, h->d_r, h->d_p1);
+    CgVecArgs va = pcg_vec_args(h, d_x, L, tol);
+    va.p = h->d_p1;
+    if (e == hipSuccess)
+        e = pcg_dot(va, L, nblk, 0, h->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(h->d_p0, h->d_p1, sizeof(double) * (size_t)h->m * L, hipMemcpyDeviceToDevice, h->stream);
+    return e;
+}
+
+// One iteration (:104-191): AP = A P with P.AP (fold: alpha = rs_old / P.AP, non-finite stops);
+// X += alpha P, R -= alpha AP, R.R -> masks, history, stop; Z = M^-1 R; R.Z -> beta, rs_old;
+// P = Z + beta P.
+hipError_t launch_pcg_ic0_iteration(mspmv_handle_s *h, mspmv_ic0_s *ic, const TilePlan &plan, double *d_x, int L,
+                                    int nblk, double tol)
+{
+    hipError_t e = launch_spmm_dot(h, plan, h->d_p0, h->d_ap, L, h->d_ctrl, h->d_partials, h->d_gtickets, h->d_red,
+                                   h->d_scal, h->d_conv, kFoldCgAlpha);
+    CgVecArgs va = pcg_vec_args(h, d_x, L, tol);
+    va.red_in = h->d_red;  // alpha_j = converged ? 0 : rs_old_j / P.AP_j, in every block
+    if (e == hipSuccess)
+        e = dispatch_vec(false, va, L, nblk, h->stream);
+    if (e == hipSuccess)
+        e = ic0_apply(h, ic, L, h->d_r, h->d_p1);
+    CgVecArgs vd = va;
+    vd.p = h->d_p1;
+    if (e == hipSuccess)
+        e = pcg_dot(vd, L, nblk, 1, h->stream);
+    va.r = h->d_p1;  // P = Z + beta P
+    if (e == hipSuccess)
+        e = launch_dist_vec(2, va, L, nblk, h->d_p0, h->stream);
+    return e;
+}
+
 }  // namespace mspmv

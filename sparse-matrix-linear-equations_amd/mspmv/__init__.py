@@ -82,6 +82,12 @@ _SIGS = {
     "mspmv_dcg_multi": (_I, [_P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
     "mspmv_dcg_multi_dev": (_I, [_P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
     "mspmv_spai_values": (_I, [ctypes.POINTER(_CsrD), _P]),
+    "mspmv_ic0_nnz": (_I, [ctypes.POINTER(_CsrD), _PI]),
+    "mspmv_ic0_factor": (_I, [ctypes.POINTER(_CsrD), _P, _P, _P, _PD]),
+    "mspmv_ic0_create": (_I, [ctypes.POINTER(_CsrD), _I, ctypes.POINTER(_P)]),
+    "mspmv_ic0_destroy": (_I, [_P]),
+    "mspmv_dpcg_ic0_multi": (_I, [_P, _P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
+    "mspmv_dpcg_ic0_multi_dev": (_I, [_P, _P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
     "mspmv_dpcg_spai_multi": (_I, [_P, _P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
     "mspmv_dpcg_spai_multi_dev": (_I, [_P, _P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
     "mspmv_time_spmm_dev": (_I, [_P, _P, _P, _I, _I, _SZ, _PD]),
@@ -430,6 +436,59 @@ class GpuCsr:
         return it.value, hist[: min(it.value, hist_cap)], st
 
 
+def ic0_factor(a: CsrMatrix):
+    """IncompleteCholesky (incomplete_cholesky_decomp.hpp:84-201) on the host: (L, shift used)."""
+    nz = ctypes.c_int()
+    _check(lib.mspmv_ic0_nnz(ctypes.byref(a._c()), ctypes.byref(nz)), "ic0_nnz")
+    ro = np.zeros(a.num_rows + 1, np.int32)
+    ci = np.zeros(max(nz.value, 1), np.int32)
+    va = np.zeros(max(nz.value, 1), np.float64)
+    sh = ctypes.c_double()
+    _check(lib.mspmv_ic0_factor(ctypes.byref(a._c()), _ptr(ro), _ptr(ci), _ptr(va), ctypes.byref(sh)), "ic0_factor")
+    return CsrMatrix.from_arrays(a.num_cols, ro, ci[: nz.value], va[: nz.value]), sh.value
+
+
+class GpuIc0:
+    """An IC(0) factor L (and L^T) resident on a device for the GPU triangular solves."""
+
+    def __init__(self, l: CsrMatrix, device: int = 0):
+        h = ctypes.c_void_p()
+        _check(lib.mspmv_ic0_create(ctypes.byref(l._c()), device, ctypes.byref(h)), "ic0_create")
+        self.h = h.value
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.mspmv_ic0_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def pcg_ic0(g: "GpuCsr", ic: GpuIc0, B: np.ndarray, max_iters: int, tolerance: float, hist_cap: int = 0):
+    """PCGSolveMultiple (mspmv_dpcg_ic0_multi): (X, iterations, history, status)."""
+    B = np.ascontiguousarray(B, np.float64)
+    if B.ndim == 1:
+        B = B[:, None]
+    L = B.shape[1]
+    X = np.empty_like(B)
+    it = ctypes.c_int()
+    hist = np.zeros(max(hist_cap, 1), np.float64)
+    st = lib.mspmv_dpcg_ic0_multi(g.h, ic.h, _ptr(B), _ptr(X), L, max_iters, tolerance, MERGE, ctypes.byref(it),
+                                  _ptr(hist) if hist_cap else None, hist_cap)
+    _check(st, "dpcg_ic0_multi", allow=(4,))
+    return X, it.value, hist[: min(it.value, hist_cap)], st
+
+
 def spai_values(a: CsrMatrix) -> np.ndarray:
     """M's values on A's pattern (mspmv_spai_values; SparseApproximateInversion,
     work_2025/cg/sparse_approximate_inversion.hpp:40-321).  Host setup, as in the reference."""
@@ -506,6 +565,29 @@ def SPAISolveMultiple(a: CsrMatrix, m: CsrMatrix, B, X, num_vectors: int, max_it
     Bm = np.asarray(B, np.float64).reshape(a.num_rows, num_vectors)
     cap = max_iters if max_errors is not None else 0
     Xs, it, hist, _ = _gpu(a).pcg_spai(_gpu(m), Bm, max_iters, tolerance, hist_cap=cap)
+    X[:] = Xs.reshape(-1)
+    if max_errors is not None:
+        max_errors.clear()
+        max_errors.extend(hist.tolist())
+    return it
+
+
+def IncompleteCholesky(a: CsrMatrix) -> CsrMatrix:
+    """work_2025/cg/incomplete_cholesky_decomp.hpp:84-201: returns L (raises if it fails)."""
+    return ic0_factor(a)[0]
+
+
+def PCGSolveMultiple(a: CsrMatrix, l: CsrMatrix, l_transpose, B, X, num_vectors: int, max_iters: int,
+                     tolerance: float, kernel_type: int = MERGE, max_errors: Optional[list] = None) -> int:
+    """work_2025/main/incomplete_cholesky.hpp:33-199.  l_transpose is accepted for signature
+    compatibility; the device factor forms its own transpose."""
+    Bm = np.asarray(B, np.float64).reshape(a.num_rows, num_vectors)
+    cap = max_iters if max_errors is not None else 0
+    ic = getattr(l, "_gpu_ic0", None)
+    if ic is None or ic.h is None:
+        ic = GpuIc0(l)
+        object.__setattr__(l, "_gpu_ic0", ic)
+    Xs, it, hist, _ = pcg_ic0(_gpu(a), ic, Bm, max_iters, tolerance, hist_cap=cap)
     X[:] = Xs.reshape(-1)
     if max_errors is not None:
         max_errors.clear()

@@ -39,6 +39,8 @@ class Oracle:
             "orc_cg_single": (_I, [_I, _P, _P, _P, _P, _P, _I, _D, _P, _I]),
             "orc_cg_multi": (_I, [_I, _I, _P, _P, _P, _P, _P, _I, _I, _D, _I, _I, _P, _I]),
             "orc_pcg_spai_multi": (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _D, _I, _I, _P, _I]),
+            "orc_ic0_factor": (_I, [_I, _P, _P, _P, _P, _P, _P, _P]),
+            "orc_pcg_ic0_multi": (_I, [_I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _D, _I, _I, _P, _I]),
             "orc_calculate_threshold": (_D, [_P, _I, _D]),
             "orc_glibc_rand_fill": (None, [ctypes.c_uint, ctypes.c_longlong, _P]),
             "orc_coo_to_csr": (None, [_I, _I, _P, _P, _P, _P, _P, _P]),
@@ -141,6 +143,33 @@ class Oracle:
         it = self.lib.orc_pcg_spai_multi(a.num_rows, a.num_nonzeros, _p(a.row_offsets), _p(a.column_indices),
                                          _p(a.values), _p(m_vals), _p(B), _p(X), L, max_iters, tol, kernel, P,
                                          _p(hist) if hist_cap else None, hist_cap)
+        return X, it, hist[: min(it, hist_cap)]
+
+    def ic0_factor(self, a):
+        """IncompleteCholesky (incomplete_cholesky_decomp.hpp:84-201) -> (l_ro, l_ci, l_va, shift)."""
+        n = a.num_rows
+        lro = np.zeros(n + 1, np.int32)
+        lci = np.zeros(max(a.num_nonzeros, 1), np.int32)
+        lva = np.zeros(max(a.num_nonzeros, 1))
+        sh = ctypes.c_double()
+        ok = self.lib.orc_ic0_factor(n, _p(a.row_offsets), _p(a.column_indices), _p(a.values), _p(lro), _p(lci),
+                                     _p(lva), ctypes.byref(sh))
+        if not ok:
+            raise RuntimeError("oracle IC(0) failed")
+        nz = int(lro[-1])
+        return lro, lci[:nz].copy(), lva[:nz].copy(), sh.value
+
+    def pcg_ic0_multi(self, a, l_ro, l_ci, l_va, B, max_iters, tol, kernel=1, P=8, hist_cap=0):
+        """PCGSolveMultiple (incomplete_cholesky.hpp:33-199) with the factor L."""
+        B = np.ascontiguousarray(B, np.float64)
+        L = B.shape[1]
+        X = np.empty_like(B)
+        hist = np.zeros(max(hist_cap, 1))
+        l_ro, l_ci, l_va = (np.ascontiguousarray(l_ro, np.int32), np.ascontiguousarray(l_ci, np.int32),
+                            np.ascontiguousarray(l_va, np.float64))
+        it = self.lib.orc_pcg_ic0_multi(a.num_rows, a.num_nonzeros, _p(a.row_offsets), _p(a.column_indices),
+                                        _p(a.values), int(l_ro[-1]), _p(l_ro), _p(l_ci), _p(l_va), _p(B), _p(X), L,
+                                        max_iters, tol, kernel, P, _p(hist) if hist_cap else None, hist_cap)
         return X, it, hist[: min(it, hist_cap)]
 
     def calculate_threshold(self, b, n, tol):
