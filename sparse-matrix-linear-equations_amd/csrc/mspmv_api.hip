@@ -911,8 +911,44 @@ mspmv_status mspmv_ic0_create(const mspmv_csr_d *l, int device, mspmv_ic0 *out)
                 uva[d] = l->values[k];
             }
     }
+    // Level sets: a row's level is 1 + the deepest level among the rows it reads (L: columns
+    // below the diagonal, solved ascending; L^T: columns above it, solved descending).  Waves
+    // take rows in (level, row) order, so every awaited row is in an earlier level, hence an
+    // earlier-dispatched wave, and a whole level's rows are solved concurrently (natural order
+    // would chain every row to its left neighbour: ~15x slower on a 2-D stencil).
+    auto order_by_level = [&](const int *rp, const int *cp, bool fwd, std::vector<int> &order) {
+        std::vector<int> lev((size_t)n, 0);
+        int maxlev = 0;
+        for (int s = 0; s < n; ++s) {
+            const int i = fwd ? s : n - 1 - s;
+            int lv = 0;
+            for (int k = rp[i]; k < rp[i + 1]; ++k) {
+                const int j = cp[k];
+                if (fwd ? j < i : j > i)
+                    lv = std::max(lv, lev[j] + 1);
+            }
+            lev[i] = lv;
+            maxlev = std::max(maxlev, lv);
+        }
+        std::vector<int> cnt((size_t)maxlev + 2, 0);
+        for (int i = 0; i < n; ++i)
+            ++cnt[(size_t)lev[i] + 1];
+        for (int l2 = 0; l2 <= maxlev; ++l2)
+            cnt[(size_t)l2 + 1] += cnt[l2];
+        order.assign((size_t)std::max(n, 1), 0);
+        for (int s = 0; s < n; ++s) {
+            const int i = fwd ? s : n - 1 - s;
+            order[(size_t)cnt[lev[i]]++] = i;
+        }
+        return n ? maxlev + 1 : 0;
+    };
+    std::vector<int> fwd_order, bwd_order;
+    const int lf = order_by_level(l->row_offsets, l->column_indices, true, fwd_order);
+    const int lb = order_by_level(uro.data(), uci.data(), false, bwd_order);
     HIP_TRY(hipSetDevice(device));
     mspmv_ic0_s *m = new mspmv_ic0_s;
+    m->levels_fwd = lf;
+    m->levels_bwd = lb;
     m->device = device;
     m->n = n;
     m->nnz = nnz;
@@ -932,6 +968,8 @@ mspmv_status mspmv_ic0_create(const mspmv_csr_d *l, int device, mspmv_ic0 *out)
     up(&m->d_uro, uro.data(), (size_t)n + 1);
     up(&m->d_uci, uci.data(), (size_t)nnz);
     up(&m->d_uva, uva.data(), (size_t)nnz);
+    up(&m->d_fwd_order, fwd_order.data(), (size_t)n);
+    up(&m->d_bwd_order, bwd_order.data(), (size_t)n);
     if (st == MSPMV_OK)
         st = dev_alloc(&m->d_ready, (size_t)std::max(n, 1));
     if (st != MSPMV_OK) {
@@ -953,6 +991,8 @@ mspmv_status mspmv_ic0_destroy(mspmv_ic0 m)
     dev_free(m->d_uro);
     dev_free(m->d_uci);
     dev_free(m->d_uva);
+    dev_free(m->d_fwd_order);
+    dev_free(m->d_bwd_order);
     dev_free(m->d_ready);
     if (m->d_y)
         (void)hipFree(m->d_y);

@@ -122,6 +122,9 @@ struct mspmv_ic0_s {
     double *d_lva = nullptr;
     int *d_uro = nullptr, *d_uci = nullptr;  // L^T (upper, diagonal first)
     double *d_uva = nullptr;
+    int *d_fwd_order = nullptr;              // [n] rows of L by dependency level (then row): wave w solves row fwd_order[w]
+    int *d_bwd_order = nullptr;              // [n] rows of L^T by backward level
+    int levels_fwd = 0, levels_bwd = 0;
     int *d_ready = nullptr;                  // [n] per-row ready flags of the running solve
     double *d_y = nullptr;                   // [n * L] forward-solve result
     size_t y_cap = 0;

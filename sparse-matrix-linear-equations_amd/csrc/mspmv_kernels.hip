@@ -1654,21 +1654,23 @@ __device__ __forceinline__ bool wait_flag(const int *f)
 // incomplete_cholesky_decomp.hpp:231-348.  Lane (q, v) takes nonzeros q, q + 64/L, ... of the
 // row for right-hand side v; a dependency j waits on ready[j], then x[j] is read (sc1 loads); a
 // fixed xor butterfly folds the row's partial sums; x[i] is stored write-through (sc1), drained,
-// and ready[i] raised.  Waves are dispatched in row order and wait only on earlier rows, so
-// every awaited row belongs to a wave already resident or finished: no deadlock.  The partial
+// and ready[i] raised.  Waves are dispatched in dependency-level order and wait only on rows of
+// earlier levels, so every awaited row belongs to a wave already resident or finished: no
+// deadlock.  The partial
 // sums are folded in a tree, not in CSR order (the reference's sequential sum): results agree to
 // rounding.  BackwardSolveMultiple's zero-diagonal rule (x = 0) is kept; a forward row takes
 // the diagonal as stored.
 template <int L, bool FWD>
 __global__ __launch_bounds__(kBlock) void k_trsv(const int *__restrict__ ro, const int *__restrict__ ci,
-                                                 const double *__restrict__ va, int n, const double *b, double *x,
+                                                 const double *__restrict__ va, int n,
+                                                 const int *__restrict__ order, const double *b, double *x,
                                                  int *ready, CgControl *ctrl)
 {
     constexpr int NZ = 64 / L;
     const int w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     if (w >= n || ctrl->done)  // done is set only by earlier launches: uniform here
         return;
-    const int i = FWD ? w : n - 1 - w;
+    const int i = order[w];  // rows in (level, row) order: awaited rows belong to earlier waves
     const int lane = threadIdx.x & 63;
     const int v = lane % L, q = lane / L;
     const int k1 = ro[i + 1];
@@ -2554,11 +2556,11 @@ static void trsv_L(const mspmv_ic0_s *ic, bool fwd, const double *b, double *x, 
 {
     const dim3 grid((ic->n + kBlock / 64 - 1) / (kBlock / 64)), block(kBlock);
     if (fwd)
-        hipLaunchKernelGGL((k_trsv<L, true>), grid, block, 0, s, ic->d_lro, ic->d_lci, ic->d_lva, ic->n, b, x,
-                           ic->d_ready, ctrl);
+        hipLaunchKernelGGL((k_trsv<L, true>), grid, block, 0, s, ic->d_lro, ic->d_lci, ic->d_lva, ic->n,
+                           ic->d_fwd_order, b, x, ic->d_ready, ctrl);
     else
-        hipLaunchKernelGGL((k_trsv<L, false>), grid, block, 0, s, ic->d_uro, ic->d_uci, ic->d_uva, ic->n, b, x,
-                           ic->d_ready, ctrl);
+        hipLaunchKernelGGL((k_trsv<L, false>), grid, block, 0, s, ic->d_uro, ic->d_uci, ic->d_uva, ic->n,
+                           ic->d_bwd_order, b, x, ic->d_ready, ctrl);
 }
 
 // Z = L^-T (L^-1 R): ForwardSolveMultiple into ic->d_y, then BackwardSolveMultiple
