@@ -127,6 +127,46 @@ bool SparseApproximateInversion(const Csr &a, Csr &l)
     return true;
 }
 
+// work_2025/cg/incomplete_cholesky_decomp.hpp:84-201: l receives L (new[] arrays, the
+// reference's non-MKL branch); false when the factorization fails after its 20 shifted attempts.
+template <typename Csr>
+bool IncompleteCholesky(const Csr &a, Csr &l)
+{
+    mspmv_csr_d d{a.num_rows, a.num_cols, a.num_nonzeros, a.row_offsets, a.column_indices, a.values};
+    int nz = 0;
+    mspmv_facade::check(mspmv_ic0_nnz(&d, &nz), "mspmv_ic0_nnz");
+    l.num_rows = a.num_rows;
+    l.num_cols = a.num_cols;
+    l.num_nonzeros = nz;
+    l.row_offsets = new int[(size_t)a.num_rows + 1];
+    l.column_indices = new int[(size_t)std::max(nz, 1)];
+    l.values = new double[(size_t)std::max(nz, 1)];
+    return mspmv_ic0_factor(&d, l.row_offsets, l.column_indices, l.values, nullptr) == MSPMV_OK;
+}
+
+// work_2025/main/incomplete_cholesky.hpp:33-199 (l_transpose accepted for the signature; the
+// device factor forms its own transpose).  The factor is uploaded once per L and cached.
+template <typename Csr, typename ValueT, typename KernelT>
+int PCGSolveMultiple(Csr &a, const Csr &l, const Csr & /*l_transpose*/, const ValueT *B, ValueT *X, int num_vectors,
+                     int max_iters, ValueT tolerance, KernelT kernel_type, std::vector<double> *max_errors = nullptr)
+{
+    static std::map<const void *, mspmv_ic0> factors;
+    mspmv_ic0 &ic = factors[(const void *)l.values];
+    if (!ic) {
+        mspmv_csr_d d{l.num_rows, l.num_cols, l.num_nonzeros, l.row_offsets, l.column_indices, l.values};
+        mspmv_facade::check(mspmv_ic0_create(&d, 0, &ic), "mspmv_ic0_create");
+    }
+    int iters = 0;
+    std::vector<double> hist(max_errors ? (size_t)max_iters : 0);
+    mspmv_facade::check(mspmv_dpcg_ic0_multi(mspmv_facade::handle_for(a), ic, B, X, num_vectors, max_iters,
+                                             tolerance, (mspmv_spmm_kernel)(int)kernel_type, &iters,
+                                             max_errors ? hist.data() : nullptr, max_errors ? max_iters : 0),
+                        "mspmv_dpcg_ic0_multi");
+    if (max_errors)
+        max_errors->assign(hist.begin(), hist.begin() + std::min<size_t>(hist.size(), (size_t)iters));
+    return iters;
+}
+
 // work_2025/main/sparse_approximate_inverse.hpp:30-230
 template <typename Csr, typename ValueT, typename KernelT>
 int SPAISolveMultiple(Csr &a, Csr &m, const ValueT *B, ValueT *X, int num_vectors, int max_iters,
