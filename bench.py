@@ -306,7 +306,10 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
                      "kernel": kname, "bytes_per_launch": bytes_launch,
-                     "kernel_ms": round(kern_ms, 5), "kernels_per_step": kps},
+                     "kernel_ms": round(kern_ms, 5), "kernels_per_step": kps,
+                     "note": "achieved = algorithmic bytes (12 B/nnz: int32 columns + f64 values, SURVEY 8(d)) / "
+                             "kernel time; the kernel streams per-tile 16-bit column offsets (10 B/nnz), so "
+                             "traffic (PMC bytes actually moved per launch) is below bytes_per_launch"},
         "spmv_gflops_per_launch": round(2.0 * a0.num_nonzeros / (kern_ms * 1e-3) / 1e9, 2),
         "reference_effective_GBps": round(ref_eff, 1),
         "setup_ms": round(gs[0].setup_ms, 2),
