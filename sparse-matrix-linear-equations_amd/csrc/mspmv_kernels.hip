@@ -352,7 +352,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_cols16(const int *__restrict__ 
 // reads plus an 11-step search and two barriers for SpMV, IPTG/4 gather chunks for SpMM).
 __global__ void k_tile_modes(const int *__restrict__ row_offsets, const int2 *__restrict__ bounds,
                              const unsigned char *__restrict__ split, int num_tiles, int gl, int max_cost,
-                             unsigned char *__restrict__ modes)
+                             int lanes, unsigned char *__restrict__ modes)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= num_tiles)
@@ -371,7 +371,7 @@ __global__ void k_tile_modes(const int *__restrict__ row_offsets, const int2 *__
         longest = max(longest, b1.y - prev);
     int best = 0, best_cost = max_cost + 1;
     for (int lg = 0; (gl << lg) <= 64; ++lg) {  // a row group stays inside one wave
-        const int groups = kBlock / (gl << lg), G = 1 << lg;
+        const int groups = lanes / (gl << lg), G = 1 << lg;
         const int rounds = (nseg + groups - 1) / groups;
         const int per_lane = (longest + G - 1) / G;
         // SpMV: LDS product reads, one step each, plus a 3-step shuffle per fold level.
@@ -440,6 +440,20 @@ __device__ __forceinline__ int pslot(int k) { return k ^ ((k >> 3) & 7); }
 // columns share cache lines) -- measured 1.4x faster than 16-byte-per-lane blocked loads,
 // whose gathers scatter over 4x more lines.  Every round's loads and gathers are issued
 // before any is consumed (indices past the tile clamp to its last nonzero).
+// Barrier over the threads that share a tile: the workgroup, or (one-wave workgroups) the wave,
+// whose LDS accesses retire in order -- only compiler reordering has to be fenced.
+template <int TB>
+__device__ __forceinline__ void tile_sync()
+{
+    if (TB == 64) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+
 template <int NJ, bool CG>
 struct StageRegs {
     int c[NJ];
@@ -447,21 +461,21 @@ struct StageRegs {
     double xv[NJ];
     double pv[CG ? NJ : 1];
 };
-template <int NJ, bool CG, bool NT>
+template <int NJ, bool CG, bool NT, int TB = kBlock>
 __device__ __forceinline__ void stage_issue(const TileArgs &a, int n0, int nnzt, int colbase, StageRegs<NJ, CG> &st)
 {
     if (colbase >= 0) {  // block-uniform: the tile's 16-bit column offsets
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-            st.c[j] = colbase + (int)ld_stream<NT>(a.cols16 + n0 + min((int)threadIdx.x + j * kBlock, nnzt - 1));
+            st.c[j] = colbase + (int)ld_stream<NT>(a.cols16 + n0 + min((int)threadIdx.x + j * TB, nnzt - 1));
     } else {
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-            st.c[j] = ld_stream<NT>(a.cols + n0 + min((int)threadIdx.x + j * kBlock, nnzt - 1));
+            st.c[j] = ld_stream<NT>(a.cols + n0 + min((int)threadIdx.x + j * TB, nnzt - 1));
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
-        st.v[j] = ld_stream<NT>(a.vals + n0 + min((int)threadIdx.x + j * kBlock, nnzt - 1));
+        st.v[j] = ld_stream<NT>(a.vals + n0 + min((int)threadIdx.x + j * TB, nnzt - 1));
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
         st.xv[j] = a.x[st.c[j]];
@@ -471,12 +485,12 @@ __device__ __forceinline__ void stage_issue(const TileArgs &a, int n0, int nnzt,
             st.pv[j] = a.p_old[st.c[j]];
     }
 }
-template <int NJ, bool CG>
+template <int NJ, bool CG, int TB = kBlock>
 __device__ __forceinline__ void stage_store(const StageRegs<NJ, CG> &st, int nnzt, double beta, double *s_prod)
 {
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-        const int k = (int)threadIdx.x + j * kBlock;
+        const int k = (int)threadIdx.x + j * TB;
         double x = st.xv[j];
         if (CG)
             x = x + beta * st.pv[j];
@@ -495,16 +509,16 @@ __device__ __forceinline__ void stage_products(const TileArgs &a, int n0, int nn
 // Per-tile LDS of the single-RHS kernels.  Products and row ends share one buffer: a tile
 // holds nrows + nnzt <= MAXI items, so the nnzt products (slots [0, nnzt) rounded up to the
 // swizzle group) followed by the nrows int row ends always fit in MAXI + 8 doubles.
-template <int IPT>
+template <int IPT, int TB = kBlock>
 struct SpmvSmem {
-    static constexpr int TILE = kBlock * IPT;
+    static constexpr int TILE = TB * IPT;
     static constexpr int MAXI = TILE + TILE / kSnapDiv;
-    static constexpr int MAXJ = (MAXI + kBlock - 1) / kBlock;
+    static constexpr int MAXJ = (MAXI + TB - 1) / TB;
     double prod[MAXI + 8];
-    int crow[kBlock];
-    int ccol[kBlock];
-    double cval[kBlock];
-    double red[kBlock / 64];
+    int crow[TB];
+    int ccol[TB];
+    double cval[TB];
+    double red[TB / 64];
     int last;
     __device__ __forceinline__ int *rowend(int nnzt) { return reinterpret_cast<int *>(prod + ((nnzt + 7) & ~7)); }
 };
@@ -513,24 +527,24 @@ struct SpmvSmem {
 // search per walker, the register walk, in-tile carries, the cross-tile carry, the row
 // stores and (CG) the p.Ap contribution.  Called uniformly by all 256 threads; ends with the
 // LDS free for the next tile.
-template <int IPT, int MODE>
-__device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT> &sm, int t, int r0, int n0, int nrows,
+template <int IPT, int MODE, int TB = kBlock>
+__device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT, TB> &sm, int t, int r0, int n0, int nrows,
                                           int nnzt, bool tail, double beta, double &dot)
 {
-    constexpr int MAXJ = SpmvSmem<IPT>::MAXJ;
+    constexpr int MAXJ = SpmvSmem<IPT, TB>::MAXJ;
     const int tid = threadIdx.x;
     const int *rend = sm.rowend(nnzt);
     const int items = nrows + nnzt;
-    const int ipt = (items + kBlock - 1) / kBlock;
+    const int ipt = (items + TB - 1) / TB;
     const int d0 = min(tid * ipt, items);
     int cx, cy;
     lds_search(d0, rend, nrows, nnzt, cx, cy);
     // The walker's end is the next walker's start: one search per thread, shared via LDS.
     sm.crow[tid] = cx;
     sm.ccol[tid] = cy;
-    __syncthreads();
-    const int ex = tid + 1 < kBlock ? sm.crow[tid + 1] : nrows;
-    const int ey = tid + 1 < kBlock ? sm.ccol[tid + 1] : nnzt;
+    tile_sync<TB>();
+    const int ex = tid + 1 < TB ? sm.crow[tid + 1] : nrows;
+    const int ey = tid + 1 < TB ? sm.ccol[tid + 1] : nnzt;
     // Does this thread's first row hold nonzeros that earlier threads of the tile consumed?
     const bool need_cin = (cx < ex) && (cy > (cx == 0 ? 0 : rend[cx - 1]));
     // This walker's products, read from LDS up front (independent reads, no dependent chain).
@@ -588,10 +602,10 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT> &sm, 
         run = 0.0;
         ++cx;
     }
-    __syncthreads();  // every walker has read its neighbour's start from crow / ccol
+    tile_sync<TB>();  // every walker has read its neighbour's start from crow / ccol
     sm.crow[tid] = ex;
     sm.cval[tid] = run;
-    __syncthreads();
+    tile_sync<TB>();
     if (pend) {  // close the row begun by earlier threads, summing their carries in thread order
         int j0 = tid - 1;
         while (j0 > 0 && sm.crow[j0 - 1] == prow)
@@ -601,12 +615,12 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT> &sm, 
             acc += sm.cval[u];
         write_row(prow, acc + pval);
     }
-    if (tid == kBlock - 1 && tail) {  // the tile's trailing partial row -> carry
-        int j0 = kBlock - 1;
+    if (tid == TB - 1 && tail) {  // the tile's trailing partial row -> carry
+        int j0 = TB - 1;
         while (j0 > 0 && sm.crow[j0 - 1] == nrows)
             --j0;
         double acc = sm.cval[j0];
-        for (int u = j0 + 1; u < kBlock; ++u)
+        for (int u = j0 + 1; u < TB; ++u)
             acc += sm.cval[u];
         a.carry_val[t] = acc;
         const int R = r0 + nrows;
@@ -615,7 +629,7 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT> &sm, 
         else if (MODE == kModeDot)
             dot += a.x[R] * acc;
     }
-    __syncthreads();  // LDS free for the next tile
+    tile_sync<TB>();  // LDS free for the next tile
 }
 
 // Row-group reduction of one tile whose products and row ends are in LDS (mode lg + 1 of
@@ -629,8 +643,8 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT> &sm, 
 // that only stores makes hipcc drain vmcnt before it, which would wait for the persistent
 // kernel's in-flight prefetch).  xr / pr: x[r0 + tid] and p_old[r0 + tid] (CG / dot modes),
 // loaded by the caller for tid <= nrows.
-template <int IPT, int MODE>
-__device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT> &sm, int t, int r0, int nrows,
+template <int IPT, int MODE, int TB = kBlock>
+__device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT, TB> &sm, int t, int r0, int nrows,
                                            int nnzt, bool tail, double beta, double &dot, int lg, double xr,
                                            double pr)
 {
@@ -658,13 +672,13 @@ __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT> &sm,
             v += __shfl_xor(v, off);
         return v;
     };
-    const int nfast = min(nseg, kBlock);
-    for (int r = tid >> lg; r < nfast; r += kBlock >> lg) {  // uniform within a group
+    const int nfast = min(nseg, TB);
+    for (int r = tid >> lg; r < nfast; r += TB >> lg) {  // uniform within a group
         const double v = seg_sum(r);
         if (lane == 0)
             sm.cval[r] = v;
     }
-    for (int r = kBlock + (tid >> lg); r < nseg; r += kBlock >> lg) {  // rare: > kBlock segments
+    for (int r = TB + (tid >> lg); r < nseg; r += TB >> lg) {  // rare: > TB segments
         const double v = seg_sum(r);
         if (lane == 0) {
             const int R = r0 + r;
@@ -686,7 +700,7 @@ __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT> &sm,
             }
         }
     }
-    __syncthreads();
+    tile_sync<TB>();
     if (tid < nfast) {
         const double v = sm.cval[tid];
         if (tid < nrows) {
@@ -707,19 +721,19 @@ __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT> &sm,
                 dot += xr * v;
         }
     }
-    __syncthreads();  // LDS free for the next tile
+    tile_sync<TB>();  // LDS free for the next tile
 }
 
 // One tile's reduction, by its plan-time mode (a.rmode[t]); tail = a.split[t + 1].
-template <int IPT, int MODE>
-__device__ __forceinline__ void reduce_tile(const TileArgs &a, SpmvSmem<IPT> &sm, int t, int r0, int n0, int nrows,
+template <int IPT, int MODE, int TB = kBlock>
+__device__ __forceinline__ void reduce_tile(const TileArgs &a, SpmvSmem<IPT, TB> &sm, int t, int r0, int n0, int nrows,
                                             int nnzt, int mode, bool tail, double beta, double &dot, double xr,
                                             double pr)
 {
     if (mode == 0)
-        walk_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, tail, beta, dot);
+        walk_tile<IPT, MODE, TB>(a, sm, t, r0, n0, nrows, nnzt, tail, beta, dot);
     else
-        group_tile<IPT, MODE>(a, sm, t, r0, nrows, nnzt, tail, beta, dot, mode - 1, xr, pr);
+        group_tile<IPT, MODE, TB>(a, sm, t, r0, nrows, nnzt, tail, beta, dot, mode - 1, xr, pr);
 }
 
 // x[r0 + tid] and p_old[r0 + tid] for the row-group epilogue (CG / dot modes), tid <= nrows.
@@ -804,17 +818,19 @@ __device__ __forceinline__ void cg1_publish(const TileArgs &a, SpmvSmem<IPT> &sm
     }
 }
 
-// Single right-hand side, one tile per workgroup.  TILE = 256*IPT merge items nominal, up to
-// 1.25*TILE after snapping.  CG: gathers p = r + beta*p_old on the fly (UpdatePSingle,
-// single_strategy.hpp:89-97, fused into the SpMV), writes p for its rows, Ap, and p.Ap by
-// linearity.
-template <int IPT, int MODE, bool NT>
-__global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
+// Single right-hand side, one tile per workgroup of TB threads.  TILE = TB*IPT merge items
+// nominal, up to 1.125*TILE after snapping.  CG: gathers p = r + beta*p_old on the fly
+// (UpdatePSingle, single_strategy.hpp:89-97, fused into the SpMV), writes p for its rows, Ap, and
+// p.Ap by linearity.  TB = 64 (one-wave workgroups, SpMV only): every wave owns its tile, so no
+// workgroup barrier ties a wave's progress to its siblings' gather latencies.
+template <int IPT, int MODE, bool NT, int TB = kBlock>
+__global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
 {
+    static_assert(TB == kBlock || MODE == kModeSpmv, "one-wave tiles run the plain SpMV only");
     constexpr bool CG = MODE == kModeCg;
-    constexpr int TILE = SpmvSmem<IPT>::TILE;
-    constexpr int MAXJ = SpmvSmem<IPT>::MAXJ;
-    __shared__ SpmvSmem<IPT> sm;
+    constexpr int TILE = SpmvSmem<IPT, TB>::TILE;
+    constexpr int MAXJ = SpmvSmem<IPT, TB>::MAXJ;
+    __shared__ SpmvSmem<IPT, TB> sm;
     const int tid = threadIdx.x;
     // CG: stop flag loaded now, tested after the stream and gathers are issued (see k_spmm_tile)
     const int stopped = MODE != kModeSpmv ? a.ctrl->done : 0;
@@ -829,27 +845,27 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
     // CG: the update's r.r partials are loaded first; summed (-> stop test, beta) once this
     // tile's stream and gathers are in flight.  Block-uniform, as is every branch on nnzt.
     PartRegs<CG ? kUpdateMaxBlocks / kBlock : 1> pin;
-    if (CG)
+    if constexpr (CG)
         part_load(a.part_in, a.n_part_in, pin);
     auto head = [&]() {  // the stop flag is tested before cg1_head records anything
         if (stopped)
             go = false;
-        else if (CG)
+        else if constexpr (CG)
             go = cg1_head(a, part_sum(pin, sm.red), beta);
     };
     const int colbase = a.cols16 ? a.colbase[t] : -1;
     if (nnzt > 0 && nnzt <= TILE) {  // the common case: no snapped-in extra nonzeros
         StageRegs<IPT, CG> st;
-        stage_issue<IPT, CG, NT>(a, n0, nnzt, colbase, st);
+        stage_issue<IPT, CG, NT, TB>(a, n0, nnzt, colbase, st);
         head();
         if (go)
-            stage_store<IPT, CG>(st, nnzt, beta, sm.prod);
+            stage_store<IPT, CG, TB>(st, nnzt, beta, sm.prod);
     } else if (nnzt > TILE) {
         StageRegs<MAXJ, CG> st;
-        stage_issue<MAXJ, CG, NT>(a, n0, nnzt, colbase, st);
+        stage_issue<MAXJ, CG, NT, TB>(a, n0, nnzt, colbase, st);
         head();
         if (go)
-            stage_store<MAXJ, CG>(st, nnzt, beta, sm.prod);
+            stage_store<MAXJ, CG, TB>(st, nnzt, beta, sm.prod);
     } else {
         head();
     }
@@ -858,16 +874,16 @@ __global__ __launch_bounds__(kBlock) void k_spmv_tile(TileArgs a)
     // Row ends after the staging: measured faster here than issuing them with the stream
     // (+0.9 us on the pwtk shape), unlike the multi-RHS kernel.
     int *rend = sm.rowend(nnzt);
-    for (int i = tid; i < nrows; i += kBlock)
+    for (int i = tid; i < nrows; i += TB)
         rend[i] = a.row_offsets[r0 + 1 + i] - n0;
-    __syncthreads();
+    tile_sync<TB>();
     double dot = 0.0;
     double xr, pr;
     row_operands<MODE>(a, r0, nrows, xr, pr);
-    reduce_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, a.rmode[t], a.split[t + 1] != 0, beta, dot, xr, pr);
-    if (MODE == kModeCg)
+    reduce_tile<IPT, MODE, TB>(a, sm, t, r0, n0, nrows, nnzt, a.rmode[t], a.split[t + 1] != 0, beta, dot, xr, pr);
+    if constexpr (MODE == kModeCg)
         cg1_publish<IPT>(a, sm, t, a.num_tiles, dot);
-    else if (MODE == kModeDot)
+    else if constexpr (MODE == kModeDot)
         dot_epilogue<IPT>(a, sm, t, dot);
 }
 
@@ -1822,6 +1838,7 @@ struct SpmvTuning {
     int rg_cost = 48; // k_tile_modes budget for row-group tiles (0: merge walk everywhere)
     int spmm_rg_cost = -1;  // the same for the multi-RHS kernels (-1: scaled to the SpMM tile)
     int cols16 = 1;   // single-RHS plans carry 16-bit column offsets where a tile's span allows
+    int tb = 256;     // threads per single-RHS SpMV tile: 256 (workgroup tiles) or 64 (one-wave tiles)
 };
 static const SpmvTuning &spmv_tuning()
 {
@@ -1849,6 +1866,8 @@ static const SpmvTuning &spmv_tuning()
             v.spmm_rg_cost = atoi(e);
         if (const char *e = getenv("MSPMV_SPMV_C16"))
             v.cols16 = atoi(e) != 0;
+        if (const char *e = getenv("MSPMV_SPMV_TB"))
+            v.tb = atoi(e) == 64 ? 64 : 256;
         return v;
     }();
     return t;
@@ -1869,7 +1888,7 @@ std::string spmv_kernel_name(const mspmv_handle_s *h)
 {
     const SpmvTuning &t = spmv_tuning();
     return std::string(t.persist ? "k_spmv_persist<" : "k_spmv_tile<") + std::to_string(t.ipt) + ",0," +
-           (stream_nt(h) ? "true>" : "false>");
+           (stream_nt(h) ? "true" : "false") + (t.tb == 64 && !t.persist ? ",64>" : ">");
 }
 
 // SpMM tile depth: measured best 8 items per lane group for L <= 4 (fem-blocked pwtk shape,
@@ -1883,7 +1902,7 @@ int spmm_iptg_for(int L)
 int tile_items_for(int L)
 {
     if (L == 1)
-        return kBlock * spmv_tuning().ipt;
+        return spmv_tuning().tb * spmv_tuning().ipt;
     return (kBlock / (L / 2)) * spmm_iptg_for(L);
 }
 
@@ -1924,8 +1943,9 @@ hipError_t launch_tile_modes(const int *d_row_offsets, const int2 *d_bounds, con
     const SpmvTuning &tu = spmv_tuning();
     // SpMM budget: twice the walk's gather chunks (4 steps each) plus its search
     const int cost = L == 1 ? tu.rg_cost : tu.spmm_rg_cost >= 0 ? tu.spmm_rg_cost : 2 * (4 * (spmm_iptg_for(L) / 4) + 2);
+    const int lanes = L == 1 ? tu.tb : kBlock;  // threads sharing one tile
     hipLaunchKernelGGL(k_tile_modes, dim3((num_tiles + 255) / 256), dim3(256), 0, s, d_row_offsets, d_bounds, d_split,
-                       num_tiles, L == 1 ? 1 : L / 2, cost, d_modes);
+                       num_tiles, L == 1 ? 1 : L / 2, cost, lanes, d_modes);
     return hipGetLastError();
 }
 
@@ -2018,6 +2038,11 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_c
                 launch_spmv_persist<I, MODE, true>(a, s, num_cus, tu.bpc);                         \
             else                                                                                   \
                 launch_spmv_persist<I, MODE, false>(a, s, num_cus, tu.bpc);                        \
+        } else if (MODE == kModeSpmv && tu.tb == 64) {                                             \
+            if (nt)                                                                                \
+                hipLaunchKernelGGL((k_spmv_tile<I, kModeSpmv, true, 64>), grid, dim3(64), 0, s, a);   \
+            else                                                                                   \
+                hipLaunchKernelGGL((k_spmv_tile<I, kModeSpmv, false, 64>), grid, dim3(64), 0, s, a);  \
         } else if (nt)                                                                             \
             hipLaunchKernelGGL((k_spmv_tile<I, MODE, true>), grid, block, 0, s, a);                   \
         else                                                                                       \
