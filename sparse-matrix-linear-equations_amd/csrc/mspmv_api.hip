@@ -198,7 +198,10 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
             return fail(MSPMV_ERR_HIP);
         }
     }
-    if (L == 1 && T > 0 && h->nnz > 0 && spmv_cols16_enabled()) {  // the single-RHS kernels' 16-bit stream
+    // the single-RHS kernels' 16-bit column stream; keyed on the tile size, not L, because the
+    // L = 2 SpMM shares the single-RHS plan.  (The SpMM itself keeps int32 columns: it is gather
+    // bound, and the 16-bit stream measured 0% at L = 4/8 and 7% slower at L = 16.)
+    if (tile == tile_items_for(1) && T > 0 && h->nnz > 0 && spmv_cols16_enabled()) {
         if ((st = dev_alloc(&p.d_colbase, (size_t)T)) != MSPMV_OK ||
             (st = dev_alloc(&p.d_cols16, (size_t)h->nnz + kNnzPad)) != MSPMV_OK)
             return fail(st);
