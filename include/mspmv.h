@@ -107,7 +107,9 @@ MSPMV_API mspmv_status mspmv_dspmv(mspmv_handle h, const double *x, double *y);
 /* Device pointers, asynchronous on the handle's stream. */
 MSPMV_API mspmv_status mspmv_dspmv_dev(mspmv_handle h, const double *d_x, double *d_y);
 /* Y = A X for L right-hand sides, row-major panels (OmpMergeCsrmm, merge_based.hpp:46-153).
- * L in {1, 2, 4, 8, 16}. */
+ * Any L >= 1: the tile kernels run widths 1, 2, 4, 8, 16; other even L run as column chunks of
+ * those widths over the same panels (stride L), odd L > 1 through a copy padded to L + 1
+ * columns.  Even-L panels must be 16-byte aligned. */
 MSPMV_API mspmv_status mspmv_dspmm(mspmv_handle h, const double *X, double *Y, int L);
 MSPMV_API mspmv_status mspmv_dspmm_dev(mspmv_handle h, const double *d_X, double *d_Y, int L);
 
@@ -126,7 +128,9 @@ MSPMV_API mspmv_status mspmv_dcg_single_dev(mspmv_handle h, const double *d_b, d
  * lock-step recurrences on interleaved n x L panels, per-column converged masks
  * (alpha = beta = 0 once converged), stop when all columns converged.  max_err_hist
  * (optional) receives the per-iteration max over ALL columns of sqrt(r.r)/||b||
- * (:132-155).  L in {1, 2, 4, 8, 16}. */
+ * (:132-155).  Any L >= 1: widths outside {1, 2, 4, 8, 16} are solved as independent column
+ * groups of those widths (the recurrences are per column), iteration count = the groups'
+ * maximum, history = the max over groups with finished groups frozen, as the reference's. */
 MSPMV_API mspmv_status mspmv_dcg_multi(mspmv_handle h, const double *B, double *X, int L, int max_iters, double tolerance,
                              mspmv_spmm_kernel kernel, int *iters, double *max_err_hist, int hist_cap);
 MSPMV_API mspmv_status mspmv_dcg_multi_dev(mspmv_handle h, const double *d_B, double *d_X, int L, int max_iters,
@@ -147,7 +151,8 @@ MSPMV_API mspmv_status mspmv_spai_values(const mspmv_csr_d *a, double *m_values)
  * converged or P.AP == 0), X += alpha P, R -= alpha AP, stop test on sqrt(R.R)/||B_j|| with the
  * per-column masks and the max-over-columns history, Z = M R, beta = R.Z/rs_old (0 when converged
  * or rs_old == 0), P = Z + beta P.  `m` is M's handle (same shape and device as `a`); both SpMMs
- * are merge-path tile kernels.  L in {1, 2, 4, 8, 16}; interleaved n x L panels. */
+ * are merge-path tile kernels.  Any L >= 1 (column groups as mspmv_dcg_multi); interleaved
+ * n x L panels. */
 MSPMV_API mspmv_status mspmv_dpcg_spai_multi(mspmv_handle a, mspmv_handle m, const double *B, double *X, int L,
                                              int max_iters, double tolerance, mspmv_spmm_kernel kernel, int *iters,
                                              double *max_err_hist, int hist_cap);

@@ -147,9 +147,14 @@ hipError_t launch_pack_cols16(const int *d_cols, const int2 *d_bounds, int num_t
 bool spmv_cols16_enabled();
 // y = A x (L == 1) or Y = A X (row-major panels), tile kernel + optional carry fix-up.
 hipError_t launch_spmm(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
-                       int *kernels_launched);
-hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L);
-hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L);
+                       int *kernels_launched, int ld = 0);
+// dst[i][j] = (j < cols ? src[i][j] : 0) for i < rows, j < dcols (row-major, strides lds / ldd).
+hipError_t launch_panel_copy(const double *src, int lds, double *dst, int ldd, long long rows, int cols, int dcols,
+                             hipStream_t s);
+// ld: panel leading dimension in doubles (0: L, whole panels)
+hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
+                                 int ld = 0);
+hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L, int ld = 0);
 // Nominal tile size (merge items per tile) used for L right-hand sides.
 int tile_items_for(int L);
 std::string spmv_kernel_name(const mspmv_handle_s *h);

@@ -419,6 +419,9 @@ struct TileArgs {
     // single-RHS plans: per-tile 16-bit column offsets (TilePlan::d_colbase / d_cols16; null: off)
     const int *colbase;
     const unsigned short *cols16;
+    // SpMM: leading dimension of the x / y panels in doubles (L for whole panels; a column
+    // chunk of a wider panel otherwise, mspmv_dspmm with L outside {1, 2, 4, 8, 16})
+    int ld;
 };
 
 // Tile-kernel modes.
@@ -1035,7 +1038,7 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
     const bool tail = a.split[t + 1] != 0;
     const int nseg = nrows + (tail ? 1 : 0);
     auto panel = [&](int c) {
-        double2 xv = *reinterpret_cast<const double2 *>(a.x + (size_t)c * L + 2 * lane);
+        double2 xv = *reinterpret_cast<const double2 *>(a.x + (size_t)c * a.ld + 2 * lane);
         return xv;
     };
     for (int r = tid / W; r < nseg; r += kBlock / W) {  // uniform within a group
@@ -1044,7 +1047,7 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
         // MODE 2: the row's own x, issued ahead of the row's gathers (used after them)
         double2 xx = make_double2(0.0, 0.0);
         if (MODE == kModeDot && sub == 0)
-            xx = *reinterpret_cast<const double2 *>(a.x + (size_t)(r0 + r) * L + 2 * lane);
+            xx = *reinterpret_cast<const double2 *>(a.x + (size_t)(r0 + r) * a.ld + 2 * lane);
         double2 acc = make_double2(0.0, 0.0);
         int k = s0 + sub;
         // batches of 8 panel-row gathers in flight per lane (the SpMM is gather-latency bound:
@@ -1087,7 +1090,7 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
             acc.y += __shfl_xor(acc.y, off * GL);
         }
         if (sub == 0) {
-            const size_t off = (size_t)(r0 + r) * L + 2 * lane;
+            const size_t off = (size_t)(r0 + r) * a.ld + 2 * lane;
             if (r < nrows)
                 *reinterpret_cast<double2 *>(a.y + off) = acc;
             else  // the trailing partial row -> carry (k_fixup adds it in tile order)
@@ -1189,7 +1192,7 @@ k_spmm_tile(TileArgs a)
     const bool need_cin = (cx < ex) && (cy > (cx == 0 ? 0 : s_rowend[cx - 1]));
 
     auto write_row = [&](int row, double2 val) {
-        const size_t off = (size_t)(r0 + row) * L + 2 * lane;
+        const size_t off = (size_t)(r0 + row) * a.ld + 2 * lane;
         *reinterpret_cast<double2 *>(a.y + off) = val;
         if (MODE == kModeDot) {
             const double2 xx = *reinterpret_cast<const double2 *>(a.x + off);
@@ -1215,7 +1218,7 @@ k_spmm_tile(TileArgs a)
         for (int jj = 0; jj < WJ; ++jj) {
             const int k = min(cy + j0 + jj, ey - 1);
             vv[jj] = s_val[k];
-            xr[jj] = *reinterpret_cast<const double2 *>(a.x + (size_t)s_col[k] * L + 2 * lane);
+            xr[jj] = *reinterpret_cast<const double2 *>(a.x + (size_t)s_col[k] * a.ld + 2 * lane);
         }
 #pragma unroll
         for (int jj = 0; jj < WJ; ++jj) {
@@ -1281,7 +1284,7 @@ k_spmm_tile(TileArgs a)
         }
         *reinterpret_cast<double2 *>(a.carry_val + (size_t)t * L + 2 * lane) = acc;
         if (MODE == kModeDot) {
-            const size_t off = (size_t)(r0 + nrows) * L + 2 * lane;
+            const size_t off = (size_t)(r0 + nrows) * a.ld + 2 * lane;
             const double2 xx = *reinterpret_cast<const double2 *>(a.x + off);
             dot.x += xx.x * acc.x;
             dot.y += xx.y * acc.y;
@@ -1369,7 +1372,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_dot(const double *part, int T, 
 // One thread per (carry, column); the first carry of each row's run sums the run.
 __global__ void k_fixup(const int *__restrict__ carry_tiles, const int *__restrict__ carry_rows, int nc,
                         const double *__restrict__ carry_val, double *__restrict__ Y, int L,
-                        const CgControl *ctrl)
+                        const CgControl *ctrl, int ld)
 {
     if (ctrl && ctrl->done)
         return;
@@ -1383,7 +1386,7 @@ __global__ void k_fixup(const int *__restrict__ carry_tiles, const int *__restri
     double sum = carry_val[(size_t)carry_tiles[i] * L + j];
     for (int u = i + 1; u < nc && carry_rows[u] == R; ++u)
         sum += carry_val[(size_t)carry_tiles[u] * L + j];
-    Y[(size_t)R * L + j] = sum + Y[(size_t)R * L + j];
+    Y[(size_t)R * ld + j] = sum + Y[(size_t)R * ld + j];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1967,6 +1970,7 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
         a.colbase = plan.d_colbase;
         a.cols16 = plan.d_cols16;
     }
+    a.ld = L;
     return a;
 }
 
@@ -2069,30 +2073,62 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_c
     return hipGetLastError();
 }
 
-hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L)
+hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
+                                 int ld)
 {
     if (plan.num_tiles == 0)
         return hipSuccess;
-    return launch_tile<kModeSpmv>(make_args(h, plan, d_X, d_Y, L), L, h->stream, h->num_cus, stream_nt(h));
+    TileArgs a = make_args(h, plan, d_X, d_Y, L);
+    if (ld > 0)
+        a.ld = ld;
+    return launch_tile<kModeSpmv>(a, L, h->stream, h->num_cus, stream_nt(h));
 }
 
-hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L)
+hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L, int ld)
 {
+    if (ld <= 0)
+        ld = L;
     if (plan.num_carries == 0)
         return hipSuccess;
     const int n = plan.num_carries * L;
     hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, h->stream, plan.d_carry_tiles,
-                       plan.d_carry_rows, plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)nullptr);
+                       plan.d_carry_rows, plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)nullptr, ld);
+    return hipGetLastError();
+}
+
+// Column block copy between row-major panels: dst[i][j] = (j < cols ? src[i][j] : 0) for
+// j < dcols (dcols > cols: the zero column of an odd-L panel padded to even width).  Gathers a
+// column group out of a wider panel, scatters it back, pads and unpads.
+__global__ void k_panel_copy(const double *__restrict__ src, int lds, double *__restrict__ dst, int ldd,
+                             long long rows, int cols, int dcols)
+{
+    const long long total = rows * dcols;
+    for (long long e = blockIdx.x * (long long)blockDim.x + threadIdx.x; e < total;
+         e += (long long)gridDim.x * blockDim.x) {
+        const long long i = e / dcols;
+        const int j = (int)(e - i * dcols);
+        dst[i * ldd + j] = j < cols ? src[i * lds + j] : 0.0;
+    }
+}
+
+hipError_t launch_panel_copy(const double *src, int lds, double *dst, int ldd, long long rows, int cols, int dcols,
+                             hipStream_t s)
+{
+    const long long total = rows * dcols;
+    if (total <= 0)
+        return hipSuccess;
+    const long long b = std::min<long long>((total + kBlock - 1) / kBlock, 8192);
+    hipLaunchKernelGGL(k_panel_copy, dim3((unsigned)b), dim3(kBlock), 0, s, src, lds, dst, ldd, rows, cols, dcols);
     return hipGetLastError();
 }
 
 hipError_t launch_spmm(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
-                       int *kernels_launched)
+                       int *kernels_launched, int ld)
 {
-    hipError_t e = launch_spmm_tile_only(h, plan, d_X, d_Y, L);
+    hipError_t e = launch_spmm_tile_only(h, plan, d_X, d_Y, L, ld);
     if (e != hipSuccess)
         return e;
-    e = launch_fixup(h, plan, d_Y, L);
+    e = launch_fixup(h, plan, d_Y, L, ld);
     if (kernels_launched)
         *kernels_launched = (plan.num_tiles ? 1 : 0) + (plan.num_carries ? 1 : 0);
     return e;
@@ -2308,7 +2344,7 @@ static hipError_t launch_fixup_ctrl(mspmv_handle_s *h, const TilePlan &plan, dou
         return hipSuccess;
     const int n = plan.num_carries * L;
     hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, h->stream, plan.d_carry_tiles, plan.d_carry_rows,
-                       plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)h->d_ctrl);
+                       plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)h->d_ctrl, L);
     return hipGetLastError();
 }
 
@@ -2450,7 +2486,7 @@ hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double
     if (plan.num_carries) {
         const int n = plan.num_carries * L;
         hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, h->stream, plan.d_carry_tiles,
-                           plan.d_carry_rows, plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)ctrl);
+                           plan.d_carry_rows, plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)ctrl, L);
         if ((e = hipGetLastError()) != hipSuccess)
             return e;
     }

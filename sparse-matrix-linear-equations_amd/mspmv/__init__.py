@@ -30,7 +30,8 @@ SIMPLE, MERGE, NONZERO_SPLIT = 0, 1, 2  # SpmmKernel, work_2025/types.hpp:11-16
 STATUS = {
     0: "OK", 1: "INVALID", 2: "HIP", 3: "OOM", 4: "BREAKDOWN", 5: "RCCL", 6: "UNSUPPORTED", 7: "IO",
 }
-SUPPORTED_L = (1, 2, 4, 8, 16)
+SUPPORTED_L = (1, 2, 4, 8, 16)  # native tile-kernel widths; SpMM and the CGs take any L >= 1
+# (column chunks / groups of these widths; the sharded CG and the timing helpers native only)
 
 
 class MspmvError(RuntimeError):

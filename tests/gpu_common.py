@@ -71,3 +71,24 @@ def check_parity(a, y_gpu, y_seq, X, plan, L):
     assert bad.size == 0, f"{len(bad)} entries exceed the reordering bound, e.g. row {bad[:3]}"
     assert np.all(np.isfinite(y_gpu) == np.isfinite(y_seq))
     return int(mask.sum()), a.num_rows
+
+
+def chunk_widths(L):
+    """Column chunks mspmv_dspmm runs for a width outside {1, 2, 4, 8, 16} (mspmv_api.hip
+    spmm_chunks): odd L > 1 padded to L + 1, then 16, 8, 4, 2 greedily; [(offset, width)]."""
+    Lp = L + 1 if L > 1 and L % 2 else L
+    out, c0 = [], 0
+    while c0 < Lp:
+        w = 16
+        while w > Lp - c0:
+            w //= 2
+        out.append((c0, w))
+        c0 += w
+    return out
+
+
+def check_parity_chunked(a, g, Y, Yseq, X, L):
+    """check_parity per column chunk, each against its own width's tile plan."""
+    for c0, w in chunk_widths(L):
+        c1 = min(c0 + w, L)
+        check_parity(a, Y[:, c0:c1], Yseq[:, c0:c1], X[:, c0:c1], g.tile_plan(w), w)

@@ -82,6 +82,27 @@ def test_cg_multi_vs_oracle(orc, L):
     assert np.linalg.norm(Xg - Xo) <= 1e-8 * np.linalg.norm(Xo)
 
 
+@pytest.mark.parametrize("L", [3, 32])
+def test_cg_multi_any_width_vs_oracle(orc, L):
+    """num_vectors outside {1, 2, 4, 8, 16} (preconditioner_benchmark.cpp:401 runs 32): column
+    groups of native widths; iteration count, max-over-all-columns history and X as the oracle's
+    single L-wide solve."""
+    a = spd_cases()["fem2d"]()
+    n = a.num_rows
+    flat = orc.glibc_rand(42, n * L)
+    B = flat.reshape(n, L)
+    tol = orc.calculate_threshold(flat, n, 1e-5)
+    Xo, it_o, ho = orc.cg_multi(a, B, 5000, tol, kernel=1, P=8, hist_cap=5000)
+    with mspmv.GpuCsr(a) as g:
+        Xg, it_g, hg, st = g.cg_multi(B, 5000, tol, hist_cap=5000)
+    assert st == 0
+    assert iter_match(it_g, it_o, ho, tol), (it_g, it_o)
+    k = min(len(hg), len(ho))
+    np.testing.assert_allclose(hg[:k], ho[:k], rtol=0, atol=1e-10)
+    for j in range(L):
+        assert np.linalg.norm(Xg[:, j] - Xo[:, j]) <= 1e-8 * np.linalg.norm(Xo[:, j])
+
+
 def test_cg_multi_masks_columns_converge_at_different_iterations(orc):
     """Columns of very different difficulty: converged columns freeze (alpha = beta = 0)
     while the rest continue (no_pretreatment.hpp:109-120, 163-176)."""

@@ -44,7 +44,7 @@ def test_spmv_cli_market(tmp_path):
         f.write(f"{a.num_rows} {a.num_cols} {a.num_nonzeros}\n")
         rows = np.repeat(np.arange(a.num_rows), np.diff(a.row_offsets))
         for r, c, v in zip(rows, a.column_indices, a.values):
-            f.write(f"{r + 1} {c + 1} {v!r}\n")
+            f.write(f"{r + 1} {c + 1} {float(v)!r}\n")
     r = run("mspmv_spmv", f"--mtx={p}", "--i=20")
     assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr
     out = tmp_path / "g.csv"
@@ -58,3 +58,26 @@ def test_spmv_cli_market(tmp_path):
     assert r.returncode == 0 and "Min time" in r.stdout, r.stdout + r.stderr
     lines = open(out2).read().strip().splitlines()
     assert lines[0] == "iteration,max_error" and len(lines) > 2
+
+
+def test_precond_cli(tmp_path):
+    """preconditioner_benchmark.cpp's CSV: NONE / IC0 / SPAI rows, the preconditioned solves
+    converging in fewer iterations on an SPD stencil; num_vectors 32 (the reference's default,
+    column groups of 16)."""
+    a = mspmv.CsrMatrix.synth_stencil(0, 2500, 50)
+    p = tmp_path / "spd.mtx"
+    with open(p, "w") as f:
+        f.write("%%MatrixMarket matrix coordinate real general\n")
+        f.write(f"{a.num_rows} {a.num_cols} {a.num_nonzeros}\n")
+        rows = np.repeat(np.arange(a.num_rows), np.diff(a.row_offsets))
+        for r, c, v in zip(rows, a.column_indices, a.values):
+            f.write(f"{r + 1} {c + 1} {float(v)!r}\n")
+    r = run("mspmv_precond", f"--mtx={p}", f"--output_dir={tmp_path}", "--timing_iters=2")
+    assert r.returncode == 0 and "All benchmarks completed." in r.stdout, r.stdout + r.stderr
+    head, *rows = open(tmp_path / "spd_prepare.csv").read().strip().splitlines()
+    assert head == "PREPARE_TYPE,preprocess_ms,solve_ms,total_ms,gflops,iterations"
+    got = {f[0]: f for f in (row.split(",") for row in rows)}
+    assert list(got) == ["NONE", "IC0", "SPAI"]
+    its = {k: int(v[5]) for k, v in got.items()}
+    assert all(v > 0 for v in its.values()) and its["IC0"] < its["NONE"] and its["SPAI"] < its["NONE"], its
+    assert float(got["IC0"][1]) > 0 and float(got["NONE"][1]) == 0.0

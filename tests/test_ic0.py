@@ -67,7 +67,7 @@ def _iter_match(it_g, it_o, hist_o, tol):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", list(spd_small()))
-@pytest.mark.parametrize("L", [1, 4, 8])
+@pytest.mark.parametrize("L", [1, 4, 8, 32])
 def test_gpu_pcg_ic0_vs_oracle(gpu_available, orc, name, L):
     a = spd_small()[name]()
     l, _ = mspmv.ic0_factor(a)

@@ -48,7 +48,7 @@ def test_market_duplicates_and_order(tmp_path, orc):
     with open(p, "w") as f:
         f.write("%%MatrixMarket matrix coordinate real general\n% random with duplicates\n40 30 500\n")
         for r, c, v in zip(rows, cols, vals):
-            f.write(f"{r} {c} {v!r}\n")
+            f.write(f"{r} {c} {float(v)!r}\n")
     a = mspmv.CsrMatrix.from_market(str(p))
     rc, b = orc.read_market(str(p))
     assert rc == 0
