@@ -31,6 +31,7 @@ import ctypes
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -247,6 +248,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-cg", action="store_true")
+    ap.add_argument("--cg-timeout", type=float, default=300.0,
+                    help="N > 1: seconds allowed for the sharded CG before the headline prints without it")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the hot-matrix and scatter-band side measurements (profiling runs: the "
                          "headline kernel's rocprofv3 average then covers exactly the timed launches)")
@@ -254,6 +257,8 @@ def main():
 
     d = Dist(args.gpus)
     dev = d.local
+    if os.environ.get("MSPMV_BENCH_SHARE_DEVICE") == "1":  # rehearsal of N > 1 on a one-GPU box
+        dev = d.local % max(mspmv.device_count(), 1)
     if mspmv.device_count() <= dev:
         raise SystemExit(f"rank {d.rank}: no HIP device {dev}")
 
@@ -340,6 +345,24 @@ def main():
         result["cpu_baseline"]["gpu_vs_cpu_max_rel_diff"] = rel
         result["speedup_vs_cpu"] = round(value / cb["value"], 1)
     if not args.no_cg:
+        # The sharded CG (N > 1) has only ever run in the driver's multi-GPU bench: if its RCCL
+        # exchange hangs (or one rank fails while the others wait in a collective), the headline
+        # line must still print -- rank 0 prints what it has and every rank exits.
+        cg_lock, cg_state = threading.Lock(), {"done": False}
+
+        def _cg_watchdog():
+            with cg_lock:
+                if cg_state["done"]:
+                    return
+            if d.rank == 0:
+                result["cg_error"] = f"sharded CG did not finish within {args.cg_timeout:.0f} s"
+                print(json.dumps(result), flush=True)
+            sys.stderr.flush()
+            os._exit(0)
+        watchdog = threading.Timer(args.cg_timeout, _cg_watchdog) if d.world > 1 else None
+        if watchdog:
+            watchdog.daemon = True
+            watchdog.start()
         try:
             if d.world == 1:
                 result["cg_single"] = run_cg_single(dev, min(args.cpu_seconds, 10.0), not args.no_cpu)
@@ -348,6 +371,10 @@ def main():
                 result["spmv_nlpkkt120_size"] = large
         except Exception as e:  # the headline line must still print
             result["cg_error"] = repr(e)[:300]
+        with cg_lock:
+            cg_state["done"] = True
+        if watchdog:
+            watchdog.cancel()
 
     if d.rank == 0:
         print(json.dumps(result), flush=True)
