@@ -826,6 +826,10 @@ __device__ __forceinline__ void cg1_publish(const TileArgs &a, SpmvSmem<IPT> &sm
 // (UpdatePSingle, single_strategy.hpp:89-97, fused into the SpMV), writes p for its rows, Ap, and
 // p.Ap by linearity.  TB = 64 (one-wave workgroups, SpMV only): every wave owns its tile, so no
 // workgroup barrier ties a wave's progress to its siblings' gather latencies.
+#if MSPMV_LAB_ABLATE == 9  // lab build only (tools/lab/stamps.py): per-tile phase stamps
+constexpr int kLabStampTiles = 1 << 17;
+__device__ unsigned long long g_lab_stamps[kLabStampTiles * 6];
+#endif
 template <int IPT, int MODE, bool NT, int TB = kBlock>
 __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
 {
@@ -835,6 +839,9 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
     constexpr int MAXJ = SpmvSmem<IPT, TB>::MAXJ;
     __shared__ SpmvSmem<IPT, TB> sm;
     const int tid = threadIdx.x;
+#if MSPMV_LAB_ABLATE == 9
+    const unsigned long long lab_t0 = wall_clock64();
+#endif
     // CG: stop flag loaded now, tested after the stream and gathers are issued (see k_spmm_tile)
     const int stopped = MODE != kModeSpmv ? a.ctrl->done : 0;
     const int t = xcd_tile(blockIdx.x, a.num_tiles);
@@ -876,14 +883,33 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
         return;
     // Row ends after the staging: measured faster here than issuing them with the stream
     // (+0.9 us on the pwtk shape), unlike the multi-RHS kernel.
+#if MSPMV_LAB_ABLATE == 9
+    __syncthreads();
+    const unsigned long long lab_t1 = wall_clock64();
+#endif
     int *rend = sm.rowend(nnzt);
     for (int i = tid; i < nrows; i += TB)
         rend[i] = a.row_offsets[r0 + 1 + i] - n0;
     tile_sync<TB>();
+#if MSPMV_LAB_ABLATE == 9
+    const unsigned long long lab_t2 = wall_clock64();
+#endif
     double dot = 0.0;
     double xr, pr;
     row_operands<MODE>(a, r0, nrows, xr, pr);
     reduce_tile<IPT, MODE, TB>(a, sm, t, r0, n0, nrows, nnzt, a.rmode[t], a.split[t + 1] != 0, beta, dot, xr, pr);
+#if MSPMV_LAB_ABLATE == 9
+    __syncthreads();
+    if (tid == 0 && MODE == kModeSpmv && t < kLabStampTiles) {
+        unsigned long long *o = g_lab_stamps + (size_t)t * 6;
+        o[0] = lab_t0;
+        o[1] = lab_t1;
+        o[2] = lab_t2;
+        o[3] = wall_clock64();
+        o[4] = (unsigned long long)__smid();
+        o[5] = (unsigned long long)blockIdx.x;
+    }
+#endif
     if constexpr (MODE == kModeCg)
         cg1_publish<IPT>(a, sm, t, a.num_tiles, dot);
     else if constexpr (MODE == kModeDot)
@@ -2706,3 +2732,10 @@ hipError_t launch_pcg_ic0_iteration(mspmv_handle_s *h, mspmv_ic0_s *ic, const Ti
 }
 
 }  // namespace mspmv
+
+#if MSPMV_LAB_ABLATE == 9
+extern "C" __attribute__((visibility("default"))) int mspmv_lab_stamps(unsigned long long *host, int tiles)
+{
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mspmv::g_lab_stamps), sizeof(unsigned long long) * 6 * tiles);
+}
+#endif

@@ -1,3 +1,11 @@
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_gpu_dist.py -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread -rs > gpurun_out/tdist.log 2>&1; rc=$?; tail -6 gpurun_out/tdist.log; [ $rc -le 1 ] || exit $rc
-MSPMV_BENCH_SHARE_DEVICE=1 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu --no-extras --cg-timeout 150 > gpurun_out/b2.json 2> gpurun_out/b2.err; rc=$?; echo "bench2 rc=$rc"; cat gpurun_out/b2.json; tail -20 gpurun_out/b2.err; exit $rc
+for r in 1 2; do for v in base prod abl10; do
+  lib=tools/lab/libmspmv_$v.so; [ $v = prod ] && lib=sparse-matrix-linear-equations_amd/mspmv/libmspmv.so
+  echo "fem $v $(MSPMV_LIB=$lib timeout -k 10 200 python tools/spmv_sweep.py --child | cut -c 150-330)" || exit 1
+done; done
+for v in base prod abl10; do
+  lib=tools/lab/libmspmv_$v.so; [ $v = prod ] && lib=sparse-matrix-linear-equations_amd/mspmv/libmspmv.so
+  echo "nlp $v $(MSPMV_LIB=$lib SWEEP_SHAPE=nlpkkt SWEEP_L=1 SWEEP_BATCH=1 timeout -k 10 200 python tools/spmv_sweep.py --child | cut -c 150-330)" || exit 1
+  echo "cg1 $v $(MSPMV_LIB=$lib timeout -k 10 200 python tools/cg_probe.py --child 2>&1 | tail -1 | cut -c 1-300)" || exit 1
+done
+MSPMV_LIB=tools/lab/libmspmv_abl9.so timeout -k 10 200 python tools/lab/stamps.py > gpurun_out/stamps_fem2.json
