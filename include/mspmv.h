@@ -212,6 +212,11 @@ MSPMV_API mspmv_status mspmv_last_kernel_ms(mspmv_handle h, double *tile_kernel_
  * bit-identical to SpmvGold). */
 MSPMV_API mspmv_status mspmv_tile_plan(mspmv_handle h, int L, int *num_tiles, int *tile_items, int *num_carries,
                                        mspmv_coord *bounds);
+/* Single-RHS plan: how many tiles stream 16-bit column offsets (*tiles_cols16) and how many
+ * gather x through a per-tile column dictionary (*tiles_dict: tiles whose scattered columns
+ * make direct gathers line-bound; the sorted distinct columns are gathered once into LDS).
+ * Either output may be null. */
+MSPMV_API mspmv_status mspmv_tile_streams(mspmv_handle h, int *tiles_cols16, int *tiles_dict);
 /* Each tile's in-tile reduction for L right-hand sides (num_tiles entries): 0 = merge walk
  * (one walker per thread, or per L/2 lanes), g > 0 = row groups with 2^(g-1) nonzero-parallel
  * lanes per row (times L/2 column-pair lanes for L > 1).  g = 1 sums each row sequentially in

@@ -86,6 +86,9 @@ static void free_plan(TilePlan &p)
     dev_free(p.d_carry_val);
     dev_free(p.d_colbase);
     dev_free(p.d_cols16);
+    dev_free(p.d_dict);
+    dev_free(p.d_ndict);
+    dev_free(p.d_idx16);
 }
 
 // Build (once) the tile plan for L right-hand sides, validating on the host every bound the
@@ -224,6 +227,36 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
             dev_free(p.d_cols16);
             p.d_colbase = nullptr;
             p.d_cols16 = nullptr;
+        }
+    }
+    if (tile == tile_items_for(1) && T > 0 && h->nnz > 0 && spmv_dict_enabled()) {
+        if ((st = dev_alloc(&p.d_dict, (size_t)h->nnz + kNnzPad)) != MSPMV_OK ||
+            (st = dev_alloc(&p.d_ndict, (size_t)T)) != MSPMV_OK ||
+            (st = dev_alloc(&p.d_idx16, (size_t)h->nnz + kNnzPad)) != MSPMV_OK)
+            return fail(st);
+        e = hipMemsetAsync(p.d_dict, 0, sizeof(int) * ((size_t)h->nnz + kNnzPad), h->stream);
+        if (e == hipSuccess)
+            e = hipMemsetAsync(p.d_idx16, 0, sizeof(unsigned short) * ((size_t)h->nnz + kNnzPad), h->stream);
+        if (e == hipSuccess)
+            e = launch_build_dict(h->d_cols, p.d_bounds, T, maxi, p.d_dict, p.d_ndict, p.d_idx16, h->stream);
+        std::vector<int> hnd((size_t)T);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(hnd.data(), p.d_ndict, sizeof(int) * T, hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) {
+            set_error(std::string("column dictionaries: ") + hipGetErrorString(e));
+            return fail(MSPMV_ERR_HIP);
+        }
+        for (int v : hnd)
+            p.num_tiles_dict += v > 0;
+        if (p.num_tiles_dict == 0) {  // no tile takes one: drop the arrays, the kernel skips the test
+            dev_free(p.d_dict);
+            dev_free(p.d_ndict);
+            dev_free(p.d_idx16);
+            p.d_dict = nullptr;
+            p.d_ndict = nullptr;
+            p.d_idx16 = nullptr;
         }
     }
     auto res = h->plans.emplace(tile, p);
@@ -1333,6 +1366,18 @@ mspmv_status mspmv_tile_modes(mspmv_handle h, int L, unsigned char *modes)
     ST_TRY(get_plan(h, L, &plan));
     if (plan->num_tiles)
         HIP_TRY(hipMemcpy(modes, plan->d_modes[l_index(L)], plan->num_tiles, hipMemcpyDeviceToHost));
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_tile_streams(mspmv_handle h, int *tiles_cols16, int *tiles_dict)
+{
+    ST_TRY(check_handle(h));
+    const TilePlan *plan = nullptr;
+    ST_TRY(get_plan(h, 1, &plan));
+    if (tiles_cols16)
+        *tiles_cols16 = plan->d_cols16 ? plan->num_tiles16 : 0;
+    if (tiles_dict)
+        *tiles_dict = plan->d_dict ? plan->num_tiles_dict : 0;
     return MSPMV_OK;
 }
 

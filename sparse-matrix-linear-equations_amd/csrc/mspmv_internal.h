@@ -51,6 +51,13 @@ struct TilePlan {
     int *d_colbase = nullptr;           // [num_tiles]
     unsigned short *d_cols16 = nullptr; // [nnz + kNnzPad]
     int num_tiles16 = 0;                // tiles on the 16-bit stream
+    // Single-RHS plans, MSPMV_SPMV_DICT=1: per-tile column dictionaries (k_build_dict).  Tile t's
+    // distinct columns ascending in dict[n0 ..] (ndict[t] of them), each nonzero's position in
+    // that list in idx16[k].  Null when not built.
+    int *d_dict = nullptr;              // [nnz + kNnzPad]
+    int *d_ndict = nullptr;             // [num_tiles]
+    unsigned short *d_idx16 = nullptr;  // [nnz + kNnzPad]
+    int num_tiles_dict = 0;             // tiles that gather through their dictionary
 };
 
 // Device-resident CG scalars (one set per right-hand side column).
@@ -145,6 +152,9 @@ hipError_t launch_snap(const int *d_row_offsets, int m, int2 *d_bounds, unsigned
 hipError_t launch_pack_cols16(const int *d_cols, const int2 *d_bounds, int num_tiles, int *d_colbase,
                               unsigned short *d_cols16, hipStream_t s);
 bool spmv_cols16_enabled();
+bool spmv_dict_enabled();
+hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_tiles, int max_items, int *d_dict,
+                             int *d_ndict, unsigned short *d_idx16, hipStream_t s);
 // y = A x (L == 1) or Y = A X (row-major panels), tile kernel + optional carry fix-up.
 hipError_t launch_spmm(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
                        int *kernels_launched, int ld = 0);

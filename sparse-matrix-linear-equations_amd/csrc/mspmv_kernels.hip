@@ -342,6 +342,114 @@ __global__ __launch_bounds__(kBlock) void k_pack_cols16(const int *__restrict__ 
             cols16[k] = (unsigned short)(cols[k] - base);
 }
 
+// Per-tile column dictionary (plan time, single-RHS plans): one workgroup per
+// tile sorts the tile's column ids in LDS (bitonic, N = power of two >= the tile's nonzeros),
+// keeps the distinct ones in ascending order -> dict[n0 + d], d < ndict[t] (stored in the tile's
+// own nonzero range: ndict <= nnzt), and rewrites every nonzero as its dictionary position ->
+// idx16[k].  The kernel then gathers each distinct x once per tile instead of once per nonzero.
+template <int N>
+__global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ cols, const int2 *__restrict__ bounds,
+                                                       int *__restrict__ dict, int *__restrict__ ndict,
+                                                       unsigned short *__restrict__ idx16, int ratio)
+{
+    __shared__ int keys[N];
+    __shared__ int uniq[N];
+    __shared__ int s_scan[kBlock];
+    const int t = blockIdx.x, tid = threadIdx.x;
+    const int n0 = bounds[t].y, nz = bounds[t + 1].y - n0;
+    for (int i = tid; i < N; i += kBlock)
+        keys[i] = i < nz ? cols[n0 + i] : 0x7fffffff;
+    __syncthreads();
+    for (int k = 2; k <= N; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < N; i += kBlock) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const int a = keys[i], b = keys[ixj];
+                    if ((a > b) == ((i & k) == 0)) {
+                        keys[i] = b;
+                        keys[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    // distinct keys: thread tid scans its contiguous chunk [tid*C, (tid+1)*C)
+    constexpr int C = N / kBlock;
+    int cnt = 0;
+    for (int c = 0; c < C; ++c) {
+        const int i = tid * C + c;
+        cnt += (i < nz && (i == 0 || keys[i] != keys[i - 1])) ? 1 : 0;
+    }
+    s_scan[tid] = cnt;
+    __syncthreads();
+    for (int off = 1; off < kBlock; off <<= 1) {  // inclusive Hillis-Steele scan
+        const int v = tid >= off ? s_scan[tid - off] : 0;
+        __syncthreads();
+        s_scan[tid] += v;
+        __syncthreads();
+    }
+    int pos = s_scan[tid] - cnt;
+    for (int c = 0; c < C; ++c) {
+        const int i = tid * C + c;
+        if (i < nz && (i == 0 || keys[i] != keys[i - 1]))
+            uniq[pos++] = keys[i];
+    }
+    const int nu = s_scan[kBlock - 1];
+    __syncthreads();
+    // Cache lines one gather instruction touches (64 consecutive entries, 16 doubles per 128-B
+    // line), summed over the tile: direct (nonzeros in CSR order, as the kernel stripes them)
+    // vs through the sorted dictionary.  The dictionary is taken only where direct gathers are
+    // line-bound (>= 1 line per 2 nonzeros: scattered columns) and sorting saves >= 1/4 of the
+    // lines; elsewhere (FEM blocks, stencils: ~0.2 lines per nonzero, served by L1/L2) its LDS
+    // round trip measured a wash or a loss, and on random columns (power law) sorting saves
+    // nothing.
+    int ld = 0, lu = 0;
+    for (int c = 0; c < C; ++c) {
+        const int i = tid * C + c;
+        if (i < nz)
+            ld += ((i & 63) == 0 || (cols[n0 + i] >> 4) != (cols[n0 + i - 1] >> 4)) ? 1 : 0;
+        if (i < nu)
+            lu += ((i & 63) == 0 || (uniq[i] >> 4) != (uniq[i - 1] >> 4)) ? 1 : 0;
+    }
+    s_scan[tid] = ld;
+    __syncthreads();
+    for (int off = kBlock / 2; off > 0; off >>= 1) {
+        if (tid < off)
+            s_scan[tid] += s_scan[tid + off];
+        __syncthreads();
+    }
+    const int lines_direct = s_scan[0];
+    __syncthreads();
+    s_scan[tid] = lu;
+    __syncthreads();
+    for (int off = kBlock / 2; off > 0; off >>= 1) {
+        if (tid < off)
+            s_scan[tid] += s_scan[tid + off];
+        __syncthreads();
+    }
+    const int lines_dict = s_scan[0];
+    const bool use = ratio > 0 && nz > 0 && 2 * lines_direct >= nz && 4 * lines_dict <= 3 * lines_direct;
+    if (tid == 0)
+        ndict[t] = use ? nu : 0;
+    if (!use)
+        return;
+    for (int d = tid; d < nu; d += kBlock)
+        dict[n0 + d] = uniq[d];
+    for (int i = tid; i < nz; i += kBlock) {
+        const int c = cols[n0 + i];
+        int lo = 0, hi = nu - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (uniq[mid] < c)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        idx16[n0 + i] = (unsigned short)lo;
+    }
+}
+
 // Per-tile choice of the in-tile reduction (one thread per tile, at plan time; gl = lanes per
 // nonzero: 1 for SpMV, L/2 column-pair lanes for SpMM).  The tile's row segments -- its complete rows plus the trailing partial row of a
 // split boundary -- are either summed by row groups of G = 2^lg lanes (mode lg + 1) or, when
@@ -419,6 +527,10 @@ struct TileArgs {
     // single-RHS plans: per-tile 16-bit column offsets (TilePlan::d_colbase / d_cols16; null: off)
     const int *colbase;
     const unsigned short *cols16;
+    // single-RHS plans with column dictionaries (TilePlan::d_dict; null: off)
+    const int *dict;
+    const int *ndict;
+    const unsigned short *idx16;
     // SpMM: leading dimension of the x / y panels in doubles (L for whole panels; a column
     // chunk of a wider panel otherwise, mspmv_dspmm with L outside {1, 2, 4, 8, 16})
     int ld;
@@ -507,6 +619,52 @@ __device__ __forceinline__ void stage_products(const TileArgs &a, int n0, int nn
     StageRegs<NJ, CG> st;
     stage_issue<NJ, CG, NT>(a, n0, nnzt, -1, st);
     stage_store<NJ, CG>(st, nnzt, beta, s_prod);
+}
+
+// Dictionary staging (plain SpMV, plans built with MSPMV_SPMV_DICT=1): the tile's distinct
+// columns are gathered once each (DJ per thread in flight, clamped), parked in LDS, and every
+// nonzero's product reads its x there through its 16-bit dictionary position.  The products are
+// the same values as the direct path (val * x[col]), so results are bit-identical to it.
+template <int NJ, bool NT, int TB>
+__device__ __forceinline__ void dict_stage(const TileArgs &a, double *s_prod, int nd, int n0, int nnzt)
+{
+    constexpr int DJ = 3;
+    const int tid = threadIdx.x;
+    int ix[NJ];
+    double v[NJ];
+    int dc[DJ];
+    double dx[DJ];
+#pragma unroll
+    for (int u = 0; u < DJ; ++u)
+        dc[u] = ld_stream<NT>(a.dict + n0 + min(tid + u * TB, nd - 1));
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+        ix[j] = ld_stream<NT>(a.idx16 + n0 + min(tid + j * TB, nnzt - 1));
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+        v[j] = ld_stream<NT>(a.vals + n0 + min(tid + j * TB, nnzt - 1));
+#pragma unroll
+    for (int u = 0; u < DJ; ++u)
+        dx[u] = a.x[dc[u]];
+    double *s_x = s_prod;  // nd <= nnzt: the dictionary's x fits the product slots
+#pragma unroll
+    for (int u = 0; u < DJ; ++u)
+        if (tid + u * TB < nd)
+            s_x[tid + u * TB] = dx[u];
+    for (int d = tid + DJ * TB; d < nd; d += TB)  // rare: > DJ * TB distinct columns
+        s_x[d] = a.x[a.dict[n0 + d]];
+    tile_sync<TB>();
+    double pr[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+        pr[j] = v[j] * s_x[ix[j]];
+    tile_sync<TB>();
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int k = tid + j * TB;
+        if (k < nnzt)
+            s_prod[pslot(k)] = pr[j];
+    }
 }
 
 // Per-tile LDS of the single-RHS kernels.  Products and row ends share one buffer: a tile
@@ -864,7 +1022,19 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
             go = cg1_head(a, part_sum(pin, sm.red), beta);
     };
     const int colbase = a.cols16 ? a.colbase[t] : -1;
-    if (nnzt > 0 && nnzt <= TILE) {  // the common case: no snapped-in extra nonzeros
+    bool staged = false;
+    if constexpr (MODE == kModeSpmv) {
+        const int nd = a.dict ? a.ndict[t] : 0;  // > 0: this tile gathers through its dictionary
+        if (nd > 0) {
+            if (nnzt <= TILE)
+                dict_stage<IPT, NT, TB>(a, sm.prod, nd, n0, nnzt);
+            else
+                dict_stage<MAXJ, NT, TB>(a, sm.prod, nd, n0, nnzt);
+            staged = true;
+        }
+    }
+    if (staged) {
+    } else if (nnzt > 0 && nnzt <= TILE) {  // the common case: no snapped-in extra nonzeros
         StageRegs<IPT, CG> st;
         stage_issue<IPT, CG, NT, TB>(a, n0, nnzt, colbase, st);
         head();
@@ -1868,6 +2038,8 @@ struct SpmvTuning {
     int spmm_rg_cost = -1;  // the same for the multi-RHS kernels (-1: scaled to the SpMM tile)
     int cols16 = 1;   // single-RHS plans carry 16-bit column offsets where a tile's span allows
     int tb = 256;     // threads per single-RHS SpMV tile: 256 (workgroup tiles) or 64 (one-wave tiles)
+    int dict = 1;     // single-RHS SpMV through per-tile column dictionaries (k_build_dict) when
+                      // a tile's nonzeros repeat its distinct columns >= dict_ratio times (0: off)
 };
 static const SpmvTuning &spmv_tuning()
 {
@@ -1895,6 +2067,8 @@ static const SpmvTuning &spmv_tuning()
             v.spmm_rg_cost = atoi(e);
         if (const char *e = getenv("MSPMV_SPMV_C16"))
             v.cols16 = atoi(e) != 0;
+        if (const char *e = getenv("MSPMV_SPMV_DICT"))
+            v.dict = atoi(e) > 0 ? atoi(e) : 0;
         if (const char *e = getenv("MSPMV_SPMV_TB"))
             v.tb = atoi(e) == 64 ? 64 : 256;
         return v;
@@ -1954,6 +2128,21 @@ hipError_t launch_pack_cols16(const int *d_cols, const int2 *d_bounds, int num_t
 }
 
 bool spmv_cols16_enabled() { return spmv_tuning().cols16 != 0; }
+bool spmv_dict_enabled() { return spmv_tuning().dict > 0; }
+
+hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_tiles, int max_items, int *d_dict,
+                             int *d_ndict, unsigned short *d_idx16, hipStream_t s)
+{
+    if (max_items <= 4096)
+        hipLaunchKernelGGL(k_build_dict<4096>, dim3(num_tiles), dim3(kBlock), 0, s, d_cols, d_bounds, d_dict, d_ndict,
+                           d_idx16, spmv_tuning().dict);
+    else if (max_items <= 8192)
+        hipLaunchKernelGGL(k_build_dict<8192>, dim3(num_tiles), dim3(kBlock), 0, s, d_cols, d_bounds, d_dict, d_ndict,
+                           d_idx16, spmv_tuning().dict);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
 
 hipError_t launch_snap(const int *d_row_offsets, int m, int2 *d_bounds, unsigned char *d_split, int num_tiles,
                        int snap, hipStream_t s)
@@ -1995,6 +2184,9 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
     if (L == 1) {
         a.colbase = plan.d_colbase;
         a.cols16 = plan.d_cols16;
+        a.dict = plan.d_dict;
+        a.ndict = plan.d_ndict;
+        a.idx16 = plan.d_idx16;
     }
     a.ld = L;
     return a;

@@ -96,6 +96,7 @@ _SIGS = {
     "mspmv_time_spmm_batch_dev": (_I, [_I, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _I,
                                        _PD, _PD, _PI]),
     "mspmv_tile_plan": (_I, [_P, _I, _PI, _PI, _PI, ctypes.POINTER(Coord)]),
+    "mspmv_tile_streams": (_I, [_P, _PI, _PI]),
     "mspmv_tile_modes": (_I, [_P, _I, _P]),
     "mspmv_spmv_kernel_name": (ctypes.c_char_p, [_P]),
     "mspmv_device_malloc": (_I, [_I, _SZ, ctypes.POINTER(_P)]),
@@ -352,6 +353,12 @@ class GpuCsr:
         _check(lib.mspmv_tile_modes(self.h, L, _ptr(modes)), "tile_modes")
         return {"num_tiles": nt.value, "tile_items": ti.value, "num_carries": nc.value, "bounds": bounds,
                 "modes": modes[: nt.value]}
+
+    def tile_streams(self):
+        """(tiles on 16-bit column offsets, tiles gathering through column dictionaries)."""
+        c16, dic = ctypes.c_int(), ctypes.c_int()
+        _check(lib.mspmv_tile_streams(self.h, ctypes.byref(c16), ctypes.byref(dic)), "tile_streams")
+        return c16.value, dic.value
 
     def kernel_name(self) -> str:
         """The single-RHS SpMV kernel instantiation used for this matrix (rocprofv3's name)."""

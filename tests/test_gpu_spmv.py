@@ -145,6 +145,20 @@ def test_spmm_any_width(orc, name, L):
         check_parity_chunked(a, g, Y, orc.csr_spmm_t(a, X), X, L)
 
 
+def test_column_dictionary_tiles(orc):
+    """Scattered-band tiles gather x through sorted per-tile column dictionaries (k_build_dict);
+    FEM / stencil tiles keep the direct gathers (power-law tiles: either, by their line counts).
+    Either way the products are val * x[col]: unsplit rows bit-identical to SpmvGold."""
+    cases = synth_cases()
+    for name, want in (("cant_small", True), ("fem2d", False), ("stencil27", False), ("powerlaw", None)):
+        a = cases[name]()
+        x = np.random.default_rng(4).uniform(-1, 1, a.num_cols)
+        with mspmv.GpuCsr(a) as g:
+            _, nd = g.tile_streams()
+            assert want is None or (nd > 0) == want, (name, nd)
+            check_parity(a, g.spmv(x), orc.spmv_gold(a, x), x, g.tile_plan(1), 1)
+
+
 def test_deterministic_repeat():
     a = mspmv.CsrMatrix.synth_powerlaw(30000, 30000, 900000, exponent=1.4, seed=9)
     x = np.random.default_rng(1).uniform(-1, 1, a.num_cols)

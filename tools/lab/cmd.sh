@@ -1,11 +1,5 @@
 set -o pipefail
-for r in 1 2; do for v in base prod abl10; do
-  lib=tools/lab/libmspmv_$v.so; [ $v = prod ] && lib=sparse-matrix-linear-equations_amd/mspmv/libmspmv.so
-  echo "fem $v $(MSPMV_LIB=$lib timeout -k 10 200 python tools/spmv_sweep.py --child | cut -c 150-330)" || exit 1
-done; done
-for v in base prod abl10; do
-  lib=tools/lab/libmspmv_$v.so; [ $v = prod ] && lib=sparse-matrix-linear-equations_amd/mspmv/libmspmv.so
-  echo "nlp $v $(MSPMV_LIB=$lib SWEEP_SHAPE=nlpkkt SWEEP_L=1 SWEEP_BATCH=1 timeout -k 10 200 python tools/spmv_sweep.py --child | cut -c 150-330)" || exit 1
-  echo "cg1 $v $(MSPMV_LIB=$lib timeout -k 10 200 python tools/cg_probe.py --child 2>&1 | tail -1 | cut -c 1-300)" || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_gpu_spmv.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/tdict.log 2>&1; rc=$?; tail -4 gpurun_out/tdict.log; [ $rc -eq 0 ] || exit $rc
+for d in 0 1; do
+  echo "band dict=$d $(MSPMV_SPMV_DICT=$d SWEEP_SHAPE=band SWEEP_BATCH=2 timeout -k 10 200 python tools/spmv_sweep.py --child | cut -c 180-330)" || exit 1
 done
-MSPMV_LIB=tools/lab/libmspmv_abl9.so timeout -k 10 200 python tools/lab/stamps.py > gpurun_out/stamps_fem2.json
