@@ -357,6 +357,30 @@ __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ c
     __shared__ int s_scan[kBlock];
     const int t = blockIdx.x, tid = threadIdx.x;
     const int n0 = bounds[t].y, nz = bounds[t + 1].y - n0;
+    // Cache lines one gather instruction touches (64 consecutive entries, 16 doubles per 128-B
+    // line), summed over the tile: first direct (nonzeros in CSR order, as the kernel stripes
+    // them); a tile below 1 line per 2 nonzeros keeps direct gathers and skips the sort.
+    constexpr int C = N / kBlock;
+    int ld = 0;
+    for (int c = 0; c < C; ++c) {
+        const int i = tid * C + c;
+        if (i < nz)
+            ld += ((i & 63) == 0 || (cols[n0 + i] >> 4) != (cols[n0 + i - 1] >> 4)) ? 1 : 0;
+    }
+    s_scan[tid] = ld;
+    __syncthreads();
+    for (int off = kBlock / 2; off > 0; off >>= 1) {
+        if (tid < off)
+            s_scan[tid] += s_scan[tid + off];
+        __syncthreads();
+    }
+    const int lines_direct = s_scan[0];
+    if (ratio <= 0 || nz == 0 || 2 * lines_direct < nz) {
+        if (tid == 0)
+            ndict[t] = 0;
+        return;
+    }
+    __syncthreads();
     for (int i = tid; i < N; i += kBlock)
         keys[i] = i < nz ? cols[n0 + i] : 0x7fffffff;
     __syncthreads();
@@ -375,7 +399,6 @@ __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ c
             __syncthreads();
         }
     // distinct keys: thread tid scans its contiguous chunk [tid*C, (tid+1)*C)
-    constexpr int C = N / kBlock;
     int cnt = 0;
     for (int c = 0; c < C; ++c) {
         const int i = tid * C + c;
@@ -397,30 +420,16 @@ __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ c
     }
     const int nu = s_scan[kBlock - 1];
     __syncthreads();
-    // Cache lines one gather instruction touches (64 consecutive entries, 16 doubles per 128-B
-    // line), summed over the tile: direct (nonzeros in CSR order, as the kernel stripes them)
-    // vs through the sorted dictionary.  The dictionary is taken only where direct gathers are
-    // line-bound (>= 1 line per 2 nonzeros: scattered columns) and sorting saves >= 1/4 of the
-    // lines; elsewhere (FEM blocks, stencils: ~0.2 lines per nonzero, served by L1/L2) its LDS
-    // round trip measured a wash or a loss, and on random columns (power law) sorting saves
-    // nothing.
-    int ld = 0, lu = 0;
+    // ... then through the sorted dictionary.  The dictionary is taken only where direct gathers
+    // are line-bound (>= 1 line per 2 nonzeros: scattered columns) and sorting saves >= 1/4 of
+    // the lines; elsewhere (FEM blocks, stencils: ~0.2 lines per nonzero, served by L1/L2) its
+    // LDS round trip measured a wash or a loss, and on random columns sorting saves nothing.
+    int lu = 0;
     for (int c = 0; c < C; ++c) {
         const int i = tid * C + c;
-        if (i < nz)
-            ld += ((i & 63) == 0 || (cols[n0 + i] >> 4) != (cols[n0 + i - 1] >> 4)) ? 1 : 0;
         if (i < nu)
             lu += ((i & 63) == 0 || (uniq[i] >> 4) != (uniq[i - 1] >> 4)) ? 1 : 0;
     }
-    s_scan[tid] = ld;
-    __syncthreads();
-    for (int off = kBlock / 2; off > 0; off >>= 1) {
-        if (tid < off)
-            s_scan[tid] += s_scan[tid + off];
-        __syncthreads();
-    }
-    const int lines_direct = s_scan[0];
-    __syncthreads();
     s_scan[tid] = lu;
     __syncthreads();
     for (int off = kBlock / 2; off > 0; off >>= 1) {
@@ -429,7 +438,7 @@ __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ c
         __syncthreads();
     }
     const int lines_dict = s_scan[0];
-    const bool use = ratio > 0 && nz > 0 && 2 * lines_direct >= nz && 4 * lines_dict <= 3 * lines_direct;
+    const bool use = 4 * lines_dict <= 3 * lines_direct;
     if (tid == 0)
         ndict[t] = use ? nu : 0;
     if (!use)
