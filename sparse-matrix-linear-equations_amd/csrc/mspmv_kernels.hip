@@ -1931,6 +1931,72 @@ __global__ __launch_bounds__(kBlock) void k_trsv(const int *__restrict__ ro, con
     }
 }
 
+// The same solve with data-tagged values instead of flags: the output starts filled with a NaN
+// pattern no arithmetic produces (kTrsvPending, written by one 32-bit fill), a row's x values are
+// stored by single 8-B write-through stores, and a consumer lane polls the very value it needs
+// until the pattern is gone -- one memory round trip per dependency hop instead of flag, drain
+// and payload.  Bounded like wait_flag (a stall is reported, never hung).
+constexpr unsigned kTrsvPendingWord = 0x7ff4deadu;
+constexpr unsigned long long kTrsvPending = 0x7ff4dead7ff4deadull;
+
+__device__ __forceinline__ bool wait_value(const double *p, double &out)
+{
+    for (int it = 0; it < (1 << 20); ++it) {
+        const double v = load_sc1(p);
+        if ((unsigned long long)__double_as_longlong(v) != kTrsvPending) {
+            out = v;
+            return true;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    out = 0.0;
+    return false;
+}
+
+template <int L, bool FWD>
+__global__ __launch_bounds__(kBlock) void k_trsv_tagged(const int *__restrict__ ro, const int *__restrict__ ci,
+                                                        const double *__restrict__ va, int n,
+                                                        const int *__restrict__ order, const double *b, double *x,
+                                                        CgControl *ctrl)
+{
+    constexpr int NZ = 64 / L;
+    const int w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    if (w >= n || ctrl->done)  // done is set only by earlier launches: uniform here
+        return;
+    const int i = order[w];  // rows in (level, row) order: awaited rows belong to earlier waves
+    const int lane = threadIdx.x & 63;
+    const int v = lane % L, q = lane / L;
+    const int k1 = ro[i + 1];
+    double sum = 0.0, diag = 0.0;
+    bool ok = true;
+    for (int k0 = ro[i]; k0 < k1; k0 += NZ) {
+        const int k = k0 + q;
+        if (k < k1) {
+            const int j = ci[k];
+            const double a = va[k];
+            if (j == i) {
+                diag = a;
+            } else {
+                double xj;
+                ok = wait_value(&x[(size_t)j * L + v], xj) && ok;
+                sum += a * xj;
+            }
+        }
+    }
+#pragma unroll
+    for (int off = L; off < 64; off <<= 1) {
+        sum += __shfl_xor(sum, off);
+        diag += __shfl_xor(diag, off);
+    }
+    if (q == 0) {
+        const double bi = b[(size_t)i * L + v];
+        const double xi = (!FWD && diag == 0.0) ? 0.0 : (bi - sum) / diag;
+        store_sc1(&x[(size_t)i * L + v], xi);
+    }
+    if (__ballot(!ok) != 0 && lane == 0)
+        ctrl->breakdown = 2;  // a dependency never arrived (reported, never hung)
+}
+
 // R.Z per column and the PCG scalars after it (PCGSolveMultiple): mode 0 (init, :96-104)
 // rs_old = R.Z; mode 1 (:171-185) beta = converged ? 0 : R.Z / rs_old, rs_old = R.Z.
 template <int L>
@@ -2047,6 +2113,8 @@ struct SpmvTuning {
     int spmm_rg_cost = -1;  // the same for the multi-RHS kernels (-1: scaled to the SpMM tile)
     int cols16 = 1;   // single-RHS plans carry 16-bit column offsets where a tile's span allows
     int tb = 256;     // threads per single-RHS SpMV tile: 256 (workgroup tiles) or 64 (one-wave tiles)
+    int tile_items = 0;  // single-RHS nominal merge items per tile (0: tb * ipt; smaller: fewer per thread)
+    int trsv_tagged = 1;  // IC(0) solves: data-tagged values (1) or ready flags (0)
     int dict = 1;     // single-RHS SpMV through per-tile column dictionaries (k_build_dict) when
                       // a tile's nonzeros repeat its distinct columns >= dict_ratio times (0: off)
 };
@@ -2078,6 +2146,10 @@ static const SpmvTuning &spmv_tuning()
             v.cols16 = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMV_DICT"))
             v.dict = atoi(e) > 0 ? atoi(e) : 0;
+        if (const char *e = getenv("MSPMV_TRSV_TAGGED"))
+            v.trsv_tagged = atoi(e) != 0;
+        if (const char *e = getenv("MSPMV_SPMV_TILE"))
+            v.tile_items = atoi(e);
         if (const char *e = getenv("MSPMV_SPMV_TB"))
             v.tb = atoi(e) == 64 ? 64 : 256;
         return v;
@@ -2113,8 +2185,11 @@ int spmm_iptg_for(int L)
 
 int tile_items_for(int L)
 {
-    if (L == 1)
-        return spmv_tuning().tb * spmv_tuning().ipt;
+    if (L == 1) {
+        const int full = spmv_tuning().tb * spmv_tuning().ipt;
+        const int want = spmv_tuning().tile_items;  // 0: full tiles
+        return want > 0 ? std::max(64, std::min(want, full)) : full;
+    }
     return (kBlock / (L / 2)) * spmm_iptg_for(L);
 }
 
@@ -2843,6 +2918,15 @@ template <int L>
 static void trsv_L(const mspmv_ic0_s *ic, bool fwd, const double *b, double *x, CgControl *ctrl, hipStream_t s)
 {
     const dim3 grid((ic->n + kBlock / 64 - 1) / (kBlock / 64)), block(kBlock);
+    if (spmv_tuning().trsv_tagged) {
+        if (fwd)
+            hipLaunchKernelGGL((k_trsv_tagged<L, true>), grid, block, 0, s, ic->d_lro, ic->d_lci, ic->d_lva, ic->n,
+                               ic->d_fwd_order, b, x, ctrl);
+        else
+            hipLaunchKernelGGL((k_trsv_tagged<L, false>), grid, block, 0, s, ic->d_uro, ic->d_uci, ic->d_uva, ic->n,
+                               ic->d_bwd_order, b, x, ctrl);
+        return;
+    }
     if (fwd)
         hipLaunchKernelGGL((k_trsv<L, true>), grid, block, 0, s, ic->d_lro, ic->d_lci, ic->d_lva, ic->n,
                            ic->d_fwd_order, b, x, ic->d_ready, ctrl);
@@ -2857,13 +2941,16 @@ static hipError_t ic0_apply(mspmv_handle_s *h, mspmv_ic0_s *ic, int L, const dou
 {
     if (ic->n == 0)
         return hipSuccess;
+    const bool tagged = spmv_tuning().trsv_tagged != 0;
     for (int pass = 0; pass < 2; ++pass) {
-        hipError_t e = hipMemsetAsync(ic->d_ready, 0, sizeof(int) * (size_t)ic->n, h->stream);
-        if (e != hipSuccess)
-            return e;
         const bool fwd = pass == 0;
         const double *in = fwd ? r : ic->d_y;
         double *out = fwd ? ic->d_y : z;
+        hipError_t e = tagged ? hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(out), kTrsvPendingWord,
+                                                  2 * (size_t)ic->n * L, h->stream)
+                              : hipMemsetAsync(ic->d_ready, 0, sizeof(int) * (size_t)ic->n, h->stream);
+        if (e != hipSuccess)
+            return e;
         switch (L) {
         case 1: trsv_L<1>(ic, fwd, in, out, h->d_ctrl, h->stream); break;
         case 2: trsv_L<2>(ic, fwd, in, out, h->d_ctrl, h->stream); break;
