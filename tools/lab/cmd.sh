@@ -1,3 +1,4 @@
 set -o pipefail
-timeout -k 10 300 python -u -m pytest tests/test_ic0.py tests/test_gpu_tools.py -m gpu -x -q -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/tic.log 2>&1; rc=$?; tail -2 gpurun_out/tic.log; [ $rc -eq 0 ] || exit $rc
-for t in 0 1; do echo "tagged=$t $(MSPMV_TRSV_TAGGED=$t timeout -k 10 300 python tools/pcg_probe.py 8 20 | cut -c 1-600)" || exit 1; done
+export TMPDIR=/tmp
+PROBE_SHAPE=nlpkkt timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/cgm -o cgm -- python3 tools/cg_probe.py --child > gpurun_out/cgm.json 2>/dev/null || exit 1
+cat gpurun_out/cgm.json; cut -d, -f1-5 gpurun_out/cgm/cgm_kernel_stats.csv | cut -c 1-150 | head -20
