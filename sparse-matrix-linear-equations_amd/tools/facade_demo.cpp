@@ -1,6 +1,8 @@
 // facade_demo -- a reference-style C++ caller using include/mspmv.hpp unchanged call sites:
 // the CsrMatrix<double,int> field layout (sparse_matrix.h:648-653), OmpMergeCsrmv /
-// OmpMergeCsrmm / CGSolveSingle / CGSolveMultiple with the reference's argument lists.
+// OmpMergeCsrmm / CGSolveSingle / CGSolveMultiple (and, at num_vectors = 32 as cpu_spmm_v2 and
+// preconditioner_benchmark default, OmpMergeCsrmm, IncompleteCholesky + PCGSolveMultiple,
+// SparseApproximateInversion + SPAISolveMultiple) with the reference's argument lists.
 // Prints one line per call; exit code 0 when every result checks out against a host loop.
 #include <cmath>
 #include <cstdio>
@@ -54,8 +56,41 @@ int main()
         const int itm = CGSolveMultiple(a, B.data(), XS.data(), L, 5000, 1e-10, NONZERO_SPLIT, &errs);
         printf("CGSolveSingle %d iters, CGSolveMultiple %d iters (last max err %.3g)\n", it1, itm,
                errs.empty() ? -1.0 : errs.back());
+        // num_vectors = 32: column chunks of the native widths over the same row-major panels
+        const int L32 = 32;
+        std::vector<double> X32((size_t)m * L32), Y32((size_t)m * L32), B32((size_t)m * L32), S32((size_t)m * L32);
+        for (size_t i = 0; i < X32.size(); ++i)
+            X32[i] = B32[i] = 0.5 + (double)((i * 2654435761u) % 1000) / 1000.0;
+        OmpMergeCsrmm(8, a, a.row_offsets + 1, a.column_indices, a.values, X32.data(), Y32.data(), L32);
+        double err32 = 0;
+        for (int r = 0; r < m; ++r)
+            for (int j = 0; j < L32; ++j) {
+                double s = 0, ab = 0;
+                for (int k = ro[r]; k < ro[r + 1]; ++k) {
+                    s += va[k] * X32[(size_t)ci[k] * L32 + j];
+                    ab += std::fabs(va[k] * X32[(size_t)ci[k] * L32 + j]);
+                }
+                err32 = std::max(err32, std::fabs(s - Y32[(size_t)r * L32 + j]) / std::max(ab, 1e-300));
+            }
+        printf("OmpMergeCsrmm num_vectors=32 max err relative to |A||X| %.3g\n", err32);
+        CsrMatrix<double, int> l{}, mi{};
+        const bool icok = IncompleteCholesky(a, l);
+        std::vector<double> e_ic, e_spai;
+        const int itic = icok ? PCGSolveMultiple(a, l, l, B32.data(), S32.data(), L32, 5000, 1e-10, MERGE, &e_ic) : -1;
+        const bool spok = SparseApproximateInversion(a, mi);
+        const int itsp = spok ? SPAISolveMultiple(a, mi, B32.data(), S32.data(), L32, 5000, 1e-10, MERGE, &e_spai) : -1;
+        printf("IncompleteCholesky %d, PCGSolveMultiple(32) %d iters; SparseApproximateInversion %d, "
+               "SPAISolveMultiple(32) %d iters\n", (int)icok, itic, (int)spok, itsp);
+        for (auto *c : {&l, &mi}) {
+            delete[] c->row_offsets;
+            delete[] c->column_indices;
+            delete[] c->values;
+        }
+        mspmv_facade_release(mi);
         mspmv_facade_release(a);
-        return (err < 1e-12 && it1 > 0 && itm > 0 && !errs.empty() && errs.back() < 1e-10) ? 0 : 2;
+        const bool ok32 = err32 < 1e-12 && itic > 0 && itsp > 0 && !e_ic.empty() && e_ic.back() < 1e-10 &&
+                          !e_spai.empty() && e_spai.back() < 1e-10;
+        return (err < 1e-12 && it1 > 0 && itm > 0 && !errs.empty() && errs.back() < 1e-10 && ok32) ? 0 : 2;
     } catch (const std::exception &e) {
         printf("error: %s\n", e.what());
         return 3;

@@ -133,7 +133,7 @@ def test_spmm_synthetic(orc, name, L):
 
 
 @pytest.mark.parametrize("name", ["powerlaw", "fem2d"])
-@pytest.mark.parametrize("L", [3, 6, 12, 24, 32, 40])
+@pytest.mark.parametrize("L", [3, 6, 12, 24, 32, 40, 128])
 def test_spmm_any_width(orc, name, L):
     """num_vectors outside {1, 2, 4, 8, 16} (OmpMergeCsrmm takes any; cpu_spmm_v2 defaults to
     32, eval_vectors.sh sweeps 1..1024): column chunks of the native widths with panel stride L,
