@@ -633,7 +633,8 @@ mspmv_status mspmv_dspmv(mspmv_handle h, const double *x, double *y) { return ms
 // ---- CG ------------------------------------------------------------------------------------
 static mspmv_status ensure_cg_workspace(mspmv_handle_s *h, int L, int nblk, int num_tiles, int hist_cap)
 {
-    const size_t elems = (size_t)h->m * L;
+    // L = 1: the pipelined CG's p buffers hold {r, p} interleaved (2 m doubles each)
+    const size_t elems = (size_t)h->m * std::max(L, 2);
     if (elems > h->cg_cap_elems) {
         dev_free(h->d_r);
         dev_free(h->d_p0);

@@ -509,9 +509,10 @@ struct TileArgs {
     const int *__restrict__ row_offsets;
     const int *__restrict__ cols;
     const double *__restrict__ vals;
-    const double *__restrict__ x;      // SpMV/SpMM: x / X.   CG: r (residual)
-    const double *__restrict__ p_old;  // CG: previous search direction
-    double *__restrict__ p_new;        // CG: p = r + beta p, written for the tile's rows
+    const double *__restrict__ x;      // SpMV/SpMM: x / X.   CG: {r, p_old} interleaved (cg_rp)
+    const double *__restrict__ p_old;  // (unused by the single-RHS CG: p_old rides with r in x)
+    double *__restrict__ p_new;        // CG: the {r, p} buffer of the next iteration; p = r + beta p_old
+                                       // is written for the tile's rows at p_new[2 R + 1] (cg_pstore)
     double *__restrict__ y;            // SpMV/SpMM: y / Y.   CG: Ap
     const int2 *__restrict__ bounds;
     const unsigned char *__restrict__ split;
@@ -552,6 +553,17 @@ struct TileArgs {
 //   2: y = A x plus x.y over the rows (by linearity), last block writes dot_out (the
 //      row-sharded CG, whose x = [p_own | p_halo] was updated and exchanged beforehand).
 enum : int { kModeSpmv = 0, kModeCg = 1, kModeDot = 2 };
+
+// Single-RHS pipelined CG keeps r and p interleaved, {r_i, p_i} per row (16 B): the fused
+// p = r + beta p_old gather at every nonzero's column is one 16-B load instead of two 8-B loads
+// on separate cache lines (the same operands, so the same rounding).  Two such buffers
+// alternate by iteration parity: the SpMV reads {r_k, p_{k-1}} and writes p_k into the other
+// one, the update reads r_k here and p_k there and writes r_{k+1} next to p_k.
+__device__ __forceinline__ double2 cg_rp(const TileArgs &a, long long i)
+{
+    return reinterpret_cast<const double2 *>(a.x)[i];
+}
+__device__ __forceinline__ void cg_pstore(const TileArgs &a, long long i, double p) { a.p_new[2 * i + 1] = p; }
 
 // LDS slot of tile-local product k: an XOR swizzle inside each aligned group of 8 doubles,
 // so walkers 8 products apart hit different banks, while staging writes and row-group reads
@@ -600,13 +612,17 @@ __device__ __forceinline__ void stage_issue(const TileArgs &a, int n0, int nnzt,
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
         st.v[j] = ld_stream<NT>(a.vals + n0 + min((int)threadIdx.x + j * TB, nnzt - 1));
+    if constexpr (CG) {
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-        st.xv[j] = a.x[st.c[j]];
-    if (CG) {
+        for (int j = 0; j < NJ; ++j) {
+            const double2 v = cg_rp(a, st.c[j]);
+            st.xv[j] = v.x;
+            st.pv[j] = v.y;
+        }
+    } else {
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-            st.pv[j] = a.p_old[st.c[j]];
+            st.xv[j] = a.x[st.c[j]];
     }
 }
 template <int NJ, bool CG, int TB = kBlock>
@@ -728,8 +744,9 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT, TB> &
         const int R = r0 + row;
         a.y[R] = val;
         if (MODE == kModeCg) {
-            const double pn = a.x[R] + beta * a.p_old[R];
-            a.p_new[R] = pn;
+            const double2 v = cg_rp(a, R);
+            const double pn = v.x + beta * v.y;
+            cg_pstore(a, R, pn);
             dot += pn * val;
         } else if (MODE == kModeDot) {
             dot += a.x[R] * val;
@@ -794,8 +811,10 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT, TB> &
             acc += sm.cval[u];
         a.carry_val[t] = acc;
         const int R = r0 + nrows;
-        if (MODE == kModeCg)
-            dot += (a.x[R] + beta * a.p_old[R]) * acc;
+        if (MODE == kModeCg) {
+            const double2 v = cg_rp(a, R);
+            dot += (v.x + beta * v.y) * acc;
+        }
         else if (MODE == kModeDot)
             dot += a.x[R] * acc;
     }
@@ -811,7 +830,7 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT, TB> &
 // Row results go through LDS (sm.cval) and are stored by one thread per row afterwards: one
 // coalesced store per tile, and no global memory operation inside the reduction loop (a loop
 // that only stores makes hipcc drain vmcnt before it, which would wait for the persistent
-// kernel's in-flight prefetch).  xr / pr: x[r0 + tid] and p_old[r0 + tid] (CG / dot modes),
+// kernel's in-flight prefetch).  xr / pr: r and p_old (CG) or x (dot mode) of row r0 + tid,
 // loaded by the caller for tid <= nrows.
 template <int IPT, int MODE, int TB = kBlock>
 __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT, TB> &sm, int t, int r0, int nrows,
@@ -855,17 +874,19 @@ __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT, TB> 
             if (r < nrows) {
                 a.y[R] = v;
                 if (MODE == kModeCg) {
-                    const double pn = a.x[R] + beta * a.p_old[R];
-                    a.p_new[R] = pn;
+                    const double2 w = cg_rp(a, R);
+                    const double pn = w.x + beta * w.y;
+                    cg_pstore(a, R, pn);
                     dot += pn * v;
                 } else if (MODE == kModeDot) {
                     dot += a.x[R] * v;
                 }
             } else {
                 a.carry_val[t] = v;
-                if (MODE == kModeCg)
-                    dot += (a.x[R] + beta * a.p_old[R]) * v;
-                else if (MODE == kModeDot)
+                if (MODE == kModeCg) {
+                    const double2 w = cg_rp(a, R);
+                    dot += (w.x + beta * w.y) * v;
+                } else if (MODE == kModeDot)
                     dot += a.x[R] * v;
             }
         }
@@ -878,7 +899,7 @@ __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT, TB> 
             a.y[R] = v;
             if (MODE == kModeCg) {
                 const double pn = xr + beta * pr;
-                a.p_new[R] = pn;
+                cg_pstore(a, R, pn);
                 dot += pn * v;
             } else if (MODE == kModeDot) {
                 dot += xr * v;
@@ -906,16 +927,20 @@ __device__ __forceinline__ void reduce_tile(const TileArgs &a, SpmvSmem<IPT, TB>
         group_tile<IPT, MODE, TB>(a, sm, t, r0, nrows, nnzt, tail, beta, dot, mode - 1, xr, pr);
 }
 
-// x[r0 + tid] and p_old[r0 + tid] for the row-group epilogue (CG / dot modes), tid <= nrows.
+// x[r0 + tid] (dot mode), or r and p_old at r0 + tid (CG), for the row-group epilogue, tid <= nrows.
 template <int MODE>
 __device__ __forceinline__ void row_operands(const TileArgs &a, int r0, int nrows, double &xr, double &pr)
 {
     xr = pr = 0.0;
     if (MODE != kModeSpmv && (int)threadIdx.x <= nrows) {
         const int R = min(r0 + (int)threadIdx.x, a.m - 1);
-        xr = a.x[R];
-        if (MODE == kModeCg)
-            pr = a.p_old[R];
+        if constexpr (MODE == kModeCg) {
+            const double2 v = cg_rp(a, R);
+            xr = v.x;
+            pr = v.y;
+        } else {
+            xr = a.x[R];
+        }
     }
 }
 
@@ -2496,10 +2521,9 @@ hipError_t launch_dist_vec(int which, const CgVecArgs &a, int L, int nblk, doubl
 struct Cg1Args {
     long long m;
     double *x;
-    double *r;
-    double *p0;            // init: p0 = b
+    double *rp;            // init: {r, p_0} = {b, b}.  update: {r_k, p_{k-1}} (r_k read at rp[2 i])
+    double *rp_next;       // update: {., p_k} -> {r_{k+1}, p_k} (p_k read, r_{k+1} written)
     const double *b;       // init
-    const double *p;       // update: p of this iteration
     const double *ap;
     CgScalars *scal;
     CgControl *ctrl;
@@ -2511,7 +2535,8 @@ struct Cg1Args {
     int hist_cap;
 };
 
-// x = 0, r = p0 = b, and this block's b.b partial (the first SpMV sums them: rs_0, ||b||).
+// x = 0, {r, p_0} = {b, b} (interleaved, see cg_rp), and this block's b.b partial (the first
+// SpMV sums them: rs_0, ||b||).
 __global__ __launch_bounds__(kBlock) void k_cg1_init(Cg1Args a)
 {
     __shared__ double s_red[kBlock / 64];
@@ -2519,8 +2544,7 @@ __global__ __launch_bounds__(kBlock) void k_cg1_init(Cg1Args a)
     for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < a.m; i += (long long)gridDim.x * kBlock) {
         const double b = a.b[i];
         a.x[i] = 0.0;
-        a.r[i] = b;
-        a.p0[i] = b;
+        reinterpret_cast<double2 *>(a.rp)[i] = make_double2(b, b);
         acc += b * b;
     }
     const double t = block_sum(acc, s_red);
@@ -2543,10 +2567,10 @@ __global__ __launch_bounds__(kBlock) void k_cg1_update(Cg1Args a)
     const long long i0 = (long long)blockIdx.x * kBlock + tid;
     double p = 0.0, q = 0.0, x = 0.0, r = 0.0;  // the first element's operands, in flight under the sum
     if (i0 < a.m) {
-        p = a.p[i0];
+        p = a.rp_next[2 * i0 + 1];
         q = a.ap[i0];
         x = a.x[i0];
-        r = a.r[i0];
+        r = a.rp[2 * i0];
     }
     const double pAp = part_sum(pin, s_red);
     const double alpha = a.scal[0].rs_par[a.parity] / pAp;
@@ -2562,15 +2586,15 @@ __global__ __launch_bounds__(kBlock) void k_cg1_update(Cg1Args a)
     double acc = 0.0;
     for (long long i = i0; i < a.m; i += stride) {
         if (i != i0) {
-            p = a.p[i];
+            p = a.rp_next[2 * i + 1];
             q = a.ap[i];
             x = a.x[i];
-            r = a.r[i];
+            r = a.rp[2 * i];
         }
         x = x + alpha * p;
         r = r + nal * q;
         a.x[i] = x;
-        a.r[i] = r;
+        a.rp_next[2 * i] = r;
         acc += r * r;
     }
     const double t = block_sum(acc, s_red);
@@ -2610,8 +2634,7 @@ static Cg1Args cg1_args(mspmv_handle_s *h, double *d_x)
     Cg1Args a{};
     a.m = h->m;
     a.x = d_x;
-    a.r = h->d_r;
-    a.p0 = h->d_p0;
+    a.rp = h->d_p0;  // {r, p} of parity 0; the iterations alternate d_p0 / d_p1 (2 m doubles each)
     a.ap = h->d_ap;
     a.scal = h->d_scal;
     a.ctrl = h->d_ctrl;
@@ -2698,11 +2721,10 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *
 {
     if (cg_split_iteration(L))
         return launch_cg_iteration_split(h, plan, d_x, L, nblk, tol);
-    double *p_old = parity ? h->d_p1 : h->d_p0;
-    double *p_new = parity ? h->d_p0 : h->d_p1;
-    TileArgs ta = make_args(h, plan, h->d_r, h->d_ap, 1);
-    ta.p_old = p_old;
-    ta.p_new = p_new;
+    double *rp_old = parity ? h->d_p1 : h->d_p0;  // {r_k, p_{k-1}} interleaved (cg_rp)
+    double *rp_new = parity ? h->d_p0 : h->d_p1;  // receives p_k, then r_{k+1}
+    TileArgs ta = make_args(h, plan, rp_old, h->d_ap, 1);
+    ta.p_new = rp_new;
     ta.scal = h->d_scal;
     ta.ctrl = h->d_ctrl;
     ta.partials = h->d_partials;
@@ -2719,7 +2741,8 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *
     if ((e = launch_fixup_ctrl(h, plan, h->d_ap, 1)) != hipSuccess)
         return e;
     Cg1Args a = cg1_args(h, d_x);
-    a.p = p_new;
+    a.rp = rp_old;
+    a.rp_next = rp_new;
     long long off = 0;
     int count = 0;
     consumer_level(plan.num_tiles, kConsumeTile, 1, &off, &count);
