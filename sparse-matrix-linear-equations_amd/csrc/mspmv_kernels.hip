@@ -1003,14 +1003,17 @@ template <int IPT>
 __device__ __forceinline__ void cg1_publish(const TileArgs &a, SpmvSmem<IPT> &sm, int slot, int nslots, double dot)
 {
     const double tsum = block_sum(dot, sm.red);
-    if (threadIdx.x == 0) {
+    if (nslots <= kConsumeTile) {  // the update kernel sums them: the launch boundary orders the store
+        if (threadIdx.x == 0)
+            a.partials[slot] = tsum;
+        return;
+    }
+    if (threadIdx.x == 0) {  // a ticket tree folds them: publish at agent scope, drained
         store_sc1(&a.partials[slot], tsum);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    if (nslots > kConsumeTile) {
-        __syncthreads();
-        publish_partials<1>(a.partials, a.gtickets, slot, nslots, kConsumeTile, sm.cval, sm.red, &sm.last);
-    }
+    __syncthreads();
+    publish_partials<1>(a.partials, a.gtickets, slot, nslots, kConsumeTile, sm.cval, sm.red, &sm.last);
 }
 
 // Single right-hand side, one tile per workgroup of TB threads.  TILE = TB*IPT merge items

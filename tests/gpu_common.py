@@ -48,10 +48,13 @@ def abs_bound(a, X):
     X = np.asarray(X, np.float64)
     if X.ndim == 1:
         X = X[:, None]
-    lens = np.diff(a.row_offsets).astype(np.int64)
-    rows = np.repeat(np.arange(a.num_rows), lens)
+    ro = a.row_offsets.astype(np.int64)
+    lens = np.diff(ro)
     acc = np.zeros((a.num_rows, X.shape[1]))
-    np.add.at(acc, rows, np.abs(a.values)[:, None] * np.abs(X[a.column_indices]))
+    if a.num_nonzeros:  # segment sums over the non-empty rows (fast at 10^8 nonzeros)
+        prod = np.abs(a.values)[:, None] * np.abs(X[a.column_indices])
+        ne = lens > 0
+        acc[ne] = np.add.reduceat(prod, ro[:-1][ne], axis=0)
     return acc, lens
 
 
