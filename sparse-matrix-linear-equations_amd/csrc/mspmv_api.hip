@@ -229,7 +229,10 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
             p.d_cols16 = nullptr;
         }
     }
-    if (tile == tile_items_for(1) && T > 0 && h->nnz > 0 && spmv_dict_enabled()) {
+    // multi-RHS: only the L = 16 plan (k_spmm_tile's DICT path runs at L = 16 only)
+    const bool multi = tile != tile_items_for(1);
+    const bool want = multi ? L == 16 && tile != tile_items_for(8) && spmm_dict_enabled() : spmv_dict_enabled();
+    if (T > 0 && h->nnz > 0 && want) {
         if ((st = dev_alloc(&p.d_dict, (size_t)h->nnz + kNnzPad)) != MSPMV_OK ||
             (st = dev_alloc(&p.d_ndict, (size_t)T)) != MSPMV_OK ||
             (st = dev_alloc(&p.d_idx16, (size_t)h->nnz + kNnzPad)) != MSPMV_OK)
@@ -238,7 +241,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
         if (e == hipSuccess)
             e = hipMemsetAsync(p.d_idx16, 0, sizeof(unsigned short) * ((size_t)h->nnz + kNnzPad), h->stream);
         if (e == hipSuccess)
-            e = launch_build_dict(h->d_cols, p.d_bounds, T, maxi, p.d_dict, p.d_ndict, p.d_idx16, h->stream);
+            e = launch_build_dict(h->d_cols, p.d_bounds, T, maxi, p.d_dict, p.d_ndict, p.d_idx16, h->stream, multi);
         std::vector<int> hnd((size_t)T);
         if (e == hipSuccess)
             e = hipMemcpyAsync(hnd.data(), p.d_ndict, sizeof(int) * T, hipMemcpyDeviceToHost, h->stream);
@@ -1379,6 +1382,19 @@ mspmv_status mspmv_tile_streams(mspmv_handle h, int *tiles_cols16, int *tiles_di
         *tiles_cols16 = plan->d_cols16 ? plan->num_tiles16 : 0;
     if (tiles_dict)
         *tiles_dict = plan->d_dict ? plan->num_tiles_dict : 0;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_plan_dict_tiles(mspmv_handle h, int L, int *tiles_dict)
+{
+    ST_TRY(check_handle(h));
+    if (!tiles_dict)
+        return invalid("null out pointer");
+    if (!supported_L(L))
+        return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
+    const TilePlan *plan = nullptr;
+    ST_TRY(get_plan(h, L, &plan));
+    *tiles_dict = plan->d_dict && (L == 1 || L == 16) ? plan->num_tiles_dict : 0;
     return MSPMV_OK;
 }
 

@@ -154,7 +154,11 @@ hipError_t launch_pack_cols16(const int *d_cols, const int2 *d_bounds, int num_t
 bool spmv_cols16_enabled();
 bool spmv_dict_enabled();
 hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_tiles, int max_items, int *d_dict,
-                             int *d_ndict, unsigned short *d_idx16, hipStream_t s);
+                             int *d_ndict, unsigned short *d_idx16, hipStream_t s, bool multi);
+bool spmm_dict_enabled();
+// Multi-RHS column dictionaries: the distinct panel rows a tile parks in LDS (16 KB per workgroup).
+constexpr int kSpmmDictBytes = 16384;
+constexpr int spmm_dict_max(int L) { return kSpmmDictBytes / (8 * L); }
 // y = A x (L == 1) or Y = A X (row-major panels), tile kernel + optional carry fix-up.
 hipError_t launch_spmm(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
                        int *kernels_launched, int ld = 0);

@@ -347,10 +347,13 @@ __global__ __launch_bounds__(kBlock) void k_pack_cols16(const int *__restrict__ 
 // keeps the distinct ones in ascending order -> dict[n0 + d], d < ndict[t] (stored in the tile's
 // own nonzero range: ndict <= nnzt), and rewrites every nonzero as its dictionary position ->
 // idx16[k].  The kernel then gathers each distinct x once per tile instead of once per nonzero.
+// ratio < 0: a multi-RHS plan (k_spmm_tile parks the distinct panel rows in LDS): every tile
+// whose nonzeros repeat its distinct columns at least twice and has at most dmax of them takes
+// its dictionary, without the single-RHS line test.
 template <int N>
 __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ cols, const int2 *__restrict__ bounds,
                                                        int *__restrict__ dict, int *__restrict__ ndict,
-                                                       unsigned short *__restrict__ idx16, int ratio)
+                                                       unsigned short *__restrict__ idx16, int ratio, int dmax)
 {
     __shared__ int keys[N];
     __shared__ int uniq[N];
@@ -375,7 +378,7 @@ __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ c
         __syncthreads();
     }
     const int lines_direct = s_scan[0];
-    if (ratio <= 0 || nz == 0 || 2 * lines_direct < nz) {
+    if (ratio == 0 || nz == 0 || (ratio > 0 && 2 * lines_direct < nz)) {
         if (tid == 0)
             ndict[t] = 0;
         return;
@@ -438,7 +441,7 @@ __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ c
         __syncthreads();
     }
     const int lines_dict = s_scan[0];
-    const bool use = 4 * lines_dict <= 3 * lines_direct;
+    const bool use = ratio > 0 ? 4 * lines_dict <= 3 * lines_direct : (nu <= dmax && 2 * nu <= nz);
     if (tid == 0)
         ndict[t] = use ? nu : 0;
     if (!use)
@@ -1257,10 +1260,12 @@ __global__ __launch_bounds__(kBlock) void k_spmv_persist(TileArgs a, int tpb)
 // the products of nonzeros j, j+Gp, ... of the row in order from 0.0 (four panel-row gathers
 // in flight), a fixed xor butterfly over j folds the group, and j = 0 writes the row.
 // Gp = 1 is the row-by-row CSR-order sum of the reference's row-split SpMM, bit for bit.
-template <int L, int MODE>
+// DICT: s_col holds each nonzero's position in the tile's column dictionary and the panel rows
+// are read from s_panel (parked there by k_spmm_tile) -- the same operands, the same sums.
+template <int L, int MODE, bool DICT = false>
 __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_col, const double *s_val,
                                                 const int *rend, int t, int r0, int nrows, int nnzt,
-                                                double2 &dot, int lgp)
+                                                double2 &dot, int lgp, const double2 *s_panel = nullptr)
 {
     constexpr int GL = L / 2;
     const int Gp = 1 << lgp;
@@ -1271,8 +1276,10 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
     const bool tail = a.split[t + 1] != 0;
     const int nseg = nrows + (tail ? 1 : 0);
     auto panel = [&](int c) {
-        double2 xv = *reinterpret_cast<const double2 *>(a.x + (size_t)c * a.ld + 2 * lane);
-        return xv;
+        if constexpr (DICT)
+            return s_panel[c * GL + lane];
+        else
+            return *reinterpret_cast<const double2 *>(a.x + (size_t)c * a.ld + 2 * lane);
     };
     for (int r = tid / W; r < nseg; r += kBlock / W) {  // uniform within a group
         const int s0 = r == 0 ? 0 : rend[r - 1];
@@ -1341,16 +1348,23 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
 // merge_based.hpp:84-127).  TILE = (256/(L/2)) groups * IPTG items.
 // Workgroups per CU the multi-RHS tile's LDS allows, capped at 7: the register budget is pinned
 // to it (the dot mode would otherwise need 90 VGPRs and fall to 5 workgroups at L = 8).
-constexpr int spmm_waves_per_eu(int L, int IPTG)
+constexpr int spmm_waves_per_eu(int L, int IPTG, bool DICT = false)
 {
     const int items = (kBlock / (L / 2)) * IPTG;
-    const int lds = 16 * (items + items / kSnapDiv) + 6144;  // + s_crow, s_cval, s_red2
+    const int lds = 16 * (items + items / kSnapDiv) + 6144 + (DICT ? kSpmmDictBytes : 0);  // + s_crow, s_cval, s_red2
     const int w = 163840 / lds;
     return w < 1 ? 1 : w > 7 ? 7 : w;
 }
 
-template <int L, int IPTG, int MODE, bool NT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(spmm_waves_per_eu(L, IPTG)))) void
+// DICT: tiles with a column dictionary (multi-RHS plans, k_build_dict) gather each distinct
+// panel row once, coalesced (the dictionary is sorted: neighbouring columns share lines), into
+// LDS, and the row groups read the panel there: at L = 16 a FEM-blocked tile repeats each of
+// its columns ~6 times.  Walk-mode tiles and tiles without one gather directly.  Measured
+// (pwtk shape): L = 16 130 -> 106 us; at L = 4 and 8 it lost (47 -> 55, 63 -> 67 us; the
+// 27-point nlpkkt120 size at L = 8 505 -> 590 us: the extra dependent round trip and the
+// occupancy the 16 KB panel costs outweigh 64-B gathers), so only L = 16 plans build one.
+template <int L, int IPTG, int MODE, bool NT, bool DICT = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(spmm_waves_per_eu(L, IPTG, DICT)))) void
 k_spmm_tile(TileArgs a)
 {
     static_assert(MODE != kModeCg, "multi-RHS CG runs the split iteration (MODE 2)");
@@ -1366,6 +1380,9 @@ k_spmm_tile(TileArgs a)
     __shared__ int s_crow[NG];
     __shared__ double2 s_cval[NG * GL];
     __shared__ double2 s_red2[kBlock / 64][GL];
+    constexpr int DMAX = DICT ? spmm_dict_max(L) : 1;
+    constexpr int DJ = (DMAX + NG - 1) / NG;  // dictionary entries per lane group (4)
+    __shared__ double2 s_panel[DICT ? DMAX * GL : 1];
 
     const int tid = threadIdx.x;
     const int g = tid / GL;
@@ -1381,6 +1398,19 @@ k_spmm_tile(TileArgs a)
     const int nrows = b1.x - r0;
     const int nnzt = b1.y - n0;
     const int items = nrows + nnzt;
+    const int rmode = a.rmode[t];
+    int nd = 0;  // > 0: this tile reads its panel rows from s_panel
+    if constexpr (DICT) {
+        nd = a.ndict[t];
+        if (nd > DMAX || rmode == 0)
+            nd = 0;
+    }
+    int dcol[DJ];
+    if constexpr (DICT) {  // the dictionary's columns first: the panel gathers wait on them
+#pragma unroll
+        for (int u = 0; u < DJ; ++u)
+            dcol[u] = nd > 0 ? a.dict[n0 + min(g + u * NG, nd - 1)] : 0;
+    }
 
     // Every round's loads are issued before any is stored to LDS (indices clamped into the
     // tile), the first round of row ends with them: one memory round trip per tile, not STG.
@@ -1388,12 +1418,30 @@ k_spmm_tile(TileArgs a)
     if (nnzt > 0) {  // block-uniform
         int cst[STG];
         double vst[STG];
+        if (DICT && nd > 0) {
 #pragma unroll
-        for (int j = 0; j < STG; ++j)
-            cst[j] = ld_stream<NT>(a.cols + n0 + min(tid + j * kBlock, nnzt - 1));
+            for (int j = 0; j < STG; ++j)
+                cst[j] = (int)ld_stream<NT>(a.idx16 + n0 + min(tid + j * kBlock, nnzt - 1));
+        } else {
+#pragma unroll
+            for (int j = 0; j < STG; ++j)
+                cst[j] = ld_stream<NT>(a.cols + n0 + min(tid + j * kBlock, nnzt - 1));
+        }
 #pragma unroll
         for (int j = 0; j < STG; ++j)
             vst[j] = ld_stream<NT>(a.vals + n0 + min(tid + j * kBlock, nnzt - 1));
+        if constexpr (DICT) {
+            if (nd > 0) {  // each distinct panel row once: lane group g takes entries g, g + NG, ...
+                double2 pv[DJ];
+#pragma unroll
+                for (int u = 0; u < DJ; ++u)
+                    pv[u] = *reinterpret_cast<const double2 *>(a.x + (size_t)dcol[u] * a.ld + 2 * lane);
+#pragma unroll
+                for (int u = 0; u < DJ; ++u)
+                    if (g + u * NG < nd)
+                        s_panel[(g + u * NG) * GL + lane] = pv[u];
+            }
+        }
 #pragma unroll
         for (int j = 0; j < STG; ++j) {
             const int k = tid + j * kBlock;
@@ -1412,8 +1460,9 @@ k_spmm_tile(TileArgs a)
         return;
 
     double2 dot = make_double2(0.0, 0.0);
-    const int rmode = a.rmode[t];
-    if (rmode != 0) {
+    if (DICT && nd > 0) {
+        spmm_group_rows<L, MODE, true>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, dot, rmode - 1, s_panel);
+    } else if (rmode != 0) {
         spmm_group_rows<L, MODE>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, dot, rmode - 1);
     } else {
     const int ipt = (items + NG - 1) / NG;
@@ -2242,15 +2291,28 @@ hipError_t launch_pack_cols16(const int *d_cols, const int2 *d_bounds, int num_t
 bool spmv_cols16_enabled() { return spmv_tuning().cols16 != 0; }
 bool spmv_dict_enabled() { return spmv_tuning().dict > 0; }
 
-hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_tiles, int max_items, int *d_dict,
-                             int *d_ndict, unsigned short *d_idx16, hipStream_t s)
+bool spmm_dict_enabled()
 {
+    static const bool on = [] {
+        const char *e = getenv("MSPMV_SPMM_DICT");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return on;
+}
+
+// multi: a multi-RHS plan (dictionaries of at most spmm_dict_max(2) entries, the widest any
+// L sharing the tile size can park; each kernel checks its own limit)
+hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_tiles, int max_items, int *d_dict,
+                             int *d_ndict, unsigned short *d_idx16, hipStream_t s, bool multi)
+{
+    const int ratio = multi ? -1 : spmv_tuning().dict;
+    const int dmax = multi ? spmm_dict_max(2) : 1 << 30;
     if (max_items <= 4096)
         hipLaunchKernelGGL(k_build_dict<4096>, dim3(num_tiles), dim3(kBlock), 0, s, d_cols, d_bounds, d_dict, d_ndict,
-                           d_idx16, spmv_tuning().dict);
+                           d_idx16, ratio, dmax);
     else if (max_items <= 8192)
         hipLaunchKernelGGL(k_build_dict<8192>, dim3(num_tiles), dim3(kBlock), 0, s, d_cols, d_bounds, d_dict, d_ndict,
-                           d_idx16, spmv_tuning().dict);
+                           d_idx16, ratio, dmax);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -2296,10 +2358,10 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
     if (L == 1) {
         a.colbase = plan.d_colbase;
         a.cols16 = plan.d_cols16;
-        a.dict = plan.d_dict;
-        a.ndict = plan.d_ndict;
-        a.idx16 = plan.d_idx16;
     }
+    a.dict = plan.d_dict;
+    a.ndict = plan.d_ndict;
+    a.idx16 = plan.d_idx16;
     a.ld = L;
     return a;
 }
@@ -2336,10 +2398,20 @@ template <int LL, int I, int MODE>
 static void launch_spmm_nt(const TileArgs &a, hipStream_t s, bool nt)
 {
     if constexpr (MODE != kModeCg) {
+        const dim3 grid(a.num_tiles), block(kBlock);
+        if constexpr (LL == 16 && I != 32) {  // plans with column dictionaries (L = 16 only, below)
+            if (a.dict) {
+                if (nt)
+                    hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, true, true>), grid, block, 0, s, a);
+                else
+                    hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, false, true>), grid, block, 0, s, a);
+                return;
+            }
+        }
         if (nt)
-            hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, true>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, true>), grid, block, 0, s, a);
         else
-            hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, false>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
+            hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, false>), grid, block, 0, s, a);
     }
 }
 

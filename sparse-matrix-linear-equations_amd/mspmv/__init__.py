@@ -97,6 +97,7 @@ _SIGS = {
                                        _PD, _PD, _PI]),
     "mspmv_tile_plan": (_I, [_P, _I, _PI, _PI, _PI, ctypes.POINTER(Coord)]),
     "mspmv_tile_streams": (_I, [_P, _PI, _PI]),
+    "mspmv_plan_dict_tiles": (_I, [_P, _I, _PI]),
     "mspmv_tile_modes": (_I, [_P, _I, _P]),
     "mspmv_spmv_kernel_name": (ctypes.c_char_p, [_P]),
     "mspmv_device_malloc": (_I, [_I, _SZ, ctypes.POINTER(_P)]),
@@ -360,6 +361,11 @@ class GpuCsr:
         _check(lib.mspmv_tile_streams(self.h, ctypes.byref(c16), ctypes.byref(dic)), "tile_streams")
         return c16.value, dic.value
 
+    def dict_tiles(self, L: int = 1) -> int:
+        """Tiles of the L-column plan that gather through a column dictionary."""
+        n = ctypes.c_int()
+        _check(lib.mspmv_plan_dict_tiles(self.h, L, ctypes.byref(n)), "plan_dict_tiles")
+        return n.value
     def kernel_name(self) -> str:
         """The single-RHS SpMV kernel instantiation used for this matrix (rocprofv3's name)."""
         return lib.mspmv_spmv_kernel_name(self.h).decode()

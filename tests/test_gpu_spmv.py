@@ -160,6 +160,20 @@ def test_column_dictionary_tiles(orc):
             check_parity(a, g.spmv(x), orc.spmv_gold(a, x), x, g.tile_plan(1), 1)
 
 
+def test_spmm16_column_dictionary_tiles(orc):
+    """L = 16 tiles that park their distinct panel rows in LDS (k_spmm_tile DICT): the same
+    products in the same order as direct gathers, so the same parity rule; a FEM-blocked shape
+    (6 rows per node share their columns) makes most tiles take a dictionary."""
+    a = mspmv.CsrMatrix.synth_fem_blocked(6000, 320000, 6, 200, seed=4)
+    X = np.random.default_rng(8).uniform(-1, 1, (a.num_cols, 16))
+    with mspmv.GpuCsr(a) as g:
+        Y = g.spmm(X)
+        plan = g.tile_plan(16)
+        assert g.dict_tiles(16) > plan["num_tiles"] // 2, (g.dict_tiles(16), plan["num_tiles"])
+        assert g.dict_tiles(8) == 0
+        check_parity(a, Y, orc.csr_spmm_t(a, X), X, plan, 16)
+
+
 def test_deterministic_repeat():
     a = mspmv.CsrMatrix.synth_powerlaw(30000, 30000, 900000, exponent=1.4, seed=9)
     x = np.random.default_rng(1).uniform(-1, 1, a.num_cols)
