@@ -219,7 +219,7 @@ MSPMV_API mspmv_status mspmv_tile_plan(mspmv_handle h, int L, int *num_tiles, in
 MSPMV_API mspmv_status mspmv_tile_streams(mspmv_handle h, int *tiles_cols16, int *tiles_dict);
 /* The L-column plan's tiles that carry a column dictionary (*tiles_dict).  L = 1: as
  * mspmv_tile_streams.  L = 16: the SpMM parks each such tile's distinct panel rows in LDS and
- * reads them there (row-group tiles with at most 128 distinct columns, each repeated >= 2
+ * reads them there (row-group tiles with at most 64 distinct columns, each repeated >= 2
  * times on average); other widths build none (0). */
 MSPMV_API mspmv_status mspmv_plan_dict_tiles(mspmv_handle h, int L, int *tiles_dict);
 /* Each tile's in-tile reduction for L right-hand sides (num_tiles entries): 0 = merge walk

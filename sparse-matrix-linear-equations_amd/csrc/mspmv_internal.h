@@ -156,8 +156,13 @@ bool spmv_dict_enabled();
 hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_tiles, int max_items, int *d_dict,
                              int *d_ndict, unsigned short *d_idx16, hipStream_t s, bool multi);
 bool spmm_dict_enabled();
-// Multi-RHS column dictionaries: the distinct panel rows a tile parks in LDS (16 KB per workgroup).
-constexpr int kSpmmDictBytes = 16384;
+// Multi-RHS column dictionaries: the distinct panel rows a tile parks in LDS, 8 KB per workgroup
+// (L = 16: 64 rows), which keeps 7 workgroups per CU; 16 KB (5 per CU) measured 105 vs 102 us and
+// 24 KB 119 us on the pwtk shape.
+#ifndef MSPMV_SPMM_DICT_BYTES
+#define MSPMV_SPMM_DICT_BYTES 8192  // lab builds override (tools/lab/build_variant.sh)
+#endif
+constexpr int kSpmmDictBytes = MSPMV_SPMM_DICT_BYTES;
 constexpr int spmm_dict_max(int L) { return kSpmmDictBytes / (8 * L); }
 // y = A x (L == 1) or Y = A X (row-major panels), tile kernel + optional carry fix-up.
 hipError_t launch_spmm(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,

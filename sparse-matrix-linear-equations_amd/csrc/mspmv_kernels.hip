@@ -1360,7 +1360,7 @@ constexpr int spmm_waves_per_eu(int L, int IPTG, bool DICT = false)
 // panel row once, coalesced (the dictionary is sorted: neighbouring columns share lines), into
 // LDS, and the row groups read the panel there: at L = 16 a FEM-blocked tile repeats each of
 // its columns ~6 times.  Walk-mode tiles and tiles without one gather directly.  Measured
-// (pwtk shape): L = 16 130 -> 106 us; at L = 4 and 8 it lost (47 -> 55, 63 -> 67 us; the
+// (pwtk shape): L = 16 130 -> 102 us; at L = 4 and 8 it lost (47 -> 55, 63 -> 67 us; the
 // 27-point nlpkkt120 size at L = 8 505 -> 590 us: the extra dependent round trip and the
 // occupancy the 16 KB panel costs outweigh 64-B gathers), so only L = 16 plans build one.
 template <int L, int IPTG, int MODE, bool NT, bool DICT = false>
@@ -2300,13 +2300,13 @@ bool spmm_dict_enabled()
     return on;
 }
 
-// multi: a multi-RHS plan (dictionaries of at most spmm_dict_max(2) entries, the widest any
-// L sharing the tile size can park; each kernel checks its own limit)
+// multi: the L = 16 plan (dictionaries of at most spmm_dict_max(16) entries: what its kernel
+// parks in LDS; the kernel checks the limit again)
 hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_tiles, int max_items, int *d_dict,
                              int *d_ndict, unsigned short *d_idx16, hipStream_t s, bool multi)
 {
     const int ratio = multi ? -1 : spmv_tuning().dict;
-    const int dmax = multi ? spmm_dict_max(2) : 1 << 30;
+    const int dmax = multi ? spmm_dict_max(16) : 1 << 30;
     if (max_items <= 4096)
         hipLaunchKernelGGL(k_build_dict<4096>, dim3(num_tiles), dim3(kBlock), 0, s, d_cols, d_bounds, d_dict, d_ndict,
                            d_idx16, ratio, dmax);

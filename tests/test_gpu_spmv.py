@@ -163,8 +163,9 @@ def test_column_dictionary_tiles(orc):
 def test_spmm16_column_dictionary_tiles(orc):
     """L = 16 tiles that park their distinct panel rows in LDS (k_spmm_tile DICT): the same
     products in the same order as direct gathers, so the same parity rule; a FEM-blocked shape
-    (6 rows per node share their columns) makes most tiles take a dictionary."""
-    a = mspmv.CsrMatrix.synth_fem_blocked(6000, 320000, 6, 200, seed=4)
+    (6 rows per node share their columns, 5 nodes per row in a +-3-node band) lets nearly
+    every tile take one (<= 64 distinct columns per 512-item tile)."""
+    a = mspmv.CsrMatrix.synth_fem_blocked(6000, 180000, 6, 3, seed=4)
     X = np.random.default_rng(8).uniform(-1, 1, (a.num_cols, 16))
     with mspmv.GpuCsr(a) as g:
         Y = g.spmm(X)
