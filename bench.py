@@ -396,17 +396,21 @@ def main():
         # The sharded CG (N > 1) has only ever run in the driver's multi-GPU bench: if its RCCL
         # exchange hangs (or one rank fails while the others wait in a collective), the headline
         # line must still print -- rank 0 prints what it has and every rank exits.
+        # A hang is a failure: the watchdog prints the line (so the headline is on record) and
+        # exits non-zero.  The lock is held through its print and exit, and the main thread
+        # marks the CG done under the same lock, so exactly one thread ever prints.
         cg_lock, cg_state = threading.Lock(), {"done": False}
 
         def _cg_watchdog():
             with cg_lock:
                 if cg_state["done"]:
                     return
-            if d.rank == 0:
-                result["cg_error"] = f"sharded CG did not finish within {args.cg_timeout:.0f} s"
-                print(json.dumps(result), flush=True)
-            sys.stderr.flush()
-            os._exit(0)
+                if d.rank == 0:
+                    result["cg_error"] = f"sharded CG did not finish within {args.cg_timeout:.0f} s"
+                    print(json.dumps(result), flush=True)
+                print(f"rank {d.rank}: sharded CG hung (> {args.cg_timeout:.0f} s), exiting 3", file=sys.stderr)
+                sys.stderr.flush()
+                os._exit(3)
         watchdog = threading.Timer(args.cg_timeout, _cg_watchdog) if d.world > 1 else None
         if watchdog:
             watchdog.daemon = True

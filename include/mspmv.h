@@ -42,7 +42,9 @@ typedef enum mspmv_status {
     MSPMV_ERR_BREAKDOWN = 4,     /* CG: p.Ap <= 0 or non-finite (the reference has no guard) */
     MSPMV_ERR_RCCL = 5,          /* a collective failed */
     MSPMV_ERR_UNSUPPORTED = 6,   /* e.g. L outside the compiled set */
-    MSPMV_ERR_IO = 7             /* MatrixMarket read/parse failure */
+    MSPMV_ERR_IO = 7,            /* MatrixMarket read/parse failure */
+    MSPMV_ERR_STALL = 8          /* IC(0) apply: a triangular-solve dependency never became ready
+                                    (the solve stopped; X is not a solution) */
 } mspmv_status;
 
 /* Mirror of CsrMatrix<double,int> fields, sparse_matrix.h:648-653.  row_offsets has
@@ -126,7 +128,11 @@ MSPMV_API mspmv_status mspmv_dcg_single_dev(mspmv_handle h, const double *d_b, d
                                   int *iters, double *resid_hist, int hist_cap);
 /* Block multi-RHS CG, CGSolveMultiple (work_2025/main/no_pretreatment.hpp:32-197): L
  * lock-step recurrences on interleaved n x L panels, per-column converged masks
- * (alpha = beta = 0 once converged), stop when all columns converged.  max_err_hist
+ * (alpha = beta = 0 once converged), stop when all columns converged.  Breakdown is per
+ * column: a column whose p.Ap gives a non-finite alpha (e.g. a zero RHS column, 0/0) is frozen
+ * at its last finite iterate and left out of the history (the reference's column turns NaN and
+ * never converges); the other columns keep iterating, and the call returns
+ * MSPMV_ERR_BREAKDOWN with X holding every column's result.  max_err_hist
  * (optional) receives the per-iteration max over ALL columns of sqrt(r.r)/||b||
  * (:132-155).  Any L >= 1: widths outside {1, 2, 4, 8, 16} are solved as independent column
  * groups of those widths (the recurrences are per column), iteration count = the groups'
@@ -169,13 +175,20 @@ MSPMV_API mspmv_status mspmv_dpcg_spai_multi_dev(mspmv_handle a, mspmv_handle m,
 MSPMV_API mspmv_status mspmv_ic0_nnz(const mspmv_csr_d *a, int *nnz_l);
 MSPMV_API mspmv_status mspmv_ic0_factor(const mspmv_csr_d *a, int *l_row_offsets, int *l_cols, double *l_vals,
                                         double *shift);
+/* TransposeCsr (work_2025/cg/incomplete_cholesky_decomp.hpp:11-78) on the host: out_row_offsets
+ * [num_cols+1], out_cols / out_vals [num_nonzeros] receive A^T in CSR, each row's entries in
+ * ascending column order (the reference's counting sort). */
+MSPMV_API mspmv_status mspmv_csr_transpose(const mspmv_csr_d *in, int *out_row_offsets, int *out_cols,
+                                           double *out_vals);
 /* Upload L and its transpose (TransposeCsr, :11-78) for the GPU triangular solves. */
 MSPMV_API mspmv_status mspmv_ic0_create(const mspmv_csr_d *l, int device, mspmv_ic0 *out);
 MSPMV_API mspmv_status mspmv_ic0_destroy(mspmv_ic0 m);
 /* PCGSolveMultiple (work_2025/main/incomplete_cholesky.hpp:33-199) on the GPU: Z = L^-T L^-1 R by
  * two sync-free triangular solves per application (one wave per row, per-row ready flags),
  * merge-path SpMM for A P, the reference's masks and max-residual history.  A stalled solve
- * (a dependency never ready) is reported as MSPMV_ERR_BREAKDOWN, never a hang. */
+ * (a dependency never ready) stops the iteration and is reported as MSPMV_ERR_STALL, never a
+ * hang.  mspmv_ic0_create rejects a factor with an entry above the diagonal or a row without
+ * its diagonal (either would make a solve wait forever). */
 MSPMV_API mspmv_status mspmv_dpcg_ic0_multi(mspmv_handle a, mspmv_ic0 m, const double *B, double *X, int L,
                                             int max_iters, double tolerance, mspmv_spmm_kernel kernel, int *iters,
                                             double *max_err_hist, int hist_cap);
@@ -222,6 +235,12 @@ MSPMV_API mspmv_status mspmv_tile_streams(mspmv_handle h, int *tiles_cols16, int
  * reads them there (row-group tiles with at most 64 distinct columns, each repeated >= 2
  * times on average); other widths build none (0). */
 MSPMV_API mspmv_status mspmv_plan_dict_tiles(mspmv_handle h, int L, int *tiles_dict);
+/* Tiles of the L-column plan staged by node blocks (*tiles_blk): runs of consecutive rows whose
+ * column lists are prefixes of one list (FEM unknowns of one mesh node) read that list once and
+ * gather each of its x entries once for all the run's rows; the products, their LDS slots and the
+ * reduction are those of the striped staging, so results are bit-identical to it.  Tiles that
+ * hold whole rows only, <= 16 run chunks, mean run height >= ~1.7 (others: 0). */
+MSPMV_API mspmv_status mspmv_plan_block_tiles(mspmv_handle h, int L, int *tiles_blk);
 /* Each tile's in-tile reduction for L right-hand sides (num_tiles entries): 0 = merge walk
  * (one walker per thread, or per L/2 lanes), g > 0 = row groups with 2^(g-1) nonzero-parallel
  * lanes per row (times L/2 column-pair lanes for L > 1).  g = 1 sums each row sequentially in

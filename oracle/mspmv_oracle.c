@@ -467,7 +467,8 @@ ORC_EXPORT int orc_cg_multi(int num_rows, int num_nonzeros, const int *row_offse
         double max_relative_error = 0.0;
         for (int i = 0; i < L; ++i) {
             double rel_error = sqrt(rs_new[i]) / b_norms[i];
-            max_relative_error = max_relative_error > rel_error ? max_relative_error : rel_error;
+            /* std::max(max, rel) = (max < rel) ? rel : max: a NaN rel is skipped */
+            max_relative_error = max_relative_error < rel_error ? rel_error : max_relative_error;
             if (!converged[i] && rel_error < tolerance)
                 converged[i] = 1;
             if (converged[i])
@@ -564,7 +565,8 @@ ORC_EXPORT int orc_pcg_spai_multi(int num_rows, int num_nonzeros, const int *row
         double max_relative_error = 0.0;
         for (int i = 0; i < L; ++i) {
             double rel_error = sqrt(pAp[i]) / b_norms[i];
-            max_relative_error = max_relative_error > rel_error ? max_relative_error : rel_error;
+            /* std::max(max, rel) = (max < rel) ? rel : max: a NaN rel is skipped */
+            max_relative_error = max_relative_error < rel_error ? rel_error : max_relative_error;
             if (!converged[i] && rel_error < tolerance)
                 converged[i] = 1;
             if (converged[i])
@@ -784,7 +786,8 @@ ORC_EXPORT int orc_pcg_ic0_multi(int num_rows, int num_nonzeros, const int *row_
         double max_relative_error = 0.0;
         for (int i = 0; i < L; ++i) {
             double rel_error = sqrt(rn[i]) / b_norms[i];
-            max_relative_error = max_relative_error > rel_error ? max_relative_error : rel_error;
+            /* std::max(max, rel) = (max < rel) ? rel : max: a NaN rel is skipped */
+            max_relative_error = max_relative_error < rel_error ? rel_error : max_relative_error;
             if (!converged[i] && rel_error < tolerance)
                 converged[i] = 1;
             if (converged[i])

@@ -3,6 +3,7 @@
 #include "mspmv_internal.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -18,6 +19,12 @@ void set_error(const std::string &msg) { g_err = msg; }
 hipError_t launch_flush(void *p, size_t bytes, hipStream_t s);
 
 }  // namespace mspmv
+
+unsigned long long mspmv_next_generation()
+{
+    static std::atomic<unsigned long long> next{1};
+    return next.fetch_add(1, std::memory_order_relaxed);
+}
 
 using namespace mspmv;
 
@@ -89,6 +96,7 @@ static void free_plan(TilePlan &p)
     dev_free(p.d_dict);
     dev_free(p.d_ndict);
     dev_free(p.d_idx16);
+    dev_free(p.d_blk);
 }
 
 // Build (once) the tile plan for L right-hand sides, validating on the host every bound the
@@ -227,6 +235,29 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
             dev_free(p.d_cols16);
             p.d_colbase = nullptr;
             p.d_cols16 = nullptr;
+        }
+    }
+    // node blocks: single-RHS plan on the 16-bit stream only (the runs' pattern columns are read there)
+    if (tile == tile_items_for(1) && p.d_cols16 && spmv_blocks_enabled()) {
+        if ((st = dev_alloc(&p.d_blk, (size_t)T * kBlkPerTile)) != MSPMV_OK)
+            return fail(st);
+        e = launch_build_blocks(h->d_row_offsets, h->d_cols, p.d_bounds, p.d_split, p.d_colbase, T, p.d_blk,
+                                h->stream);
+        std::vector<uint4> hb0((size_t)T);
+        if (e == hipSuccess)  // entry 0 of every tile: its run count
+            e = hipMemcpy2DAsync(hb0.data(), sizeof(uint4), p.d_blk, sizeof(uint4) * kBlkPerTile, sizeof(uint4), T,
+                                 hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) {
+            set_error(std::string("node blocks: ") + hipGetErrorString(e));
+            return fail(MSPMV_ERR_HIP);
+        }
+        for (const uint4 &d : hb0)
+            p.num_tiles_blk += ((d.y >> 16) & 255u) > 0;
+        if (p.num_tiles_blk == 0) {
+            dev_free(p.d_blk);
+            p.d_blk = nullptr;
         }
     }
     // multi-RHS: only the L = 16 plan (k_spmm_tile's DICT path runs at L = 16 only)
@@ -769,7 +800,9 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
             reinterpret_cast<const void *>((intptr_t)L), reinterpret_cast<const void *>((intptr_t)nblk),
             reinterpret_cast<const void *>((intptr_t)use_cap), hm, mplan,
             hm ? (const void *)hm->d_vals : nullptr, ic, ic ? (const void *)ic->d_y : nullptr,
-            ic ? (const void *)ic->d_lva : nullptr};
+            ic ? (const void *)ic->d_lva : nullptr,
+            reinterpret_cast<const void *>((uintptr_t)(hm ? hm->gen : 0)),
+            reinterpret_cast<const void *>((uintptr_t)(ic ? ic->gen : 0))};
         if (!h->cg_exec || h->cg_graph_key != key) {
             if (h->cg_exec)
                 (void)hipGraphExecDestroy(h->cg_exec);
@@ -875,11 +908,15 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
             HIP_TRY(hipMemcpy(hist, h->d_hist, sizeof(double) * nh, hipMemcpyDeviceToHost));
     }
     if (fin.breakdown == 2) {
+        if (iters)
+            *iters = fin.iter;
         set_error("IC(0) apply: a triangular-solve dependency never became ready (solve stalled)");
-        return MSPMV_ERR_BREAKDOWN;
+        return MSPMV_ERR_STALL;
     }
     if (fin.breakdown) {
-        set_error("CG breakdown: p.Ap gave a non-finite alpha at iteration " + std::to_string(it));
+        set_error(L == 1 ? "CG breakdown: p.Ap gave a non-finite alpha at iteration " + std::to_string(it)
+                         : "CG breakdown: p.Ap gave a non-finite alpha in at least one column (frozen; the "
+                           "other columns were solved)");
         return MSPMV_ERR_BREAKDOWN;
     }
     return MSPMV_OK;
@@ -909,6 +946,7 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
     std::vector<std::vector<double>> gh;
     std::vector<int> git;
     int total = 0;
+    bool broke = false;  // a group's CG broke down: keep solving the other groups, report it at the end
     for (int c0 = 0; c0 < L && st == MSPMV_OK;) {
         const int w = native_chunk(L - c0);
         hipError_t e = launch_panel_copy(d_b + c0, L, gb, w, (long long)m, w, w, h->stream);
@@ -920,7 +958,11 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
         std::vector<double> hg((size_t)cap);
         int it = 0;
         st = cg_solve_native(h, gb, gx, w, max_iters, tol, &it, cap ? hg.data() : nullptr, cap, hm, ic);
-        if (st == MSPMV_OK || st == MSPMV_ERR_BREAKDOWN) {
+        if (st == MSPMV_ERR_BREAKDOWN) {
+            broke = true;
+            st = MSPMV_OK;
+        }
+        if (st == MSPMV_OK) {
             e = launch_panel_copy(gx, w, d_x + c0, L, (long long)m, w, w, h->stream);
             if (e == hipSuccess)
                 e = hipStreamSynchronize(h->stream);
@@ -936,6 +978,11 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
     }
     dev_free(gb);
     dev_free(gx);
+    if (st == MSPMV_OK && broke) {
+        set_error("CG breakdown: p.Ap gave a non-finite alpha in at least one column (frozen; the other "
+                  "columns were solved)");
+        st = MSPMV_ERR_BREAKDOWN;
+    }
     if (iters)
         *iters = total;
     for (int k = 0; k < std::min(total, cap); ++k) {
@@ -1045,6 +1092,20 @@ mspmv_status mspmv_ic0_create(const mspmv_csr_d *l, int device, mspmv_ic0 *out)
     for (int k = 0; k < nnz; ++k)
         if (l->column_indices[k] < 0 || l->column_indices[k] >= n)
             return invalid("column index out of range");
+    // A lower-triangular factor with every diagonal present (IncompleteCholesky keeps A's lower
+    // pattern, diagonal included): an entry above the diagonal would make the forward solve wait
+    // on a row of a later level, a missing diagonal would divide by zero -- reject both here
+    // rather than stall on the GPU.
+    for (int r = 0; r < n; ++r) {
+        bool diag = false;
+        for (int k = l->row_offsets[r]; k < l->row_offsets[r + 1]; ++k) {
+            if (l->column_indices[k] > r)
+                return invalid("IC(0) factor has an entry above the diagonal in row " + std::to_string(r));
+            diag = diag || l->column_indices[k] == r;
+        }
+        if (!diag)
+            return invalid("IC(0) factor row " + std::to_string(r) + " has no diagonal entry");
+    }
     // TransposeCsr (incomplete_cholesky_decomp.hpp:11-78): counting sort by column, rows in order
     std::vector<int> uro((size_t)n + 1, 0), uci((size_t)std::max(nnz, 1));
     std::vector<double> uva((size_t)std::max(nnz, 1));
@@ -1382,6 +1443,19 @@ mspmv_status mspmv_tile_streams(mspmv_handle h, int *tiles_cols16, int *tiles_di
         *tiles_cols16 = plan->d_cols16 ? plan->num_tiles16 : 0;
     if (tiles_dict)
         *tiles_dict = plan->d_dict ? plan->num_tiles_dict : 0;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_plan_block_tiles(mspmv_handle h, int L, int *tiles_blk)
+{
+    ST_TRY(check_handle(h));
+    if (!tiles_blk)
+        return invalid("null out pointer");
+    if (!supported_L(L))
+        return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
+    const TilePlan *plan = nullptr;
+    ST_TRY(get_plan(h, L, &plan));
+    *tiles_blk = plan->d_blk ? plan->num_tiles_blk : 0;
     return MSPMV_OK;
 }
 

@@ -144,3 +144,40 @@ extern "C" MSPMV_API mspmv_status mspmv_ic0_factor(const mspmv_csr_d *a, int *l_
     mspmv::set_error("ic0: Incomplete Cholesky factorization failed after 20 attempts");
     return MSPMV_ERR_BREAKDOWN;
 }
+
+// TransposeCsr (work_2025/cg/incomplete_cholesky_decomp.hpp:11-78): counting sort by column with
+// rows visited in order, so each output row lists its entries by ascending input row, as the
+// reference's.  Host code (setup of the IC(0) preconditioner, as in the reference).
+extern "C" MSPMV_API mspmv_status mspmv_csr_transpose(const mspmv_csr_d *in, int *out_row_offsets, int *out_cols,
+                                                      double *out_vals)
+{
+    if (!in || in->num_rows < 0 || in->num_cols < 0 || in->num_nonzeros < 0 || !in->row_offsets ||
+        !out_row_offsets || (in->num_nonzeros > 0 && (!in->column_indices || !in->values || !out_cols || !out_vals))) {
+        mspmv::set_error("csr_transpose: bad arguments");
+        return MSPMV_ERR_INVALID;
+    }
+    const int m = in->num_rows, n = in->num_cols, nnz = in->num_nonzeros;
+    if (in->row_offsets[0] != 0 || in->row_offsets[m] != nnz) {
+        mspmv::set_error("csr_transpose: row_offsets inconsistent with num_nonzeros");
+        return MSPMV_ERR_INVALID;
+    }
+    for (int k = 0; k < nnz; ++k)
+        if (in->column_indices[k] < 0 || in->column_indices[k] >= n) {
+            mspmv::set_error("csr_transpose: column index out of range");
+            return MSPMV_ERR_INVALID;
+        }
+    std::vector<int> pos((size_t)n + 1, 0);
+    for (int k = 0; k < nnz; ++k)
+        ++pos[(size_t)in->column_indices[k] + 1];
+    for (int c = 0; c < n; ++c)
+        pos[(size_t)c + 1] += pos[c];
+    for (int c = 0; c <= n; ++c)
+        out_row_offsets[c] = pos[c];
+    for (int r = 0; r < m; ++r)
+        for (int k = in->row_offsets[r]; k < in->row_offsets[r + 1]; ++k) {
+            const int d = pos[in->column_indices[k]]++;
+            out_cols[d] = r;
+            out_vals[d] = in->values[k];
+        }
+    return MSPMV_OK;
+}

@@ -58,6 +58,10 @@ struct TilePlan {
     int *d_ndict = nullptr;             // [num_tiles]
     unsigned short *d_idx16 = nullptr;  // [nnz + kNnzPad]
     int num_tiles_dict = 0;             // tiles that gather through their dictionary
+    // Single-RHS plans: node-block run descriptors (k_build_blocks), kBlkMax (16) per tile, entry 0
+    // of a tile holding its count (0: striped staging).  Null when no tile qualifies.
+    uint4 *d_blk = nullptr;             // [num_tiles * 16]
+    int num_tiles_blk = 0;              // tiles staged by node blocks
 };
 
 // Device-resident CG scalars (one set per right-hand side column).
@@ -82,7 +86,13 @@ struct CgControl {
 
 }  // namespace mspmv
 
+// Every handle and IC(0) factor gets a process-unique generation number at creation, so a cached
+// CG graph that baked in another object's buffers is never replayed against a new object the
+// allocator happened to place at the same address (mspmv_api.hip, cg_solve_native).
+unsigned long long mspmv_next_generation();
+
 struct mspmv_handle_s {
+    unsigned long long gen = mspmv_next_generation();
     int device = 0;
     int num_cus = 256;
     hipStream_t stream = nullptr;
@@ -123,6 +133,7 @@ struct mspmv_handle_s {
 // IC(0) factor on the device (mspmv_ic0_create): L and its transpose for the two sync-free
 // triangular solves of the preconditioner apply, their ready flags and the intermediate Y.
 struct mspmv_ic0_s {
+    unsigned long long gen = mspmv_next_generation();
     int device = 0;
     int n = 0, nnz = 0;
     int *d_lro = nullptr, *d_lci = nullptr;  // L (lower, diagonal last in each row)
@@ -153,6 +164,12 @@ hipError_t launch_pack_cols16(const int *d_cols, const int2 *d_bounds, int num_t
                               unsigned short *d_cols16, hipStream_t s);
 bool spmv_cols16_enabled();
 bool spmv_dict_enabled();
+// Node blocks (runs of rows sharing one column list) for the single-RHS plan; needs cols16.
+bool spmv_blocks_enabled();
+constexpr int kBlkPerTile = 16;  // == kBlkMax in the kernels
+hipError_t launch_build_blocks(const int *d_row_offsets, const int *d_cols, const int2 *d_bounds,
+                               const unsigned char *d_split, const int *d_colbase, int num_tiles, uint4 *d_blk,
+                               hipStream_t s);
 hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_tiles, int max_items, int *d_dict,
                              int *d_ndict, unsigned short *d_idx16, hipStream_t s, bool multi);
 bool spmm_dict_enabled();

@@ -462,6 +462,91 @@ __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ c
     }
 }
 
+// ---- node blocks (plan time, single-RHS plans) --------------------------------------------
+// FEM matrices store several unknowns per mesh node (pwtk: 6 DOF), and every row of a node lists
+// the same columns.  A tile whose rows come in such runs -- consecutive rows whose column lists
+// are prefixes of one list P (equal lists included; a row shortened by the matrix edge too) --
+// stages them "column-owner" style: lane j reads P[j] once, gathers x[P[j]] once and multiplies
+// it into every row of the run.  Only P's 16-bit column offsets cross HBM (1/h of the tile's
+// column stream) and there is one gather per distinct (run, column) instead of one per nonzero.
+// The products land in the same LDS slots as the striped staging writes, so the reduction --
+// and every result bit -- is unchanged.
+//
+// Descriptor of one run chunk (16 B; at most kBlkMax per tile, tile t's at blk[t * kBlkMax ..]):
+//   x: vofs (nonzero offset of the run's first row in the tile, bits 0-15) | j0 (first pattern
+//      column of this chunk, 16-23) | wc (chunk width <= 64, 24-31)
+//   y: h (rows, <= 8, bits 0-7) | p (row holding P, 8-15) | nd (descriptor count, in entry 0 only,
+//      16-23; 0 = the tile stages the plain way)
+//   z, w: the h row lengths, 8 bits each (rows of a run are <= 255 long)
+constexpr int kBlkMax = 16;
+constexpr int kBlkRows = 8;
+
+__device__ __forceinline__ int blk_len(const uint4 &d, int i)
+{
+    return (int)(((i < 4 ? d.z : d.w) >> (8 * (i & 3))) & 255u);
+}
+
+// One thread per tile.  A tile qualifies when it holds whole rows only (no split boundary), is on
+// the 16-bit column stream, fits in kBlkMax chunks, and its runs share columns enough to pay: the
+// pattern columns summed over its runs at most 3/5 of its nonzeros (mean run height >= ~1.7).
+__global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *__restrict__ cols,
+                               const int2 *__restrict__ bounds, const unsigned char *__restrict__ split,
+                               const int *__restrict__ colbase, int num_tiles, uint4 *__restrict__ blk)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= num_tiles)
+        return;
+    uint4 *out = blk + (size_t)t * kBlkMax;
+    out[0] = make_uint4(0, 0, 0, 0);
+    const int2 b0 = bounds[t], b1 = bounds[t + 1];
+    const int r0 = b0.x, r1 = b1.x, n0 = b0.y, n1 = b1.y;
+    if (split[t] || split[t + 1] || colbase[t] < 0 || n1 <= n0 || row_offsets[r0] != n0 || row_offsets[r1] != n1)
+        return;
+    uint4 d[kBlkMax];
+    int nd = 0, sum_w = 0;
+    int r = r0;
+    while (r < r1) {
+        const int g = r, gs = row_offsets[g];
+        int p = g, plen = row_offsets[g + 1] - gs;
+        unsigned lens[2] = {0u, 0u};
+        int h = 0;
+        for (; r < r1 && h < kBlkRows; ++r, ++h) {
+            const int s = row_offsets[r], len = row_offsets[r + 1] - s;
+            if (len > 255)
+                return;
+            if (h > 0) {  // a prefix of P, or P a prefix of it
+                const int ps = row_offsets[p], m = min(len, plen);
+                bool same = true;
+                for (int q = 0; q < m && same; ++q)
+                    same = cols[s + q] == cols[ps + q];
+                if (!same)
+                    break;
+                if (len > plen) {
+                    p = r;
+                    plen = len;
+                }
+            }
+            lens[h >> 2] |= (unsigned)len << (8 * (h & 3));
+        }
+        sum_w += plen;
+        const int vofs = gs - n0;
+        for (int j0 = 0; j0 < plen || (j0 == 0 && plen == 0); j0 += 64) {
+            if (nd == kBlkMax || j0 > 255)
+                return;
+            const int wc = min(64, plen - j0);
+            d[nd++] = make_uint4((unsigned)vofs | ((unsigned)j0 << 16) | ((unsigned)wc << 24),
+                                 (unsigned)h | ((unsigned)(p - g) << 8), lens[0], lens[1]);
+            if (plen == 0)
+                break;
+        }
+    }
+    if (5 * sum_w > 3 * (n1 - n0))
+        return;
+    d[0].y |= (unsigned)nd << 16;
+    for (int i = nd - 1; i >= 0; --i)  // entry 0 last: nd > 0 only once the tile's set is complete
+        out[i] = d[i];
+}
+
 // Per-tile choice of the in-tile reduction (one thread per tile, at plan time; gl = lanes per
 // nonzero: 1 for SpMV, L/2 column-pair lanes for SpMM).  The tile's row segments -- its complete rows plus the trailing partial row of a
 // split boundary -- are either summed by row groups of G = 2^lg lanes (mode lg + 1) or, when
@@ -540,6 +625,8 @@ struct TileArgs {
     // single-RHS plans: per-tile 16-bit column offsets (TilePlan::d_colbase / d_cols16; null: off)
     const int *colbase;
     const unsigned short *cols16;
+    // single-RHS plans with node blocks (TilePlan::d_blk, k_build_blocks; null: off)
+    const uint4 *blk;
     // single-RHS plans with column dictionaries (TilePlan::d_dict; null: off)
     const int *dict;
     const int *ndict;
@@ -692,6 +779,98 @@ __device__ __forceinline__ void dict_stage(const TileArgs &a, double *s_prod, in
         const int k = tid + j * TB;
         if (k < nnzt)
             s_prod[pslot(k)] = pr[j];
+    }
+}
+
+// Node-block staging (k_build_blocks): wave w takes the tile's run chunks w, w + 4, ..., two per
+// round.  Per chunk, lane l owns pattern column j = j0 + l: one 16-bit column offset of row P,
+// one gather (x, or CG's {r, p}), and the values of that column in every row of the run that is
+// long enough -- all of a round's loads issued before any is consumed.  The products
+// val * x[col] (CG: val * (r + beta p)) go to the tile's usual LDS slots.  `head` runs once
+// between the first round's loads and its products (CG: stop test + beta, as the striped path).
+template <bool CG>
+struct BlkRegs {
+    int c[2];
+    double v[2][kBlkRows];
+    double xv[2];
+    double pv[CG ? 2 : 1];
+};
+
+__device__ __forceinline__ uint4 blk_read(const uint4 &bd, int di)
+{
+    return make_uint4((unsigned)__builtin_amdgcn_readlane((int)bd.x, di),
+                      (unsigned)__builtin_amdgcn_readlane((int)bd.y, di),
+                      (unsigned)__builtin_amdgcn_readlane((int)bd.z, di),
+                      (unsigned)__builtin_amdgcn_readlane((int)bd.w, di));
+}
+
+template <bool CG, bool NT, int TB, typename Head>
+__device__ __forceinline__ void blk_stage(const TileArgs &a, const uint4 &bd, int nd, int n0, int colbase,
+                                          double *s_prod, double &beta, Head &&head)
+{
+    constexpr int NW = TB / 64;  // waves sharing the tile
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    for (int round = 0; round * 2 * NW < nd; ++round) {
+        BlkRegs<CG> st;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int di = wave + NW * (2 * round + s);
+            st.c[s] = 0;
+#pragma unroll
+            for (int i = 0; i < kBlkRows; ++i)
+                st.v[s][i] = 0.0;
+            if (di < nd) {  // wave-uniform
+                const uint4 d = blk_read(bd, di);
+                const int vofs = d.x & 0xffff, j0 = (d.x >> 16) & 255, wc = d.x >> 24;
+                const int h = d.y & 255, p = (d.y >> 8) & 255;
+                const int j = j0 + lane;
+                int start = 0, pstart = 0;
+#pragma unroll
+                for (int i = 0; i < kBlkRows; ++i) {
+                    pstart = i == p ? start : pstart;
+                    const int len = blk_len(d, i);
+                    if (i < h && j < len)
+                        st.v[s][i] = ld_stream<NT>(a.vals + n0 + vofs + start + j);
+                    start += i < h ? len : 0;
+                }
+                if (lane < wc)
+                    st.c[s] = colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + j);
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            if constexpr (CG) {
+                const double2 v = cg_rp(a, st.c[s]);
+                st.xv[s] = v.x;
+                st.pv[s] = v.y;
+            } else {
+                st.xv[s] = a.x[st.c[s]];
+            }
+        }
+        if (round == 0 && !head())
+            return;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int di = wave + NW * (2 * round + s);
+            if (di < nd) {
+                const uint4 d = blk_read(bd, di);
+                const int vofs = d.x & 0xffff, j0 = (d.x >> 16) & 255;
+                const int h = d.y & 255;
+                const int j = j0 + lane;
+                double x = st.xv[s];
+                if (CG)
+                    x = x + beta * st.pv[s];
+                int start = 0;
+#pragma unroll
+                for (int i = 0; i < kBlkRows; ++i) {
+                    const int len = blk_len(d, i);
+                    if (i < h && j < len)
+                        s_prod[pslot(vofs + start + j)] = st.v[s][i] * x;
+                    start += i < h ? len : 0;
+                }
+            }
+        }
     }
 }
 
@@ -1062,8 +1241,19 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
             go = cg1_head(a, part_sum(pin, sm.red), beta);
     };
     const int colbase = a.cols16 ? a.colbase[t] : -1;
+    // node-block descriptors of this tile, loaded beside its bounds (entry 0 holds the count)
+    uint4 bd = make_uint4(0u, 0u, 0u, 0u);
+    if (a.blk && (tid & 63) < kBlkMax)
+        bd = a.blk[(size_t)t * kBlkMax + (tid & 63)];
+    const int nblk = a.blk ? (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 16) & 255u) : 0;
     bool staged = false;
-    if constexpr (MODE == kModeSpmv) {
+    if (nblk > 0) {
+        blk_stage<CG, NT, TB>(a, bd, nblk, n0, colbase, sm.prod, beta, [&]() {
+            head();
+            return go;
+        });
+        staged = true;
+    } else if constexpr (MODE == kModeSpmv) {
         const int nd = a.dict ? a.ndict[t] : 0;  // > 0: this tile gathers through its dictionary
         if (nd > 0) {
             if (nnzt <= TILE)
@@ -1598,6 +1788,10 @@ k_spmm_tile(TileArgs a)
     }
 }
 
+// Per-column state in CgVecArgs::conv / TileArgs::conv: 0 iterating, 1 converged (the
+// reference's converged[] mask), kConvBroken = p.Ap gave a non-finite alpha (frozen).
+constexpr unsigned char kConvBroken = 2;
+
 // What the fold's last block derives from the totals (k_fold_dot `mode`).
 enum : int { kFoldDot = 0, kFoldCgAlpha = 1, kFoldPcgAlpha = 2, kFoldPcgBeta = 3, kFoldPcgInit = 4 };
 
@@ -1630,11 +1824,15 @@ __global__ __launch_bounds__(kBlock) void k_fold_dot(const double *part, int T, 
         const double d = s_out[tid];
         dot_out[tid] = d;
         if (mode == kFoldCgAlpha && !conv[tid]) {
+            // Per-column breakdown (no_pretreatment.hpp:109-120 has no guard: a zero RHS column
+            // gives alpha = 0/0 and a NaN column that never converges).  The column is frozen
+            // (conv = kConvBroken: alpha = beta = 0 from here on, x and r keep their last finite
+            // values, left out of the max-error history as the reference's NaN is) and the
+            // other columns keep iterating.
             const double alpha = scal[tid].rs_old / d;
             if (!(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
+                const_cast<unsigned char *>(conv)[tid] = kConvBroken;
                 ctrl->breakdown = 1;
-                ctrl->done = 1;
-                ctrl->iters_out = ctrl->iter + 1;
             }
         } else if (mode == kFoldPcgAlpha) {  // sparse_approximate_inverse.hpp:131-138
             CgScalars &s = scal[tid];
@@ -1646,6 +1844,18 @@ __global__ __launch_bounds__(kBlock) void k_fold_dot(const double *part, int T, 
             s.rs_old = d;
         } else if (mode == kFoldPcgInit) {  // :99-100
             scal[tid].rs_old = d;
+        }
+    }
+    if (mode == kFoldCgAlpha) {
+        __syncthreads();
+        if (tid == 0 && ctrl->breakdown) {  // every column converged or broken: stop here
+            int live = 0;
+            for (int j = 0; j < L; ++j)
+                live += conv[j] == 0;
+            if (live == 0) {
+                ctrl->done = 1;
+                ctrl->iters_out = ctrl->iter + 1;
+            }
         }
     }
 }
@@ -1812,10 +2022,16 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(CgVecArgs a)
     const long long stride = (long long)gridDim.x * kBlock;
     const long long i0 = (long long)blockIdx.x * kBlock + tid;
     double2 al;
-    if (a.red_in) {  // sharded: alpha_j = rs_old_j / (all-reduced p.Ap)_j, masked (no_pretreatment.hpp:109-120)
+    if (a.red_in) {  // alpha_j = rs_old_j / (reduced p.Ap)_j, masked (no_pretreatment.hpp:109-120)
+        // A non-finite alpha (breakdown of column j) applies as 0: x_j and r_j stay finite and
+        // the column is frozen (k_fold_dot on one GPU, k_dist_finish when sharded).
+        auto masked = [&](int j) {
+            const double al = a.conv[j] ? 0.0 : a.scal[j].rs_old / a.red_in[j];
+            return (al == al && fabs(al) < HUGE_VAL) ? al : 0.0;
+        };
         const int j0 = L == 1 ? 0 : 2 * (int)(i0 % GL);
-        al.x = a.conv[j0] ? 0.0 : a.scal[j0].rs_old / a.red_in[j0];
-        al.y = L == 1 ? al.x : (a.conv[j0 + 1] ? 0.0 : a.scal[j0 + 1].rs_old / a.red_in[j0 + 1]);
+        al.x = masked(j0);
+        al.y = L == 1 ? al.x : masked(j0 + 1);
     } else if (L == 1) {
         al.x = a.scal[0].alpha;
         al.y = al.x;
@@ -1863,10 +2079,13 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(CgVecArgs a)
                 const double rs_new = s_out[j];
                 s.rs_new = rs_new;
                 const double rel = sqrt(rs_new) / s.b_norm;
-                maxrel = maxrel > rel ? maxrel : rel;  // std::max(max, rel): NaN rel is skipped
+                // std::max(max, rel): a NaN rel is skipped -- as is a broken-down column, whose
+                // reference counterpart is NaN from its breakdown on
+                if (a.conv[j] != kConvBroken)
+                    maxrel = maxrel < rel ? rel : maxrel;  // std::max: a NaN rel is skipped
                 if (!a.conv[j] && rel < a.tol)
                     a.conv[j] = 1;
-                nconv += a.conv[j];
+                nconv += a.conv[j] != 0;
             }
             if (a.hist && iter < a.hist_cap)
                 a.hist[iter] = maxrel;
@@ -2003,8 +2222,10 @@ __global__ __launch_bounds__(kBlock) void k_trsv(const int *__restrict__ ro, con
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0) {
         __hip_atomic_store(&ready[i], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (!ok)
-            ctrl->breakdown = 2;  // a dependency never became ready (reported, never hung)
+        if (!ok) {  // a dependency never became ready: reported (MSPMV_ERR_STALL), never hung;
+            ctrl->breakdown = 2;  // later waves and launches see done and return at once
+            __hip_atomic_store(&ctrl->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -2070,8 +2291,10 @@ __global__ __launch_bounds__(kBlock) void k_trsv_tagged(const int *__restrict__ 
         const double xi = (!FWD && diag == 0.0) ? 0.0 : (bi - sum) / diag;
         store_sc1(&x[(size_t)i * L + v], xi);
     }
-    if (__ballot(!ok) != 0 && lane == 0)
-        ctrl->breakdown = 2;  // a dependency never arrived (reported, never hung)
+    if (__ballot(!ok) != 0 && lane == 0) {  // a dependency never arrived: MSPMV_ERR_STALL, never hung
+        ctrl->breakdown = 2;
+        __hip_atomic_store(&ctrl->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // R.Z per column and the PCG scalars after it (PCGSolveMultiple): mode 0 (init, :96-104)
@@ -2129,16 +2352,15 @@ __global__ void k_dist_finish(CgVecArgs a)
     if (threadIdx.x != 0 || a.ctrl->done)
         return;
     const int iter = a.ctrl->iter;
+    // The update (k_cg_update with red_in) already applied alpha = 0 to broken columns: their
+    // x and r stay as they were; here they are marked and frozen (k_fold_dot's rule, per column).
     for (int j = 0; j < L; ++j) {
         if (a.conv[j])
             continue;
         const double alpha = a.scal[j].rs_old / a.red_in[j];
         if (!(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
             a.ctrl->breakdown = 1;
-            a.ctrl->done = 1;
-            a.ctrl->iters_out = iter + 1;
-            a.ctrl->iter = iter + 1;
-            return;
+            a.conv[j] = kConvBroken;
         }
     }
     int nconv = 0;
@@ -2148,10 +2370,11 @@ __global__ void k_dist_finish(CgVecArgs a)
         const double rs_new = a.red_out[j];
         s.rs_new = rs_new;
         const double rel = sqrt(rs_new) / s.b_norm;
-        maxrel = maxrel > rel ? maxrel : rel;
+        if (a.conv[j] != kConvBroken)
+            maxrel = maxrel < rel ? rel : maxrel;  // std::max: a NaN rel is skipped
         if (!a.conv[j] && rel < a.tol)
             a.conv[j] = 1;
-        nconv += a.conv[j];
+        nconv += a.conv[j] != 0;
     }
     if (a.hist && iter < a.hist_cap)
         a.hist[iter] = maxrel;
@@ -2192,6 +2415,7 @@ struct SpmvTuning {
     int tb = 256;     // threads per single-RHS SpMV tile: 256 (workgroup tiles) or 64 (one-wave tiles)
     int tile_items = 0;  // single-RHS nominal merge items per tile (0: tb * ipt; smaller: fewer per thread)
     int trsv_tagged = 1;  // IC(0) solves: data-tagged values (1) or ready flags (0)
+    int blocks = 1;   // single-RHS tiles staged by node blocks where rows share columns (k_build_blocks)
     int dict = 1;     // single-RHS SpMV through per-tile column dictionaries (k_build_dict) when
                       // a tile's nonzeros repeat its distinct columns >= dict_ratio times (0: off)
 };
@@ -2221,6 +2445,8 @@ static const SpmvTuning &spmv_tuning()
             v.spmm_rg_cost = atoi(e);
         if (const char *e = getenv("MSPMV_SPMV_C16"))
             v.cols16 = atoi(e) != 0;
+        if (const char *e = getenv("MSPMV_SPMV_BLOCKS"))
+            v.blocks = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMV_DICT"))
             v.dict = atoi(e) > 0 ? atoi(e) : 0;
         if (const char *e = getenv("MSPMV_TRSV_TAGGED"))
@@ -2290,6 +2516,19 @@ hipError_t launch_pack_cols16(const int *d_cols, const int2 *d_bounds, int num_t
 
 bool spmv_cols16_enabled() { return spmv_tuning().cols16 != 0; }
 bool spmv_dict_enabled() { return spmv_tuning().dict > 0; }
+bool spmv_blocks_enabled() { return spmv_tuning().blocks != 0; }
+
+hipError_t launch_build_blocks(const int *d_row_offsets, const int *d_cols, const int2 *d_bounds,
+                               const unsigned char *d_split, const int *d_colbase, int num_tiles, uint4 *d_blk,
+                               hipStream_t s)
+{
+    static_assert(kBlkMax == kBlkPerTile, "descriptor stride");
+    if (num_tiles <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_build_blocks, dim3((num_tiles + 127) / 128), dim3(128), 0, s, d_row_offsets, d_cols, d_bounds,
+                       d_split, d_colbase, num_tiles, d_blk);
+    return hipGetLastError();
+}
 
 bool spmm_dict_enabled()
 {
@@ -2358,6 +2597,7 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
     if (L == 1) {
         a.colbase = plan.d_colbase;
         a.cols16 = plan.d_cols16;
+        a.blk = plan.d_blk;
     }
     a.dict = plan.d_dict;
     a.ndict = plan.d_ndict;

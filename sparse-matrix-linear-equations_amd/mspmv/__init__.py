@@ -29,7 +29,11 @@ SIMPLE, MERGE, NONZERO_SPLIT = 0, 1, 2  # SpmmKernel, work_2025/types.hpp:11-16
 
 STATUS = {
     0: "OK", 1: "INVALID", 2: "HIP", 3: "OOM", 4: "BREAKDOWN", 5: "RCCL", 6: "UNSUPPORTED", 7: "IO",
+    8: "STALL",
 }
+# CG calls return their status beside X: BREAKDOWN (4) is a per-column numerical event (the
+# frozen columns are reported, the others solved), so it is returned, not raised; everything
+# else -- STALL (8, an IC(0) triangular solve that never progressed) included -- raises.
 SUPPORTED_L = (1, 2, 4, 8, 16)  # native tile-kernel widths; SpMM and the CGs take any L >= 1
 # (column chunks / groups of these widths; the sharded CG and the timing helpers native only)
 
@@ -86,6 +90,7 @@ _SIGS = {
     "mspmv_ic0_nnz": (_I, [ctypes.POINTER(_CsrD), _PI]),
     "mspmv_ic0_factor": (_I, [ctypes.POINTER(_CsrD), _P, _P, _P, _PD]),
     "mspmv_ic0_create": (_I, [ctypes.POINTER(_CsrD), _I, ctypes.POINTER(_P)]),
+    "mspmv_csr_transpose": (_I, [ctypes.POINTER(_CsrD), _P, _P, _P]),
     "mspmv_ic0_destroy": (_I, [_P]),
     "mspmv_dpcg_ic0_multi": (_I, [_P, _P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
     "mspmv_dpcg_ic0_multi_dev": (_I, [_P, _P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
@@ -98,6 +103,7 @@ _SIGS = {
     "mspmv_tile_plan": (_I, [_P, _I, _PI, _PI, _PI, ctypes.POINTER(Coord)]),
     "mspmv_tile_streams": (_I, [_P, _PI, _PI]),
     "mspmv_plan_dict_tiles": (_I, [_P, _I, _PI]),
+    "mspmv_plan_block_tiles": (_I, [_P, _I, _PI]),
     "mspmv_tile_modes": (_I, [_P, _I, _P]),
     "mspmv_spmv_kernel_name": (ctypes.c_char_p, [_P]),
     "mspmv_device_malloc": (_I, [_I, _SZ, ctypes.POINTER(_P)]),
@@ -370,6 +376,12 @@ class GpuCsr:
         """The single-RHS SpMV kernel instantiation used for this matrix (rocprofv3's name)."""
         return lib.mspmv_spmv_kernel_name(self.h).decode()
 
+    def plan_block_tiles(self, L: int = 1) -> int:
+        """Tiles of the L-column plan staged by node blocks (mspmv_plan_block_tiles)."""
+        n = ctypes.c_int()
+        _check(lib.mspmv_plan_block_tiles(self.h, L, ctypes.byref(n)), "plan_block_tiles")
+        return n.value
+
     def spmv(self, x: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(x, np.float64)
         assert x.shape == (self.num_cols,)
@@ -527,6 +539,15 @@ def time_spmm_batch(gs, dXs, dYs, L: int, reps: int):
 # ----------------------------------------------------------------------------------------
 # the reference's operator names (drop-in facade)
 # ----------------------------------------------------------------------------------------
+def _note_breakdown(st: int, where: str) -> None:
+    """The reference-named solvers return an iteration count only, as the reference's do; a CG
+    breakdown (non-finite alpha in some column: that column frozen, the others solved) is
+    surfaced as a RuntimeWarning instead of passing silently."""
+    if st == 4:
+        import warnings
+        warnings.warn(f"{where}: {lib.mspmv_last_error().decode(errors='replace')}", RuntimeWarning, stacklevel=3)
+
+
 def _gpu(a: CsrMatrix) -> GpuCsr:
     g = getattr(a, "_gpu", None)
     if g is None or g.h is None:
@@ -549,7 +570,8 @@ def OmpMergeCsrmm(num_threads, a: CsrMatrix, row_end_offsets, column_indices, va
 
 def CGSolveSingle(a: CsrMatrix, b, x, max_iters: int, tolerance: float) -> int:
     """work_2025/main/single_strategy.hpp:102-170; returns the iteration count."""
-    xs, it, _, _ = _gpu(a).cg_single(b, max_iters, tolerance)
+    xs, it, _, st = _gpu(a).cg_single(b, max_iters, tolerance)
+    _note_breakdown(st, "CGSolveSingle")
     x[:] = xs
     return it
 
@@ -559,7 +581,8 @@ def CGSolveMultiple(a: CsrMatrix, B, X, num_vectors: int, max_iters: int, tolera
     """work_2025/main/no_pretreatment.hpp:32-197 on flat interleaved n x num_vectors panels."""
     Bm = np.asarray(B, np.float64).reshape(a.num_rows, num_vectors)
     cap = max_iters if max_errors is not None else 0
-    Xs, it, hist, _ = _gpu(a).cg_multi(Bm, max_iters, tolerance, kernel_type, hist_cap=cap)
+    Xs, it, hist, st = _gpu(a).cg_multi(Bm, max_iters, tolerance, kernel_type, hist_cap=cap)
+    _note_breakdown(st, "CGSolveMultiple")
     X[:] = Xs.reshape(-1)
     if max_errors is not None:
         max_errors.clear()
@@ -578,7 +601,8 @@ def SPAISolveMultiple(a: CsrMatrix, m: CsrMatrix, B, X, num_vectors: int, max_it
     """work_2025/main/sparse_approximate_inverse.hpp:30-230 on flat interleaved n x num_vectors panels."""
     Bm = np.asarray(B, np.float64).reshape(a.num_rows, num_vectors)
     cap = max_iters if max_errors is not None else 0
-    Xs, it, hist, _ = _gpu(a).pcg_spai(_gpu(m), Bm, max_iters, tolerance, hist_cap=cap)
+    Xs, it, hist, st = _gpu(a).pcg_spai(_gpu(m), Bm, max_iters, tolerance, hist_cap=cap)
+    _note_breakdown(st, "SPAISolveMultiple")
     X[:] = Xs.reshape(-1)
     if max_errors is not None:
         max_errors.clear()
@@ -601,7 +625,8 @@ def PCGSolveMultiple(a: CsrMatrix, l: CsrMatrix, l_transpose, B, X, num_vectors:
     if ic is None or ic.h is None:
         ic = GpuIc0(l)
         object.__setattr__(l, "_gpu_ic0", ic)
-    Xs, it, hist, _ = pcg_ic0(_gpu(a), ic, Bm, max_iters, tolerance, hist_cap=cap)
+    Xs, it, hist, st = pcg_ic0(_gpu(a), ic, Bm, max_iters, tolerance, hist_cap=cap)
+    _note_breakdown(st, "PCGSolveMultiple")
     X[:] = Xs.reshape(-1)
     if max_errors is not None:
         max_errors.clear()

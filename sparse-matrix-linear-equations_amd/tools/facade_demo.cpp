@@ -1,4 +1,6 @@
-// facade_demo -- a reference-style C++ caller using include/mspmv.hpp unchanged call sites:
+// facade_demo -- a reference-style C++ caller using include/mspmv.hpp in namespace mode
+// (`using namespace mspmv_ref`; the drop-in mode against the reference's real CsrMatrix is
+// oracle/dropin_check.cpp) with unchanged call sites:
 // the CsrMatrix<double,int> field layout (sparse_matrix.h:648-653), OmpMergeCsrmv /
 // OmpMergeCsrmm / CGSolveSingle / CGSolveMultiple (and, at num_vectors = 32 as cpu_spmm_v2 and
 // preconditioner_benchmark default, OmpMergeCsrmm, IncompleteCholesky + PCGSolveMultiple,
@@ -18,6 +20,7 @@ struct CsrMatrix {  // the reference's field names and order
     ValueT *values;
 };
 enum SpmmKernel { SIMPLE, MERGE, NONZERO_SPLIT };  // work_2025/types.hpp:11-16
+using namespace mspmv_ref;
 
 int main()
 {
@@ -86,8 +89,8 @@ int main()
             delete[] c->column_indices;
             delete[] c->values;
         }
-        mspmv_facade_release(mi);
-        mspmv_facade_release(a);
+        release(mi);
+        release(a);
         const bool ok32 = err32 < 1e-12 && itic > 0 && itsp > 0 && !e_ic.empty() && e_ic.back() < 1e-10 &&
                           !e_spai.empty() && e_spai.back() < 1e-10;
         return (err < 1e-12 && it1 > 0 && itm > 0 && !errs.empty() && errs.back() < 1e-10 && ok32) ? 0 : 2;

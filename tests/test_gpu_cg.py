@@ -223,3 +223,65 @@ def test_cg_pipelined_and_split_iterations_match_oracle(orc, tmp_path, split):
     k = min(len(d["h1"]), len(h1o))
     np.testing.assert_allclose(d["h1"][:k], h1o[:k], rtol=0, atol=1e-10)
     assert np.linalg.norm(d["x1"] - xo) <= 1e-8 * np.linalg.norm(xo)
+
+
+@pytest.mark.parametrize("L", [8, 16])
+@pytest.mark.parametrize("name", ["fem2d", "stencil27"])
+def test_cg_multi_vs_oracle_nonzero_split(orc, name, L):
+    """cpu_multicg.cpp:202 runs TestCGMultipleRHS with SpmmKernel NONZERO_SPLIT
+    (nonzero_splitting.hpp:49-150, behind no_pretreatment.hpp:93's memset(AP, 0)): the oracle
+    restated that way, with the reference's g_omp_threads = 8 partition (hyper_parameters.hpp:11),
+    against the GPU (which always runs its merge-path SpMM; the kernels differ only in how split
+    rows round)."""
+    a = spd_cases()[name]()
+    n = a.num_rows
+    flat = orc.glibc_rand(42, n * L)
+    B = flat.reshape(n, L)
+    tol = orc.calculate_threshold(flat, n, 1e-5)                  # cpu_multicg.cpp:168 quirk
+    Xo, it_o, ho = orc.cg_multi(a, B, 5000, tol, kernel=mspmv.NONZERO_SPLIT, P=8, hist_cap=5000)
+    with mspmv.GpuCsr(a) as g:
+        Xg, it_g, hg, st = g.cg_multi(B, 5000, tol, kernel=mspmv.NONZERO_SPLIT, hist_cap=5000)
+    assert st == 0 and it_o < 5000
+    assert iter_match(it_g, it_o, ho, tol), (it_g, it_o)
+    k = min(len(hg), len(ho))
+    np.testing.assert_allclose(hg[:k], ho[:k], rtol=0, atol=1e-10)
+    for j in range(L):
+        assert np.linalg.norm(Xg[:, j] - Xo[:, j]) <= 1e-8 * np.linalg.norm(Xo[:, j])
+
+
+@pytest.mark.parametrize("L,zero_cols", [(4, [1]), (8, [0, 5]), (32, [3, 17])])
+def test_cg_multi_zero_column_breaks_down_alone(orc, L, zero_cols):
+    """A zero RHS column gives p.Ap = 0 and alpha = 0/0 in that column only.  The reference
+    (no_pretreatment.hpp:109-161) turns the column into NaN, skips it in the max-error history
+    (std::max) and never converges it; here the column is frozen at x = 0 (its exact solution),
+    reported as MSPMV_ERR_BREAKDOWN, and every other column is solved exactly as the oracle
+    solves it: the history matches the oracle's on the GPU's iterations, the other columns'
+    X within 1e-8.  L = 32 runs as column groups: every group is solved, the broken ones too."""
+    a = spd_cases()["fem2d"]()
+    n = a.num_rows
+    B = orc.glibc_rand(42, n * L).reshape(n, L).copy()
+    B[:, zero_cols] = 0.0
+    tol = 1e-9
+    Xo, it_o, ho = orc.cg_multi(a, B, 3000, tol, kernel=1, P=8, hist_cap=3000)
+    assert it_o == 3000                          # the reference never converges the NaN column
+    assert np.all(np.isnan(Xo[:, zero_cols]))
+    with mspmv.GpuCsr(a) as g:
+        Xg, it_g, hg, st = g.cg_multi(B, 3000, tol, hist_cap=3000)
+    assert st == 4 and 0 < it_g < 3000
+    assert np.all(Xg[:, zero_cols] == 0.0)
+    np.testing.assert_allclose(hg, ho[:it_g], rtol=0, atol=1e-10)
+    assert hg[-1] < tol
+    for j in range(L):
+        if j not in zero_cols:
+            assert np.linalg.norm(Xg[:, j] - Xo[:, j]) <= 1e-8 * np.linalg.norm(Xo[:, j]), j
+
+
+def test_cg_multi_breakdown_warns_in_facade(orc):
+    a = spd_cases()["fem2d"]()
+    n, L = a.num_rows, 2
+    B = orc.glibc_rand(42, n * L).reshape(n, L).copy()
+    B[:, 1] = 0.0
+    X = np.empty(n * L)
+    with pytest.warns(RuntimeWarning, match="breakdown"):
+        it = mspmv.CGSolveMultiple(a, B.reshape(-1), X, L, 3000, 1e-9)
+    assert 0 < it < 3000 and np.all(X.reshape(n, L)[:, 1] == 0.0)

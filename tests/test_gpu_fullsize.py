@@ -9,10 +9,11 @@ the SuiteSparse matrices, which are not available offline), through the C-ABI.
   OmpCsrSpmmT (row_splitting.hpp:15-54), same bound.
 * Single CG (configs[3], parabolic_fem shape, the cpu_singlecg tol = 1e-5 ||b|| quirk) against
   the oracle's CGSolveSingle, within the reference's own thread-count envelope (see the test).
-* Multi CG (configs[4], nlpkkt120 size, L = 8): the first 3 iterations against the oracle's
-  CGSolveMultiple (history within 1e-10, X within 1e-8 relative), and the full solve through
-  a size-independent property: every column's true residual ||b_j - A x_j|| / ||b_j|| below
-  the threshold the solve stopped on.
+* Multi CG (configs[4], nlpkkt120 size, L = 8): the whole solve against the oracle's
+  CGSolveMultiple run with NONZERO_SPLIT as cpu_multicg.cpp:202 runs it (history within 1e-10
+  wherever the reference reproduces itself across thread counts, X within 1e-8 relative), plus
+  a size-independent property: every column's true residual ||b_j - A x_j|| / ||b_j|| below the
+  threshold the solve stopped on.
 """
 import numpy as np
 import pytest
@@ -93,19 +94,43 @@ def test_cg_single_full_size(orc):
 
 
 def test_cg_multi_full_size(orc):
+    """configs[4] at its full size, compared over the WHOLE solve against the oracle run as
+    cpu_multicg runs it: SpmmKernel NONZERO_SPLIT (cpu_multicg.cpp:202) with the partition and
+    OpenMP reductions of T threads (g_omp_threads).  The reference's rounding depends on T, so the
+    oracle is run at two thread counts first: on the prefix where those two agree to 1e-10 (the
+    reference reproduces itself there) the GPU history must match to 1e-10 too; past it (if any)
+    it must stay within 4x the oracle's own spread.  Iterations within one, every column's X
+    within 1e-8 relative of the oracle's where the prefix covers the whole solve, and every
+    column's true residual below the threshold the solve stopped on."""
     a = full_cases()["nlpkkt120"]()
     n, L = a.num_rows, 8
     B = np.random.default_rng(42).uniform(0, 1, (n, L))
     thr = orc.calculate_threshold(B.reshape(-1), n, 1e-5)   # cpu_multicg.cpp:168 quirk
-    Xo, it_o, ho = orc.cg_multi(a, B, 3, thr, kernel=1, P=8, hist_cap=8)
+    runs, t0 = {}, orc.lib.orc_max_threads()
+    try:
+        for t in sorted({max(2, min(8, t0)), max(2, t0)} | {4}):
+            orc.lib.orc_set_threads(t)
+            runs[t] = orc.cg_multi(a, B, 50000, thr, kernel=mspmv.NONZERO_SPLIT, P=t, hist_cap=50000)
+    finally:
+        orc.lib.orc_set_threads(t0)
+    ts = sorted(runs)
+    Xo, it_o, ho = runs[ts[-1]]
+    assert 3 < it_o < 50000
+    k = min(len(r[2]) for r in runs.values())
+    spread = np.max([np.abs(runs[t][2][:k] - ho[:k]) for t in ts[:-1]], axis=0)
+    agree = int(np.argmax(spread > 1e-10)) if np.any(spread > 1e-10) else k   # reproducible prefix
     with mspmv.GpuCsr(a) as g:
-        Xg, it_g, hg, st = g.cg_multi(B, 3, thr, hist_cap=8)
-        assert st == 0 and it_g == it_o == 3
-        np.testing.assert_allclose(hg, ho, rtol=0, atol=1e-10)
-        assert np.linalg.norm(Xg - Xo) <= 1e-8 * np.linalg.norm(Xo)
-        Xf, it_f, hf, st = g.cg_multi(B, 50000, thr, hist_cap=50000)
-    assert st == 0 and 3 < it_f < 50000
-    assert hf[-1] < thr <= hf[-2]
-    R = B - orc.csr_spmm_t(a, Xf)
+        Xg, it_g, hg, st = g.cg_multi(B, 50000, thr, kernel=mspmv.NONZERO_SPLIT, hist_cap=50000)
+    assert st == 0 and abs(it_g - it_o) <= 1, (it_g, it_o)
+    k = min(k, len(hg))
+    np.testing.assert_allclose(hg[:agree], ho[:agree], rtol=0, atol=1e-10)
+    env = np.maximum.accumulate(spread[:k])
+    np.testing.assert_array_less(np.abs(hg[:k] - ho[:k]), 4 * env + 1e-10)
+    if agree >= min(it_g, it_o):
+        assert it_g == it_o
+        for j in range(L):
+            assert np.linalg.norm(Xg[:, j] - Xo[:, j]) <= 1e-8 * np.linalg.norm(Xo[:, j]), j
+    assert hg[-1] < thr <= hg[-2]
+    R = B - orc.csr_spmm_t(a, Xg)
     rel = np.linalg.norm(R, axis=0) / np.linalg.norm(B, axis=0)
     assert np.all(rel < thr), rel

@@ -26,6 +26,21 @@ def test_facade_demo():
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+def test_dropin_check_on_gpu():
+    """oracle/_ref/dropin_check (built in the container from the reference's own sparse_matrix.h /
+    utils.h / hyper_parameters.hpp + include/mspmv_dropin.hpp, tests/test_dropin.py): every
+    reference entry point a driver calls -- TestOmpMergeCsrmv, OmpMergeCsrmm, CGSolveSingle,
+    TestCGSolveSingle, CGSolveMultiple(NONZERO_SPLIT), TestCGMultipleRHS, IncompleteCholesky,
+    TransposeCsr, PCGSolveMultiple, TestPCGMultipleRHS, SparseApproximateInversion,
+    SPAISolveMultiple, TestCGMultipleSPAI -- on a real CsrMatrix<double,int>, checked against the
+    reference's own SpmvGold / OmpCsrSpmmT compiled into the same binary."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "dropin_check")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/dropin_check not built (needs the reference checkout at build time)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "DROP-IN CHECK PASSED" in r.stdout, r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("args", [["--grid2d=300"], ["--grid3d=40"], ["--wheel=5000"], ["--dense=64"]])
 def test_spmv_cli_quiet_line(args):
     r = run("mspmv_spmv", *args, "--quiet", "--i=50")
