@@ -237,11 +237,13 @@ MSPMV_API mspmv_status mspmv_tile_streams(mspmv_handle h, int *tiles_cols16, int
 MSPMV_API mspmv_status mspmv_plan_dict_tiles(mspmv_handle h, int L, int *tiles_dict);
 /* Tiles of the L-column plan staged by node blocks (*tiles_blk): runs of consecutive rows whose
  * column lists are prefixes of one list (FEM unknowns of one mesh node) read that list once and
- * gather each of its x entries once for all the run's rows; the products, their LDS slots and the
- * reduction are those of the striped staging, so results are bit-identical to it.  Tiles that
- * hold whole rows only, <= 16 run chunks, mean run height >= ~1.7 (others: 0). */
+ * gather each of its x entries once for all the run's rows.  Runs <= 64 columns wide are summed
+ * in registers by a fixed lane tree (tile mode 255); wider ones go through the striped path's
+ * LDS slots and reduction (bit-identical to it).  Tiles that hold whole rows only, <= 16 run
+ * chunks, mean run height >= ~1.7 (others: 0). */
 MSPMV_API mspmv_status mspmv_plan_block_tiles(mspmv_handle h, int L, int *tiles_blk);
-/* Each tile's in-tile reduction for L right-hand sides (num_tiles entries): 0 = merge walk
+/* Each tile's in-tile reduction for L right-hand sides (num_tiles entries; 255 = a node-block
+ * tile summed in registers by a fixed lane tree, see mspmv_plan_block_tiles): 0 = merge walk
  * (one walker per thread, or per L/2 lanes), g > 0 = row groups with 2^(g-1) nonzero-parallel
  * lanes per row (times L/2 column-pair lanes for L > 1).  g = 1 sums each row sequentially in
  * CSR order -> bit-identical to SpmvGold / the row-split SpMM for rows the tile holds whole. */

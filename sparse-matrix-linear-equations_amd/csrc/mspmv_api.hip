@@ -243,18 +243,28 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
             return fail(st);
         e = launch_build_blocks(h->d_row_offsets, h->d_cols, p.d_bounds, p.d_split, p.d_colbase, T, p.d_blk,
                                 h->stream);
-        std::vector<uint4> hb0((size_t)T);
-        if (e == hipSuccess)  // entry 0 of every tile: its run count
-            e = hipMemcpy2DAsync(hb0.data(), sizeof(uint4), p.d_blk, sizeof(uint4) * kBlkPerTile, sizeof(uint4), T,
-                                 hipMemcpyDeviceToHost, h->stream);
+        std::vector<uint4> hd((size_t)T * kBlkPerTile);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(hd.data(), p.d_blk, sizeof(uint4) * hd.size(), hipMemcpyDeviceToHost, h->stream);
         if (e == hipSuccess)
             e = hipStreamSynchronize(h->stream);
         if (e != hipSuccess) {
             set_error(std::string("node blocks: ") + hipGetErrorString(e));
             return fail(MSPMV_ERR_HIP);
         }
-        for (const uint4 &d : hb0)
-            p.num_tiles_blk += ((d.y >> 16) & 255u) > 0;
+        p.h_blk_reg.assign((size_t)T, 0);
+        for (int t = 0; t < T; ++t) {
+            const uint4 *d = &hd[(size_t)t * kBlkPerTile];
+            const int nd = (int)((d[0].y >> 8) & 255u);
+            if (nd == 0)
+                continue;
+            ++p.num_tiles_blk;
+            bool one = true;  // the kernel's own test: every chunk starts at pattern column 0
+            for (int i = 0; i < nd; ++i)
+                one = one && ((d[i].x >> 16) & 255u) == 0;
+            p.h_blk_reg[(size_t)t] = one;
+            p.num_tiles_reg += one;
+        }
         if (p.num_tiles_blk == 0) {
             dev_free(p.d_blk);
             p.d_blk = nullptr;
@@ -1431,6 +1441,10 @@ mspmv_status mspmv_tile_modes(mspmv_handle h, int L, unsigned char *modes)
     ST_TRY(get_plan(h, L, &plan));
     if (plan->num_tiles)
         HIP_TRY(hipMemcpy(modes, plan->d_modes[l_index(L)], plan->num_tiles, hipMemcpyDeviceToHost));
+    if (L == 1 && plan->d_blk)  // node-block tiles reduced in registers (lane tree, not the plan's mode)
+        for (int t = 0; t < plan->num_tiles; ++t)
+            if (plan->h_blk_reg[(size_t)t])
+                modes[t] = 255;
     return MSPMV_OK;
 }
 

@@ -62,6 +62,9 @@ struct TilePlan {
     // of a tile holding its count (0: striped staging).  Null when no tile qualifies.
     uint4 *d_blk = nullptr;             // [num_tiles * 16]
     int num_tiles_blk = 0;              // tiles staged by node blocks
+    int num_tiles_reg = 0;              // of those, tiles reduced in registers (h_blk_reg)
+    std::vector<unsigned char> h_blk_reg;  // [num_tiles] 1: every run one chunk wide (the SpMV reduces
+                                           // such tiles in registers; mspmv_tile_modes reports 255)
 };
 
 // Device-resident CG scalars (one set per right-hand side column).

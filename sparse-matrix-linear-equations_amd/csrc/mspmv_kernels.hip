@@ -475,8 +475,8 @@ __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ c
 // Descriptor of one run chunk (16 B; at most kBlkMax per tile, tile t's at blk[t * kBlkMax ..]):
 //   x: vofs (nonzero offset of the run's first row in the tile, bits 0-15) | j0 (first pattern
 //      column of this chunk, 16-23) | wc (chunk width <= 64, 24-31)
-//   y: h (rows, <= 8, bits 0-7) | p (row holding P, 8-15) | nd (descriptor count, in entry 0 only,
-//      16-23; 0 = the tile stages the plain way)
+//   y: h (rows, 1..8, bits 0-3) | p (row holding P, 4-6) | nd (descriptor count, in entry 0 only,
+//      8-15; 0 = the tile stages the plain way) | rofs (the run's first row in the tile, 16-31)
 //   z, w: the h row lengths, 8 bits each (rows of a run are <= 255 long)
 constexpr int kBlkMax = 16;
 constexpr int kBlkRows = 8;
@@ -535,14 +535,15 @@ __global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *_
                 return;
             const int wc = min(64, plen - j0);
             d[nd++] = make_uint4((unsigned)vofs | ((unsigned)j0 << 16) | ((unsigned)wc << 24),
-                                 (unsigned)h | ((unsigned)(p - g) << 8), lens[0], lens[1]);
+                                 (unsigned)h | ((unsigned)(p - g) << 4) | ((unsigned)(g - r0) << 16), lens[0],
+                                 lens[1]);
             if (plen == 0)
                 break;
         }
     }
     if (5 * sum_w > 3 * (n1 - n0))
         return;
-    d[0].y |= (unsigned)nd << 16;
+    d[0].y |= (unsigned)nd << 8;
     for (int i = nd - 1; i >= 0; --i)  // entry 0 last: nd > 0 only once the tile's set is complete
         out[i] = d[i];
 }
@@ -625,8 +626,10 @@ struct TileArgs {
     // single-RHS plans: per-tile 16-bit column offsets (TilePlan::d_colbase / d_cols16; null: off)
     const int *colbase;
     const unsigned short *cols16;
-    // single-RHS plans with node blocks (TilePlan::d_blk, k_build_blocks; null: off)
+    // single-RHS plans with node blocks (TilePlan::d_blk, k_build_blocks; null: off); all_reg:
+    // every tile reduces in registers (host side: launch k_spmv_blk)
     const uint4 *blk;
+    int all_reg;
     // single-RHS plans with column dictionaries (TilePlan::d_dict; null: off)
     const int *dict;
     const int *ndict;
@@ -823,7 +826,7 @@ __device__ __forceinline__ void blk_stage(const TileArgs &a, const uint4 &bd, in
             if (di < nd) {  // wave-uniform
                 const uint4 d = blk_read(bd, di);
                 const int vofs = d.x & 0xffff, j0 = (d.x >> 16) & 255, wc = d.x >> 24;
-                const int h = d.y & 255, p = (d.y >> 8) & 255;
+                const int h = d.y & 15, p = (d.y >> 4) & 7;
                 const int j = j0 + lane;
                 int start = 0, pstart = 0;
 #pragma unroll
@@ -856,7 +859,7 @@ __device__ __forceinline__ void blk_stage(const TileArgs &a, const uint4 &bd, in
             if (di < nd) {
                 const uint4 d = blk_read(bd, di);
                 const int vofs = d.x & 0xffff, j0 = (d.x >> 16) & 255;
-                const int h = d.y & 255;
+                const int h = d.y & 15;
                 const int j = j0 + lane;
                 double x = st.xv[s];
                 if (CG)
@@ -868,6 +871,121 @@ __device__ __forceinline__ void blk_stage(const TileArgs &a, const uint4 &bd, in
                     if (i < h && j < len)
                         s_prod[pslot(vofs + start + j)] = st.v[s][i] * x;
                     start += i < h ? len : 0;
+                }
+            }
+        }
+    }
+}
+
+// Sum of 8 per-lane values over the wave by a reduce-scatter butterfly (xor 32, 16, 8 halve the
+// values each lane carries, then xor 4, 2, 1 finish): lanes 8i .. 8i+7 end up holding row i's
+// total (i = lane >> 3).  10 double shuffles for 8 sums instead of 48 for 8 full butterflies;
+// the order is fixed, so results are bit-for-bit reproducible.
+__device__ __forceinline__ double rows8_sum(const double (&p)[kBlkRows])
+{
+    const int lane = threadIdx.x & 63;
+    const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+    double q4[4], q2[2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        q4[k] = (b5 ? p[k + 4] : p[k]) + __shfl_xor(b5 ? p[k] : p[k + 4], 32);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        q2[k] = (b4 ? q4[k + 2] : q4[k]) + __shfl_xor(b4 ? q4[k] : q4[k + 2], 16);
+    double v = (b3 ? q2[1] : q2[0]) + __shfl_xor(b3 ? q2[0] : q2[1], 8);
+    v += __shfl_xor(v, 4);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 1);
+    return v;
+}
+
+// Node-block tiles whose runs are at most 64 columns wide (one chunk each: FEM node rows) skip
+// LDS altogether: lane j of the run's wave holds the products of pattern column j in every row
+// of the run, rows8_sum folds them across the wave, and lane 8i stores row i (y; CG: p for the
+// row, p.Ap; dot mode: x.(Ax)).  No row-end staging, no barrier, no LDS round trip -- the
+// tile's life is its loads plus a few shuffles.  Rows are summed by a fixed lane tree, so they
+// are reproducible and within 2 (len+1) eps (|A||x|)_i of the sequential CSR-order sum
+// (mspmv_tile_modes reports these tiles as 255).
+template <int MODE, bool NT, int TB, typename Head>
+__device__ __forceinline__ void blk_rows(const TileArgs &a, const uint4 &bd, int nd, int r0, int n0, int colbase,
+                                         double &beta, double &dot, Head &&head)
+{
+    constexpr bool CG = MODE == kModeCg;
+    constexpr int NW = TB / 64;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int myrow = lane >> 3;  // the run row this lane stores (lanes 8i)
+    for (int round = 0; round * 2 * NW < nd; ++round) {
+        BlkRegs<CG> st;
+        double2 ro[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int di = wave + NW * (2 * round + s);
+            st.c[s] = 0;
+            ro[s] = make_double2(0.0, 0.0);
+#pragma unroll
+            for (int i = 0; i < kBlkRows; ++i)
+                st.v[s][i] = 0.0;
+            if (di < nd) {  // wave-uniform
+                const uint4 d = blk_read(bd, di);
+                const int vofs = d.x & 0xffff, wc = d.x >> 24;
+                const int h = d.y & 15, p = (d.y >> 4) & 7, rofs = d.y >> 16;
+                int start = 0, pstart = 0;
+#pragma unroll
+                for (int i = 0; i < kBlkRows; ++i) {
+                    pstart = i == p ? start : pstart;
+                    const int len = blk_len(d, i);
+                    if (i < h && lane < len)
+                        st.v[s][i] = ld_stream<NT>(a.vals + n0 + vofs + start + lane);
+                    start += i < h ? len : 0;
+                }
+                if (lane < wc)
+                    st.c[s] = colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + lane);
+                if (MODE != kModeSpmv && (lane & 7) == 0 && myrow < h) {
+                    const int R = r0 + rofs + myrow;
+                    if constexpr (CG)
+                        ro[s] = cg_rp(a, R);
+                    else
+                        ro[s].x = a.x[R];
+                }
+            }
+        }
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            if constexpr (CG) {
+                const double2 v = cg_rp(a, st.c[s]);
+                st.xv[s] = v.x;
+                st.pv[s] = v.y;
+            } else {
+                st.xv[s] = a.x[st.c[s]];
+            }
+        }
+        if (round == 0 && !head())
+            return;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int di = wave + NW * (2 * round + s);
+            if (di < nd) {
+                const uint4 d = blk_read(bd, di);
+                const int h = d.y & 15, rofs = d.y >> 16;
+                double x = st.xv[s];
+                if (CG)
+                    x = x + beta * st.pv[s];
+                double pr[kBlkRows];
+#pragma unroll
+                for (int i = 0; i < kBlkRows; ++i)
+                    pr[i] = (i < h && lane < blk_len(d, i)) ? st.v[s][i] * x : 0.0;
+                const double sum = rows8_sum(pr);
+                if ((lane & 7) == 0 && myrow < h) {
+                    const int R = r0 + rofs + myrow;
+                    a.y[R] = sum;
+                    if constexpr (CG) {
+                        const double pn = ro[s].x + beta * ro[s].y;
+                        cg_pstore(a, R, pn);
+                        dot += pn * sum;
+                    } else if constexpr (MODE == kModeDot) {
+                        dot += ro[s].x * sum;
+                    }
                 }
             }
         }
@@ -1128,8 +1246,8 @@ __device__ __forceinline__ void row_operands(const TileArgs &a, int r0, int nrow
 
 // Dot-mode epilogue (split multi-RHS / row-sharded CG): this block's x.(Ax) partial ->
 // partials[slot], a plain store; k_fold_dot (a later launch) sums the partials in tile order.
-template <int IPT>
-__device__ __forceinline__ void dot_epilogue(const TileArgs &a, SpmvSmem<IPT> &sm, int slot, double dot)
+template <typename SM>
+__device__ __forceinline__ void dot_epilogue(const TileArgs &a, SM &sm, int slot, double dot)
 {
     const double tsum = block_sum(dot, sm.red);
     if (threadIdx.x == 0)
@@ -1181,8 +1299,8 @@ __device__ __forceinline__ bool cg1_head(const TileArgs &a, double rs, double &b
 
 // Pipelined single-RHS CG tail of the SpMV: this tile's p.Ap partial, for the update kernel
 // to sum (folded by group tickets only beyond kConsumeTile tiles).
-template <int IPT>
-__device__ __forceinline__ void cg1_publish(const TileArgs &a, SpmvSmem<IPT> &sm, int slot, int nslots, double dot)
+template <typename SM>
+__device__ __forceinline__ void cg1_publish(const TileArgs &a, SM &sm, int slot, int nslots, double dot)
 {
     const double tsum = block_sum(dot, sm.red);
     if (nslots <= kConsumeTile) {  // the update kernel sums them: the launch boundary orders the store
@@ -1245,8 +1363,24 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
     uint4 bd = make_uint4(0u, 0u, 0u, 0u);
     if (a.blk && (tid & 63) < kBlkMax)
         bd = a.blk[(size_t)t * kBlkMax + (tid & 63)];
-    const int nblk = a.blk ? (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 16) & 255u) : 0;
+    const int nblk = a.blk ? (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u) : 0;
     bool staged = false;
+    // every run one chunk wide (block-uniform: each wave holds all descriptors): no LDS at all
+    const bool blk_reg = nblk > 0 && __ballot((tid & 63) < nblk && ((bd.x >> 16) & 255u) != 0) == 0;
+    if (blk_reg) {
+        double dot = 0.0;
+        blk_rows<MODE, NT, TB>(a, bd, nblk, r0, n0, colbase, beta, dot, [&]() {
+            head();
+            return go;
+        });
+        if (!go)
+            return;
+        if constexpr (MODE == kModeCg)
+            cg1_publish(a, sm, t, a.num_tiles, dot);
+        else if constexpr (MODE == kModeDot)
+            dot_epilogue(a, sm, t, dot);
+        return;
+    }
     if (nblk > 0) {
         blk_stage<CG, NT, TB>(a, bd, nblk, n0, colbase, sm.prod, beta, [&]() {
             head();
@@ -1311,9 +1445,51 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
     }
 #endif
     if constexpr (MODE == kModeCg)
-        cg1_publish<IPT>(a, sm, t, a.num_tiles, dot);
+        cg1_publish(a, sm, t, a.num_tiles, dot);
     else if constexpr (MODE == kModeDot)
-        dot_epilogue<IPT>(a, sm, t, dot);
+        dot_epilogue(a, sm, t, dot);
+}
+
+// Single right-hand side, plans whose EVERY tile is a register node-block tile (FEM matrices such
+// as pwtk): the tile kernel without any LDS staging (only the CG / dot-mode epilogue's 2 KB), so
+// occupancy is set by registers alone -- 8 workgroups (32 waves) per CU instead of the 7 that
+// k_spmv_tile's 22.6 KB of LDS allow.  Same per-tile work as k_spmv_tile's blk_rows path.
+struct BlkSmem {
+    double red[kBlock / 64];
+    double cval[kBlock];
+    int last;
+};
+
+template <int MODE, bool NT>
+__global__ __launch_bounds__(kBlock) void k_spmv_blk(TileArgs a)
+{
+    constexpr bool CG = MODE == kModeCg;
+    __shared__ BlkSmem sm;
+    const int tid = threadIdx.x;
+    const int stopped = MODE != kModeSpmv ? a.ctrl->done : 0;
+    const int t = xcd_tile(blockIdx.x, a.num_tiles);
+    const int2 b0 = a.bounds[t];
+    const int colbase = a.colbase[t];
+    const uint4 bd = (tid & 63) < kBlkMax ? a.blk[(size_t)t * kBlkMax + (tid & 63)] : make_uint4(0u, 0u, 0u, 0u);
+    const int nblk = (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u);
+    double beta = 0.0, dot = 0.0;
+    bool go = true;
+    PartRegs<CG ? kUpdateMaxBlocks / kBlock : 1> pin;
+    if constexpr (CG)
+        part_load(a.part_in, a.n_part_in, pin);
+    blk_rows<MODE, NT, kBlock>(a, bd, nblk, b0.x, b0.y, colbase, beta, dot, [&]() {
+        if (stopped)
+            go = false;
+        else if constexpr (CG)
+            go = cg1_head(a, part_sum(pin, sm.red), beta);
+        return go;
+    });
+    if (!go)
+        return;
+    if constexpr (MODE == kModeCg)
+        cg1_publish(a, sm, t, a.num_tiles, dot);
+    else if constexpr (MODE == kModeDot)
+        dot_epilogue(a, sm, t, dot);
 }
 
 // Single right-hand side, persistent and software-pipelined.  Workgroup v (XCD-grouped) walks
@@ -1439,7 +1615,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_persist(TileArgs a, int tpb)
             pipe_tile<IPT, MODE, NT>(a, sm, s_b, s_mode, a.m, i, ntl, t_begin + i, A, B, beta, dot);
     }
     if (MODE == kModeDot) {  // one partial per tile: the run's sum at its first tile, zeros after
-        dot_epilogue<IPT>(a, sm, t_begin, dot);
+        dot_epilogue(a, sm, t_begin, dot);
         for (int i = 1 + tid; i < ntl; i += kBlock)
             a.partials[t_begin + i] = 0.0;
     }
@@ -2416,6 +2592,7 @@ struct SpmvTuning {
     int tile_items = 0;  // single-RHS nominal merge items per tile (0: tb * ipt; smaller: fewer per thread)
     int trsv_tagged = 1;  // IC(0) solves: data-tagged values (1) or ready flags (0)
     int blocks = 1;   // single-RHS tiles staged by node blocks where rows share columns (k_build_blocks)
+    int blkreg = 1;   // plans of register node-block tiles only run the LDS-free k_spmv_blk
     int dict = 1;     // single-RHS SpMV through per-tile column dictionaries (k_build_dict) when
                       // a tile's nonzeros repeat its distinct columns >= dict_ratio times (0: off)
 };
@@ -2447,6 +2624,8 @@ static const SpmvTuning &spmv_tuning()
             v.cols16 = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMV_BLOCKS"))
             v.blocks = atoi(e) != 0;
+        if (const char *e = getenv("MSPMV_SPMV_BLKREG"))
+            v.blkreg = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMV_DICT"))
             v.dict = atoi(e) > 0 ? atoi(e) : 0;
         if (const char *e = getenv("MSPMV_TRSV_TAGGED"))
@@ -2474,6 +2653,10 @@ bool stream_nt(const mspmv_handle_s *h)
 std::string spmv_kernel_name(const mspmv_handle_s *h)
 {
     const SpmvTuning &t = spmv_tuning();
+    const auto it = h->plans.find(tile_items_for(1));
+    if (it != h->plans.end() && it->second.d_blk && it->second.num_tiles_reg == it->second.num_tiles && t.blkreg &&
+        t.tb == kBlock && !t.persist)
+        return std::string("k_spmv_blk<0,") + (stream_nt(h) ? "true>" : "false>");
     return std::string(t.persist ? "k_spmv_persist<" : "k_spmv_tile<") + std::to_string(t.ipt) + ",0," +
            (stream_nt(h) ? "true" : "false") + (t.tb == 64 && !t.persist ? ",64>" : ">");
 }
@@ -2598,6 +2781,7 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
         a.colbase = plan.d_colbase;
         a.cols16 = plan.d_cols16;
         a.blk = plan.d_blk;
+        a.all_reg = plan.d_blk && plan.num_tiles_reg == plan.num_tiles && spmv_tuning().blkreg && spmv_tuning().tb == kBlock;
     }
     a.dict = plan.d_dict;
     a.ndict = plan.d_ndict;
@@ -2677,6 +2861,16 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_c
         return hipErrorInvalidValue;
     switch (L) {
     case 1: {
+        // every tile a register node-block tile: the LDS-free kernel (SpMV and dot mode; the CG
+        // form's consumer-side partial sums take it to 86 VGPRs, 5 waves/SIMD, so the pipelined
+        // CG keeps k_spmv_tile, whose blk_rows path does the same per-tile work)
+        if (a.all_reg && !tu.persist && MODE != kModeCg) {
+            if (nt)
+                hipLaunchKernelGGL((k_spmv_blk<MODE == kModeCg ? kModeSpmv : MODE, true>), grid, block, 0, s, a);
+            else
+                hipLaunchKernelGGL((k_spmv_blk<MODE == kModeCg ? kModeSpmv : MODE, false>), grid, block, 0, s, a);
+            break;
+        }
 #define MSPMV_SPMV_CASE(I)                                                                          \
     case I:                                                                                        \
         if (tu.persist && MODE != kModeCg) {                                                       \

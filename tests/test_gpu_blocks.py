@@ -2,10 +2,12 @@
 share their column list, so a tile stages each run's list once (16-bit offsets of its longest
 row) and gathers each x once for all the run's rows.
 
-The products and their LDS slots are those of the striped staging and the in-tile reduction is
-unchanged, so results must be BIT-IDENTICAL with node blocks switched off (MSPMV_SPMV_BLOCKS=0,
-run in a child process since the tuning is read once per process), and within the usual parity
-rule against the oracle's SpmvGold (cpu_spmv.cpp:241-265).  Covered: equal-length node rows,
+Runs at most 64 columns wide are summed in registers by a fixed lane tree (tile mode 255): those
+rows are within the reordering bound 2 (len+1) eps (|A||x|)_i of the oracle's SpmvGold
+(cpu_spmv.cpp:241-265) and reproducible bit for bit.  Wider runs keep the striped path's LDS
+slots and reduction: every row outside register tiles must be BIT-IDENTICAL to the run with node
+blocks switched off (MSPMV_SPMV_BLOCKS=0, in a child process since the tuning is read once per
+process).  Covered: equal-length node rows,
 prefix runs (rows of one node 52 and 53 long, as the pwtk-shaped generator makes them), rows
 wider than 64 columns (pattern chunks), runs longer than 8 rows (split), empty rows inside runs,
 a Kronecker FEM matrix solved by the pipelined single-RHS CG (blocks in the fused CG SpMV), and
@@ -91,18 +93,30 @@ def spmv_in_child(tmp_path, a, x, blocks):
     return d["y"], int(d["nb"])
 
 
+def register_rows(a, plan):
+    """Rows of tiles the kernel reduces in registers (tile mode 255)."""
+    mask = np.zeros(a.num_rows, bool)
+    for t in np.flatnonzero(plan["modes"][: plan["num_tiles"]] == 255):
+        mask[plan["bounds"][t][0]:plan["bounds"][t + 1][0]] = True
+    return mask
+
+
 @pytest.mark.parametrize("name", list(cases()))
 def test_blocks_parity(orc, tmp_path, name):
     a = cases()[name]()
     x = np.random.default_rng(7).uniform(-1, 1, a.num_cols)
     with mspmv.GpuCsr(a) as g:
         nb = g.plan_block_tiles(1)
+        plan = g.tile_plan(1)
         y = g.spmv(x)
-        check_parity(a, y, orc.spmv_gold(a, x), x, g.tile_plan(1), 1)
+        y2 = g.spmv(x)
+        check_parity(a, y, orc.spmv_gold(a, x), x, plan, 1)
     assert nb > 0, "no tile took the node-block staging"
+    assert y.tobytes() == y2.tobytes()  # fixed reduction order: run-to-run reproducible
     y_off, nb_off = spmv_in_child(tmp_path, a, x, 0)
     assert nb_off == 0
-    assert y.tobytes() == y_off.tobytes(), "node-block staging changed result bits"
+    keep = ~register_rows(a, plan)  # LDS-path rows: the striped staging's bits exactly
+    assert y[keep].tobytes() == y_off[keep].tobytes(), "node-block staging changed LDS-path result bits"
 
 
 def test_blocks_not_taken_without_shared_columns():
@@ -135,5 +149,3 @@ def test_blocks_full_pwtk_shape(orc, tmp_path):
         y = g.spmv(x)
         check_parity(a, y, orc.spmv_gold(a, x), x, g.tile_plan(1), 1)
     assert nb >= 0.9 * nt, (nb, nt)
-    y_off, _ = spmv_in_child(tmp_path, a, x, 0)
-    assert y.tobytes() == y_off.tobytes()
