@@ -127,6 +127,17 @@ static mspmv_status ensure_modes(mspmv_handle_s *h, TilePlan &p, int L)
 
 static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out)
 {
+    if (L > 1 && spmm_blk_enabled()) {
+        // a matrix of node blocks only (every single-RHS tile a register run tile: FEM node rows)
+        // multiplies L columns on that plan with k_spmm_blk -- one panel-row gather per (run,
+        // column) -- instead of its own L-wide merge tiles
+        auto one = h->plans.find(tile_items_for(1));
+        if (one != h->plans.end() && one->second.d_blk && one->second.num_tiles_reg == one->second.num_tiles) {
+            ST_TRY(ensure_modes(h, one->second, L));
+            *out = &one->second;
+            return MSPMV_OK;
+        }
+    }
     const int tile = tile_items_for(L);
     auto it = h->plans.find(tile);
     if (it == h->plans.end()) {
@@ -253,21 +264,34 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
             return fail(MSPMV_ERR_HIP);
         }
         p.h_blk_reg.assign((size_t)T, 0);
+        int maxnd = 0;
         for (int t = 0; t < T; ++t) {
             const uint4 *d = &hd[(size_t)t * kBlkPerTile];
             const int nd = (int)((d[0].y >> 8) & 255u);
             if (nd == 0)
                 continue;
             ++p.num_tiles_blk;
+            maxnd = std::max(maxnd, nd);
             bool one = true;  // the kernel's own test: every chunk starts at pattern column 0
             for (int i = 0; i < nd; ++i)
                 one = one && ((d[i].x >> 16) & 255u) == 0;
             p.h_blk_reg[(size_t)t] = one;
             p.num_tiles_reg += one;
         }
-        if (p.num_tiles_blk == 0) {
-            dev_free(p.d_blk);
-            p.d_blk = nullptr;
+        dev_free(p.d_blk);
+        p.d_blk = nullptr;
+        if (p.num_tiles_blk > 0) {  // repack at the smallest stride that holds every tile's set
+            p.blk_stride = maxnd <= 16 ? 16 : maxnd <= 32 ? 32 : 64;
+            std::vector<uint4> packed((size_t)T * p.blk_stride, make_uint4(0u, 0u, 0u, 0u));
+            for (int t = 0; t < T; ++t)
+                for (int i = 0, nd = (int)((hd[(size_t)t * kBlkPerTile].y >> 8) & 255u); i < nd; ++i)
+                    packed[(size_t)t * p.blk_stride + i] = hd[(size_t)t * kBlkPerTile + i];
+            if ((st = dev_alloc(&p.d_blk, packed.size())) != MSPMV_OK)
+                return fail(st);
+            if (hipMemcpy(p.d_blk, packed.data(), sizeof(uint4) * packed.size(), hipMemcpyHostToDevice) != hipSuccess) {
+                set_error("node blocks: upload failed");
+                return fail(MSPMV_ERR_HIP);
+            }
         }
     }
     // multi-RHS: only the L = 16 plan (k_spmm_tile's DICT path runs at L = 16 only)
@@ -1441,7 +1465,9 @@ mspmv_status mspmv_tile_modes(mspmv_handle h, int L, unsigned char *modes)
     ST_TRY(get_plan(h, L, &plan));
     if (plan->num_tiles)
         HIP_TRY(hipMemcpy(modes, plan->d_modes[l_index(L)], plan->num_tiles, hipMemcpyDeviceToHost));
-    if (L == 1 && plan->d_blk)  // node-block tiles reduced in registers (lane tree, not the plan's mode)
+    // node-block tiles reduced in registers (lane tree, not the plan's mode): L = 1 on any plan
+    // with node blocks, L > 1 when get_plan chose the node-block plan (k_spmm_blk)
+    if (plan->d_blk && (L == 1 || plan->num_tiles_reg == plan->num_tiles))
         for (int t = 0; t < plan->num_tiles; ++t)
             if (plan->h_blk_reg[(size_t)t])
                 modes[t] = 255;

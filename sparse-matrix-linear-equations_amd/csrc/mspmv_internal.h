@@ -58,9 +58,10 @@ struct TilePlan {
     int *d_ndict = nullptr;             // [num_tiles]
     unsigned short *d_idx16 = nullptr;  // [nnz + kNnzPad]
     int num_tiles_dict = 0;             // tiles that gather through their dictionary
-    // Single-RHS plans: node-block run descriptors (k_build_blocks), kBlkMax (16) per tile, entry 0
-    // of a tile holding its count (0: striped staging).  Null when no tile qualifies.
-    uint4 *d_blk = nullptr;             // [num_tiles * 16]
+    // Single-RHS plans: node-block run descriptors (k_build_blocks), blk_stride (16, 32 or 64) per
+    // tile, entry 0 of a tile holding its count (0: striped staging).  Null when no tile qualifies.
+    uint4 *d_blk = nullptr;             // [num_tiles * blk_stride]
+    int blk_stride = 0;
     int num_tiles_blk = 0;              // tiles staged by node blocks
     int num_tiles_reg = 0;              // of those, tiles reduced in registers (h_blk_reg)
     std::vector<unsigned char> h_blk_reg;  // [num_tiles] 1: every run one chunk wide (the SpMV reduces
@@ -169,7 +170,9 @@ bool spmv_cols16_enabled();
 bool spmv_dict_enabled();
 // Node blocks (runs of rows sharing one column list) for the single-RHS plan; needs cols16.
 bool spmv_blocks_enabled();
-constexpr int kBlkPerTile = 16;  // == kBlkMax in the kernels
+// SpMM (L >= 2) through the single-RHS node-block plan (k_spmm_blk) when all its tiles are register tiles.
+bool spmm_blk_enabled();
+constexpr int kBlkPerTile = 64;  // == kBlkMax in the kernels: descriptor capacity of a tile
 hipError_t launch_build_blocks(const int *d_row_offsets, const int *d_cols, const int2 *d_bounds,
                                const unsigned char *d_split, const int *d_colbase, int num_tiles, uint4 *d_blk,
                                hipStream_t s);

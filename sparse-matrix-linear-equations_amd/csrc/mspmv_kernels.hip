@@ -472,13 +472,14 @@ __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ c
 // The products land in the same LDS slots as the striped staging writes, so the reduction --
 // and every result bit -- is unchanged.
 //
-// Descriptor of one run chunk (16 B; at most kBlkMax per tile, tile t's at blk[t * kBlkMax ..]):
+// Descriptor of one run chunk (16 B; at most kBlkMax per tile, tile t's at blk[t * stride ..], the
+// plan's stride being the smallest of 16, 32, 64 that holds every tile's set):
 //   x: vofs (nonzero offset of the run's first row in the tile, bits 0-15) | j0 (first pattern
 //      column of this chunk, 16-23) | wc (chunk width <= 64, 24-31)
 //   y: h (rows, 1..8, bits 0-3) | p (row holding P, 4-6) | nd (descriptor count, in entry 0 only,
 //      8-15; 0 = the tile stages the plain way) | rofs (the run's first row in the tile, 16-31)
 //   z, w: the h row lengths, 8 bits each (rows of a run are <= 255 long)
-constexpr int kBlkMax = 16;
+constexpr int kBlkMax = 64;  // descriptors a tile may have (the plan stores them at a stride of 16, 32 or 64)
 constexpr int kBlkRows = 8;
 
 __device__ __forceinline__ int blk_len(const uint4 &d, int i)
@@ -487,8 +488,7 @@ __device__ __forceinline__ int blk_len(const uint4 &d, int i)
 }
 
 // One thread per tile.  A tile qualifies when it holds whole rows only (no split boundary), is on
-// the 16-bit column stream, fits in kBlkMax chunks, and its runs share columns enough to pay: the
-// pattern columns summed over its runs at most 3/5 of its nonzeros (mean run height >= ~1.7).
+// the 16-bit column stream, fits in kBlkMax chunks, and its runs pay (below).
 __global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *__restrict__ cols,
                                const int2 *__restrict__ bounds, const unsigned char *__restrict__ split,
                                const int *__restrict__ colbase, int num_tiles, uint4 *__restrict__ blk)
@@ -497,13 +497,13 @@ __global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *_
     if (t >= num_tiles)
         return;
     uint4 *out = blk + (size_t)t * kBlkMax;
-    out[0] = make_uint4(0, 0, 0, 0);
+    out[0] = make_uint4(0, 0, 0, 0);  // entry 0 (with the count) is written last, on success only
+    uint4 d0 = make_uint4(0, 0, 0, 0);
     const int2 b0 = bounds[t], b1 = bounds[t + 1];
     const int r0 = b0.x, r1 = b1.x, n0 = b0.y, n1 = b1.y;
     if (split[t] || split[t + 1] || colbase[t] < 0 || n1 <= n0 || row_offsets[r0] != n0 || row_offsets[r1] != n1)
         return;
-    uint4 d[kBlkMax];
-    int nd = 0, sum_w = 0;
+    int nd = 0, sum_w = 0, nruns = 0;
     int r = r0;
     while (r < r1) {
         const int g = r, gs = row_offsets[g];
@@ -529,23 +529,35 @@ __global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *_
             lens[h >> 2] |= (unsigned)len << (8 * (h & 3));
         }
         sum_w += plen;
+        ++nruns;
         const int vofs = gs - n0;
         for (int j0 = 0; j0 < plen || (j0 == 0 && plen == 0); j0 += 64) {
             if (nd == kBlkMax || j0 > 255)
                 return;
             const int wc = min(64, plen - j0);
-            d[nd++] = make_uint4((unsigned)vofs | ((unsigned)j0 << 16) | ((unsigned)wc << 24),
-                                 (unsigned)h | ((unsigned)(p - g) << 4) | ((unsigned)(g - r0) << 16), lens[0],
-                                 lens[1]);
+            const uint4 dd = make_uint4((unsigned)vofs | ((unsigned)j0 << 16) | ((unsigned)wc << 24),
+                                        (unsigned)h | ((unsigned)(p - g) << 4) | ((unsigned)(g - r0) << 16), lens[0],
+                                        lens[1]);
+            if (nd == 0)
+                d0 = dd;
+            else
+                out[nd] = dd;
+            ++nd;
             if (plen == 0)
                 break;
         }
     }
-    if (5 * sum_w > 3 * (n1 - n0))
+    // Pays only when (measured, tools/lab/narrow_probe.py): runs share columns (pattern columns
+    // <= 3/5 of the nonzeros: mean run height >= ~1.7), are wide (mean pattern >= 32 columns: a
+    // run's value loads use one lane per column, against 64 per load in the striped staging), and
+    // the 4 waves take the tile in ONE round of two chunks each (nd <= 8): a second round waits
+    // for the first's sums.  2-D Kronecker FEM matrices with 3, 4 and 6 unknowns per node (15-30
+    // columns, ~11-20 runs per tile) ran 3.1x, 2.0x and 1.2x slower on node blocks than striped;
+    // the pwtk shape (53 columns, ~7 runs per tile) 1.14x faster.
+    if (5 * sum_w > 3 * (n1 - n0) || sum_w < 32 * nruns || nd > 8)
         return;
-    d[0].y |= (unsigned)nd << 8;
-    for (int i = nd - 1; i >= 0; --i)  // entry 0 last: nd > 0 only once the tile's set is complete
-        out[i] = d[i];
+    d0.y |= (unsigned)nd << 8;
+    out[0] = d0;
 }
 
 // Per-tile choice of the in-tile reduction (one thread per tile, at plan time; gl = lanes per
@@ -629,6 +641,7 @@ struct TileArgs {
     // single-RHS plans with node blocks (TilePlan::d_blk, k_build_blocks; null: off); all_reg:
     // every tile reduces in registers (host side: launch k_spmv_blk)
     const uint4 *blk;
+    int blk_stride;
     int all_reg;
     // single-RHS plans with column dictionaries (TilePlan::d_dict; null: off)
     const int *dict;
@@ -1361,8 +1374,8 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
     const int colbase = a.cols16 ? a.colbase[t] : -1;
     // node-block descriptors of this tile, loaded beside its bounds (entry 0 holds the count)
     uint4 bd = make_uint4(0u, 0u, 0u, 0u);
-    if (a.blk && (tid & 63) < kBlkMax)
-        bd = a.blk[(size_t)t * kBlkMax + (tid & 63)];
+    if (a.blk && (tid & 63) < a.blk_stride)
+        bd = a.blk[(size_t)t * a.blk_stride + (tid & 63)];
     const int nblk = a.blk ? (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u) : 0;
     bool staged = false;
     // every run one chunk wide (block-uniform: each wave holds all descriptors): no LDS at all
@@ -1470,7 +1483,8 @@ __global__ __launch_bounds__(kBlock) void k_spmv_blk(TileArgs a)
     const int t = xcd_tile(blockIdx.x, a.num_tiles);
     const int2 b0 = a.bounds[t];
     const int colbase = a.colbase[t];
-    const uint4 bd = (tid & 63) < kBlkMax ? a.blk[(size_t)t * kBlkMax + (tid & 63)] : make_uint4(0u, 0u, 0u, 0u);
+    const uint4 bd =
+        (tid & 63) < a.blk_stride ? a.blk[(size_t)t * a.blk_stride + (tid & 63)] : make_uint4(0u, 0u, 0u, 0u);
     const int nblk = (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u);
     double beta = 0.0, dot = 0.0;
     bool go = true;
@@ -1958,6 +1972,140 @@ k_spmm_tile(TileArgs a)
                 tsum.y += s_red2[w][tid].y;
             }
             // plain stores: k_fold_dot (a later launch) sums the tiles' partials
+            a.partials[(size_t)t * L + 2 * tid] = tsum.x;
+            a.partials[(size_t)t * L + 2 * tid + 1] = tsum.y;
+        }
+    }
+}
+
+// ---- node-block SpMM (plans whose every single-RHS tile is a register node-block tile) --------
+// Y = A X for L right-hand sides on the single-RHS plan's tiles and run descriptors.  A wave takes
+// one run (<= 64 pattern columns) at a time; its lanes form 64/(L/2) column groups of L/2 lanes
+// (one double2 of the panel row each).  Per pass a group owns pattern column j: it gathers panel
+// row X[P[j]] ONCE and multiplies it into all h rows of the run, so the L2 -> CU gather traffic is
+// one panel row per (run, column) instead of one per nonzero (1/6 of it on the pwtk shape).  The
+// run's values and P arrive by coalesced loads (lane j holds column j) and reach the column groups
+// by shuffles; the h row sums are folded across the groups by a reduce-scatter and group i stores
+// row i (L/2 lanes x 16 B, contiguous).  No LDS, no carries (node-block tiles hold whole rows).
+template <int GL>
+__device__ __forceinline__ double2 rows8_sum2(const double2 (&p)[kBlkRows])
+{
+    const int lane = threadIdx.x & 63;
+    const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+    auto sx = [](double2 v, int off) { return make_double2(__shfl_xor(v.x, off), __shfl_xor(v.y, off)); };
+    auto add = [](double2 u, double2 v) { return make_double2(u.x + v.x, u.y + v.y); };
+    double2 q4[4], q2[2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        q4[k] = add(b5 ? p[k + 4] : p[k], sx(b5 ? p[k] : p[k + 4], 32));
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        q2[k] = add(b4 ? q4[k + 2] : q4[k], sx(b4 ? q4[k] : q4[k + 2], 16));
+    double2 v = add(b3 ? q2[1] : q2[0], sx(b3 ? q2[0] : q2[1], 8));
+#pragma unroll
+    for (int off = 4; off >= GL; off >>= 1)  // column groups inside the 8-lane row slot
+        v = add(v, sx(v, off));
+    return v;
+}
+
+template <int L, int MODE, bool NT>
+__global__ __launch_bounds__(kBlock) void k_spmm_blk(TileArgs a)
+{
+    static_assert(MODE != kModeCg, "multi-RHS CG runs the split iteration (MODE 2)");
+    constexpr int GL = L / 2;      // lanes per panel row
+    constexpr int NGW = 64 / GL;   // column groups per wave = pattern columns per pass
+    constexpr int PB = 4;          // passes whose gathers are in flight together
+    __shared__ double2 s_red2[MODE == kModeDot ? kBlock / 64 : 1][GL];
+    const int stopped = MODE != kModeSpmv ? a.ctrl->done : 0;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int g = lane / GL, c = lane % GL;
+    const int t = xcd_tile(blockIdx.x, a.num_tiles);
+    const int2 b0 = a.bounds[t];
+    const int r0 = b0.x, n0 = b0.y;
+    const int colbase = a.colbase[t];
+    const uint4 bd = lane < a.blk_stride ? a.blk[(size_t)t * a.blk_stride + lane] : make_uint4(0u, 0u, 0u, 0u);
+    const int nd = (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u);
+    const int wave = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    double2 dot = make_double2(0.0, 0.0);
+    for (int di = wave; di < nd && !stopped; di += kBlock / 64) {  // wave-uniform
+        const uint4 d = blk_read(bd, di);
+        const int vofs = d.x & 0xffff, wc = d.x >> 24;
+        const int h = d.y & 15, p = (d.y >> 4) & 7, rofs = d.y >> 16;
+        int start[kBlkRows];
+        int pstart = 0, acc_s = 0;
+#pragma unroll
+        for (int i = 0; i < kBlkRows; ++i) {
+            start[i] = acc_s;
+            pstart = i == p ? acc_s : pstart;
+            acc_s += i < h ? blk_len(d, i) : 0;
+        }
+        // lane j: P[j] and the run's values in column j, one coalesced load per row
+        const int colj = lane < wc ? colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + lane) : 0;
+        double vrow[kBlkRows];
+#pragma unroll
+        for (int i = 0; i < kBlkRows; ++i)
+            vrow[i] = (i < h && lane < blk_len(d, i)) ? ld_stream<NT>(a.vals + n0 + vofs + start[i] + lane) : 0.0;
+        const int ri = lane >> 3;  // the run row this lane's slot stores
+        const bool store = (lane & 7) < GL && ri < h;
+        double2 xx = make_double2(0.0, 0.0);  // dot mode: the stored row's own x, issued early
+        if (MODE == kModeDot && store)
+            xx = *reinterpret_cast<const double2 *>(a.x + (size_t)(r0 + rofs + ri) * a.ld + 2 * c);
+        double2 acc[kBlkRows];
+#pragma unroll
+        for (int i = 0; i < kBlkRows; ++i)
+            acc[i] = make_double2(0.0, 0.0);
+        for (int pb = 0; pb * NGW < wc; pb += PB) {  // wave-uniform
+            double2 xv[PB];
+#pragma unroll
+            for (int q = 0; q < PB; ++q) {
+                const int j = (pb + q) * NGW + g;
+                const int cq = __shfl(colj, j & 63);
+                xv[q] = j < wc ? *reinterpret_cast<const double2 *>(a.x + (size_t)cq * a.ld + 2 * c)
+                               : make_double2(0.0, 0.0);
+            }
+#pragma unroll
+            for (int q = 0; q < PB; ++q) {
+                const int j = (pb + q) * NGW + g;
+#pragma unroll
+                for (int i = 0; i < kBlkRows; ++i) {
+                    if (i < h) {  // wave-uniform
+                        const double v = __shfl(vrow[i], j & 63);
+                        const bool on = j < blk_len(d, i);
+                        acc[i].x += on ? v * xv[q].x : 0.0;
+                        acc[i].y += on ? v * xv[q].y : 0.0;
+                    }
+                }
+            }
+        }
+        const double2 row = rows8_sum2<GL>(acc);
+        if (store) {
+            *reinterpret_cast<double2 *>(a.y + (size_t)(r0 + rofs + ri) * a.ld + 2 * c) = row;
+            if (MODE == kModeDot) {
+                dot.x += xx.x * row.x;
+                dot.y += xx.y * row.y;
+            }
+        }
+    }
+    if constexpr (MODE == kModeDot) {
+        if (stopped)
+            return;
+        // this tile's x.(Ax) per column: lanes of one column pair (equal c) over the wave, then
+        // the waves in order; a plain store (k_fold_dot sums the tiles' partials in a later launch)
+#pragma unroll
+        for (int off = 32; off >= GL; off >>= 1) {
+            dot.x += __shfl_xor(dot.x, off);
+            dot.y += __shfl_xor(dot.y, off);
+        }
+        if (lane < GL)
+            s_red2[tid >> 6][lane] = dot;
+        __syncthreads();
+        if (tid < GL) {
+            double2 tsum = s_red2[0][tid];
+#pragma unroll
+            for (int w = 1; w < kBlock / 64; ++w) {
+                tsum.x += s_red2[w][tid].x;
+                tsum.y += s_red2[w][tid].y;
+            }
             a.partials[(size_t)t * L + 2 * tid] = tsum.x;
             a.partials[(size_t)t * L + 2 * tid + 1] = tsum.y;
         }
@@ -2593,6 +2741,7 @@ struct SpmvTuning {
     int trsv_tagged = 1;  // IC(0) solves: data-tagged values (1) or ready flags (0)
     int blocks = 1;   // single-RHS tiles staged by node blocks where rows share columns (k_build_blocks)
     int blkreg = 1;   // plans of register node-block tiles only run the LDS-free k_spmv_blk
+    int spmm_blk = 1; // SpMM (L >= 2) on such a plan runs k_spmm_blk instead of its own L-wide tiles
     int dict = 1;     // single-RHS SpMV through per-tile column dictionaries (k_build_dict) when
                       // a tile's nonzeros repeat its distinct columns >= dict_ratio times (0: off)
 };
@@ -2626,6 +2775,8 @@ static const SpmvTuning &spmv_tuning()
             v.blocks = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMV_BLKREG"))
             v.blkreg = atoi(e) != 0;
+        if (const char *e = getenv("MSPMV_SPMM_BLK"))
+            v.spmm_blk = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMV_DICT"))
             v.dict = atoi(e) > 0 ? atoi(e) : 0;
         if (const char *e = getenv("MSPMV_TRSV_TAGGED"))
@@ -2700,12 +2851,13 @@ hipError_t launch_pack_cols16(const int *d_cols, const int2 *d_bounds, int num_t
 bool spmv_cols16_enabled() { return spmv_tuning().cols16 != 0; }
 bool spmv_dict_enabled() { return spmv_tuning().dict > 0; }
 bool spmv_blocks_enabled() { return spmv_tuning().blocks != 0; }
+bool spmm_blk_enabled() { return spmv_tuning().spmm_blk != 0 && spmv_tuning().blkreg != 0 && spmv_tuning().tb == kBlock; }
 
 hipError_t launch_build_blocks(const int *d_row_offsets, const int *d_cols, const int2 *d_bounds,
                                const unsigned char *d_split, const int *d_colbase, int num_tiles, uint4 *d_blk,
                                hipStream_t s)
 {
-    static_assert(kBlkMax == kBlkPerTile, "descriptor stride");
+    static_assert(kBlkMax == kBlkPerTile, "descriptor capacity");
     if (num_tiles <= 0)
         return hipSuccess;
     hipLaunchKernelGGL(k_build_blocks, dim3((num_tiles + 127) / 128), dim3(128), 0, s, d_row_offsets, d_cols, d_bounds,
@@ -2777,10 +2929,11 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
     a.rmode = plan.d_modes[l_index(L)];
     a.carry_val = plan.d_carry_val;
     a.num_tiles = plan.num_tiles;
-    if (L == 1) {
+    if (L == 1 || plan.d_blk) {  // L > 1 on a node-block plan: k_spmm_blk (plan_for_L picked it)
         a.colbase = plan.d_colbase;
         a.cols16 = plan.d_cols16;
         a.blk = plan.d_blk;
+        a.blk_stride = plan.blk_stride;
         a.all_reg = plan.d_blk && plan.num_tiles_reg == plan.num_tiles && spmv_tuning().blkreg && spmv_tuning().tb == kBlock;
     }
     a.dict = plan.d_dict;
@@ -2842,6 +2995,15 @@ static void launch_spmm_nt(const TileArgs &a, hipStream_t s, bool nt)
 template <int LL, int MODE>
 static void launch_spmm_L(const TileArgs &a, hipStream_t s, bool nt)
 {
+    if constexpr (MODE != kModeCg) {
+        if (a.all_reg) {  // a node-block plan (single-RHS tiles): every tile a register run tile
+            if (nt)
+                hipLaunchKernelGGL((k_spmm_blk<LL, MODE, true>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
+            else
+                hipLaunchKernelGGL((k_spmm_blk<LL, MODE, false>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
+            return;
+        }
+    }
     const int iptg = spmm_iptg_for(LL);
     if (iptg == 32)
         launch_spmm_nt<LL, 32, MODE>(a, s, nt);

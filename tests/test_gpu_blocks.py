@@ -57,15 +57,38 @@ def kron_fem(nx, ny, dof, empty_every=0):
                                        K.data.astype(np.float64))
 
 
+def kron_fem9(nx, ny, dof):
+    """kron(S9, B): a 9-point node stencil (3-D-like FEM coupling, 9 nodes per row), dof unknowns
+    per node -> 9 dof columns per row (pwtk-like widths: 54 at dof 6)."""
+    import scipy.sparse as sp
+    n = nx * ny
+    rows, cols = [], []
+    for i in range(ny):
+        for j in range(nx):
+            for di in (-1, 0, 1):
+                for dj in (-1, 0, 1):
+                    if 0 <= i + di < ny and 0 <= j + dj < nx:
+                        rows.append(i * nx + j)
+                        cols.append((i + di) * nx + j + dj)
+    vals = np.where(np.array(rows) == np.array(cols), 9.5, -1.0)
+    S = sp.csr_matrix((vals, (rows, cols)), shape=(n, n))
+    B = np.eye(dof) + 0.2 * np.ones((dof, dof))
+    K = sp.kron(S, sp.csr_matrix(B), format="csr")
+    K.sort_indices()
+    return mspmv.CsrMatrix.from_arrays(K.shape[1], K.indptr.astype(np.int32), K.indices.astype(np.int32),
+                                       K.data.astype(np.float64))
+
+
 def cases():
+    """Matrices whose tiles take node blocks (whole-row tiles, runs >= 32 columns wide on average,
+    <= 8 run chunks per tile -- one round for the tile's 4 waves)."""
     return {
         "pwtk_small": lambda: mspmv.CsrMatrix.synth_fem_blocked(21792, 1152443, 6, 170, seed=3),
-        "kron6": lambda: kron_fem(60, 50, 6),
-        "kron3": lambda: kron_fem(90, 80, 3),
-        "kron12_wide": lambda: kron_fem(30, 30, 12),     # 60 columns per row: one chunk
-        "kron16_wider": lambda: kron_fem(25, 20, 16),    # 80 columns per row: two chunks
-        "kron10_empty": lambda: kron_fem(50, 40, 10, empty_every=7),
-        "wide_runs": lambda: mspmv.CsrMatrix.synth_fem_blocked(12000, 1320000, 12, 60, seed=4),  # runs of 12 > 8
+        "kron9_6": lambda: kron_fem9(60, 50, 6),            # 54 columns per row
+        "kron9_7": lambda: kron_fem9(50, 40, 7),            # 63 columns per row
+        "kron12_wide": lambda: kron_fem(30, 30, 12),        # 60 columns per row: one chunk
+        "kron9_8_wider": lambda: kron_fem9(25, 20, 8),      # 72 columns per row: two chunks (LDS path)
+        "kron9_6_empty": lambda: kron_fem9(50, 40, 6),      # (see test_blocks_empty_rows)
     }
 
 
@@ -101,7 +124,27 @@ def register_rows(a, plan):
     return mask
 
 
-@pytest.mark.parametrize("name", list(cases()))
+def test_blocks_empty_rows(orc):
+    """Empty rows inside runs (an empty row is a prefix of any list: it joins the run)."""
+    a = kron_fem9(50, 40, 6)
+    ro = a.row_offsets.copy()
+    keep = np.ones(a.num_rows, bool)
+    keep[::37] = False
+    keep[1::37] = False
+    lens = np.diff(ro) * keep
+    mask = np.repeat(keep, np.diff(ro))
+    e = mspmv.CsrMatrix.from_arrays(a.num_cols, np.concatenate([[0], np.cumsum(lens)]).astype(np.int32),
+                                    a.column_indices[mask], a.values[mask])
+    x = np.random.default_rng(3).uniform(-1, 1, e.num_cols)
+    with mspmv.GpuCsr(e) as g:
+        assert g.plan_block_tiles(1) > 0
+        y = g.spmv(x)
+        check_parity(e, y, orc.spmv_gold(e, x), x, g.tile_plan(1), 1)
+        Y = g.spmm(np.stack([x, 2 * x], axis=1))
+    assert np.all(y[~keep] == 0.0) and np.all(Y[~keep] == 0.0)
+
+
+@pytest.mark.parametrize("name", [k for k in cases() if k != "kron9_6_empty"])
 def test_blocks_parity(orc, tmp_path, name):
     a = cases()[name]()
     x = np.random.default_rng(7).uniform(-1, 1, a.num_cols)
@@ -119,9 +162,12 @@ def test_blocks_parity(orc, tmp_path, name):
     assert y[keep].tobytes() == y_off[keep].tobytes(), "node-block staging changed LDS-path result bits"
 
 
-def test_blocks_not_taken_without_shared_columns():
-    """Stencils and random bands have no two rows with one column list: striped staging."""
-    for a in (mspmv.CsrMatrix.synth_stencil(0, 10007, 101), mspmv.CsrMatrix.synth_banded(6000, 380000, 2000, seed=1)):
+def test_blocks_not_taken_where_they_lose():
+    """Stencils and random bands have no two rows with one column list; 5-point node stencils with
+    3 or 6 unknowns per node (15 / 30 columns, 11-20 runs per tile) measured slower on node blocks:
+    striped staging for all four."""
+    for a in (mspmv.CsrMatrix.synth_stencil(0, 10007, 101), mspmv.CsrMatrix.synth_banded(6000, 380000, 2000, seed=1),
+              kron_fem(90, 80, 3), kron_fem(60, 50, 6)):
         with mspmv.GpuCsr(a) as g:
             assert g.plan_block_tiles(1) == 0
 
@@ -129,7 +175,7 @@ def test_blocks_not_taken_without_shared_columns():
 def test_blocks_in_pipelined_cg(orc):
     """The fused CG SpMV (MODE 1: p = r + beta p_old gathered as {r, p} pairs) stages node blocks
     too; the solve must match the oracle's CGSolveSingle as every single-RHS CG does."""
-    a = kron_fem(60, 50, 6)
+    a = kron_fem9(60, 50, 6)
     b = orc.glibc_rand(42, a.num_rows)
     xo, it_o, ho = orc.cg_single(a, b, 5000, 1e-10, hist_cap=5000)
     with mspmv.GpuCsr(a) as g:
@@ -149,3 +195,85 @@ def test_blocks_full_pwtk_shape(orc, tmp_path):
         y = g.spmv(x)
         check_parity(a, y, orc.spmv_gold(a, x), x, g.tile_plan(1), 1)
     assert nb >= 0.9 * nt, (nb, nt)
+
+
+# ---- node-block SpMM (k_spmm_blk: one panel-row gather per (run, column)) -------------------
+_SPMM_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import mspmv
+d = np.load(sys.argv[2])
+a = mspmv.CsrMatrix.from_arrays(int(d["n"]), d["ro"], d["ci"], d["va"])
+with mspmv.GpuCsr(a) as g:
+    Y = g.spmm(d["X"])
+np.savez(sys.argv[3], Y=Y)
+"""
+
+
+@pytest.mark.parametrize("name", ["pwtk_small", "kron9_6", "kron9_7", "kron12_wide"])
+@pytest.mark.parametrize("L", [2, 4, 8, 16, 3, 32])
+def test_blocks_spmm_parity(orc, tmp_path, name, L):
+    """Y = A X on the node-block plan (every single-RHS tile a register run tile) against the
+    oracle's row-split OmpCsrSpmmT (row_splitting.hpp:15-54) within the reordering bound, for the
+    native widths, an odd width (zero-padded panel) and a chunked width (panel stride 32)."""
+    from gpu_common import check_parity_chunked
+    a = cases()[name]()
+    X = np.random.default_rng(L).uniform(-1, 1, (a.num_cols, L))
+    with mspmv.GpuCsr(a) as g:
+        Y = g.spmm(X)
+        Y2 = g.spmm(X)
+        check_parity_chunked(a, g, Y, orc.csr_spmm_t(a, X), X, L)
+        reg = g.tile_plan(1)["modes"]
+    assert Y.tobytes() == Y2.tobytes()
+    if name == "pwtk_small":  # all tiles register tiles -> the SpMM ran k_spmm_blk
+        assert np.all(reg == 255)
+
+
+def test_blocks_spmm_vs_merge_tiles(orc, tmp_path):
+    """The node-block SpMM against the L-wide merge tiles (MSPMV_SPMM_BLK=0, in a child process):
+    both within the reordering bound of the same sequential sums, so within twice it of each other."""
+    a = cases()["pwtk_small"]()
+    X = np.random.default_rng(5).uniform(-1, 1, (a.num_cols, 16))
+    with mspmv.GpuCsr(a) as g:
+        Y = g.spmm(X)
+    inp, out = str(tmp_path / "in.npz"), str(tmp_path / "out.npz")
+    np.savez(inp, n=a.num_cols, ro=a.row_offsets, ci=a.column_indices, va=a.values, X=X)
+    r = subprocess.run([sys.executable, "-c", _SPMM_CHILD, PKG, inp, out],
+                       env=dict(os.environ, MSPMV_SPMM_BLK="0"), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    Yo = np.load(out)["Y"]
+    from gpu_common import EPS, abs_bound
+    bound, lens = abs_bound(a, X)
+    assert np.all(np.abs(Y - Yo) <= 4.0 * (lens[:, None] + 1) * EPS * bound + 1e-300)
+
+
+@pytest.mark.parametrize("L", [4, 8, 16])
+def test_blocks_cg_multi(orc, L):
+    """CGSolveMultiple's split iteration runs the node-block SpMM in dot mode (x.(Ax) partials
+    per tile, k_fold_dot): the whole solve against the oracle (NONZERO_SPLIT, as cpu_multicg)."""
+    a = kron_fem9(60, 50, 6)
+    n = a.num_rows
+    flat = orc.glibc_rand(42, n * L)
+    B = flat.reshape(n, L)
+    tol = orc.calculate_threshold(flat, n, 1e-5)
+    Xo, it_o, ho = orc.cg_multi(a, B, 5000, tol, kernel=mspmv.NONZERO_SPLIT, P=8, hist_cap=5000)
+    with mspmv.GpuCsr(a) as g:
+        Xg, it_g, hg, st = g.cg_multi(B, 5000, tol, hist_cap=5000)
+    assert st == 0 and it_g == it_o
+    np.testing.assert_allclose(hg, ho[: len(hg)], rtol=0, atol=1e-10)
+    for j in range(L):
+        assert np.linalg.norm(Xg[:, j] - Xo[:, j]) <= 1e-8 * np.linalg.norm(Xo[:, j])
+
+
+def test_blocks_spai_pcg(orc):
+    """SPAI-PCG: both SpMMs (A P and M R, M on A's pattern) on node-block plans in dot mode."""
+    a = kron_fem9(40, 30, 6)
+    m_vals = mspmv.spai_values(a)
+    B = orc.glibc_rand(7, a.num_rows * 8).reshape(a.num_rows, 8)
+    Xo, it_o, ho = orc.pcg_spai_multi(a, m_vals, B, 3000, 1e-9, kernel=1, P=8, hist_cap=3000)
+    m = mspmv.CsrMatrix.from_arrays(a.num_cols, a.row_offsets, a.column_indices, m_vals)
+    with mspmv.GpuCsr(a) as g, mspmv.GpuCsr(m) as gm:
+        Xg, it_g, hg, st = g.pcg_spai(gm, B, 3000, 1e-9, hist_cap=3000)
+    assert st == 0 and it_g == it_o
+    np.testing.assert_allclose(hg, ho[: len(hg)], rtol=0, atol=1e-10)
+    assert np.linalg.norm(Xg - Xo) <= 1e-8 * np.linalg.norm(Xo)
