@@ -22,9 +22,13 @@ Extra fields: the scattered-band stress shape, CG iterations/s for configs[3] (s
 parabolic_fem shape) and configs[4] (8-RHS block CG, nlpkkt120 size; at N > 1 row-sharded over
 all ranks with RCCL halo exchange + dot all-reduces).
 
-Multi-GPU (--gpus N via torch.distributed.run): every rank runs its own SpMV batch on its own
-GPU (weak scaling; no data-path collective); gloo carries the barrier and the max-over-ranks
-time, and the RCCL id of the sharded CG.
+Multi-GPU (--gpus N via torch.distributed.run; run_sharded_headline): weak scaling with a real
+exchange step -- each matrix of the batch is ONE FEM-blocked matrix of N x 217,918 rows, sharded by
+merge-path row blocks; every rank generates only its pwtk-sized block, and each SpMV exchanges the
+halo rows of x over RCCL (send/recv, xGMI) while the block interior is multiplied.  value = all
+ranks' flops / max-over-ranks time; roofline = the per-rank local SpMV (no exchange).  gloo
+carries the barrier, the max-over-ranks reductions and the RCCL ids.  A watchdog turns a hang of
+the collective part into exit 3 with the line printed.
 """
 import argparse
 import ctypes
@@ -284,6 +288,114 @@ def run_cg_multi(d, dev):
     return out, spmv_large
 
 
+class Watchdog:
+    """N > 1: the collective part of the run (sharded SpMV headline, sharded CG) must finish within
+    `seconds`.  If it does not -- an RCCL hang, or a rank that failed while the others wait in a
+    collective -- rank 0 prints what it has (the headline, if measured, with an error field) and
+    every rank exits 3: a hang is reported as a failure, never as a success.  The lock is held
+    through the print and exit, and finish() takes it too, so exactly one thread prints."""
+
+    def __init__(self, d, seconds):
+        self.d, self.seconds, self.result = d, seconds, None
+        self.lock, self.done = threading.Lock(), False
+        self.timer = threading.Timer(seconds, self._fire)
+        self.timer.daemon = True
+        self.timer.start()
+
+    def _fire(self):
+        with self.lock:
+            if self.done:
+                return
+            self.done = True
+            if self.d.rank == 0:
+                out = dict(self.result or {"metric": METRIC, "value": None, "n_gpus": self.d.world})
+                out["error"] = f"multi-GPU run did not finish within {self.seconds:.0f} s (RCCL hang?)"
+                print(json.dumps(out), flush=True)
+            print(f"rank {self.d.rank}: multi-GPU run hung (> {self.seconds:.0f} s), exiting 3", file=sys.stderr)
+            sys.stderr.flush()
+            os._exit(3)
+
+    def finish(self):
+        """Mark the run finished; False if the watchdog already fired (and is exiting)."""
+        with self.lock:
+            if self.done:
+                return False
+            self.done = True
+        self.timer.cancel()
+        return True
+
+
+def run_sharded_headline(d, dev, args):
+    """N > 1 headline (weak scaling): each of the batch's matrices is ONE node-blocked FEM matrix of
+    N x 217,918 rows (N x 11,524,432 nonzeros, the pwtk shape's rows, band and seeds), sharded by
+    merge-path row blocks (mspmv_dist_partition): every rank holds a pwtk-sized row block and x's
+    slice, and each SpMV exchanges the halo rows of x with RCCL send/recv over xGMI (the row blocks
+    couple through the band) while the block interior is multiplied; the rows next to the block
+    ends follow the exchange.  At N = 1 this is exactly the single-GPU headline (no halo)."""
+    world, rank = d.world, d.rank
+    M, NNZ = PWTK["m"] * world, PWTK["nnz"] * world
+    ro = (np.arange(M + 1, dtype=np.int64) * NNZ // M).astype(np.int32)  # the generator's row offsets
+    rb = mspmv.dist_partition_offsets(ro, M, NNZ, world)
+    lo, hi = int(rb[rank]), int(rb[rank + 1])
+    dcs, dys, xps, infos, nnz_loc = [], [], [], [], 0
+    for i in range(args.batch):
+        uid = d.bcast_bytes(mspmv.comm_unique_id() if rank == 0 else None)
+        loc = mspmv.CsrMatrix.synth_fem_blocked_rows(M, NNZ, PWTK["block"], PWTK["half_band_nodes"], 1 + i, lo, hi)
+        dc = mspmv.DistCsr(uid, world, rank, dev, rb, loc)
+        xp = dc.x_ext(1)
+        mspmv.memcpy_h2d_ptr(xp, np.random.default_rng(2 + i).uniform(0.0, 1.0, M)[lo:hi])
+        dcs.append(dc)
+        xps.append(xp)
+        dys.append(mspmv.DeviceBuffer(8 * max(hi - lo, 1), dev))
+        infos.append(dc.info())
+        nnz_loc = loc.num_nonzeros
+    for _ in range(max(args.warmup, 1)):
+        for dc, xp, dy in zip(dcs, xps, dys):
+            dc.spmm_dev(xp, dy, 1, sync=False)
+    for dc in dcs:
+        dc.sync()
+    # per-rank SpMV alone (no exchange): the head / interior / tail launches back to back
+    loc_ms = float(np.mean([dc.time_local(dy, 1, 100) for dc, dy in zip(dcs, dys)]))
+    loc_ms = d.max(loc_ms)
+    d.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        for dc, xp, dy in zip(dcs, xps, dys):
+            dc.spmm_dev(xp, dy, 1, sync=False)
+    for dc in dcs:
+        dc.sync()
+    el = time.perf_counter() - t0
+    d.barrier()
+    el = d.max(el)
+    inf = infos[0]
+    m_loc, n_ext = inf["n_own"], inf["n_own"] + inf["n_halo"]
+    bytes_local = 12 * nnz_loc + 4 * (m_loc + 1) + 8 * n_ext + 8 * m_loc
+    achieved = bytes_local / (loc_ms * 1e-3) / 1e9
+    value = 2.0 * NNZ * args.batch * args.steps / el / 1e9
+    result = {
+        "metric": METRIC, "value": round(value, 2), "unit": "GFLOP/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (pwtk-shaped 6-DOF FEM-blocked CSR scaled to N x the rows, splitmix64 values; "
+                "SuiteSparse unavailable offline)",
+        "config": {"workload": f"merge-path CSR SpMV fp64, 1 RHS, batch of {args.batch} FEM-blocked matrices of "
+                               f"{world} x 217,918 rows per step, row-block sharded (configs[1] per GPU)",
+                   "m": M, "nnz": NNZ, "m_per_gpu": m_loc, "nnz_per_gpu": nnz_loc, "batch": args.batch,
+                   "parallelism": f"row-block sharding over {world} GPUs: RCCL halo exchange of x (send/recv over "
+                                  f"xGMI) overlapped with the block interior"},
+        "halo": {"rows": inf["n_halo"], "rows_sent": inf["n_send"], "bytes_per_exchange": 8 * inf["n_halo"]},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "local SpMV (head + interior + tail launches)", "bytes_per_launch": bytes_local,
+                     "kernel_ms": round(loc_ms, 5),
+                     "note": "per-rank local SpMV without the exchange, HIP events, max over ranks; algorithmic "
+                             "bytes 12 nnz + 4 (m+1) + 8 (n_own + n_halo) + 8 m of the rank's block"},
+    }
+    for dc in dcs:
+        dc.close()
+    return result
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -293,8 +405,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-cg", action="store_true")
-    ap.add_argument("--cg-timeout", type=float, default=300.0,
-                    help="N > 1: seconds allowed for the sharded CG before the headline prints without it")
+    ap.add_argument("--cg-timeout", type=float, default=400.0,
+                    help="N > 1: seconds allowed for the collective part (sharded SpMV headline + sharded CG); "
+                         "past it rank 0 prints what it has and every rank exits 3")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the hot-matrix and scatter-band side measurements (profiling runs: the "
                          "headline kernel's rocprofv3 average then covers exactly the timed launches)")
@@ -307,114 +420,100 @@ def main():
     if mspmv.device_count() <= dev:
         raise SystemExit(f"rank {d.rank}: no HIP device {dev}")
 
-    mats, gs, dxs, dys, xs = [], [], [], [], []
-    for i in range(args.batch):
-        a = mspmv.CsrMatrix.synth_fem_blocked(PWTK["m"], PWTK["nnz"], PWTK["block"], PWTK["half_band_nodes"],
-                                              seed=1 + i + 1000 * d.rank)
-        x = np.random.default_rng(2 + i + 1000 * d.rank).uniform(0.0, 1.0, a.num_cols)
-        mats.append(a)
-        gs.append(mspmv.GpuCsr(a, device=dev))
-        xs.append(x)
-        dxs.append(mspmv.DeviceBuffer.from_array(x, dev))
-        dys.append(mspmv.DeviceBuffer(8 * a.num_rows, dev))
-    a0 = mats[0]
+    # The headline runs under a watchdog at N > 1: an RCCL hang must end the job (exit 3) with
+    # the line printed so far, never hang it or pass as success.
+    guard = Watchdog(d, args.cg_timeout) if d.world > 1 else None
+    if d.world > 1 or os.environ.get("MSPMV_BENCH_SHARDED") == "1":  # the latter: the N > 1 path at N = 1 (tests)
+        result = run_sharded_headline(d, dev, args)
+        if guard:
+            guard.result = result
+    else:
+        mats, gs, dxs, dys, xs = [], [], [], [], []
+        for i in range(args.batch):
+            a = mspmv.CsrMatrix.synth_fem_blocked(PWTK["m"], PWTK["nnz"], PWTK["block"], PWTK["half_band_nodes"],
+                                                  seed=1 + i + 1000 * d.rank)
+            x = np.random.default_rng(2 + i + 1000 * d.rank).uniform(0.0, 1.0, a.num_cols)
+            mats.append(a)
+            gs.append(mspmv.GpuCsr(a, device=dev))
+            xs.append(x)
+            dxs.append(mspmv.DeviceBuffer.from_array(x, dev))
+            dys.append(mspmv.DeviceBuffer(8 * a.num_rows, dev))
+        a0 = mats[0]
 
-    mspmv.time_spmm_batch(gs, dxs, dys, 1, max(args.warmup, 1))   # warmup (untimed)
-    for g in gs:
-        g.sync()
-    d.barrier()
-    t0 = time.perf_counter()
-    step_ms_ev, kern_ms, kps = mspmv.time_spmm_batch(gs, dxs, dys, 1, args.steps)
-    for g in gs:
-        g.sync()
-    el = time.perf_counter() - t0
-    d.barrier()
-    el = d.max(el)
-    kern_ms = d.max(kern_ms)
+        mspmv.time_spmm_batch(gs, dxs, dys, 1, max(args.warmup, 1))   # warmup (untimed)
+        for g in gs:
+            g.sync()
+        d.barrier()
+        t0 = time.perf_counter()
+        step_ms_ev, kern_ms, kps = mspmv.time_spmm_batch(gs, dxs, dys, 1, args.steps)
+        for g in gs:
+            g.sync()
+        el = time.perf_counter() - t0
+        d.barrier()
+        el = d.max(el)
+        kern_ms = d.max(kern_ms)
 
-    flops = 2.0 * a0.num_nonzeros * args.batch * args.steps * d.world
-    value = flops / el / 1e9
-    bytes_launch = spmv_bytes(a0.num_rows, a0.num_cols, a0.num_nonzeros)
-    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    hot_ms = hot_kern = None
-    if not args.no_extras:
-        hot_ms, hot_kern, _ = mspmv.time_spmm_batch(gs[:1], dxs[:1], dys[:1], 1, 200)
-    kname = gs[0].kernel_name()
-    traffic, traffic_src = pmc_traffic(kname, bytes_launch)
-    ref_eff = (a0.num_nonzeros * 20 + a0.num_rows * 12) / (kern_ms * 1e-3) / 1e9  # cpu_spmv.cpp:722-726
+        flops = 2.0 * a0.num_nonzeros * args.batch * args.steps * d.world
+        value = flops / el / 1e9
+        bytes_launch = spmv_bytes(a0.num_rows, a0.num_cols, a0.num_nonzeros)
+        achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+        hot_ms = hot_kern = None
+        if not args.no_extras:
+            hot_ms, hot_kern, _ = mspmv.time_spmm_batch(gs[:1], dxs[:1], dys[:1], 1, 200)
+        kname = gs[0].kernel_name()
+        traffic, traffic_src = pmc_traffic(kname, bytes_launch)
+        ref_eff = (a0.num_nonzeros * 20 + a0.num_rows * 12) / (kern_ms * 1e-3) / 1e9  # cpu_spmv.cpp:722-726
 
-    result = {
-        "metric": METRIC, "value": round(value, 2), "unit": "GFLOP/s", "n_gpus": d.world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (pwtk-shaped 6-DOF FEM-blocked CSR, splitmix64 values; SuiteSparse unavailable offline)",
-        "config": {"workload": f"merge-path CSR SpMV fp64, 1 RHS, batch of {args.batch} pwtk-shaped matrices "
-                               f"per step per GPU (configs[1])",
-                   "m": a0.num_rows, "nnz": a0.num_nonzeros, "batch": args.batch,
-                   "parallelism": f"independent SpMV batches, {d.world} GPU(s)"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "kernel": kname, "bytes_per_launch": bytes_launch,
-                     "kernel_ms": round(kern_ms, 5), "kernels_per_step": kps,
-                     "note": "achieved = algorithmic bytes (12 B/nnz: int32 columns + f64 values, SURVEY 8(d)) / "
-                             "kernel time; the kernel streams per-tile 16-bit column offsets (10 B/nnz), so "
-                             "traffic (PMC bytes actually moved per launch) is below bytes_per_launch"},
-        "spmv_gflops_per_launch": round(2.0 * a0.num_nonzeros / (kern_ms * 1e-3) / 1e9, 2),
-        "reference_effective_GBps": round(ref_eff, 1),
-        "setup_ms": round(gs[0].setup_ms, 2),
-    }
-    if hot_ms is not None:
-        result["hot_single_matrix"] = {"ms_per_call": round(hot_ms, 5), "kernel_ms": round(hot_kern, 5),
-                                       "GBps_vs_algorithmic": round(bytes_launch / (hot_kern * 1e-3) / 1e9, 1),
-                                       "note": "one 143 MB matrix back to back: Infinity-Cache resident"}
-    for g in gs:
-        g.close()
+        result = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GFLOP/s", "n_gpus": d.world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (pwtk-shaped 6-DOF FEM-blocked CSR, splitmix64 values; SuiteSparse unavailable offline)",
+            "config": {"workload": f"merge-path CSR SpMV fp64, 1 RHS, batch of {args.batch} pwtk-shaped matrices "
+                                   f"per step per GPU (configs[1])",
+                       "m": a0.num_rows, "nnz": a0.num_nonzeros, "batch": args.batch,
+                       "parallelism": f"independent SpMV batches, {d.world} GPU(s)"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "kernel": kname, "bytes_per_launch": bytes_launch,
+                         "kernel_ms": round(kern_ms, 5), "kernels_per_step": kps,
+                         "note": "achieved = algorithmic bytes (12 B/nnz: int32 columns + f64 values, SURVEY 8(d)) / "
+                                 "kernel time; the kernel streams per-tile 16-bit column offsets (10 B/nnz), so "
+                                 "traffic (PMC bytes actually moved per launch) is below bytes_per_launch"},
+            "spmv_gflops_per_launch": round(2.0 * a0.num_nonzeros / (kern_ms * 1e-3) / 1e9, 2),
+            "reference_effective_GBps": round(ref_eff, 1),
+            "setup_ms": round(gs[0].setup_ms, 2),
+        }
+        if hot_ms is not None:
+            result["hot_single_matrix"] = {"ms_per_call": round(hot_ms, 5), "kernel_ms": round(hot_kern, 5),
+                                           "GBps_vs_algorithmic": round(bytes_launch / (hot_kern * 1e-3) / 1e9, 1),
+                                           "note": "one 143 MB matrix back to back: Infinity-Cache resident"}
+        for g in gs:
+            g.close()
 
-    if d.rank == 0 and not args.no_extras:  # stress shape: columns scattered one per band slice (x gathers hit a new line each)
-        sc = mspmv.CsrMatrix.synth_banded(PWTK["m"], PWTK["nnz"], 10000, seed=77)
-        with mspmv.GpuCsr(sc, device=dev) as g:
-            bx = mspmv.DeviceBuffer.from_array(np.random.default_rng(3).uniform(0, 1, sc.num_cols), dev)
-            by = mspmv.DeviceBuffer(8 * sc.num_rows, dev)
-            _, sk, _ = mspmv.time_spmm_batch([g], [bx], [by], 1, 100)
-        result["scatter_band_stress"] = {"kernel_ms": round(sk, 5),
-                                         "GBps_vs_algorithmic": round(bytes_launch / (sk * 1e-3) / 1e9, 1),
-                                         "note": "pwtk size, 53 columns per row scattered over +-10,000"}
+        if d.rank == 0 and not args.no_extras:  # stress shape: columns scattered one per band slice (x gathers hit a new line each)
+            sc = mspmv.CsrMatrix.synth_banded(PWTK["m"], PWTK["nnz"], 10000, seed=77)
+            with mspmv.GpuCsr(sc, device=dev) as g:
+                bx = mspmv.DeviceBuffer.from_array(np.random.default_rng(3).uniform(0, 1, sc.num_cols), dev)
+                by = mspmv.DeviceBuffer(8 * sc.num_rows, dev)
+                _, sk, _ = mspmv.time_spmm_batch([g], [bx], [by], 1, 100)
+            result["scatter_band_stress"] = {"kernel_ms": round(sk, 5),
+                                             "GBps_vs_algorithmic": round(bytes_launch / (sk * 1e-3) / 1e9, 1),
+                                             "note": "pwtk size, 53 columns per row scattered over +-10,000"}
 
-    if d.rank == 0 and not args.no_extras:
-        result["spmm16"] = run_spmm16(dev, min(args.cpu_seconds, 5.0), d.world == 1 and not args.no_cpu)
+        if d.rank == 0 and not args.no_extras:
+            result["spmm16"] = run_spmm16(dev, min(args.cpu_seconds, 5.0), d.world == 1 and not args.no_cpu)
 
-    if d.rank == 0 and d.world == 1 and not args.no_cpu:
-        y_cpu, cb = cpu_baseline(a0, xs[0], args.cpu_seconds)
-        result["cpu_baseline"] = cb
-        with mspmv.GpuCsr(a0, device=dev) as g:
-            y_gpu = g.spmv(xs[0])
-        rel = float(np.max(np.abs(y_gpu - y_cpu) / np.maximum(np.abs(y_cpu), 1e-300)))
-        result["cpu_baseline"]["gpu_vs_cpu_max_rel_diff"] = rel
-        result["speedup_vs_cpu"] = round(value / cb["value"], 1)
+        if d.rank == 0 and d.world == 1 and not args.no_cpu:
+            y_cpu, cb = cpu_baseline(a0, xs[0], args.cpu_seconds)
+            result["cpu_baseline"] = cb
+            with mspmv.GpuCsr(a0, device=dev) as g:
+                y_gpu = g.spmv(xs[0])
+            rel = float(np.max(np.abs(y_gpu - y_cpu) / np.maximum(np.abs(y_cpu), 1e-300)))
+            result["cpu_baseline"]["gpu_vs_cpu_max_rel_diff"] = rel
+            result["speedup_vs_cpu"] = round(value / cb["value"], 1)
     if not args.no_cg:
-        # The sharded CG (N > 1) has only ever run in the driver's multi-GPU bench: if its RCCL
-        # exchange hangs (or one rank fails while the others wait in a collective), the headline
-        # line must still print -- rank 0 prints what it has and every rank exits.
-        # A hang is a failure: the watchdog prints the line (so the headline is on record) and
-        # exits non-zero.  The lock is held through its print and exit, and the main thread
-        # marks the CG done under the same lock, so exactly one thread ever prints.
-        cg_lock, cg_state = threading.Lock(), {"done": False}
-
-        def _cg_watchdog():
-            with cg_lock:
-                if cg_state["done"]:
-                    return
-                if d.rank == 0:
-                    result["cg_error"] = f"sharded CG did not finish within {args.cg_timeout:.0f} s"
-                    print(json.dumps(result), flush=True)
-                print(f"rank {d.rank}: sharded CG hung (> {args.cg_timeout:.0f} s), exiting 3", file=sys.stderr)
-                sys.stderr.flush()
-                os._exit(3)
-        watchdog = threading.Timer(args.cg_timeout, _cg_watchdog) if d.world > 1 else None
-        if watchdog:
-            watchdog.daemon = True
-            watchdog.start()
         try:
             if d.world == 1:
                 result["cg_single"] = run_cg_single(dev, min(args.cpu_seconds, 10.0), not args.no_cpu)
@@ -423,11 +522,10 @@ def main():
                 result["spmv_nlpkkt120_size"] = large
         except Exception as e:  # the headline line must still print
             result["cg_error"] = repr(e)[:300]
-        with cg_lock:
-            cg_state["done"] = True
-        if watchdog:
-            watchdog.cancel()
 
+    if guard:
+        if not guard.finish():  # the watchdog fired meanwhile and owns the exit
+            return
     if d.rank == 0:
         print(json.dumps(result), flush=True)
     if d.td:

@@ -57,10 +57,25 @@ MSPMV_API mspmv_status mspmv_dist_destroy(mspmv_dist d);
 /* n_own rows owned, n_halo remote rows referenced, n_send owned rows other ranks reference. */
 MSPMV_API mspmv_status mspmv_dist_info(mspmv_dist d, int *n_own, int *n_halo, int *n_send);
 /* Y_own = (A X)_own with the halo exchange (collective).  Row-major n_own x L panels on the
- * device.  L in {1, 2, 4, 8, 16}. */
+ * device, any L >= 1.  Where the local rows have an interior (rows referencing owned columns
+ * only, >= half the local nonzeros: banded / FEM row blocks), it is multiplied on its own stream
+ * while the halo is packed and exchanged, and the rows next to the block ends follow the
+ * exchange.  Asynchronous on the local stream (every part joined into it).  Passing
+ * mspmv_dist_x_ext's buffer as d_X_own skips the copy of X_own into it. */
 MSPMV_API mspmv_status mspmv_dist_spmm_dev(mspmv_dist d, const double *d_X_own, double *d_Y_own, int L);
+/* The (n_own + n_halo) x L extended panel the SpMM reads: rows [0, n_own) are X_own (a caller
+ * writes them there directly), the rest receives the halo.  Valid until a call with a larger L. */
+MSPMV_API mspmv_status mspmv_dist_x_ext(mspmv_dist d, int L, double **d_x_ext);
+/* Block until the local stream (and every part joined into it) is idle. */
+MSPMV_API mspmv_status mspmv_dist_sync(mspmv_dist d);
+/* Local-only SpMM timing, no exchange: `reps` repetitions of the local multiply
+ * Y_own = A_local [X_own | X_halo] (whatever the halo rows hold) -- the same head / interior / tail
+ * launches the overlapped SpMM makes, back to back on one stream, HIP events around the region;
+ * *avg_ms per repetition (the per-rank SpMV time the bench's roofline uses at N > 1). */
+MSPMV_API mspmv_status mspmv_dist_time_local_dev(mspmv_dist d, double *d_Y_own, int L, int reps, double *avg_ms);
 /* Sharded CGSolveMultiple (collective): B_own / X_own are this rank's rows of the interleaved
- * n x L panels.  Iteration count, history and breakdown semantics as mspmv_dcg_multi. */
+ * n x L panels.  Iteration count, history and breakdown semantics as mspmv_dcg_multi, any L >= 1
+ * (widths outside 1, 2, 4, 8, 16 as independent column groups, every rank the same groups). */
 MSPMV_API mspmv_status mspmv_dist_cg_dev(mspmv_dist d, const double *d_B_own, double *d_X_own, int L,
                                          int max_iters, double tolerance, int *iters, double *max_err_hist,
                                          int hist_cap);

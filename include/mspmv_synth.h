@@ -33,6 +33,14 @@ MSPMV_API mspmv_status mspmv_synth_banded(int m, long long nnz, int half_band, u
 MSPMV_API mspmv_status mspmv_synth_fem_blocked(int m, long long nnz, int block, int half_band_nodes,
                                                unsigned long long seed, int *row_offsets, int *cols, double *vals);
 
+/* Rows [row_lo, row_hi) of the same matrix, for row-block sharding without building the whole
+ * matrix on every rank: row_offsets[row_hi - row_lo + 1] rebased to 0, GLOBAL column ids, every
+ * (row, position) holding the value mspmv_synth_fem_blocked gives it.  cols / vals may be NULL
+ * to size (row_offsets only). */
+MSPMV_API mspmv_status mspmv_synth_fem_blocked_rows(int m, long long nnz, int block, int half_band_nodes,
+                                                    unsigned long long seed, int row_lo, int row_hi,
+                                                    int *row_offsets, int *cols, double *vals);
+
 /* Power-law row lengths with the same contract as mspmv_synth_banded: row lengths drawn
  * from a Zipf-like law (a handful of rows hold a large share of nnz), columns spread over
  * the whole matrix.  Exercises merge-path load balance and long-row carries. */

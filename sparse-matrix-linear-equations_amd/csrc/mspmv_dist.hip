@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -91,6 +92,13 @@ struct mspmv_dist_s {
     double *d_red = nullptr;      // [2 L]: p.Ap, r.r
     double *d_hist = nullptr;
     int hist_cap = 0;
+    // SpMM overlap (mspmv_dist_spmm_dev): the local rows split into [0, int_lo) | [int_lo, int_hi)
+    // | [int_hi, n_own), the middle range referencing owned columns only.  The middle runs on its
+    // own handle's stream while `local`'s stream packs and exchanges the halo; head and tail
+    // follow the exchange.  Null handles when the split does not pay (no interior worth it).
+    mspmv_handle part[3] = {nullptr, nullptr, nullptr};
+    int int_lo = 0, int_hi = 0;
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // x ready, mid, halo, head, tail
 };
 
 extern "C" {
@@ -199,6 +207,12 @@ mspmv_status mspmv_dist_destroy(mspmv_dist d)
     dfree(d->d_hist);
     if (d->h_ctrl)
         (void)hipHostFree(d->h_ctrl);
+    for (auto &ph : d->part)
+        if (ph)
+            mspmv_destroy(ph);
+    for (auto &e : d->ev)
+        if (e)
+            (void)hipEventDestroy(e);
     if (d->local)
         mspmv_destroy(d->local);
     if (d->comm)
@@ -255,6 +269,50 @@ mspmv_status mspmv_dist_create(const unsigned char id[MSPMV_UNIQUE_ID_BYTES], in
     lc.column_indices = lcols.data();
     if ((st = mspmv_csr_create(&lc, device, &d->local)) != MSPMV_OK)
         return bail(st);
+    // interior rows: the longest contiguous run of rows that reference owned columns only (for a
+    // banded / FEM matrix cut into row blocks, everything but the rows within the band of either
+    // block end); split off only when it holds >= half the nonzeros and there is a halo at all
+    // MSPMV_DIST_FORCE_SPLIT=1 (tests): split at the row thirds even without a halo, so one GPU
+    // exercises the three-stream path (RCCL refuses two ranks on one device)
+    const char *force_env = getenv("MSPMV_DIST_FORCE_SPLIT");
+    const bool force = force_env && atoi(force_env) != 0 && d->n_own >= 3;
+    if ((nranks > 1 && n_halo > 0) || force) {
+        const int *ro = local_rows->row_offsets;
+        int best_lo = 0, best_hi = 0, cur = 0;
+        for (int r = 0; r <= d->n_own; ++r) {
+            bool inner = r < d->n_own;
+            for (int k = inner ? ro[r] : 0; inner && k < ro[r + 1]; ++k)
+                inner = lcols[k] < d->n_own;
+            if (!inner) {
+                if (r - cur > best_hi - best_lo) {
+                    best_lo = cur;
+                    best_hi = r;
+                }
+                cur = r + 1;
+            }
+        }
+        if (force) {
+            best_lo = d->n_own / 3;
+            best_hi = 2 * (d->n_own / 3);
+        }
+        if (force || 2LL * (ro[best_hi] - ro[best_lo]) >= (long long)nnz) {
+            d->int_lo = best_lo;
+            d->int_hi = best_hi;
+            const int cut[4] = {0, best_lo, best_hi, d->n_own};
+            for (int q = 0; q < 3; ++q) {
+                std::vector<int> pro((size_t)(cut[q + 1] - cut[q]) + 1);
+                for (int r = cut[q]; r <= cut[q + 1]; ++r)
+                    pro[(size_t)(r - cut[q])] = ro[r] - ro[cut[q]];
+                mspmv_csr_d pc{cut[q + 1] - cut[q], lc.num_cols, ro[cut[q + 1]] - ro[cut[q]], pro.data(),
+                               lcols.data() + ro[cut[q]], local_rows->values + ro[cut[q]]};
+                if ((st = mspmv_csr_create(&pc, device, &d->part[q])) != MSPMV_OK)
+                    return bail(st);
+            }
+            for (auto &e : d->ev)
+                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+                    return bail(fail_msg(MSPMV_ERR_HIP, "dist_create: hipEventCreate"));
+        }
+    }
     hipStream_t s = d->local->stream;
     // request lists: every rank learns the counts matrix, then sends each owner the global
     // ids it needs; the owner keeps them (as local rows) as its send list to that rank
@@ -436,30 +494,163 @@ mspmv_status get_local_plan(mspmv_dist_s *d, int L, const TilePlan **plan)
 
 extern "C" {
 
+mspmv_status mspmv_dist_x_ext(mspmv_dist d, int L, double **d_x_ext)
+{
+    if (!d || !d_x_ext || L < 1)
+        return fail_msg(MSPMV_ERR_INVALID, "dist_x_ext: bad arguments");
+    D_HIP(hipSetDevice(d->device));
+    D_ST(ensure_buffers(d, L, 1, 1, 0));
+    *d_x_ext = d->d_pext;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_dist_sync(mspmv_dist d)
+{
+    if (!d)
+        return fail_msg(MSPMV_ERR_INVALID, "null dist");
+    D_HIP(hipSetDevice(d->device));
+    D_HIP(hipStreamSynchronize(d->local->stream));
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_dist_time_local_dev(mspmv_dist d, double *d_Y_own, int L, int reps, double *avg_ms)
+{
+    if (!d || !avg_ms || L < 1 || reps < 1)
+        return fail_msg(MSPMV_ERR_INVALID, "dist_time_local: bad arguments");
+    D_HIP(hipSetDevice(d->device));
+    D_ST(ensure_buffers(d, L, 1, 1, 0));
+    // the row ranges the overlapped SpMM launches (or the whole local matrix), back to back on
+    // one stream, events around the region only (per-launch events would inflate it)
+    mspmv_handle hs[3];
+    const double *xs[3];
+    double *ys[3];
+    int n = 0;
+    const int offs[3] = {0, d->int_lo, d->int_hi};
+    if (!d->part[1]) {
+        hs[0] = d->local;
+        xs[0] = d->d_pext;
+        ys[0] = d_Y_own;
+        n = 1;
+    }
+    for (int q = 0; q < 3 && d->part[1]; ++q)
+        if (d->part[q]->m > 0) {
+            hs[n] = d->part[q];
+            xs[n] = d->d_pext;
+            ys[n] = d_Y_own + (size_t)offs[q] * L;
+            ++n;
+        }
+    double kern = 0.0;
+    int kps = 0;
+    return mspmv_time_spmm_batch_dev(n, hs, xs, ys, L, reps, avg_ms, &kern, &kps);
+}
+
 mspmv_status mspmv_dist_spmm_dev(mspmv_dist d, const double *d_X_own, double *d_Y_own, int L)
 {
     if (!d)
         return fail_msg(MSPMV_ERR_INVALID, "null dist");
-    if (!supported_L(L))
-        return fail_msg(MSPMV_ERR_UNSUPPORTED, "L must be one of 1, 2, 4, 8, 16");
+    if (L < 1)
+        return fail_msg(MSPMV_ERR_INVALID, "L must be >= 1");
     D_HIP(hipSetDevice(d->device));
-    const TilePlan *plan = nullptr;
-    D_ST(get_local_plan(d, L, &plan));
-    D_ST(ensure_buffers(d, L, 1, plan->num_tiles, 0));
+    D_ST(ensure_buffers(d, L, 1, 1, 0));
     hipStream_t s = d->local->stream;
-    if (d->n_own)
+    if (d->n_own && d_X_own != d->d_pext)
         D_HIP(hipMemcpyAsync(d->d_pext, d_X_own, sizeof(double) * (size_t)d->n_own * L, hipMemcpyDeviceToDevice, s));
+    if (!d->part[1]) {  // no interior split: exchange, then the whole local SpMM
+        D_ST(halo_exchange(d, L, nullptr));
+        return mspmv_dspmm_dev(d->local, d->d_pext, d_Y_own, L);
+    }
+    // interior rows on their own stream while this stream packs and exchanges the halo
+    mspmv_handle head = d->part[0], mid = d->part[1], tail = d->part[2];
+    D_HIP(hipEventRecord(d->ev[0], s));
+    D_HIP(hipStreamWaitEvent(mid->stream, d->ev[0], 0));
+    D_ST(mspmv_dspmm_dev(mid, d->d_pext, d_Y_own + (size_t)d->int_lo * L, L));
+    D_HIP(hipEventRecord(d->ev[1], mid->stream));
     D_ST(halo_exchange(d, L, nullptr));
-    return mspmv_dspmm_dev(d->local, d->d_pext, d_Y_own, L);
+    D_HIP(hipEventRecord(d->ev[2], s));
+    const int offs[2] = {0, d->int_hi};
+    mspmv_handle ends[2] = {head, tail};
+    for (int q = 0; q < 2; ++q) {
+        if (ends[q]->m == 0)
+            continue;
+        D_HIP(hipStreamWaitEvent(ends[q]->stream, d->ev[2], 0));
+        D_ST(mspmv_dspmm_dev(ends[q], d->d_pext, d_Y_own + (size_t)offs[q] * L, L));
+        D_HIP(hipEventRecord(d->ev[3 + q], ends[q]->stream));
+        D_HIP(hipStreamWaitEvent(s, d->ev[3 + q], 0));
+    }
+    D_HIP(hipStreamWaitEvent(s, d->ev[1], 0));
+    return MSPMV_OK;
 }
 
+static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *d_X_own, int L, int max_iters,
+                                   double tolerance, int *iters, double *max_err_hist, int hist_cap);
+
+// Any L: the L recurrences are independent per column (no_pretreatment.hpp:109-120,163-176), so a
+// width outside {1, 2, 4, 8, 16} is solved as column groups of native widths, one after another,
+// each a collective solve that every rank runs in the same order; iteration count = the groups'
+// maximum, history = the max over groups with finished groups frozen (mspmv_dcg_multi's rule).
 mspmv_status mspmv_dist_cg_dev(mspmv_dist d, const double *d_B_own, double *d_X_own, int L, int max_iters,
                                double tolerance, int *iters, double *max_err_hist, int hist_cap)
 {
     if (!d)
         return fail_msg(MSPMV_ERR_INVALID, "null dist");
-    if (!supported_L(L))
-        return fail_msg(MSPMV_ERR_UNSUPPORTED, "L must be one of 1, 2, 4, 8, 16");
+    if (L < 1)
+        return fail_msg(MSPMV_ERR_INVALID, "L must be >= 1");
+    if (supported_L(L))
+        return dist_cg_native(d, d_B_own, d_X_own, L, max_iters, tolerance, iters, max_err_hist, hist_cap);
+    D_HIP(hipSetDevice(d->device));
+    const size_t m = (size_t)std::max(d->n_own, 1);
+    const int cap = max_err_hist ? std::max(hist_cap, 0) : 0;
+    double *gb = nullptr, *gx = nullptr;
+    D_ST(dalloc(&gb, m * 16));
+    mspmv_status st = dalloc(&gx, m * 16);
+    hipStream_t s = d->local->stream;
+    std::vector<std::vector<double>> gh;
+    std::vector<int> git;
+    int total = 0;
+    bool broke = false;
+    for (int c0 = 0; c0 < L && st == MSPMV_OK;) {
+        int w = 16;
+        while (w > L - c0)
+            w >>= 1;
+        if (d->n_own && launch_panel_copy(d_B_own + c0, L, gb, w, (long long)d->n_own, w, w, s) != hipSuccess) {
+            st = fail_msg(MSPMV_ERR_HIP, "dist CG: column group copy");
+            break;
+        }
+        std::vector<double> hg((size_t)std::max(cap, 1));
+        int it = 0;
+        st = dist_cg_native(d, gb, gx, w, max_iters, tolerance, &it, cap ? hg.data() : nullptr, cap);
+        if (st == MSPMV_ERR_BREAKDOWN) {
+            broke = true;
+            st = MSPMV_OK;
+        }
+        if (st == MSPMV_OK && d->n_own &&
+            (launch_panel_copy(gx, w, d_X_own + c0, L, (long long)d->n_own, w, w, s) != hipSuccess ||
+             hipStreamSynchronize(s) != hipSuccess))
+            st = fail_msg(MSPMV_ERR_HIP, "dist CG: column group copy back");
+        total = std::max(total, it);
+        gh.push_back(std::move(hg));
+        git.push_back(it);
+        c0 += w;
+    }
+    dfree(gb);
+    dfree(gx);
+    if (iters)
+        *iters = total;
+    for (int k = 0; k < std::min(total, cap); ++k) {
+        double v = 0.0;
+        for (size_t g = 0; g < gh.size(); ++g)
+            if (git[g] > 0)
+                v = std::max(v, gh[g][(size_t)std::min(k, git[g] - 1)]);
+        max_err_hist[k] = v;
+    }
+    if (st == MSPMV_OK && broke)
+        return fail_msg(MSPMV_ERR_BREAKDOWN, "dist CG breakdown: non-finite alpha in at least one column (frozen)");
+    return st;
+}
+
+static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *d_X_own, int L, int max_iters,
+                                   double tolerance, int *iters, double *max_err_hist, int hist_cap)
+{
     if (max_iters < 0)
         return fail_msg(MSPMV_ERR_INVALID, "max_iters < 0");
     D_HIP(hipSetDevice(d->device));

@@ -73,21 +73,29 @@ mspmv_status mspmv_synth_banded(int m, long long nnz, int half_band, unsigned lo
     return MSPMV_OK;
 }
 
-mspmv_status mspmv_synth_fem_blocked(int m, long long nnz, int block, int half_band_nodes,
-                                     unsigned long long seed, int *row_offsets, int *cols, double *vals)
+// Rows [row_lo, row_hi) of the node-blocked FEM matrix (global column ids, row offsets rebased to
+// row_lo's); every value is the one the whole-matrix generator gives the same (row, position).
+static mspmv_status fem_blocked_rows(int m, long long nnz, int block, int half_band_nodes, unsigned long long seed,
+                                     int row_lo, int row_hi, int *row_offsets, int *cols, double *vals)
 {
-    if (m <= 0 || block <= 0 || nnz < 0 || nnz > 0x7fffffffLL || !row_offsets || (nnz && (!cols || !vals)))
+    if (m <= 0 || block <= 0 || nnz < 0 || nnz > 0x7fffffffLL || !row_offsets || row_lo < 0 || row_hi > m ||
+        row_lo > row_hi)
         return MSPMV_ERR_INVALID;
     const int nodes = (m + block - 1) / block;
     const long long maxlen = (nnz + m - 1) / m;
     const int maxblk = (int)((maxlen + block - 1) / block);
     if (half_band_nodes < 0 || 2LL * half_band_nodes + 1 < maxblk || maxblk > nodes)
         return MSPMV_ERR_INVALID;
+    auto ro = [&](long long i) { return (long long)(i * nnz / m); };  // global row offsets
+    const long long base = ro(row_lo);
 #pragma omp parallel for schedule(static)
-    for (int i = 0; i <= m; ++i)
-        row_offsets[i] = (int)((long long)i * nnz / m);
+    for (int i = row_lo; i <= row_hi; ++i)
+        row_offsets[i - row_lo] = (int)(ro(i) - base);
+    if (!cols || !vals)  // sizing call
+        return MSPMV_OK;
+    const int node_lo = row_lo / block, node_hi = row_hi == row_lo ? node_lo : (row_hi - 1) / block + 1;
 #pragma omp parallel for schedule(dynamic, 64)
-    for (int I = 0; I < nodes; ++I) {
+    for (int I = node_lo; I < node_hi; ++I) {
         // neighbour nodes of node I: maxblk picks, one per slice of the node band, own node forced
         int nb[1024];
         const int nblk = std::min(maxblk, 1024);
@@ -110,9 +118,10 @@ mspmv_status mspmv_synth_fem_blocked(int m, long long nnz, int block, int half_b
                 if (nb[q] <= nb[q - 1])
                     nb[q] = nb[q - 1] + 1;
         }
-        const int r_end = std::min(m, (I + 1) * block);
-        for (int i = I * block; i < r_end; ++i) {
-            const int s = row_offsets[i], ell = row_offsets[i + 1] - s;
+        const int r_beg = std::max(row_lo, I * block), r_end = std::min(row_hi, std::min(m, (I + 1) * block));
+        for (int i = r_beg; i < r_end; ++i) {
+            const long long sg = ro(i);                       // global position (values)
+            const int s = (int)(sg - base), ell = (int)(ro(i + 1) - sg);
             int k = 0;
             for (int q = 0; q < take && k < ell; ++q)
                 for (int d = 0; d < block && k < ell; ++d) {
@@ -124,10 +133,25 @@ mspmv_status mspmv_synth_fem_blocked(int m, long long nnz, int block, int half_b
             for (int extra = 0; k < ell; ++extra)  // only when the matrix edge cut a block short
                 cols[s + k++] = std::min(m - 1, (int)(((long long)nb[take - 1] + 1) * block + extra));
             for (int q = 0; q < ell; ++q)
-                vals[s + q] = 0.5 + u01(seed ^ 0x5bd1e995ull, (uint64_t)(s + q));
+                vals[s + q] = 0.5 + u01(seed ^ 0x5bd1e995ull, (uint64_t)(sg + q));
         }
     }
     return MSPMV_OK;
+}
+
+mspmv_status mspmv_synth_fem_blocked(int m, long long nnz, int block, int half_band_nodes,
+                                     unsigned long long seed, int *row_offsets, int *cols, double *vals)
+{
+    if (nnz && (!cols || !vals))
+        return MSPMV_ERR_INVALID;
+    return fem_blocked_rows(m, nnz, block, half_band_nodes, seed, 0, m, row_offsets, cols, vals);
+}
+
+mspmv_status mspmv_synth_fem_blocked_rows(int m, long long nnz, int block, int half_band_nodes,
+                                          unsigned long long seed, int row_lo, int row_hi, int *row_offsets,
+                                          int *cols, double *vals)
+{
+    return fem_blocked_rows(m, nnz, block, half_band_nodes, seed, row_lo, row_hi, row_offsets, cols, vals);
 }
 
 mspmv_status mspmv_synth_powerlaw(int m, int n, long long nnz, double exponent, unsigned long long seed,

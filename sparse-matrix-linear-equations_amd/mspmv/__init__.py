@@ -124,8 +124,12 @@ _SIGS = {
     "mspmv_dist_destroy": (_I, [_P]),
     "mspmv_dist_info": (_I, [_P, _PI, _PI, _PI]),
     "mspmv_dist_spmm_dev": (_I, [_P, _P, _P, _I]),
+    "mspmv_dist_x_ext": (_I, [_P, _I, ctypes.POINTER(_P)]),
+    "mspmv_dist_sync": (_I, [_P]),
+    "mspmv_dist_time_local_dev": (_I, [_P, _P, _I, _I, _PD]),
     "mspmv_dist_cg_dev": (_I, [_P, _P, _P, _I, _I, _D, _PI, _P, _I]),
     "mspmv_synth_fem_blocked": (_I, [_I, ctypes.c_longlong, _I, _I, ctypes.c_ulonglong, _P, _P, _P]),
+    "mspmv_synth_fem_blocked_rows": (_I, [_I, ctypes.c_longlong, _I, _I, ctypes.c_ulonglong, _I, _I, _P, _P, _P]),
     "mspmv_synth_powerlaw": (_I, [_I, _I, ctypes.c_longlong, _D, ctypes.c_ulonglong, _P, _P, _P]),
     "mspmv_synth_stencil": (_I, [_I, _I, _I, _I, _I, ctypes.c_ulonglong, _D, _P, _P, _P,
                                  ctypes.POINTER(ctypes.c_longlong)]),
@@ -238,6 +242,21 @@ class CsrMatrix:
         _check(lib.mspmv_synth_fem_blocked(m, nnz, block, half_band_nodes, seed, _ptr(ro), _ptr(ci), _ptr(va)),
                "synth_fem_blocked")
         return cls(m, m, nnz, ro, ci[:nnz], va[:nnz])
+
+    @classmethod
+    def synth_fem_blocked_rows(cls, m: int, nnz: int, block: int, half_band_nodes: int, seed: int,
+                               row_lo: int, row_hi: int) -> "CsrMatrix":
+        """Rows [row_lo, row_hi) of synth_fem_blocked(m, nnz, ...) with GLOBAL column ids (num_cols
+        = m): one rank's row block, generated without the rest of the matrix."""
+        ro = np.empty(row_hi - row_lo + 1, np.int32)
+        _check(lib.mspmv_synth_fem_blocked_rows(m, nnz, block, half_band_nodes, seed, row_lo, row_hi, _ptr(ro),
+                                                None, None), "synth_fem_blocked_rows")
+        k = int(ro[-1])
+        ci = np.empty(max(k, 1), np.int32)
+        va = np.empty(max(k, 1), np.float64)
+        _check(lib.mspmv_synth_fem_blocked_rows(m, nnz, block, half_band_nodes, seed, row_lo, row_hi, _ptr(ro),
+                                                _ptr(ci), _ptr(va)), "synth_fem_blocked_rows")
+        return cls(row_hi - row_lo, m, k, ro, ci[:k], va[:k])
 
     @classmethod
     def synth_powerlaw(cls, m: int, n: int, nnz: int, exponent: float = 1.2, seed: int = 3) -> "CsrMatrix":
@@ -645,6 +664,20 @@ def dist_partition(a: CsrMatrix, nranks: int) -> np.ndarray:
     return rb
 
 
+def dist_partition_offsets(row_offsets: np.ndarray, num_rows: int, num_nonzeros: int, nranks: int) -> np.ndarray:
+    """dist_partition from a global row_offsets array alone (ranks that never build the matrix)."""
+    ro = np.ascontiguousarray(row_offsets, np.int32)
+    rb = np.empty(nranks + 1, np.int32)
+    _check(lib.mspmv_dist_partition(_ptr(ro), num_rows, num_nonzeros, nranks, _ptr(rb)), "dist_partition")
+    return rb
+
+
+def memcpy_h2d_ptr(d_ptr: int, a: np.ndarray) -> None:
+    """Copy a host array to a raw device pointer (e.g. DistCsr.x_ext)."""
+    a = np.ascontiguousarray(a)
+    _check(lib.mspmv_memcpy_h2d(d_ptr, _ptr(a), a.nbytes), "memcpy_h2d")
+
+
 def local_rows(a: CsrMatrix, row_begin: np.ndarray, rank: int) -> CsrMatrix:
     """This rank's rows with GLOBAL column ids (num_cols = global n)."""
     lo, hi = int(row_begin[rank]), int(row_begin[rank + 1])
@@ -693,8 +726,28 @@ class DistCsr:
         _check(lib.mspmv_dist_info(self.h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)), "dist_info")
         return {"n_own": a.value, "n_halo": b.value, "n_send": c.value}
 
-    def spmm_dev(self, dX: DeviceBuffer, dY: DeviceBuffer, L: int):
-        _check(lib.mspmv_dist_spmm_dev(self.h, dX.ptr, dY.ptr, L), "dist_spmm_dev")
+    def spmm_dev(self, dX, dY: DeviceBuffer, L: int, sync: bool = True):
+        """Y_own = (A X)_own with the halo exchange.  dX: a DeviceBuffer of X_own, or the
+        extended buffer's pointer (x_ext) whose first n_own rows the caller filled."""
+        xp = dX.ptr if isinstance(dX, DeviceBuffer) else dX
+        _check(lib.mspmv_dist_spmm_dev(self.h, xp, dY.ptr, L), "dist_spmm_dev")
+        if sync:
+            self.sync()
+
+    def x_ext(self, L: int) -> int:
+        """Device pointer of the (n_own + n_halo) x L extended panel (rows [0, n_own) = X_own)."""
+        p = ctypes.c_void_p()
+        _check(lib.mspmv_dist_x_ext(self.h, L, ctypes.byref(p)), "dist_x_ext")
+        return p.value
+
+    def sync(self):
+        _check(lib.mspmv_dist_sync(self.h), "dist_sync")
+
+    def time_local(self, dY: DeviceBuffer, L: int, reps: int) -> float:
+        """Average ms of the local SpMM alone (no exchange), HIP events on the local stream."""
+        ms = ctypes.c_double()
+        _check(lib.mspmv_dist_time_local_dev(self.h, dY.ptr, L, reps, ctypes.byref(ms)), "dist_time_local")
+        return ms.value
 
     def cg_dev(self, dB: DeviceBuffer, dX: DeviceBuffer, L: int, max_iters: int, tolerance: float,
                hist_cap: int = 0):

@@ -190,3 +190,97 @@ def test_localize_roundtrip():
         np.testing.assert_array_equal(back, loc.column_indices)
         assert np.all(np.diff(halo) > 0) and counts.sum() == len(halo) and counts[rank] == 0
         assert not np.any((halo >= lo) & (halo < hi))
+
+
+# ---- the bench's weak-scaled sharded headline (bench.py run_sharded_headline), host side -------
+def _weak_worker(rank, world, port, out_dir):
+    """Each rank builds ONLY its row block of the N x pwtk-rows FEM matrix
+    (mspmv_synth_fem_blocked_rows), partitioned from the analytic row offsets
+    (dist_partition_offsets), localizes it, and exchanges halo request lists over gloo as
+    mspmv_dist_create does over RCCL; the halo x rows it receives are checked against the global x,
+    and its local SpMV (numpy on [x_own | x_halo]) against the whole matrix's rows."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    for p in (ROOT, os.path.join(ROOT, "sparse-matrix-linear-equations_amd")):
+        sys.path.insert(0, p)
+    import torch
+    import torch.distributed as td
+    import mspmv
+    td.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        m1, nnz1 = 3000 * 6, 3000 * 6 * 53
+        M, NNZ = m1 * world, nnz1 * world
+        ro = (np.arange(M + 1, dtype=np.int64) * NNZ // M).astype(np.int32)
+        rb = mspmv.dist_partition_offsets(ro, M, NNZ, world)
+        lo, hi = int(rb[rank]), int(rb[rank + 1])
+        loc = mspmv.CsrMatrix.synth_fem_blocked_rows(M, NNZ, 6, 170, 5, lo, hi)
+        lcols, halo, counts = mspmv.dist_localize(rb, rank, loc)
+        n_own = hi - lo
+        x = np.random.default_rng(9).uniform(0, 1, M)
+        # request lists: every rank tells each owner which of its rows it needs
+        cnt = torch.tensor(counts, dtype=torch.int64)
+        allc = [torch.zeros(world, dtype=torch.int64) for _ in range(world)]
+        td.all_gather(allc, cnt)
+        offs = np.concatenate([[0], np.cumsum(counts)])
+        sends = {}
+        reqs = []
+        for g in range(world):
+            if g == rank:
+                continue
+            need = int(allc[g][rank])       # rows rank g needs from me
+            buf = torch.zeros(need, dtype=torch.int64)
+            mine = torch.tensor(halo[offs[g]:offs[g + 1]].astype(np.int64))
+            if rank < g:
+                td.send(mine, g)
+                td.recv(buf, g)
+            else:
+                td.recv(buf, g)
+                td.send(mine, g)
+            sends[g] = buf.numpy()
+            reqs.append((g, need))
+        # halo exchange of x (values sent = x_own at the requested rows)
+        xh = np.zeros(len(halo))
+        for g in range(world):
+            if g == rank:
+                continue
+            out = torch.tensor(x[lo:hi][sends[g] - lo])
+            inn = torch.zeros(int(counts[g]), dtype=torch.float64)
+            if rank < g:
+                td.send(out, g)
+                td.recv(inn, g)
+            else:
+                td.recv(inn, g)
+                td.send(out, g)
+            xh[offs[g]:offs[g + 1]] = inn.numpy()
+        assert np.array_equal(xh, x[halo])
+        xe = np.concatenate([x[lo:hi], xh])
+        lens = np.diff(loc.row_offsets)
+        y = np.zeros(n_own)
+        np.add.at(y, np.repeat(np.arange(n_own), lens), loc.values * xe[lcols])
+        np.save(os.path.join(out_dir, f"y_{rank}.npy"), y)
+        np.save(os.path.join(out_dir, f"meta_{rank}.npy"), np.array([lo, hi, len(halo)]))
+    finally:
+        td.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_weak_scaled_sharding_gloo(tmp_path, world, mspmv):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    ps = [ctx.Process(target=_weak_worker, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    m1, nnz1 = 3000 * 6, 3000 * 6 * 53
+    a = mspmv.CsrMatrix.synth_fem_blocked(m1 * world, nnz1 * world, 6, 170, seed=5)
+    x = np.random.default_rng(9).uniform(0, 1, a.num_rows)
+    lens = np.diff(a.row_offsets)
+    yref = np.zeros(a.num_rows)
+    np.add.at(yref, np.repeat(np.arange(a.num_rows), lens), a.values * x[a.column_indices])
+    y = np.concatenate([np.load(tmp_path / f"y_{r}.npy") for r in range(world)])
+    np.testing.assert_allclose(y, yref, rtol=1e-13, atol=0)
+    metas = [np.load(tmp_path / f"meta_{r}.npy") for r in range(world)]
+    assert all(abs((m[1] - m[0]) - m1) <= 6 for m in metas)   # weak scaling: pwtk-sized blocks
+    assert all(0 < m[2] < 0.2 * m1 for m in metas)            # halo: a band's worth, not the matrix

@@ -104,3 +104,82 @@ def test_dist_world2_one_device(tmp_path, orc):
             pytest.skip(f"RCCL refuses two ranks on one device: {errs[0][:200]}")
         pytest.fail("; ".join(errs))
     _check(tmp_path, orc, 2, 4)
+
+
+_SPLIT_CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import mspmv
+from _oracle import Oracle
+orc = Oracle()
+a = mspmv.CsrMatrix.synth_fem_blocked(36000, 36000 * 53, 6, 340, seed=3)
+rb = mspmv.dist_partition(a, 1)
+d = mspmv.DistCsr(mspmv.comm_unique_id(), 1, 0, 0, rb, mspmv.local_rows(a, rb, 0))
+rng = np.random.default_rng(4)
+for L in (1, 3, 8):
+    X = rng.uniform(-1, 1, (a.num_rows, L))
+    dX = mspmv.DeviceBuffer.from_array(X)
+    dY = mspmv.DeviceBuffer(8 * a.num_rows * L)
+    d.spmm_dev(dX, dY, L)
+    Y = dY.download((a.num_rows, L))
+    ref = orc.csr_spmm_t(a, X)
+    bound = np.zeros_like(ref)   # reordering bound: 2 (len + 1) eps (|A| |X|)
+    np.add.at(bound, np.repeat(np.arange(a.num_rows), np.diff(a.row_offsets)),
+              np.abs(a.values)[:, None] * np.abs(X[a.column_indices]))
+    assert np.all(np.abs(Y - ref) <= 2 * 54 * 2.0 ** -53 * bound + 1e-300), L
+    xp = d.x_ext(L)                       # the copy-free form the bench uses
+    mspmv.memcpy_h2d_ptr(xp, X)
+    d.spmm_dev(xp, dY, L)
+    assert np.array_equal(dY.download((a.num_rows, L)), Y), L
+assert d.time_local(dY, 1, 5) > 0
+d.close()
+print("SPLIT OK")
+"""
+
+
+def test_dist_three_stream_split_one_gpu(tmp_path):
+    """MSPMV_DIST_FORCE_SPLIT=1: the local rows split at their thirds (head | interior | tail), the
+    interior on its own stream beside the (here empty) exchange, the ends after it, every part
+    joined into the local stream -- the overlapped SpMM of N > 1 ranks, run on one GPU (RCCL
+    refuses two ranks on one device), for L = 1, 3 (chunked) and 8, and through x_ext."""
+    import subprocess
+    env = dict(os.environ, MSPMV_DIST_FORCE_SPLIT="1")
+    r = subprocess.run([sys.executable, "-c", _SPLIT_CHILD, os.path.join(ROOT, "sparse-matrix-linear-equations_amd"),
+                        os.path.join(ROOT, "tests")], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "SPLIT OK" in r.stdout, r.stdout + r.stderr[-3000:]
+
+
+def test_dist_cg_any_width(orc):
+    """mspmv_dist_cg_dev at L = 3 and 12: column groups of native widths, every rank (here one) the
+    same groups; iterations, history and X as the oracle's single L-wide CGSolveMultiple."""
+    import mspmv
+    a = _matrix()
+    rb = mspmv.dist_partition(a, 1)
+    d = mspmv.DistCsr(mspmv.comm_unique_id(), 1, 0, 0, rb, mspmv.local_rows(a, rb, 0))
+    for L in (3, 12):
+        B = np.random.default_rng(L).uniform(0, 1, (a.num_rows, L))
+        dB = mspmv.DeviceBuffer.from_array(B)
+        dX = mspmv.DeviceBuffer(8 * a.num_rows * L)
+        it, hist, st = d.cg_dev(dB, dX, L, 3000, 1e-9, hist_cap=3000)
+        Xg = dX.download((a.num_rows, L))
+        Xo, it_o, ho = orc.cg_multi(a, B, 3000, 1e-9, kernel=1, P=8, hist_cap=3000)
+        assert st == 0 and abs(it - it_o) <= 1
+        k = min(len(hist), len(ho))
+        np.testing.assert_allclose(hist[:k], ho[:k], rtol=0, atol=1e-10)
+        assert np.linalg.norm(Xg - Xo) <= 1e-8 * np.linalg.norm(Xo)
+    d.close()
+
+
+def test_bench_sharded_headline_world1(tmp_path):
+    """bench.py's N > 1 headline (run_sharded_headline: per-rank row blocks generated alone,
+    x_ext, overlapped SpMM, local timing) run at world 1 (MSPMV_BENCH_SHARDED=1): one JSON line with
+    the contract's fields and a plausible roofline."""
+    import json
+    import subprocess
+    env = dict(os.environ, MSPMV_BENCH_SHARDED="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "2", "--no-cg",
+                        "--no-cpu"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["scaling"] == "weak" and line["value"] > 100
+    assert 0.2 < line["roofline"]["frac"] < 1.0
