@@ -153,6 +153,95 @@ def cpu_baseline(a, x, seconds):
                          f"{calls} calls in {el:.1f} s"}
 
 
+FLUSH_BYTES = 512 << 20   # >= 512 MB MALL-flush write between cold calls
+CANT = dict(m=62451, nnz=4007383, band=2000, seed=1)
+RMA10 = dict(m=46835, nnz=2374001, band=3000, seed=2)
+
+
+def gpu_spmv_hot_cold(a, dev, seed=2):
+    """One matrix's SpMV tile kernel: hot (back-to-back launches; a matrix below 256 MiB stays
+    Infinity-Cache resident) and cold (a 512 MiB flush write before every timed launch, SURVEY
+    8(d)); HIP events around each launch.  frac is priced on the cold time."""
+    x = np.random.default_rng(seed).uniform(0.0, 1.0, a.num_cols)
+    with mspmv.GpuCsr(a, device=dev) as g:
+        dx, dy = mspmv.DeviceBuffer.from_array(x, dev), mspmv.DeviceBuffer(8 * a.num_rows, dev)
+        g.time_spmm(dx, dy, 1, 5)
+        _, hot, _ = g.time_spmm(dx, dy, 1, 200)
+        _, cold, _ = g.time_spmm(dx, dy, 1, 50, FLUSH_BYTES)
+        kname = g.kernel_name()
+    nb = spmv_bytes(a.num_rows, a.num_cols, a.num_nonzeros)
+    return x, {"m": a.num_rows, "nnz": a.num_nonzeros, "kernel": kname, "bytes_per_launch": nb,
+               "hot_kernel_ms": round(hot, 5), "hot_GBps": round(nb / hot / 1e6, 1),
+               "cold_kernel_ms": round(cold, 5), "cold_GBps": round(nb / cold / 1e6, 1),
+               "gflops_cold": round(2.0 * a.num_nonzeros / cold / 1e6, 1),
+               "frac": round(nb / cold / 1e6 / HBM_PEAK_GBS, 4)}
+
+
+def _threads():
+    return max(1, min(int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1), os.cpu_count() or 1))
+
+
+def _time_calls(fn, seconds):
+    fn()
+    calls, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        calls += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and calls >= 3:
+            return calls, el
+
+
+def cpu_spmv_baselines(a, x, seconds):
+    """cpu_spmv.cpp's three CsrMV strategies on the host cores, ~`seconds` each: the merge-path
+    CsrMV, the row-split OmpCsrSpmv (:271-294) and the nonzero-split OmpNonzeroSplitCsrmm
+    (:506-570).  cpu_spmv.cpp itself needs <mkl.h>; its kernels are timed through the reference's
+    compiled work_2025 twins (oracle/_ref: OmpMergeCsrmm / OmpCsrSpmmT / OmpNonzeroSplitCsrmm at
+    num_vectors = 1, the same operation order) where that build exists, else the oracle ports."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from _oracle import REF_SO, Oracle, RefLib
+    P = _threads()
+    X = np.ascontiguousarray(x[:, None])
+    orc = Oracle()
+    legs = {}
+    if os.path.exists(REF_SO):
+        ref = RefLib()
+        fns = {"merge_OmpMergeCsrmv": (lambda: ref.merge_csrmm(a, X, P), "reference"),
+               "row_split_OmpCsrSpmv": (lambda: ref.csr_spmm_t(a, X, P), "reference"),
+               "nonzero_split_OmpNonzeroSplitCsrmm": (lambda: ref.nonzero_split_csrmm(a, X, P), "reference")}
+    else:
+        y0 = np.zeros(a.num_rows)
+        fns = {"merge_OmpMergeCsrmv": (lambda: orc.merge_csrmv(a, x, P), "port"),
+               "row_split_OmpCsrSpmv": (lambda: orc.csr_spmv(a, x), "port"),
+               "nonzero_split_OmpNonzeroSplitCsrmm": (lambda: orc.nonzero_split_csrmv_v1(a, x, min(P, 256), y0),
+                                                      "port")}
+    for name, (fn, kind) in fns.items():
+        calls, el = _time_calls(fn, seconds)
+        legs[name] = {"gflops": round(2.0 * a.num_nonzeros * calls / el / 1e9, 3),
+                      "ms_per_call": round(el / calls * 1e3, 4), "cores": P, "kind": kind,
+                      "sample": f"{calls} calls in {el:.1f} s"}
+    return legs
+
+
+def run_spmv_shapes(dev, cpu_seconds, do_cpu):
+    """configs[0] (the reference's CPU merge SpMV on cant, core count stated) beside the GPU on
+    the same cant-shaped matrix, and configs[1]'s second matrix (rma10 shape) on the GPU; both
+    fit the Infinity Cache, so hot and cold (flushed) kernel times are reported."""
+    out = {}
+    shapes = {"cant": (CANT, "configs[0]: cant-shaped banded, 64.2 nnz/row, band +-2,000"),
+              "rma10": (RMA10, "configs[1] second matrix: rma10-shaped banded, 50.7 nnz/row, band +-3,000")}
+    for name, (sh, what) in shapes.items():
+        a = mspmv.CsrMatrix.synth_banded(sh["m"], sh["nnz"], sh["band"], seed=sh["seed"])
+        x, r = gpu_spmv_hot_cold(a, dev)
+        r["workload"] = what
+        if name == "cant" and do_cpu:
+            r["cpu_baselines"] = cpu_spmv_baselines(a, x, cpu_seconds)
+            best = max(v["gflops"] for v in r["cpu_baselines"].values())
+            r["gpu_cold_vs_best_cpu"] = round(r["gflops_cold"] / best, 1)
+        out[name] = r
+    return out
+
+
 def run_spmm16(dev, cpu_seconds, do_cpu):
     """configs[2]: CSR SpMM fp64 with a 16-column row-major panel (OmpMergeCsrmm's layout,
     merge_based.hpp:46-153) on the cant and pwtk shapes; kernel time by HIP events over
@@ -170,12 +259,15 @@ def run_spmm16(dev, cpu_seconds, do_cpu):
             dY = mspmv.DeviceBuffer(8 * a.num_rows * L, dev)
             g.time_spmm(dX, dY, L, 5)
             _, kern_ms, _ = g.time_spmm(dX, dY, L, 100)
+            _, cold_ms, _ = g.time_spmm(dX, dY, L, 30, FLUSH_BYTES)
         nb = 12 * a.num_nonzeros + 4 * (a.num_rows + 1) + 8 * L * (a.num_cols + a.num_rows)
-        out[name] = {"m": a.num_rows, "nnz": a.num_nonzeros, "kernel_ms": round(kern_ms, 5),
-                     "gflops": round(2.0 * L * a.num_nonzeros / kern_ms / 1e6, 1), "bytes_per_launch": nb,
-                     "achieved_GBps": round(nb / kern_ms / 1e6, 1), "frac": round(nb / kern_ms / 1e6 / HBM_PEAK_GBS, 4),
-                     "note": "back-to-back launches; the matrix + panel fit the 256 MiB Infinity Cache"
-                             if nb < 200e6 else "back-to-back launches"}
+        out[name] = {"m": a.num_rows, "nnz": a.num_nonzeros, "bytes_per_launch": nb,
+                     "hot_kernel_ms": round(kern_ms, 5), "hot_GBps": round(nb / kern_ms / 1e6, 1),
+                     "hot_frac": round(nb / kern_ms / 1e6 / HBM_PEAK_GBS, 4),
+                     "cold_kernel_ms": round(cold_ms, 5), "gflops_cold": round(2.0 * L * a.num_nonzeros / cold_ms / 1e6, 1),
+                     "achieved_GBps": round(nb / cold_ms / 1e6, 1), "frac": round(nb / cold_ms / 1e6 / HBM_PEAK_GBS, 4),
+                     "note": "hot: back-to-back launches (matrix + panel Infinity-Cache resident); cold: a 512 MiB "
+                             "flush write before every timed launch; frac on the cold time (SURVEY 8(d))"}
         if name == "cant" and do_cpu:
             sys.path.insert(0, os.path.join(ROOT, "tests"))
             from _oracle import REF_SO, RefLib
@@ -411,9 +503,26 @@ def main():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the hot-matrix and scatter-band side measurements (profiling runs: the "
                          "headline kernel's rocprofv3 average then covers exactly the timed launches)")
+    ap.add_argument("--only", choices=["spmm16", "spmv_shapes", "cg_single", "cg_multi"],
+                    help="run one side measurement alone and print its JSON (profiling: rocprofv3 then sees only "
+                         "that leg's launches; tools/profile_legs.sh)")
     args = ap.parse_args()
 
     d = Dist(args.gpus)
+    if args.only:
+        dev = d.local
+        do_cpu = not args.no_cpu
+        if args.only == "spmm16":
+            r = run_spmm16(dev, min(args.cpu_seconds, 5.0), do_cpu)
+        elif args.only == "spmv_shapes":
+            r = run_spmv_shapes(dev, min(args.cpu_seconds, 3.0), do_cpu)
+        elif args.only == "cg_single":
+            r = run_cg_single(dev, min(args.cpu_seconds, 10.0), do_cpu)
+        else:
+            r = run_cg_multi(d, dev)[0]
+        if d.rank == 0:
+            print(json.dumps({"leg": args.only, **r}), flush=True)
+        return
     dev = d.local
     if os.environ.get("MSPMV_BENCH_SHARE_DEVICE") == "1":  # rehearsal of N > 1 on a one-GPU box
         dev = d.local % max(mspmv.device_count(), 1)
@@ -504,6 +613,7 @@ def main():
 
         if d.rank == 0 and not args.no_extras:
             result["spmm16"] = run_spmm16(dev, min(args.cpu_seconds, 5.0), d.world == 1 and not args.no_cpu)
+            result["spmv_shapes"] = run_spmv_shapes(dev, min(args.cpu_seconds, 3.0), d.world == 1 and not args.no_cpu)
 
         if d.rank == 0 and d.world == 1 and not args.no_cpu:
             y_cpu, cb = cpu_baseline(a0, xs[0], args.cpu_seconds)

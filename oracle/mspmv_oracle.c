@@ -241,8 +241,8 @@ static void orc_row_path_search(const int *row_end, int a_len, int y, int *out_x
  * faithfully, including its precondition that Y is pre-zeroed (the last nonempty
  * row and trailing empty rows only receive the `+=` of the carry fix-up;
  * CGSolveMultiple masks this with memset(AP, 0), no_pretreatment.hpp:93). */
-ORC_EXPORT void orc_nonzero_split_csrmm(int num_threads, int num_rows, int num_nonzeros, const int *row_offsets,
-                                        const int *cols, const double *vals, const double *X, double *Y, int L)
+static void nonzero_split(int num_threads, int num_rows, int num_nonzeros, const int *row_offsets, const int *cols,
+                          const double *vals, const double *X, double *Y, int L, int fixup_threads)
 {
     const int *row_end = row_offsets + 1;
     int *row_carry_out = (int *)malloc(sizeof(int) * num_threads);
@@ -282,7 +282,7 @@ ORC_EXPORT void orc_nonzero_split_csrmm(int num_threads, int num_rows, int num_n
             value_carry_out[(size_t)tid * L + i] = running_total[i];
         free(running_total);
     }
-    for (int tid = 0; tid < num_threads; ++tid) {
+    for (int tid = 0; tid < fixup_threads; ++tid) {
         int row_idx = row_carry_out[tid];
         if (row_idx < num_rows)
             for (int i = 0; i < L; i++)
@@ -290,6 +290,30 @@ ORC_EXPORT void orc_nonzero_split_csrmm(int num_threads, int num_rows, int num_n
     }
     free(row_carry_out);
     free(value_carry_out);
+}
+
+ORC_EXPORT void orc_nonzero_split_csrmm(int num_threads, int num_rows, int num_nonzeros, const int *row_offsets,
+                                        const int *cols, const double *vals, const double *X, double *Y, int L)
+{
+    nonzero_split(num_threads, num_rows, num_nonzeros, row_offsets, cols, vals, X, Y, L, num_threads);
+}
+
+/* The older single-vector twin, cpu_spmv.cpp:476-570 (RowPathSearch :476-500, OmpNonzeroSplitCsrmm
+ * :506-570): the same partition and loops at L = 1, but its fix-up stops before the last thread
+ * (`tid < num_threads - 1`, :564), so the last thread's carry is dropped.  Rows before the last
+ * nonempty row r* come out as in the work_2025 twin; y[r*] = (its prior content) + the carries of
+ * the earlier threads that ended inside r*; rows after r* keep their prior content.  y is in/out.
+ * The fixed carry arrays (`row_carry_out[256]`, :513-514) limit it to 256 threads.
+ * cpu_spmv.cpp includes <mkl.h> (:59), so it is not compiled here: this restatement is checked
+ * against the compiled work_2025 twin (tests/test_oracle_pinning.py), whose only textual
+ * difference is that fix-up bound. */
+ORC_EXPORT int orc_nonzero_split_csrmv_v1(int num_threads, int num_rows, int num_nonzeros, const int *row_offsets,
+                                          const int *cols, const double *vals, const double *x, double *y)
+{
+    if (num_threads < 1 || num_threads > 256)
+        return -1;
+    nonzero_split(num_threads, num_rows, num_nonzeros, row_offsets, cols, vals, x, y, 1, num_threads - 1);
+    return 0;
 }
 
 /* ------------------------------------------------------------------------- */

@@ -41,6 +41,7 @@ class Oracle:
             "orc_pcg_spai_multi": (_I, [_I, _I, _P, _P, _P, _P, _P, _P, _I, _I, _D, _I, _I, _P, _I]),
             "orc_ic0_factor": (_I, [_I, _P, _P, _P, _P, _P, _P, _P]),
             "orc_pcg_ic0_multi": (_I, [_I, _I, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _D, _I, _I, _P, _I]),
+            "orc_nonzero_split_csrmv_v1": (_I, [_I, _I, _I, _P, _P, _P, _P, _P]),
             "orc_calculate_threshold": (_D, [_P, _I, _D]),
             "orc_glibc_rand_fill": (None, [ctypes.c_uint, ctypes.c_longlong, _P]),
             "orc_coo_to_csr": (None, [_I, _I, _P, _P, _P, _P, _P, _P]),
@@ -114,6 +115,16 @@ class Oracle:
         self.lib.orc_nonzero_split_csrmm(P, a.num_rows, a.num_nonzeros, _p(a.row_offsets), _p(a.column_indices),
                                          _p(a.values), _p(X), _p(Y), L)
         return Y
+
+    def nonzero_split_csrmv_v1(self, a, x, P, y0):
+        """cpu_spmv.cpp's OmpNonzeroSplitCsrmm (:506-570): y is in/out (its last-row bug)."""
+        x = np.ascontiguousarray(x, np.float64)
+        y = np.array(y0, np.float64, copy=True)
+        rc = self.lib.orc_nonzero_split_csrmv_v1(P, a.num_rows, a.num_nonzeros, _p(a.row_offsets),
+                                                 _p(a.column_indices), _p(a.values), _p(x), _p(y))
+        if rc:
+            raise ValueError("P must be in [1, 256] (row_carry_out[256], cpu_spmv.cpp:513)")
+        return y
 
     def cg_single(self, a, b, max_iters, tol, hist_cap=0):
         b = np.ascontiguousarray(b, np.float64)

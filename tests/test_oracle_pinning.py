@@ -117,6 +117,46 @@ def test_merge_csrmm_bit_exact(orc, key, L):
     bits(orc.nonzero_split_csrmm(a, X, 8), G[f"m_{key}_nzsplit{L}_P8"])
 
 
+@pytest.mark.parametrize("key", MATS)
+@pytest.mark.parametrize("P", [1, 3, 8, 64, 256])
+def test_nonzero_split_v1_against_its_twin(orc, key, P):
+    """cpu_spmv.cpp's OmpNonzeroSplitCsrmm (:506-570; the file needs <mkl.h>, so it is not built
+    here) differs from the pinned work_2025 twin only in its fix-up bound (`tid < num_threads - 1`,
+    :564): every row but the last nonempty one r* is bit-identical to the twin (the compiled
+    reference where present), trailing rows keep their prior content, and y[r*] is its prior
+    content plus the carries of the threads before the last that ended inside r*, summed as the
+    reference sums them."""
+    a = csr("m_" + key)
+    x = G[f"m_{key}_x"]
+    y0 = np.random.default_rng(P).uniform(-1, 1, a.num_rows)
+    twin = (RefLib() if os.path.exists(REF_SO) else orc).nonzero_split_csrmm(a, x[:, None], P, Y0=y0[:, None])[:, 0]
+    y = orc.nonzero_split_csrmv_v1(a, x, P, y0)
+    ro, ci, va = a.row_offsets, a.column_indices, a.values
+    nnz = a.num_nonzeros
+    r_star = int(np.searchsorted(ro[1:], nnz - 1, side="right")) if nnz else 0   # RowPathSearch(nnz)
+    rows = [r for r in range(a.num_rows) if r != r_star]
+    bits(y[rows], twin[rows])
+    if r_star < a.num_rows:
+        ipt = (nnz + P - 1) // P
+        want = y0[r_star]
+        for t in range(P - 1):
+            cy, ey = min(ipt * t, nnz), min(ipt * t + ipt, nnz)
+            ex = int(np.searchsorted(ro[1:], ey - 1, side="right")) if ey else 0
+            if ex != r_star:
+                continue
+            run = 0.0
+            for k in range(max(cy, int(ro[r_star])), ey):
+                run += float(va[k]) * float(x[ci[k]])
+            want += run
+        bits(y[r_star:r_star + 1], np.array([want]))
+
+
+def test_nonzero_split_v1_thread_cap(orc):
+    a = csr("m_grid2d20")
+    with pytest.raises(ValueError):
+        orc.nonzero_split_csrmv_v1(a, np.ones(a.num_cols), 257, np.zeros(a.num_rows))
+
+
 def test_merge_equals_gold_on_unsplit_rows(orc):
     """The reference's merge CsrMV equals SpmvGold on rows no partition boundary splits."""
     a = csr("m_skew300")
