@@ -819,7 +819,7 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
         return launch_cg_iteration(h, *plan, d_x, L, i & 1, nblk, tol);
     };
 
-    constexpr int K = 32;  // iterations per graph replay (even: p buffers alternate)
+    const int K = cg_batch_iters(h->m, h->nnz, L);  // iterations per graph replay (even: p buffers alternate)
     mspmv_status st = MSPMV_OK;
     hipGraphExec_t exec = nullptr;
     if (max_iters >= K) {
@@ -836,7 +836,8 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
             hm ? (const void *)hm->d_vals : nullptr, ic, ic ? (const void *)ic->d_y : nullptr,
             ic ? (const void *)ic->d_lva : nullptr,
             reinterpret_cast<const void *>((uintptr_t)(hm ? hm->gen : 0)),
-            reinterpret_cast<const void *>((uintptr_t)(ic ? ic->gen : 0))};
+            reinterpret_cast<const void *>((uintptr_t)(ic ? ic->gen : 0)),
+            reinterpret_cast<const void *>((intptr_t)K)};
         if (!h->cg_exec || h->cg_graph_key != key) {
             if (h->cg_exec)
                 (void)hipGraphExecDestroy(h->cg_exec);

@@ -702,7 +702,7 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
         return MSPMV_OK;
     };
     // batches of K iterations, the control word of batch b inspected while b+1 is queued
-    constexpr int K = 16;
+    const int K = cg_batch_iters(d->n_own, d->local->nnz, L);
     hipEvent_t evs[2] = {nullptr, nullptr};
     D_HIP(hipEventCreateWithFlags(&evs[0], hipEventDisableTiming));
     D_HIP(hipEventCreateWithFlags(&evs[1], hipEventDisableTiming));

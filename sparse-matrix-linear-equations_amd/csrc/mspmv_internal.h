@@ -208,6 +208,8 @@ hipError_t launch_cg_init(mspmv_handle_s *h, const double *d_b, double *d_x, int
 hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *d_x, int L, int parity, int nblk,
                                double tol);
 int cg_update_blocks(long long elems);
+// Iterations per CG batch / graph replay for an m-row, nnz-nonzero matrix and L columns (mspmv_api.hip).
+int cg_batch_iters(long long m, long long nnz, int L);
 // Pipelined single-RHS CG (L == 1 unless MSPMV_CG_SPLIT=1): init (x = 0, r = p0 = b, b.b
 // partials) and, after max_iters iterations, the last stop test; grid of cg1_blocks(m).
 bool cg_split_iteration(int L);

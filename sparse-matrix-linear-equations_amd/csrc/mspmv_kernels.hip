@@ -19,6 +19,7 @@
 #include "mspmv_internal.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 
@@ -3141,6 +3142,28 @@ int cg_update_blocks(long long elems)
     if (b > 2048)
         b = 2048;
     return (int)b;
+}
+
+// Iterations per CG batch (one graph replay).  The host inspects batch b's control word while
+// b + 1 runs, so a solve launches up to 2K - 1 iterations past its convergence (each returning
+// early, but a multi-RHS SpMM still streams part of its tile before its stop test).  K = 32 wasted
+// 48 of 96 launched iterations on the nlpkkt120-size 8-RHS solve (584 us each): size K so a batch
+// lasts ~300 us at ~5 TB/s of the SURVEY 8(d) iteration bytes -- long enough to hide the host's
+// check, short enough to bound the overshoot.  Even (the p buffers alternate by parity), 2..32.
+// MSPMV_CG_BATCH overrides (lab).
+int cg_batch_iters(long long m, long long nnz, int L)
+{
+    static const int forced = [] {
+        const char *e = getenv("MSPMV_CG_BATCH");
+        return e ? atoi(e) : 0;
+    }();
+    int k = forced;
+    if (k <= 0) {
+        const double est_us = (12.0 * (double)nnz + 88.0 * (double)m * L) / 5.0e6;
+        k = (int)std::ceil(300.0 / std::max(est_us, 1.0));
+    }
+    k = (k + 1) & ~1;
+    return std::min(32, std::max(2, k));
 }
 
 template <int L>
