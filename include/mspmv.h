@@ -94,6 +94,13 @@ MSPMV_API mspmv_status mspmv_shape(mspmv_handle h, int *num_rows, int *num_cols,
 MSPMV_API double mspmv_setup_ms(mspmv_handle h);
 /* Block until all work enqueued on the handle's stream has finished. */
 MSPMV_API mspmv_status mspmv_sync(mspmv_handle h);
+/* Confine the handle's work to num_cus compute units (spread evenly over the device's CUs, so
+ * over its XCDs), or to all of them when num_cus <= 0 or >= the device's count: the handle's
+ * stream is replaced by a CU-masked one (hipExtStreamCreateWithCUMask) and launch sizing follows
+ * the new count.  The GPU counterpart of the thread count that OpenMP runs take
+ * (parallel_efficiency.cpp:67-113 sets omp_set_num_threads per point); tools/parallel_efficiency.py
+ * sweeps it.  Synchronizes the handle first. */
+MSPMV_API mspmv_status mspmv_set_cu_limit(mspmv_handle h, int num_cus);
 
 /* ---- merge-path partition ----------------------------------------------------------- */
 /* Coordinates of the num_parts+1 partition boundaries exactly as OmpMergeCsrmv computes

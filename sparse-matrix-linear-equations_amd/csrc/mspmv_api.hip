@@ -565,6 +565,44 @@ mspmv_status mspmv_sync(mspmv_handle h)
     return MSPMV_OK;
 }
 
+mspmv_status mspmv_set_cu_limit(mspmv_handle h, int num_cus)
+{
+    ST_TRY(check_handle(h));
+    HIP_TRY(hipSetDevice(h->device));
+    int total = 0;
+    HIP_TRY(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, h->device));
+    const int n = (num_cus <= 0 || num_cus >= total) ? total : num_cus;
+    hipStream_t s = nullptr;
+    if (n == total) {
+        HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    } else {
+        // CU i joins when floor((i+1) n / total) steps: n of the total, evenly spaced
+        std::vector<uint32_t> mask((size_t)(total + 31) / 32, 0u);
+        for (int i = 0; i < total; ++i)
+            if ((long long)(i + 1) * n / total > (long long)i * n / total)
+                mask[(size_t)i / 32] |= 1u << (i % 32);
+        HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+    }
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) {
+        (void)hipStreamDestroy(s);
+        set_error(std::string("set_cu_limit: ") + hipGetErrorString(e));
+        return MSPMV_ERR_HIP;
+    }
+    // the CG graph was captured on the old stream with the old launch sizing
+    if (h->cg_exec)
+        (void)hipGraphExecDestroy(h->cg_exec);
+    if (h->cg_graph)
+        (void)hipGraphDestroy(h->cg_graph);
+    h->cg_exec = nullptr;
+    h->cg_graph = nullptr;
+    h->cg_graph_key.clear();
+    (void)hipStreamDestroy(h->stream);
+    h->stream = s;
+    h->num_cus = n;
+    return MSPMV_OK;
+}
+
 mspmv_status mspmv_merge_coords(mspmv_handle h, int num_parts, mspmv_coord *coords)
 {
     ST_TRY(check_handle(h));

@@ -7,7 +7,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <string>
 #include <vector>
+
+#include <omp.h>
 
 #include "mspmv_io.h"
 
@@ -20,7 +23,10 @@ struct Coo {
 };
 
 // Stable (row, col) order: counting sort by row (stable), then a stable sort of each row by
-// column -- the same permutation std::stable_sort with CooComparator produces.
+// column -- the same permutation std::stable_sort with CooComparator produces
+// (CsrMatrix::Init, sparse_matrix.h:668-733).  Parallel and still stable: thread t counts its
+// contiguous range of entries per row, and row i's entries of thread t land after those of
+// threads < t, so every row keeps its entries in file order before the per-row column sort.
 mspmv_status coo_to_csr(const Coo &coo, int **ro_out, int **ci_out, double **va_out)
 {
     const int m = coo.rows;
@@ -34,35 +40,326 @@ mspmv_status coo_to_csr(const Coo &coo, int **ro_out, int **ci_out, double **va_
         free(va);
         return MSPMV_ERR_OOM;
     }
-    std::vector<size_t> cnt((size_t)m + 1, 0);
-    for (size_t k = 0; k < nnz; ++k) {
-        if (coo.r[k] < 0 || coo.r[k] >= m || coo.c[k] < 0 || coo.c[k] >= coo.cols) {
-            free(ro);
-            free(ci);
-            free(va);
-            return MSPMV_ERR_IO;
-        }
-        ++cnt[(size_t)coo.r[k] + 1];
+    bool bad = false;
+#pragma omp parallel for reduction(|| : bad)
+    for (long long k = 0; k < (long long)nnz; ++k)
+        bad = bad || coo.r[k] < 0 || coo.r[k] >= m || coo.c[k] < 0 || coo.c[k] >= coo.cols;
+    if (bad) {
+        free(ro);
+        free(ci);
+        free(va);
+        return MSPMV_ERR_IO;
     }
-    for (int i = 0; i < m; ++i)
-        cnt[i + 1] += cnt[i];
-    std::vector<size_t> pos(cnt.begin(), cnt.end() - 1), order(nnz);
-    for (size_t k = 0; k < nnz; ++k)
-        order[pos[coo.r[k]]++] = k;
+    // threads: enough entries each, and the per-thread row counters within ~1 GB
+    int T = std::max(1, std::min(omp_get_max_threads(), (int)(nnz / 65536)));
+    while (T > 1 && (size_t)T * ((size_t)m + 1) * sizeof(int) > (1ull << 30))
+        --T;
+    std::vector<int> cnt((size_t)T * ((size_t)m + 1), 0);
+    auto range = [&](int t, size_t &b, size_t &e) {
+        b = nnz * (size_t)t / T;
+        e = nnz * (size_t)(t + 1) / T;
+    };
+#pragma omp parallel num_threads(T)
+    {
+        const int t = omp_get_thread_num();
+        size_t b, e;
+        range(t, b, e);
+        int *c = cnt.data() + (size_t)t * ((size_t)m + 1);
+        for (size_t k = b; k < e; ++k)
+            ++c[coo.r[k]];
+    }
+    // ro[i] = entries of rows < i; cnt[t][i] becomes thread t's first slot in row i
+    std::vector<size_t> rowlen((size_t)m, 0);
+#pragma omp parallel for
+    for (long long i = 0; i < (long long)m; ++i) {
+        size_t acc = 0;
+        for (int t = 0; t < T; ++t) {
+            const int c = cnt[(size_t)t * ((size_t)m + 1) + (size_t)i];
+            cnt[(size_t)t * ((size_t)m + 1) + (size_t)i] = (int)acc;
+            acc += (size_t)c;
+        }
+        rowlen[(size_t)i] = acc;
+    }
+    size_t run = 0;
     for (int i = 0; i < m; ++i) {
-        auto b = order.begin() + (long)cnt[i], e = order.begin() + (long)cnt[i + 1];
-        std::stable_sort(b, e, [&](size_t x, size_t y) { return coo.c[x] < coo.c[y]; });
-        ro[i] = (int)cnt[i];
+        ro[i] = (int)run;
+        run += rowlen[(size_t)i];
     }
     ro[m] = (int)nnz;
-    for (size_t k = 0; k < nnz; ++k) {
-        ci[k] = coo.c[order[k]];
-        va[k] = coo.v[order[k]];
+    std::vector<size_t> order(nnz);
+#pragma omp parallel num_threads(T)
+    {
+        const int t = omp_get_thread_num();
+        size_t b, e;
+        range(t, b, e);
+        int *c = cnt.data() + (size_t)t * ((size_t)m + 1);
+        for (size_t k = b; k < e; ++k) {
+            const int r = coo.r[k];
+            order[(size_t)ro[r] + (size_t)c[r]++] = k;
+        }
+    }
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (long long i = 0; i < (long long)m; ++i) {
+        auto b = order.begin() + ro[i], e = order.begin() + ro[i + 1];
+        std::stable_sort(b, e, [&](size_t x, size_t y) { return coo.c[x] < coo.c[y]; });
+    }
+#pragma omp parallel for
+    for (long long k = 0; k < (long long)nnz; ++k) {
+        ci[k] = coo.c[order[(size_t)k]];
+        va[k] = coo.v[order[(size_t)k]];
     }
     *ro_out = ro;
     *ci_out = ci;
     *va_out = va;
     return MSPMV_OK;
+}
+
+
+// ---- MatrixMarket (CooMatrix::InitMarket, sparse_matrix.h:211-380) -------------------------
+struct MarketState {
+    bool array = false, symmetric = false, skew = false;
+    long long cur = -1, declared = 0;
+    double dflt = 1.0;
+};
+
+bool slurp(const char *path, std::vector<char> &buf)
+{
+    FILE *f = fopen(path, "rb");
+    if (!f)
+        return false;
+    bool ok = fseek(f, 0, SEEK_END) == 0;
+    const long size = ok ? ftell(f) : -1;
+    ok = ok && size >= 0 && fseek(f, 0, SEEK_SET) == 0;
+    if (ok) {
+        buf.resize((size_t)size);
+        ok = fread(buf.data(), 1, (size_t)size, f) == (size_t)size;
+    }
+    fclose(f);
+    return ok;
+}
+
+// The reference's ifs.getline(line, 1024) + good() (:247-252): a line is taken only when it ends
+// in '\n' and has at most 1022 characters; the first line that does not ends the parse.  Copies the
+// line, NUL-terminated as getline leaves it (strtol must not run on into the next line).
+inline bool take_line(const std::vector<char> &buf, size_t pos, char *line, size_t *next)
+{
+    if (pos >= buf.size())
+        return false;
+    const char *p = buf.data() + pos;
+    const size_t avail = buf.size() - pos;
+    const char *nl = (const char *)memchr(p, '\n', std::min<size_t>(avail, 1023));
+    if (!nl)
+        return false;
+    const size_t len = (size_t)(nl - p);
+    memcpy(line, p, len);
+    line[len] = '\0';
+    *next = pos + len + 1;
+    return true;
+}
+
+// One coordinate entry "row col [val]" (:318-345): strtol base 0, strtod, pattern -> default.
+inline bool parse_entry(const char *line, double dflt, int *row, int *col, double *val)
+{
+    char *t = nullptr;
+    const char *l = line;
+    *row = (int)strtol(l, &t, 0);
+    if (t == l)
+        return false;
+    l = t;
+    *col = (int)strtol(l, &t, 0);
+    if (t == l)
+        return false;
+    l = t;
+    *val = strtod(l, &t);
+    if (t == l)
+        *val = dflt;
+    return true;
+}
+
+inline void push_entry(Coo &coo, const MarketState &S, int row, int col, double val)
+{
+    coo.r.push_back(row - 1);
+    coo.c.push_back(col - 1);
+    coo.v.push_back(val);
+    if (S.symmetric && row != col) {  // mirror, skew-negated (:350-356)
+        coo.r.push_back(col - 1);
+        coo.c.push_back(row - 1);
+        coo.v.push_back(val * (S.skew ? -1 : 1));
+    }
+}
+
+// One accepted line of the reference's loop; false on a parse error (where it calls exit(1)).
+bool market_line(const char *line, MarketState &S, Coo &coo)
+{
+    if (line[0] == '%') {
+        if (line[1] == '%') {  // banner (:257-263)
+            S.symmetric = strstr(line, "symmetric") != nullptr;
+            S.skew = strstr(line, "skew") != nullptr;
+            S.array = strstr(line, "array") != nullptr;
+        }
+        return true;
+    }
+    if (S.cur == -1) {  // problem description (:273-298)
+        int nr = 0, nc = 0, nz = 0;
+        const int nparsed = sscanf(line, "%d %d %d", &nr, &nc, &nz);
+        if (!S.array && nparsed == 3)
+            S.declared = S.symmetric ? 2LL * nz : nz;
+        else if (S.array && nparsed == 2)
+            S.declared = (long long)nr * nc;
+        else
+            return false;
+        coo.rows = nr;
+        coo.cols = nc;
+        coo.r.reserve((size_t)S.declared);
+        coo.c.reserve((size_t)S.declared);
+        coo.v.reserve((size_t)S.declared);
+        S.cur = 0;
+        return true;
+    }
+    if (S.cur >= S.declared)  // more entries than declared (:303-307)
+        return false;
+    if (S.array) {  // column-major dense entries (:312-317)
+        double val;
+        if (sscanf(line, "%lf", &val) != 1)
+            return false;
+        const int col = (int)(S.cur / coo.rows);
+        const int row = (int)(S.cur - (long long)coo.rows * col);
+        coo.r.push_back(row);
+        coo.c.push_back(col);
+        coo.v.push_back(val);
+        ++S.cur;
+        if (S.symmetric && row != col) {
+            coo.r.push_back(col);
+            coo.c.push_back(row);
+            coo.v.push_back(val * (S.skew ? -1 : 1));
+            ++S.cur;
+        }
+        return true;
+    }
+    int row, col;
+    double val;
+    if (!parse_entry(line, S.dflt, &row, &col, &val))
+        return false;
+    const size_t before = coo.r.size();
+    push_entry(coo, S, row, col, val);
+    S.cur += (long long)(coo.r.size() - before);
+    return true;
+}
+
+mspmv_status market_serial(const std::vector<char> &buf, size_t pos, MarketState &S, Coo &coo)
+{
+    char line[1024];
+    size_t next;
+    while (take_line(buf, pos, line, &next)) {
+        pos = next;
+        if (!market_line(line, S, coo))
+            return MSPMV_ERR_IO;
+    }
+    return MSPMV_OK;
+}
+
+// Coordinate entries in parallel: the entry region is cut at line starts into one chunk per
+// thread; each thread parses its lines into its own arrays exactly as market_line does, noting the
+// first line that would end the reference's loop (stop), a parse error, or a banner ("%%" lines
+// reset the format flags mid-file: then the whole region is redone serially).  Chunks are taken
+// in order up to the first stop, so the entries, their order and every error decision are those
+// of the serial loop: the declared-count check (:303-307) fails iff the last taken entry line
+// starts at an entry count >= the declared one.  Returns false to ask for the serial parse.
+// MSPMV_IO_MIN_CHUNK (bytes per thread, default 1 MiB) lets tests force many chunks.
+bool market_entries_parallel(const std::vector<char> &buf, size_t pos, MarketState &S, Coo &coo, mspmv_status *st)
+{
+    const size_t region = buf.size() - pos;
+    const char *mc = getenv("MSPMV_IO_MIN_CHUNK");
+    const size_t min_chunk = std::max<size_t>(64, mc ? (size_t)atoll(mc) : (size_t)1 << 20);
+    const int T = (int)std::min<size_t>((size_t)omp_get_max_threads(), region / min_chunk);
+    if (T < 2)
+        return false;
+    std::vector<size_t> cut((size_t)T + 1, buf.size());
+    cut[0] = pos;
+    for (int t = 1; t < T; ++t) {  // the line start at or after the nominal cut
+        size_t c = pos + region * (size_t)t / (size_t)T;
+        const void *nl = memchr(buf.data() + c - 1, '\n', buf.size() - (c - 1));
+        cut[(size_t)t] = nl ? (size_t)((const char *)nl - buf.data()) + 1 : buf.size();
+    }
+    for (int t = 1; t <= T; ++t)
+        cut[(size_t)t] = std::max(cut[(size_t)t], cut[(size_t)t - 1]);
+    struct Part {
+        Coo coo;
+        bool stop = false, err = false, banner = false, any = false;
+        long long last_before = 0;  // entries of this chunk before its last entry line
+    };
+    std::vector<Part> part((size_t)T);
+#pragma omp parallel num_threads(T)
+    {
+        const int t = omp_get_thread_num();
+        Part &P = part[(size_t)t];
+        const size_t est = (cut[(size_t)t + 1] - cut[(size_t)t]) / 16 * (S.symmetric ? 2 : 1);
+        P.coo.r.reserve(est);
+        P.coo.c.reserve(est);
+        P.coo.v.reserve(est);
+        char line[1024];
+        size_t p = cut[(size_t)t], next;
+        while (p < cut[(size_t)t + 1]) {
+            if (!take_line(buf, p, line, &next)) {
+                P.stop = true;
+                break;
+            }
+            p = next;
+            if (line[0] == '%') {
+                if (line[1] == '%') {
+                    P.banner = true;
+                    break;
+                }
+                continue;
+            }
+            int row, col;
+            double val;
+            if (!parse_entry(line, S.dflt, &row, &col, &val)) {
+                P.err = true;
+                break;
+            }
+            P.last_before = (long long)P.coo.r.size();
+            P.any = true;
+            push_entry(P.coo, S, row, col, val);
+        }
+    }
+    long long total = 0, last_start = -1;
+    int used = 0;
+    for (int t = 0; t < T; ++t) {
+        const Part &P = part[(size_t)t];
+        if (P.banner)
+            return false;
+        if (P.any)
+            last_start = total + P.last_before;
+        if (P.err) {
+            *st = MSPMV_ERR_IO;
+            return true;
+        }
+        total += (long long)P.coo.r.size();
+        used = t + 1;
+        if (P.stop)
+            break;
+    }
+    if (last_start >= S.declared) {
+        *st = MSPMV_ERR_IO;
+        return true;
+    }
+    coo.r.resize((size_t)total);
+    coo.c.resize((size_t)total);
+    coo.v.resize((size_t)total);
+    std::vector<size_t> off((size_t)used + 1, 0);
+    for (int t = 0; t < used; ++t)
+        off[(size_t)t + 1] = off[(size_t)t] + part[(size_t)t].coo.r.size();
+#pragma omp parallel for num_threads(T)
+    for (int t = 0; t < used; ++t) {
+        const Coo &c = part[(size_t)t].coo;
+        std::copy(c.r.begin(), c.r.end(), coo.r.begin() + (long)off[(size_t)t]);
+        std::copy(c.c.begin(), c.c.end(), coo.c.begin() + (long)off[(size_t)t]);
+        std::copy(c.v.begin(), c.v.end(), coo.v.begin() + (long)off[(size_t)t]);
+    }
+    S.cur = total;
+    *st = MSPMV_OK;
+    return true;
 }
 
 }  // namespace
@@ -76,100 +373,30 @@ mspmv_status mspmv_market_read(const char *path, double default_value, int *num_
 {
     if (!path || !num_rows || !num_cols || !num_nonzeros || !row_offsets || !column_indices || !values)
         return MSPMV_ERR_INVALID;
-    FILE *f = fopen(path, "rb");
-    if (!f)
+    std::vector<char> buf;
+    if (!slurp(path, buf))
         return MSPMV_ERR_IO;
-    // getline(line, 1024) + good(): a line of >= 1023 characters, or a last line without a
-    // newline, ends the parse (sparse_matrix.h:247-252).
-    bool array = false, symmetric = false, skew = false;
-    long long cur = -1, declared = 0;
+    MarketState S;
     Coo coo;
-    char line[1024];
-    mspmv_status st = MSPMV_OK;
-    for (;;) {
-        if (!fgets(line, sizeof(line), f))
+    S.dflt = default_value;
+    // banner, comments and the size line: serial (they decide the format of what follows)
+    size_t pos = 0;
+    while (S.cur == -1) {
+        char line[1024];
+        size_t next;
+        if (!take_line(buf, pos, line, &next))
             break;
-        size_t len = strlen(line);
-        if (len == 0 || line[len - 1] != '\n')
-            break;
-        line[len - 1] = '\0';
-        if (line[0] == '%') {
-            if (line[1] == '%') {
-                symmetric = strstr(line, "symmetric") != nullptr;
-                skew = strstr(line, "skew") != nullptr;
-                array = strstr(line, "array") != nullptr;
-            }
-            continue;
-        }
-        if (cur == -1) {
-            int nr = 0, nc = 0, nz = 0;
-            const int nparsed = sscanf(line, "%d %d %d", &nr, &nc, &nz);
-            if (!array && nparsed == 3) {
-                declared = symmetric ? 2LL * nz : nz;
-            } else if (array && nparsed == 2) {
-                declared = (long long)nr * nc;
-            } else {
-                st = MSPMV_ERR_IO;  // "invalid problem description" (:296-298)
-                break;
-            }
-            coo.rows = nr;
-            coo.cols = nc;
-            coo.r.reserve((size_t)declared);
-            coo.c.reserve((size_t)declared);
-            coo.v.reserve((size_t)declared);
-            cur = 0;
-            continue;
-        }
-        if (cur >= declared) {
-            st = MSPMV_ERR_IO;  // more entries than declared (:303-307)
-            break;
-        }
-        int row, col;
-        double val;
-        if (array) {
-            if (sscanf(line, "%lf", &val) != 1) {
-                st = MSPMV_ERR_IO;
-                break;
-            }
-            col = (int)(cur / coo.rows);
-            row = (int)(cur - (long long)coo.rows * col);
-            coo.r.push_back(row);
-            coo.c.push_back(col);
-        } else {
-            char *l = line, *t = nullptr;
-            row = (int)strtol(l, &t, 0);  // base 0 exactly as the reference parses
-            if (t == l) {
-                st = MSPMV_ERR_IO;
-                break;
-            }
-            l = t;
-            col = (int)strtol(l, &t, 0);
-            if (t == l) {
-                st = MSPMV_ERR_IO;
-                break;
-            }
-            l = t;
-            val = strtod(l, &t);
-            if (t == l)
-                val = default_value;  // pattern matrices
-            coo.r.push_back(row - 1);
-            coo.c.push_back(col - 1);
-        }
-        coo.v.push_back(val);
-        ++cur;
-        if (symmetric && row != col) {
-            const size_t k = coo.r.size() - 1;
-            coo.r.push_back(coo.c[k]);
-            coo.c.push_back(coo.r[k]);
-            coo.v.push_back(coo.v[k] * (skew ? -1 : 1));
-            ++cur;
-        }
+        pos = next;
+        if (!market_line(line, S, coo))
+            return MSPMV_ERR_IO;
     }
-    fclose(f);
+    if (S.cur < 0)
+        return MSPMV_ERR_IO;
+    mspmv_status st = MSPMV_OK;
+    if (S.array || !market_entries_parallel(buf, pos, S, coo, &st))
+        st = market_serial(buf, pos, S, coo);  // array format (entry i's position is i), small files, banners mid-file
     if (st != MSPMV_OK)
         return st;
-    if (cur < 0)
-        return MSPMV_ERR_IO;
     *num_rows = coo.rows;
     *num_cols = coo.cols;
     *num_nonzeros = (int)coo.r.size();

@@ -77,6 +77,7 @@ _SIGS = {
     "mspmv_shape": (_I, [_P, _PI, _PI, _PI]),
     "mspmv_setup_ms": (_D, [_P]),
     "mspmv_sync": (_I, [_P]),
+    "mspmv_set_cu_limit": (_I, [_P, _I]),
     "mspmv_merge_coords": (_I, [_P, _I, ctypes.POINTER(Coord)]),
     "mspmv_dspmv": (_I, [_P, _P, _P]),
     "mspmv_dspmv_dev": (_I, [_P, _P, _P]),
@@ -363,6 +364,10 @@ class GpuCsr:
 
     def sync(self):
         _check(lib.mspmv_sync(self.h), "sync")
+
+    def set_cu_limit(self, num_cus: int):
+        """Run this handle's work on num_cus compute units (<= 0: all) -- mspmv_set_cu_limit."""
+        _check(lib.mspmv_set_cu_limit(self.h, int(num_cus)), "set_cu_limit")
 
     def merge_coords(self, num_parts: int) -> np.ndarray:
         out = (Coord * (num_parts + 1))()
