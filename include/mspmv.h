@@ -99,7 +99,9 @@ MSPMV_API mspmv_status mspmv_sync(mspmv_handle h);
  * stream is replaced by a CU-masked one (hipExtStreamCreateWithCUMask) and launch sizing follows
  * the new count.  The GPU counterpart of the thread count that OpenMP runs take
  * (parallel_efficiency.cpp:67-113 sets omp_set_num_threads per point); tools/parallel_efficiency.py
- * sweeps it.  Synchronizes the handle first. */
+ * sweeps it, one CU count per process.  One masked stream per (device, count) is created per
+ * process and shared by all handles limited to that count (a masked stream holds a hardware
+ * queue of its own; a process has few).  Synchronizes the handle first. */
 MSPMV_API mspmv_status mspmv_set_cu_limit(mspmv_handle h, int num_cus);
 
 /* ---- merge-path partition ----------------------------------------------------------- */

@@ -8,6 +8,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <vector>
 
 namespace mspmv {
@@ -537,7 +539,7 @@ mspmv_status mspmv_destroy(mspmv_handle h)
         (void)hipEventDestroy(h->ev0);
     if (h->ev1)
         (void)hipEventDestroy(h->ev1);
-    if (h->stream)
+    if (h->stream && h->own_stream)
         (void)hipStreamDestroy(h->stream);
     delete h;
     return MSPMV_OK;
@@ -565,6 +567,13 @@ mspmv_status mspmv_sync(mspmv_handle h)
     return MSPMV_OK;
 }
 
+// One CU-masked stream per (device, CU count) for the whole process, shared by every handle
+// limited to that count and never destroyed: a masked stream holds a hardware queue of its own,
+// and creating one per handle / per call ran a process out of its few queues (a launch on a
+// third masked stream never started).
+static std::mutex g_cu_mu;
+static std::map<std::pair<int, int>, hipStream_t> g_cu_streams;
+
 mspmv_status mspmv_set_cu_limit(mspmv_handle h, int num_cus)
 {
     ST_TRY(check_handle(h));
@@ -573,19 +582,31 @@ mspmv_status mspmv_set_cu_limit(mspmv_handle h, int num_cus)
     HIP_TRY(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, h->device));
     const int n = (num_cus <= 0 || num_cus >= total) ? total : num_cus;
     hipStream_t s = nullptr;
+    bool own = true;
     if (n == total) {
         HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     } else {
-        // CU i joins when floor((i+1) n / total) steps: n of the total, evenly spaced
-        std::vector<uint32_t> mask((size_t)(total + 31) / 32, 0u);
-        for (int i = 0; i < total; ++i)
-            if ((long long)(i + 1) * n / total > (long long)i * n / total)
-                mask[(size_t)i / 32] |= 1u << (i % 32);
-        HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+        std::lock_guard<std::mutex> lk(g_cu_mu);
+        auto it = g_cu_streams.find({h->device, n});
+        if (it != g_cu_streams.end()) {
+            s = it->second;
+        } else {
+            // CU i joins when floor((i+1) n / total) steps: n of the total, evenly spaced
+            std::vector<uint32_t> mask((size_t)(total + 31) / 32, 0u);
+            for (int i = 0; i < total; ++i)
+                if ((long long)(i + 1) * n / total > (long long)i * n / total)
+                    mask[(size_t)i / 32] |= 1u << (i % 32);
+            HIP_TRY(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()));
+            g_cu_streams[{h->device, n}] = s;
+        }
+        own = false;
     }
+    if (s == h->stream)
+        return MSPMV_OK;
     hipError_t e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) {
-        (void)hipStreamDestroy(s);
+        if (own)
+            (void)hipStreamDestroy(s);
         set_error(std::string("set_cu_limit: ") + hipGetErrorString(e));
         return MSPMV_ERR_HIP;
     }
@@ -597,8 +618,10 @@ mspmv_status mspmv_set_cu_limit(mspmv_handle h, int num_cus)
     h->cg_exec = nullptr;
     h->cg_graph = nullptr;
     h->cg_graph_key.clear();
-    (void)hipStreamDestroy(h->stream);
+    if (h->own_stream)
+        (void)hipStreamDestroy(h->stream);
     h->stream = s;
+    h->own_stream = own;
     h->num_cus = n;
     return MSPMV_OK;
 }

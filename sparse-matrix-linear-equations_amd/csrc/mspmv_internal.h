@@ -100,6 +100,7 @@ struct mspmv_handle_s {
     int device = 0;
     int num_cus = 256;
     hipStream_t stream = nullptr;
+    bool own_stream = true;  // false: a shared CU-masked stream (mspmv_set_cu_limit)
     int m = 0, n = 0, nnz = 0;
     int *d_row_offsets = nullptr;
     int *d_cols = nullptr;

@@ -115,39 +115,68 @@ def gflops(a, L, it, ms):
     return (2.0 * a.num_nonzeros + 10.0 * a.num_rows) * L * it / (ms / 1000.0) / 1e9
 
 
-def sweep_cus(args):
-    units = [int(v) for v in args.cus.split(",")]
-    rows, nmat = [], 0
+def cus_child(args):
+    """One CU count, every matrix: prints one 'ROW <json>' line per matrix."""
+    import json
+    u = int(args.cus)
     for name, make in matrix_set(args):
         a = make()
         if a.num_rows == 1 or a.num_cols == 1 or a.num_nonzeros == 1:
-            print(f"Skipping trivial matrix: {name}")
             continue
-        nmat += 1
-        print(f"Processing: {name} (rows={a.num_rows}, nnz={a.num_nonzeros})")
         L = args.num_vectors
         B = glibc_rhs(a.num_rows * L).reshape(a.num_rows, L)
         with mspmv.GpuCsr(a, device=args.device) as g:
+            g.set_cu_limit(u)
             dB = mspmv.DeviceBuffer.from_array(B, args.device)
             dX = mspmv.DeviceBuffer(8 * a.num_rows * L, args.device)
-            for u in units:
-                g.set_cu_limit(u)
-                g.cg_dev(dB, dX, L, args.max_iters, args.tolerance)   # warm: graph, workspace
-                best, best_it = float("inf"), 0
-                for _ in range(args.timing_iters):
-                    t0 = time.perf_counter()
-                    it, _, _ = g.cg_dev(dB, dX, L, args.max_iters, args.tolerance)
-                    ms = (time.perf_counter() - t0) * 1e3
-                    if ms < best:
-                        best, best_it = ms, it
-                gf = gflops(a, L, best_it, best)
-                rows.append([name, u, best, gf, best_it])
-                print(f"  CUs={u:3d}: {best:.3f} ms, {gf:.2f} GFLOPS", flush=True)
-            g.set_cu_limit(0)
+            g.cg_dev(dB, dX, L, args.max_iters, args.tolerance)   # warm: graph, workspace
+            best, best_it = float("inf"), 0
+            for _ in range(args.timing_iters):
+                t0 = time.perf_counter()
+                it, _, _ = g.cg_dev(dB, dX, L, args.max_iters, args.tolerance)
+                ms = (time.perf_counter() - t0) * 1e3
+                if ms < best:
+                    best, best_it = ms, it
+        print("ROW " + json.dumps([name, a.num_rows, a.num_nonzeros, u, best, gflops(a, L, best_it, best), best_it]),
+              flush=True)
+
+
+def sweep_cus(args):
+    """Each CU count in its own child process: a CU-masked stream takes a hardware queue of its own,
+    and a process holds only a few (GPU_MAX_HW_QUEUES), so one process per count keeps every
+    point on a fresh queue set."""
+    import json
+    import subprocess
+    units = [int(v) for v in args.cus.split(",")]
+    rows = []
+    for u in units:
+        cmd = [sys.executable, os.path.abspath(__file__), "--units=cus", f"--cus={u}", "--_child",
+               f"--num_vectors={args.num_vectors}", f"--timing_iters={args.timing_iters}",
+               f"--max_iters={args.max_iters}", f"--tolerance={args.tolerance}", f"--device={args.device}",
+               f"--mtx_dir={args.mtx_dir}"] + (["--synthetic"] if args.synthetic else [])
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=args.child_timeout)
+        if r.returncode != 0:
+            raise SystemExit(f"CUs={u}: child failed ({r.returncode}): {r.stderr[-1500:]}")
+        for ln in r.stdout.splitlines():
+            if ln.startswith("ROW "):
+                rows.append(json.loads(ln[4:]))
+        print(f"  CUs={u:3d}: done", flush=True)
+    names = []
+    for r in rows:
+        if r[0] not in names:
+            names.append(r[0])
+    rows.sort(key=lambda r: (names.index(r[0]), units.index(r[3])))
+    out = []
+    for name in names:
+        rs = [r for r in rows if r[0] == name]
+        print(f"Processing: {name} (rows={rs[0][1]}, nnz={rs[0][2]})")
+        for r in rs:
+            print(f"  CUs={r[3]:3d}: {r[4]:.3f} ms, {r[5]:.2f} GFLOPS")
+            out.append([name, r[3], r[4], r[5], r[6]])
         print()
-    eff = efficiency(rows, units)
-    summary(eff, nmat, "CUs")
-    save(args, rows, eff, "")
+    eff = efficiency(out, units)
+    summary(eff, len(names), "CUs")
+    save(args, out, eff, "")
 
 
 def sweep_gpus(args):
@@ -239,8 +268,12 @@ def main(argv=None):
     ap.add_argument("--gpus", default="", help="GPU counts (default 1, 2, 4, ... up to WORLD_SIZE)")
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--synthetic", action="store_true", help="built-in SPD shapes instead of --mtx_dir")
+    ap.add_argument("--child_timeout", type=float, default=600.0, help="seconds allowed per CU-count child")
+    ap.add_argument("--_child", action="store_true", help=argparse.SUPPRESS)
     # the reference spells its options --key=value; argparse accepts both forms
     args = ap.parse_args(argv)
+    if args._child:
+        return cus_child(args)
     print("=== Parallel Efficiency Benchmark ===")
     print(f"Matrix directory: {'(synthetic)' if args.synthetic else args.mtx_dir}")
     print(f"num_vectors: {args.num_vectors}")
