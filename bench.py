@@ -153,14 +153,15 @@ def cpu_baseline(a, x, seconds):
                          f"{calls} calls in {el:.1f} s"}
 
 
-FLUSH_BYTES = 512 << 20   # >= 512 MB MALL-flush write between cold calls
+FLUSH_BYTES = 512 << 20   # >= 512 MB MALL flush between cold calls (a read sweep: clean lines,
+                          # so the timed launch does not pay the flush's own write-back; MSPMV_FLUSH=write)
 CANT = dict(m=62451, nnz=4007383, band=2000, seed=1)
 RMA10 = dict(m=46835, nnz=2374001, band=3000, seed=2)
 
 
 def gpu_spmv_hot_cold(a, dev, seed=2):
     """One matrix's SpMV tile kernel: hot (back-to-back launches; a matrix below 256 MiB stays
-    Infinity-Cache resident) and cold (a 512 MiB flush write before every timed launch, SURVEY
+    Infinity-Cache resident) and cold (a 512 MiB flush read sweep before every timed launch, SURVEY
     8(d)); HIP events around each launch.  frac is priced on the cold time."""
     x = np.random.default_rng(seed).uniform(0.0, 1.0, a.num_cols)
     with mspmv.GpuCsr(a, device=dev) as g:
@@ -267,7 +268,7 @@ def run_spmm16(dev, cpu_seconds, do_cpu):
                      "cold_kernel_ms": round(cold_ms, 5), "gflops_cold": round(2.0 * L * a.num_nonzeros / cold_ms / 1e6, 1),
                      "achieved_GBps": round(nb / cold_ms / 1e6, 1), "frac": round(nb / cold_ms / 1e6 / HBM_PEAK_GBS, 4),
                      "note": "hot: back-to-back launches (matrix + panel Infinity-Cache resident); cold: a 512 MiB "
-                             "flush write before every timed launch; frac on the cold time (SURVEY 8(d))"}
+                             "flush read sweep before every timed launch; frac on the cold time (SURVEY 8(d))"}
         if name == "cant" and do_cpu:
             sys.path.insert(0, os.path.join(ROOT, "tests"))
             from _oracle import REF_SO, RefLib

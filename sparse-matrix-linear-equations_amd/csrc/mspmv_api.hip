@@ -18,7 +18,7 @@ static thread_local std::string g_err;
 
 void set_error(const std::string &msg) { g_err = msg; }
 
-hipError_t launch_flush(void *p, size_t bytes, hipStream_t s);
+hipError_t launch_flush(void *p, size_t bytes, hipStream_t s, bool fresh);
 
 }  // namespace mspmv
 
@@ -1348,6 +1348,7 @@ mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y,
         h->flush_cap = 0;
         HIP_TRY(hipMalloc(&h->d_flush, flush_bytes));
         h->flush_cap = flush_bytes;
+        HIP_TRY(launch_flush(h->d_flush, flush_bytes, h->stream, true));  // defined contents (+1.0)
     }
     // A/B lab hook: MSPMV_TIME_DOT=1 times the CG's MODE 2 SpMM (x.(AX) partials + fold) instead
     static const bool time_dot = getenv("MSPMV_TIME_DOT") != nullptr;
@@ -1361,7 +1362,7 @@ mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y,
     hipError_t e = hipSuccess;
     for (int i = 0; i < reps && e == hipSuccess; ++i) {
         if (flush_bytes)
-            e = launch_flush(h->d_flush, flush_bytes, h->stream);
+            e = launch_flush(h->d_flush, flush_bytes, h->stream, false);
         if (e == hipSuccess)
             e = hipEventRecord(ev[2 * i], h->stream);
         if (e == hipSuccess && time_dot)

@@ -1507,6 +1507,130 @@ __global__ __launch_bounds__(kBlock) void k_spmv_blk(TileArgs a)
         dot_epilogue(a, sm, t, dot);
 }
 
+// Single right-hand side, node-block plans (every tile a register run tile), persistent and
+// wave-pipelined.  The unit of work is one run chunk (k_build_blocks' descriptor: <= 8 rows of a
+// node x <= 64 pattern columns); wave w of workgroup b owns chunks w and w + 4 of the tiles
+// xcd_tile(b), xcd_tile(b + G), ... (G = gridDim.x, a multiple of 8, so they stay on one XCD).
+// At entry lane j of the wave loads unit j's descriptor, tile bounds and column base (one memory
+// round trip for the wave's whole run of <= 32 tiles); the units then go through a three-stage
+// register pipeline: unit u's x gathers are issued, then unit u + 2's values and 16-bit columns,
+// then unit u's products and row sums run -- so two chunks' streams are always in flight per
+// wave, with no metadata round trip, barrier or workgroup dispatch between them.  Per chunk the
+// arithmetic is blk_rows' (the same products summed by the same rows8_sum tree), so y is
+// bit-identical to k_spmv_blk's.
+constexpr int kRunsMaxTiles = 32;  // tiles per workgroup: 2 units each in one wave's 64 lanes
+
+struct RunMeta {  // lane j: unit j
+    uint4 d;
+    int n0, r0, colbase, ok;
+};
+
+struct RunStage {
+    double v[kBlkRows];
+    double x;
+    int c;
+};
+
+__device__ __forceinline__ uint4 run_desc(const RunMeta &m, int j)
+{
+    return make_uint4((unsigned)__builtin_amdgcn_readlane((int)m.d.x, j),
+                      (unsigned)__builtin_amdgcn_readlane((int)m.d.y, j),
+                      (unsigned)__builtin_amdgcn_readlane((int)m.d.z, j),
+                      (unsigned)__builtin_amdgcn_readlane((int)m.d.w, j));
+}
+
+template <bool NT>
+__device__ __forceinline__ void run_issue(const TileArgs &a, const RunMeta &m, int j, RunStage &s)
+{
+    const int lane = threadIdx.x & 63;
+    s.c = 0;
+    if (!__builtin_amdgcn_readlane(m.ok, j))  // an empty unit (the tile has fewer chunks)
+        return;
+    const uint4 d = run_desc(m, j);
+    const int n0 = __builtin_amdgcn_readlane(m.n0, j), colbase = __builtin_amdgcn_readlane(m.colbase, j);
+    const int vofs = d.x & 0xffff, wc = d.x >> 24;
+    const int h = d.y & 15, p = (d.y >> 4) & 7;
+    int start = 0, pstart = 0;
+#pragma unroll
+    for (int i = 0; i < kBlkRows; ++i) {
+        pstart = i == p ? start : pstart;
+        const int len = blk_len(d, i);
+        if (i < h && lane < len)
+            s.v[i] = ld_stream<NT>(a.vals + n0 + vofs + start + lane);
+        start += i < h ? len : 0;
+    }
+    if (lane < wc)
+        s.c = colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + lane);
+}
+
+__device__ __forceinline__ void run_gather(const TileArgs &a, const RunMeta &m, int j, RunStage &s)
+{
+    const int wc = __builtin_amdgcn_readlane(m.ok, j) ? (int)((unsigned)__builtin_amdgcn_readlane((int)m.d.x, j) >> 24) : 0;
+    s.x = 0.0;
+    if ((threadIdx.x & 63) < wc)
+        s.x = a.x[s.c];
+}
+
+__device__ __forceinline__ void run_finish(const TileArgs &a, const RunMeta &m, int j, const RunStage &s)
+{
+    if (!__builtin_amdgcn_readlane(m.ok, j))
+        return;
+    const int lane = threadIdx.x & 63;
+    const uint4 d = run_desc(m, j);
+    const int h = d.y & 15, rofs = d.y >> 16;
+    double pr[kBlkRows];
+#pragma unroll
+    for (int i = 0; i < kBlkRows; ++i)
+        pr[i] = (i < h && lane < blk_len(d, i)) ? s.v[i] * s.x : 0.0;
+    const double sum = rows8_sum(pr);
+    const int myrow = lane >> 3;
+    if ((lane & 7) == 0 && myrow < h)
+        a.y[__builtin_amdgcn_readlane(m.r0, j) + rofs + myrow] = sum;
+}
+
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void k_spmv_runs(TileArgs a)
+{
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int G = gridDim.x, b = blockIdx.x, T = a.num_tiles;
+    const int U = 2 * ((T - b + G - 1) / G);  // the host keeps this <= 2 * kRunsMaxTiles
+    RunMeta m{};
+    if (lane < U) {
+        const int t = xcd_tile(b + (lane >> 1) * G, T);
+        const uint4 *bt = a.blk + (size_t)t * a.blk_stride;
+        const int di = w + 4 * (lane & 1);  // < 8 <= blk_stride: always inside the tile's set
+        const uint4 d0 = bt[0], dc = bt[di];
+        const int2 b0 = a.bounds[t];
+        m.colbase = a.colbase[t];
+        m.d = di == 0 ? d0 : dc;
+        m.ok = di < (int)((d0.y >> 8) & 255u);
+        m.n0 = b0.y;
+        m.r0 = b0.x;
+    }
+    RunStage A, B, C;
+    run_issue<NT>(a, m, 0, A);
+    run_issue<NT>(a, m, 1, B);  // U >= 2
+    for (int u = 0; u < U; u += 3) {
+        run_gather(a, m, u, A);
+        if (u + 2 < U)
+            run_issue<NT>(a, m, u + 2, C);
+        run_finish(a, m, u, A);
+        if (u + 1 >= U)
+            break;
+        run_gather(a, m, u + 1, B);
+        if (u + 3 < U)
+            run_issue<NT>(a, m, u + 3, A);
+        run_finish(a, m, u + 1, B);
+        if (u + 2 >= U)
+            break;
+        run_gather(a, m, u + 2, C);
+        if (u + 4 < U)
+            run_issue<NT>(a, m, u + 4, B);
+        run_finish(a, m, u + 2, C);
+    }
+}
+
 // Single right-hand side, persistent and software-pipelined.  Workgroup v (XCD-grouped) walks
 // the contiguous tile run [v*tpb, min((v+1)*tpb, T)); its bounds, reduction modes and tail
 // flags are staged in LDS once.  Two register stages (A, B) ping-pong, so no register copy of
@@ -2716,10 +2840,23 @@ __global__ void k_dist_finish(CgVecArgs a)
     a.ctrl->iter = iter + 1;
 }
 
+// Cache flush between cold calls: by default a READ sweep of a buffer larger than the L2s and
+// the 256 MiB Infinity Cache, so the measured kernel finds its data evicted and the caches full
+// of clean lines.  A write sweep (MSPMV_FLUSH=write, the first flush of every buffer) leaves them
+// full of dirty lines instead, whose write-back the measured kernel then pays as it evicts them
+// (measured: the cant-shaped SpMV 31.5 us after a write sweep against 15.5 us hot).
 __global__ void k_flush(double *p, long long n, double v)
 {
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
         p[i] = v;
+}
+__global__ void k_flush_read(const double *p, long long n, double *sink)
+{
+    double acc = 0.0;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        acc += __builtin_nontemporal_load(p + i);
+    if (acc == -1.0)  // never (the buffer holds +1.0): keeps the loads live without a store
+        *sink = acc;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2742,6 +2879,7 @@ struct SpmvTuning {
     int trsv_tagged = 1;  // IC(0) solves: data-tagged values (1) or ready flags (0)
     int blocks = 1;   // single-RHS tiles staged by node blocks where rows share columns (k_build_blocks)
     int blkreg = 1;   // plans of register node-block tiles only run the LDS-free k_spmv_blk
+    int runs = 0;     // ... or, for the plain SpMV, the persistent wave-pipelined k_spmv_runs
     int spmm_blk = 1; // SpMM (L >= 2) on such a plan runs k_spmm_blk instead of its own L-wide tiles
     int dict = 1;     // single-RHS SpMV through per-tile column dictionaries (k_build_dict) when
                       // a tile's nonzeros repeat its distinct columns >= dict_ratio times (0: off)
@@ -2776,6 +2914,8 @@ static const SpmvTuning &spmv_tuning()
             v.blocks = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMV_BLKREG"))
             v.blkreg = atoi(e) != 0;
+        if (const char *e = getenv("MSPMV_SPMV_RUNS"))
+            v.runs = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMM_BLK"))
             v.spmm_blk = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMV_DICT"))
@@ -2808,7 +2948,7 @@ std::string spmv_kernel_name(const mspmv_handle_s *h)
     const auto it = h->plans.find(tile_items_for(1));
     if (it != h->plans.end() && it->second.d_blk && it->second.num_tiles_reg == it->second.num_tiles && t.blkreg &&
         t.tb == kBlock && !t.persist)
-        return std::string("k_spmv_blk<0,") + (stream_nt(h) ? "true>" : "false>");
+        return std::string(t.runs ? "k_spmv_runs<" : "k_spmv_blk<0,") + (stream_nt(h) ? "true>" : "false>");
     return std::string(t.persist ? "k_spmv_persist<" : "k_spmv_tile<") + std::to_string(t.ipt) + ",0," +
            (stream_nt(h) ? "true" : "false") + (t.tb == 64 && !t.persist ? ",64>" : ">");
 }
@@ -2972,6 +3112,23 @@ static void launch_spmv_persist(const TileArgs &a, hipStream_t s, int num_cus, i
     }
 }
 
+// k_spmv_runs grid: as many workgroups as are resident at once, fewer when that evens out the
+// tiles per workgroup, a multiple of 8 (each workgroup's tiles then stay on its XCD).
+template <bool NTV>
+static void launch_spmv_runs(const TileArgs &a, hipStream_t s, int num_cus)
+{
+    static int occ = 0;
+    if (occ < 1 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_spmv_runs<NTV>, kBlock, 0) != hipSuccess ||
+                    occ < 1))
+        occ = 1;
+    const long long slots = (long long)std::max(num_cus, 1) * occ;
+    const long long per = std::min<long long>((a.num_tiles + slots - 1) / slots, kRunsMaxTiles);
+    long long g = (a.num_tiles + per - 1) / per;
+    if (g > 8)
+        g = (g + 7) & ~7LL;  // up: a workgroup never gets more than kRunsMaxTiles tiles
+    hipLaunchKernelGGL((k_spmv_runs<NTV>), dim3((unsigned)g), dim3(kBlock), 0, s, a);
+}
+
 template <int LL, int I, int MODE>
 static void launch_spmm_nt(const TileArgs &a, hipStream_t s, bool nt)
 {
@@ -3027,6 +3184,13 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_c
         // every tile a register node-block tile: the LDS-free kernel (SpMV and dot mode; the CG
         // form's consumer-side partial sums take it to 86 VGPRs, 5 waves/SIMD, so the pipelined
         // CG keeps k_spmv_tile, whose blk_rows path does the same per-tile work)
+        if (a.all_reg && !tu.persist && MODE == kModeSpmv && tu.runs) {
+            if (nt)
+                launch_spmv_runs<true>(a, s, num_cus);
+            else
+                launch_spmv_runs<false>(a, s, num_cus);
+            break;
+        }
         if (a.all_reg && !tu.persist && MODE != kModeCg) {
             if (nt)
                 hipLaunchKernelGGL((k_spmv_blk<MODE == kModeCg ? kModeSpmv : MODE, true>), grid, block, 0, s, a);
@@ -3530,10 +3694,17 @@ hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double
     return hipGetLastError();
 }
 
-hipError_t launch_flush(void *p, size_t bytes, hipStream_t s)
+hipError_t launch_flush(void *p, size_t bytes, hipStream_t s, bool fresh)
 {
+    static const bool write_mode = [] {
+        const char *e = getenv("MSPMV_FLUSH");
+        return e && std::string(e) == "write";
+    }();
     const long long n = (long long)(bytes / sizeof(double));
-    hipLaunchKernelGGL(k_flush, dim3(2048), dim3(256), 0, s, (double *)p, n, 1.0);
+    if (fresh || write_mode)
+        hipLaunchKernelGGL(k_flush, dim3(2048), dim3(256), 0, s, (double *)p, n, 1.0);
+    else
+        hipLaunchKernelGGL(k_flush_read, dim3(2048), dim3(256), 0, s, (const double *)p, n, (double *)p);
     return hipGetLastError();
 }
 
