@@ -160,10 +160,24 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
 {
     const int tile = tile_items_for(L);
     TilePlan p;
-    p.tile_items = tile;
-    p.snap = tile / kSnapDiv;
     const long long total = (long long)h->m + h->nnz;
-    p.num_tiles = (int)((total + tile - 1) / tile);
+    int step = tile, snap = tile / kSnapDiv;
+    if (tile == tile_items_for(1)) {
+        // A grid a few tiles over one resident generation of workgroups takes two tile lifetimes
+        // (the parabolic_fem shape: 2,052 tiles on 2,048 slots).  Stretch the tiles into the
+        // snap slack so they fit one generation: MAXI (step + snap) is unchanged, rows entered by
+        // more than the smaller snap distance stay split (carries, k_fixup).
+        const long long slots = (long long)h->num_cus * spmv_tile_blocks_per_cu();
+        const long long t0 = (total + tile - 1) / tile;
+        const long long fit = slots > 0 ? (total + slots - 1) / slots : 0;
+        if (slots > 0 && t0 > slots && fit + 16 <= tile + tile / kSnapDiv) {
+            step = (int)fit;
+            snap = tile + tile / kSnapDiv - step;  // >= 16
+        }
+    }
+    p.tile_items = step;
+    p.snap = snap;
+    p.num_tiles = (int)((total + step - 1) / step);
     const int T = p.num_tiles;
     mspmv_status st;
     if ((st = dev_alloc(&p.d_bounds, (size_t)T + 1)) != MSPMV_OK ||
@@ -177,7 +191,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
         free_plan(p);
         return s;
     };
-    hipError_t e = launch_merge_coords(h->d_row_offsets, h->m, h->nnz, tile, T, p.d_bounds, h->stream);
+    hipError_t e = launch_merge_coords(h->d_row_offsets, h->m, h->nnz, step, T, p.d_bounds, h->stream);
     if (e == hipSuccess)
         e = launch_snap(h->d_row_offsets, h->m, p.d_bounds, p.d_split, T, p.snap, h->stream);
     std::vector<int2> hb((size_t)T + 1);

@@ -200,6 +200,8 @@ hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const 
 hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L, int ld = 0);
 // Nominal tile size (merge items per tile) used for L right-hand sides.
 int tile_items_for(int L);
+// Resident single-RHS tile workgroups per CU at the default tile shape (0: non-default tuning).
+int spmv_tile_blocks_per_cu();
 std::string spmv_kernel_name(const mspmv_handle_s *h);
 bool stream_nt(const mspmv_handle_s *h);
 bool supported_L(int L);

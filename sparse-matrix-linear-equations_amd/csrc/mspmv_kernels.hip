@@ -1015,12 +1015,15 @@ struct SpmvSmem {
     static constexpr int MAXI = TILE + TILE / kSnapDiv;
     static constexpr int MAXJ = (MAXI + TB - 1) / TB;
     double prod[MAXI + 8];
-    int crow[TB];
-    int ccol[TB];
-    double cval[TB];
     double red[TB / 64];
     int last;
     __device__ __forceinline__ int *rowend(int nnzt) { return reinterpret_cast<int *>(prod + ((nnzt + 7) & ~7)); }
+    // Once a tile's walk has consumed its products and row ends, the walkers' closing pass
+    // (row ends reached, carries) reuses the front of prod as scratch: no separate arrays, so a
+    // workgroup's LDS is the product buffer alone (18.5 KB at IPT = 8: 8 workgroups per CU).
+    __device__ __forceinline__ double *scratch_val() { return prod; }
+    __device__ __forceinline__ int *scratch_row() { return reinterpret_cast<int *>(prod + TB); }
+    static_assert(MAXI + 8 >= TB + TB / 2, "scratch must fit the product buffer");
 };
 
 // Everything after staging, for one tile whose products and row ends are in LDS: one merge
@@ -1037,14 +1040,12 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT, TB> &
     const int items = nrows + nnzt;
     const int ipt = (items + TB - 1) / TB;
     const int d0 = min(tid * ipt, items);
-    int cx, cy;
+    int cx, cy, ex = nrows, ey = nnzt;
     lds_search(d0, rend, nrows, nnzt, cx, cy);
-    // The walker's end is the next walker's start: one search per thread, shared via LDS.
-    sm.crow[tid] = cx;
-    sm.ccol[tid] = cy;
-    tile_sync<TB>();
-    const int ex = tid + 1 < TB ? sm.crow[tid + 1] : nrows;
-    const int ey = tid + 1 < TB ? sm.ccol[tid + 1] : nnzt;
+    // The walker's end is the next walker's start: searched here too (no LDS exchange, so the
+    // workgroup needs no scratch arrays beside the product buffer).
+    if (tid + 1 < TB)
+        lds_search(min(d0 + ipt, items), rend, nrows, nnzt, ex, ey);
     // Does this thread's first row hold nonzeros that earlier threads of the tile consumed?
     const bool need_cin = (cx < ex) && (cy > (cx == 0 ? 0 : rend[cx - 1]));
     // This walker's products, read from LDS up front (independent reads, no dependent chain).
@@ -1103,26 +1104,28 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT, TB> &
         run = 0.0;
         ++cx;
     }
-    tile_sync<TB>();  // every walker has read its neighbour's start from crow / ccol
-    sm.crow[tid] = ex;
-    sm.cval[tid] = run;
+    tile_sync<TB>();  // every walker is done with the products and row ends: scratch may reuse them
+    int *s_row = sm.scratch_row();
+    double *s_val = sm.scratch_val();
+    s_row[tid] = ex;
+    s_val[tid] = run;
     tile_sync<TB>();
     if (pend) {  // close the row begun by earlier threads, summing their carries in thread order
         int j0 = tid - 1;
-        while (j0 > 0 && sm.crow[j0 - 1] == prow)
+        while (j0 > 0 && s_row[j0 - 1] == prow)
             --j0;
-        double acc = sm.cval[j0];
+        double acc = s_val[j0];
         for (int u = j0 + 1; u < tid; ++u)
-            acc += sm.cval[u];
+            acc += s_val[u];
         write_row(prow, acc + pval);
     }
     if (tid == TB - 1 && tail) {  // the tile's trailing partial row -> carry
         int j0 = TB - 1;
-        while (j0 > 0 && sm.crow[j0 - 1] == nrows)
+        while (j0 > 0 && s_row[j0 - 1] == nrows)
             --j0;
-        double acc = sm.cval[j0];
+        double acc = s_val[j0];
         for (int u = j0 + 1; u < TB; ++u)
-            acc += sm.cval[u];
+            acc += s_val[u];
         a.carry_val[t] = acc;
         const int R = r0 + nrows;
         if (MODE == kModeCg) {
@@ -1141,11 +1144,10 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT, TB> &
 // butterfly folds the group.  G = 1 is the sequential CSR-order sum of SpmvGold
 // (cpu_spmv.cpp:241-265), bit for bit.  A few instructions per product, against the walk's
 // merge search and per-item row-end test, for tiles whose rows are alike.
-// Row results go through LDS (sm.cval) and are stored by one thread per row afterwards: one
-// coalesced store per tile, and no global memory operation inside the reduction loop (a loop
-// that only stores makes hipcc drain vmcnt before it, which would wait for the persistent
-// kernel's in-flight prefetch).  xr / pr: r and p_old (CG) or x (dot mode) of row r0 + tid,
-// loaded by the caller for tid <= nrows.
+// The group's lane 0 stores the row (G = 1: thread r stores row r, one coalesced store per
+// round, as a staged store would be); no LDS beyond the product buffer.  xr / pr: r and p_old
+// (CG) or x (dot mode) of row r0 + tid, loaded by the caller for tid <= nrows -- the operands
+// of the rows a G = 1 thread owns first; other rows load their own.
 template <int IPT, int MODE, int TB = kBlock>
 __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT, TB> &sm, int t, int r0, int nrows,
                                            int nnzt, bool tail, double beta, double &dot, int lg, double xr,
@@ -1175,55 +1177,36 @@ __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT, TB> 
             v += __shfl_xor(v, off);
         return v;
     };
-    const int nfast = min(nseg, TB);
-    for (int r = tid >> lg; r < nfast; r += TB >> lg) {  // uniform within a group
+    for (int r = tid >> lg; r < nseg; r += TB >> lg) {  // uniform within a group
         const double v = seg_sum(r);
-        if (lane == 0)
-            sm.cval[r] = v;
-    }
-    for (int r = TB + (tid >> lg); r < nseg; r += TB >> lg) {  // rare: > TB segments
-        const double v = seg_sum(r);
-        if (lane == 0) {
-            const int R = r0 + r;
-            if (r < nrows) {
-                a.y[R] = v;
-                if (MODE == kModeCg) {
-                    const double2 w = cg_rp(a, R);
-                    const double pn = w.x + beta * w.y;
-                    cg_pstore(a, R, pn);
-                    dot += pn * v;
-                } else if (MODE == kModeDot) {
-                    dot += a.x[R] * v;
-                }
+        if (lane != 0)
+            continue;
+        const int R = r0 + r;
+        double ox = xr, op = pr;  // the row's operands: preloaded when r is this thread's own row
+        if (MODE != kModeSpmv && r != tid) {
+            if constexpr (MODE == kModeCg) {
+                const double2 w = cg_rp(a, R);
+                ox = w.x;
+                op = w.y;
             } else {
-                a.carry_val[t] = v;
-                if (MODE == kModeCg) {
-                    const double2 w = cg_rp(a, R);
-                    dot += (w.x + beta * w.y) * v;
-                } else if (MODE == kModeDot)
-                    dot += a.x[R] * v;
+                ox = a.x[R];
             }
         }
-    }
-    tile_sync<TB>();
-    if (tid < nfast) {
-        const double v = sm.cval[tid];
-        if (tid < nrows) {
-            const int R = r0 + tid;
+        if (r < nrows) {
             a.y[R] = v;
             if (MODE == kModeCg) {
-                const double pn = xr + beta * pr;
+                const double pn = ox + beta * op;
                 cg_pstore(a, R, pn);
                 dot += pn * v;
             } else if (MODE == kModeDot) {
-                dot += xr * v;
+                dot += ox * v;
             }
         } else {  // the trailing partial row -> carry (k_fixup adds it in tile order)
             a.carry_val[t] = v;
             if (MODE == kModeCg)
-                dot += (xr + beta * pr) * v;
+                dot += (ox + beta * op) * v;
             else if (MODE == kModeDot)
-                dot += xr * v;
+                dot += ox * v;
         }
     }
     tile_sync<TB>();  // LDS free for the next tile
@@ -1327,7 +1310,7 @@ __device__ __forceinline__ void cg1_publish(const TileArgs &a, SM &sm, int slot,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    publish_partials<1>(a.partials, a.gtickets, slot, nslots, kConsumeTile, sm.cval, sm.red, &sm.last);
+    publish_partials<1>(a.partials, a.gtickets, slot, nslots, kConsumeTile, sm.prod, sm.red, &sm.last);
 }
 
 // Single right-hand side, one tile per workgroup of TB threads.  TILE = TB*IPT merge items
@@ -1339,8 +1322,17 @@ __device__ __forceinline__ void cg1_publish(const TileArgs &a, SM &sm, int slot,
 constexpr int kLabStampTiles = 1 << 17;
 __device__ unsigned long long g_lab_stamps[kLabStampTiles * 6];
 #endif
+// Waves per SIMD the pipelined CG's tile kernel is compiled for (MODE 1): unconstrained it takes
+// 92 VGPRs (5 waves, 5 workgroups per CU); a lab build can ask the compiler for more
+// (-DMSPMV_CG_WAVES=7 or 8) at the price of fewer loads in flight per wave.
+#ifndef MSPMV_CG_WAVES
+#define MSPMV_CG_WAVES 0
+#endif
+constexpr int spmv_tile_waves(int mode) { return mode == 1 && MSPMV_CG_WAVES > 0 ? MSPMV_CG_WAVES : 1; }
+
 template <int IPT, int MODE, bool NT, int TB = kBlock>
-__global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(spmv_tile_waves(MODE)))) void
+k_spmv_tile(TileArgs a)
 {
     static_assert(TB == kBlock || MODE == kModeSpmv, "one-wave tiles run the plain SpMV only");
     constexpr bool CG = MODE == kModeCg;
@@ -2139,7 +2131,10 @@ __global__ __launch_bounds__(kBlock) void k_spmm_blk(TileArgs a)
     static_assert(MODE != kModeCg, "multi-RHS CG runs the split iteration (MODE 2)");
     constexpr int GL = L / 2;      // lanes per panel row
     constexpr int NGW = 64 / GL;   // column groups per wave = pattern columns per pass
-    constexpr int PB = 4;          // passes whose gathers are in flight together
+#ifndef MSPMV_SPMM_BLK_PB
+#define MSPMV_SPMM_BLK_PB 4
+#endif
+    constexpr int PB = MSPMV_SPMM_BLK_PB;  // passes whose gathers are in flight together
     __shared__ double2 s_red2[MODE == kModeDot ? kBlock / 64 : 1][GL];
     const int stopped = MODE != kModeSpmv ? a.ctrl->done : 0;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -2959,6 +2954,20 @@ int spmm_iptg_for(int L)
 {
     const int i = spmv_tuning().spmm_iptg;
     return i ? i : (L >= 8 ? 16 : 8);
+}
+
+int spmv_tile_blocks_per_cu()
+{
+    static const int occ = [] {
+        const SpmvTuning &t = spmv_tuning();
+        int a = 0, b = 0;
+        if (t.ipt != 8 || t.tb != kBlock || t.tile_items || t.persist ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_spmv_tile<8, kModeSpmv, false>, kBlock, 0) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_spmv_tile<8, kModeCg, false>, kBlock, 0) != hipSuccess)
+            return 0;
+        return std::min(a, b);
+    }();
+    return occ;
 }
 
 int tile_items_for(int L)
