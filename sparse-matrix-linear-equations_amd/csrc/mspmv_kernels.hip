@@ -2134,7 +2134,10 @@ __global__ __launch_bounds__(kBlock) void k_spmm_blk(TileArgs a)
 #ifndef MSPMV_SPMM_BLK_PB
 #define MSPMV_SPMM_BLK_PB 4
 #endif
-    constexpr int PB = MSPMV_SPMM_BLK_PB;  // passes whose gathers are in flight together
+    // passes whose gathers are in flight together (measured on the pwtk shape, L = 16: 2 and 8
+    // slower than 4; fused multiply-adds instead of the guarded mul + add, also slower, 96 -> 128
+    // VGPRs before the per-row pass skips, no faster at 96: the kernel waits on memory)
+    constexpr int PB = MSPMV_SPMM_BLK_PB;
     __shared__ double2 s_red2[MODE == kModeDot ? kBlock / 64 : 1][GL];
     const int stopped = MODE != kModeSpmv ? a.ctrl->done : 0;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -2185,15 +2188,17 @@ __global__ __launch_bounds__(kBlock) void k_spmm_blk(TileArgs a)
             }
 #pragma unroll
             for (int q = 0; q < PB; ++q) {
-                const int j = (pb + q) * NGW + g;
+                const int jb = (pb + q) * NGW;  // the pass's first pattern column (wave-uniform)
+                const int j = jb + g;
 #pragma unroll
                 for (int i = 0; i < kBlkRows; ++i) {
-                    if (i < h) {  // wave-uniform
-                        const double v = __shfl(vrow[i], j & 63);
-                        const bool on = j < blk_len(d, i);
-                        acc[i].x += on ? v * xv[q].x : 0.0;
-                        acc[i].y += on ? v * xv[q].y : 0.0;
-                    }
+                    const int len = blk_len(d, i);
+                    if (i >= h || jb >= len)  // wave-uniform: row i has no column in this pass
+                        continue;
+                    const double v = __shfl(vrow[i], j & 63);
+                    const bool on = j < len;
+                    acc[i].x += on ? v * xv[q].x : 0.0;
+                    acc[i].y += on ? v * xv[q].y : 0.0;
                 }
             }
         }
