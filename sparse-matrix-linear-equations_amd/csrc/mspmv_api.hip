@@ -348,6 +348,10 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
     return MSPMV_OK;
 }
 
+namespace mspmv {
+mspmv_status plan_for(mspmv_handle_s *h, int L, const TilePlan **out) { return get_plan(h, L, out); }
+}  // namespace mspmv
+
 static mspmv_status validate_host_csr(const mspmv_csr_d *a)
 {
     if (!a)

@@ -480,14 +480,8 @@ mspmv_status halo_exchange(mspmv_dist_s *d, int L, const CgControl *ctrl)
 
 mspmv_status get_local_plan(mspmv_dist_s *d, int L, const TilePlan **plan)
 {
-    // mspmv_tile_plan builds (once) and returns the plan; the internal pointer comes from the map
-    int nt = 0;
-    D_ST(mspmv_tile_plan(d->local, L, &nt, nullptr, nullptr, nullptr));
-    auto it = d->local->plans.find(tile_items_for(L));
-    if (it == d->local->plans.end())
-        return fail_msg(MSPMV_ERR_INVALID, "local tile plan missing");
-    *plan = &it->second;
-    return MSPMV_OK;
+    // the plan the local handle's kernels use for L (the node-block plan for L > 1 on FEM blocks)
+    return plan_for(d->local, L, plan);
 }
 
 }  // namespace
@@ -659,7 +653,17 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
     const long long elems = (long long)d->n_own * L;
     const int nblk = cg_update_blocks(std::max(elems, 2LL));
     const int cap = max_err_hist ? std::max(hist_cap, 0) : 0;
-    D_ST(ensure_buffers(d, L, nblk, plan->num_tiles, cap));
+    // overlapped iteration (the local rows split head | interior | tail, as mspmv_dist_spmm_dev):
+    // each part's dot-mode tiles write their p.Ap partials at the part's offset, one fold sums
+    // the three in tile order
+    const TilePlan *pp[3] = {nullptr, nullptr, nullptr};
+    int toff[4] = {0, 0, 0, 0};
+    const bool split = d->part[1] != nullptr;
+    for (int q = 0; q < 3 && split; ++q) {
+        D_ST(plan_for(d->part[q], L, &pp[q]));
+        toff[q + 1] = toff[q] + pp[q]->num_tiles;
+    }
+    D_ST(ensure_buffers(d, L, nblk, std::max(plan->num_tiles, toff[3]), cap));
     hipStream_t s = d->local->stream;
     DistVecArgs va{};
     va.n_elems = elems;
@@ -691,8 +695,26 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
     auto iteration = [&]() -> mspmv_status {
         DistVecArgs a = va;
         D_HIP(launch_dist_vec_mirror(2, a, L, nblk, d->d_pext, s));       // p = r + beta p
-        D_ST(halo_exchange(d, L, d->d_ctrl));                               // p halo rows
-        D_HIP(launch_spmm_dot(d->local, *plan, d->d_pext, d->d_ap, L, d->d_ctrl, d->d_partials, d->d_gtickets, pAp));
+        if (!split) {
+            D_ST(halo_exchange(d, L, d->d_ctrl));                           // p halo rows
+            D_HIP(launch_spmm_dot(d->local, *plan, d->d_pext, d->d_ap, L, d->d_ctrl, d->d_partials, d->d_gtickets,
+                                  pAp));
+        } else {
+            // the interior (owned columns only) on its own stream beside the exchange
+            mspmv_handle mid = d->part[1];
+            D_HIP(hipEventRecord(d->ev[0], s));
+            D_HIP(hipStreamWaitEvent(mid->stream, d->ev[0], 0));
+            D_HIP(launch_spmm_dot_tiles(mid, *pp[1], d->d_pext, d->d_ap + (size_t)d->int_lo * L, L, d->d_ctrl,
+                                        d->d_partials + (size_t)toff[1] * L, mid->stream, d->int_lo));
+            D_HIP(hipEventRecord(d->ev[1], mid->stream));
+            D_ST(halo_exchange(d, L, d->d_ctrl));                           // p halo rows
+            const int rofs[3] = {0, d->int_lo, d->int_hi};
+            for (int q = 0; q < 3; q += 2)
+                D_HIP(launch_spmm_dot_tiles(d->part[q], *pp[q], d->d_pext, d->d_ap + (size_t)rofs[q] * L, L,
+                                            d->d_ctrl, d->d_partials + (size_t)toff[q] * L, s, rofs[q]));
+            D_HIP(hipStreamWaitEvent(s, d->ev[1], 0));
+            D_HIP(launch_fold_dot(toff[3], L, d->d_partials, d->d_gtickets, pAp, nullptr, nullptr, d->d_ctrl, -1, s));
+        }
         D_NCCL(ncclAllReduce(pAp, pAp, L, ncclFloat64, ncclSum, d->comm, s));
         a.red_in = pAp;
         a.red_out = rr;

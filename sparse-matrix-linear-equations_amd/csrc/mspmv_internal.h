@@ -263,6 +263,14 @@ hipError_t launch_dist_pack(const double *p, const int *idx, long long n_elems, 
 hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
                            CgControl *ctrl, double *partials, unsigned *gtickets, double *dot_out,
                            CgScalars *scal = nullptr, const unsigned char *conv = nullptr, int fold_mode = -1);
+// The two halves of launch_spmm_dot, for SpMMs split over several handles (the row-sharded CG's
+// head | interior | tail): each part's tiles write their partials at its offset, one fold sums all.
+hipError_t launch_spmm_dot_tiles(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
+                                 CgControl *ctrl, double *partials, hipStream_t s, long long row_off);
+hipError_t launch_fold_dot(int T, int L, double *partials, unsigned *gtickets, double *dot_out, CgScalars *scal,
+                           const unsigned char *conv, CgControl *ctrl, int fold_mode, hipStream_t s);
+// The tile plan a handle's kernels use for L right-hand sides (built on first use).
+mspmv_status plan_for(mspmv_handle_s *h, int L, const TilePlan **out);
 // SPAI-preconditioned block CG (SPAISolveMultiple, work_2025/main/sparse_approximate_inverse.hpp:
 // 30-230) on A's handle h with the preconditioner's handle hm (same shape and device): init
 // (X = 0, R = B, Z = M R, P = Z, rs_old = R.Z) and one iteration (AP = A P -> alpha; X, R update

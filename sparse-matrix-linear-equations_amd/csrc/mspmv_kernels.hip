@@ -612,6 +612,8 @@ struct TileArgs {
     const int *__restrict__ cols;
     const double *__restrict__ vals;
     const double *__restrict__ x;      // SpMV/SpMM: x / X.   CG: {r, p_old} interleaved (cg_rp)
+    const double *__restrict__ xr;     // MODE 2: the rows' own x (row R at xr[R * ld]) for x.(Ax) --
+                                       // x itself unless the handle is a row range of x's rows
     const double *__restrict__ p_old;  // (unused by the single-RHS CG: p_old rides with r in x)
     double *__restrict__ p_new;        // CG: the {r, p} buffer of the next iteration; p = r + beta p_old
                                        // is written for the tile's rows at p_new[2 R + 1] (cg_pstore)
@@ -960,7 +962,7 @@ __device__ __forceinline__ void blk_rows(const TileArgs &a, const uint4 &bd, int
                     if constexpr (CG)
                         ro[s] = cg_rp(a, R);
                     else
-                        ro[s].x = a.x[R];
+                        ro[s].x = a.xr[R];
                 }
             }
         }
@@ -1064,7 +1066,7 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT, TB> &
             cg_pstore(a, R, pn);
             dot += pn * val;
         } else if (MODE == kModeDot) {
-            dot += a.x[R] * val;
+            dot += a.xr[R] * val;
         }
     };
     double run = 0.0;
@@ -1133,7 +1135,7 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT, TB> &
             dot += (v.x + beta * v.y) * acc;
         }
         else if (MODE == kModeDot)
-            dot += a.x[R] * acc;
+            dot += a.xr[R] * acc;
     }
     tile_sync<TB>();  // LDS free for the next tile
 }
@@ -1189,7 +1191,7 @@ __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT, TB> 
                 ox = w.x;
                 op = w.y;
             } else {
-                ox = a.x[R];
+                ox = a.xr[R];
             }
         }
         if (r < nrows) {
@@ -1236,7 +1238,7 @@ __device__ __forceinline__ void row_operands(const TileArgs &a, int r0, int nrow
             xr = v.x;
             pr = v.y;
         } else {
-            xr = a.x[R];
+            xr = a.xr[R];
         }
     }
 }
@@ -1784,7 +1786,7 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
         // MODE 2: the row's own x, issued ahead of the row's gathers (used after them)
         double2 xx = make_double2(0.0, 0.0);
         if (MODE == kModeDot && sub == 0)
-            xx = *reinterpret_cast<const double2 *>(a.x + (size_t)(r0 + r) * a.ld + 2 * lane);
+            xx = *reinterpret_cast<const double2 *>(a.xr + (size_t)(r0 + r) * a.ld + 2 * lane);
         double2 acc = make_double2(0.0, 0.0);
         int k = s0 + sub;
         // batches of 8 panel-row gathers in flight per lane (the SpMM is gather-latency bound:
@@ -1974,7 +1976,7 @@ k_spmm_tile(TileArgs a)
         const size_t off = (size_t)(r0 + row) * a.ld + 2 * lane;
         *reinterpret_cast<double2 *>(a.y + off) = val;
         if (MODE == kModeDot) {
-            const double2 xx = *reinterpret_cast<const double2 *>(a.x + off);
+            const double2 xx = *reinterpret_cast<const double2 *>(a.xr + off);
             dot.x += xx.x * val.x;
             dot.y += xx.y * val.y;
         }
@@ -2064,7 +2066,7 @@ k_spmm_tile(TileArgs a)
         *reinterpret_cast<double2 *>(a.carry_val + (size_t)t * L + 2 * lane) = acc;
         if (MODE == kModeDot) {
             const size_t off = (size_t)(r0 + nrows) * a.ld + 2 * lane;
-            const double2 xx = *reinterpret_cast<const double2 *>(a.x + off);
+            const double2 xx = *reinterpret_cast<const double2 *>(a.xr + off);
             dot.x += xx.x * acc.x;
             dot.y += xx.y * acc.y;
         }
@@ -2172,7 +2174,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_blk(TileArgs a)
         const bool store = (lane & 7) < GL && ri < h;
         double2 xx = make_double2(0.0, 0.0);  // dot mode: the stored row's own x, issued early
         if (MODE == kModeDot && store)
-            xx = *reinterpret_cast<const double2 *>(a.x + (size_t)(r0 + rofs + ri) * a.ld + 2 * c);
+            xx = *reinterpret_cast<const double2 *>(a.xr + (size_t)(r0 + rofs + ri) * a.ld + 2 * c);
         double2 acc[kBlkRows];
 #pragma unroll
         for (int i = 0; i < kBlkRows; ++i)
@@ -3078,6 +3080,7 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
     a.cols = h->d_cols;
     a.vals = h->d_vals;
     a.x = X;
+    a.xr = X;
     a.y = Y;
     a.bounds = plan.d_bounds;
     a.split = plan.d_split;
@@ -3665,37 +3668,45 @@ hipError_t launch_dist_pack(const double *p, const int *idx, long long n_elems, 
 
 // Y = A X with x.(AX) per column reduced into dot_out (MODE 2), plus the carry fix-up and the
 // partials fold.  scal / conv (single-GPU split CG) add the non-finite-alpha stop.
-hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
-                           CgControl *ctrl, double *partials, unsigned *gtickets, double *dot_out,
-                           CgScalars *scal, const unsigned char *conv, int fold_mode)
+// The dot-mode SpMM's tile kernel (+ carries) on stream s: Y = A X and one x.(AX) partial per tile
+// at partials[t * L ..] (plain stores, summed by launch_fold_dot in a later launch).
+hipError_t launch_spmm_dot_tiles(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
+                                 CgControl *ctrl, double *partials, hipStream_t s, long long row_off)
 {
-    const int mode = fold_mode >= 0 ? fold_mode : scal ? kFoldCgAlpha : kFoldDot;
-    if (plan.num_tiles == 0)  // a rank without rows contributes 0 to the all-reduce
-        return hipMemsetAsync(dot_out, 0, sizeof(double) * L, h->stream);
+    if (plan.num_tiles == 0)
+        return hipSuccess;
     TileArgs ta = make_args(h, plan, d_X, d_Y, L);
+    ta.xr = d_X + row_off * L;  // the handle's rows start at row row_off of X
     ta.ctrl = ctrl;
     ta.partials = partials;
-    ta.gtickets = gtickets;
-    ta.dot_out = dot_out;
-    hipError_t e = launch_tile<kModeDot>(ta, L, h->stream, h->num_cus, stream_nt(h));
+    hipError_t e = launch_tile<kModeDot>(ta, L, s, h->num_cus, stream_nt(h));
     if (e != hipSuccess)
         return e;
     if (plan.num_carries) {
         const int n = plan.num_carries * L;
-        hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, h->stream, plan.d_carry_tiles,
-                           plan.d_carry_rows, plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)ctrl, L);
-        if ((e = hipGetLastError()) != hipSuccess)
-            return e;
+        hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, s, plan.d_carry_tiles, plan.d_carry_rows,
+                           plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)ctrl, L);
+        e = hipGetLastError();
     }
-    const int T = plan.num_tiles;
+    return e;
+}
+
+// Sum T tiles' partials [T][L] in tile order into dot_out (k_fold_dot; partials_capacity() leaves
+// room for the fold's levels after the T * L partials).
+hipError_t launch_fold_dot(int T, int L, double *partials, unsigned *gtickets, double *dot_out, CgScalars *scal,
+                           const unsigned char *conv, CgControl *ctrl, int fold_mode, hipStream_t s)
+{
+    const int mode = fold_mode >= 0 ? fold_mode : scal ? kFoldCgAlpha : kFoldDot;
+    if (T == 0)  // no rows: contributes 0 (a rank's share of the all-reduce)
+        return hipMemsetAsync(dot_out, 0, sizeof(double) * L, s);
     const int G = std::max(1, std::min(256, (T + 63) / 64));  // >= 64 tiles per fold block
     const int q = (T + G - 1) / G;
-    double *lvl = partials + (size_t)T * L;  // partials_capacity() leaves room for these levels
+    double *lvl = partials + (size_t)T * L;
     switch (L) {
 #define MSPMV_FOLD(LL)                                                                             \
     case LL:                                                                                       \
-        hipLaunchKernelGGL((k_fold_dot<LL>), dim3(G), dim3(kBlock), 0, h->stream, partials, T, q, lvl, gtickets, \
-                           dot_out, scal, conv, ctrl, mode);                                       \
+        hipLaunchKernelGGL((k_fold_dot<LL>), dim3(G), dim3(kBlock), 0, s, partials, T, q, lvl, gtickets, dot_out, \
+                           scal, conv, ctrl, mode);                                                \
         break;
         MSPMV_FOLD(1)
         MSPMV_FOLD(2)
@@ -3706,6 +3717,16 @@ hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
+}
+
+hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
+                           CgControl *ctrl, double *partials, unsigned *gtickets, double *dot_out,
+                           CgScalars *scal, const unsigned char *conv, int fold_mode)
+{
+    hipError_t e = launch_spmm_dot_tiles(h, plan, d_X, d_Y, L, ctrl, partials, h->stream, 0);
+    if (e != hipSuccess)
+        return e;
+    return launch_fold_dot(plan.num_tiles, L, partials, gtickets, dot_out, scal, conv, ctrl, fold_mode, h->stream);
 }
 
 hipError_t launch_flush(void *p, size_t bytes, hipStream_t s, bool fresh)
