@@ -991,9 +991,10 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
                 break;
         }
     }
-    if (st == MSPMV_OK && pipelined && max_iters > 0) {
-        // the last iteration's stop test (a no-op once the solve has stopped)
-        hipError_t ef = launch_cg1_finish(h, max_iters & 1, nblk);
+    if (st == MSPMV_OK && max_iters > 0 && !hm && !ic) {
+        // pipelined: the last iteration's stop test (a no-op once the solve has stopped); both
+        // forms: the deferred x += alpha p of the last update
+        hipError_t ef = pipelined ? launch_cg1_finish(h, d_x, max_iters & 1, nblk) : launch_cg_xflush(h, d_x, L, nblk);
         if (ef != hipSuccess) {
             set_error(std::string("CG finish launch: ") + hipGetErrorString(ef));
             st = MSPMV_ERR_HIP;

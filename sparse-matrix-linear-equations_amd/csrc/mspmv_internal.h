@@ -85,7 +85,9 @@ struct CgControl {
     int iters_out;   // iteration count to report (the reference's return value)
     int breakdown;   // 1 if p.Ap <= 0 or non-finite was met
     int iter_par[2]; // single-RHS pipelined CG: iteration index handed to the next SpMV, by parity
-    unsigned reserved[2];
+    int x_pending;   // multi-RHS split CG: x += alpha p of the last update not applied yet (k_cg_update
+                     // sets it, the next p update applies the term, the fold after it clears it)
+    unsigned reserved;
 };
 
 }  // namespace mspmv
@@ -214,11 +216,14 @@ int cg_update_blocks(long long elems);
 // Iterations per CG batch / graph replay for an m-row, nnz-nonzero matrix and L columns (mspmv_api.hip).
 int cg_batch_iters(long long m, long long nnz, int L);
 // Pipelined single-RHS CG (L == 1 unless MSPMV_CG_SPLIT=1): init (x = 0, r = p0 = b, b.b
-// partials) and, after max_iters iterations, the last stop test; grid of cg1_blocks(m).
+// partials) and, after the loop, the last stop test (after max_iters iterations) and the last deferred
+// x += alpha p (k_cg1_xflush, always); grid of cg1_blocks(m).
 bool cg_split_iteration(int L);
 int cg1_blocks(long long m);
 hipError_t launch_cg1_init(mspmv_handle_s *h, const double *d_b, double *d_x, int nblk);
-hipError_t launch_cg1_finish(mspmv_handle_s *h, int parity, int nblk);
+hipError_t launch_cg1_finish(mspmv_handle_s *h, double *d_x, int parity, int nblk);
+// Split (multi-RHS) CG: the last deferred x += alpha p after the loop (a no-op when none is pending).
+hipError_t launch_cg_xflush(mspmv_handle_s *h, double *d_x, int L, int nblk);
 // Offset (doubles) and count of the partials level a consumer sums: levels of a fan-in
 // kSlotGroup tree are folded while more than `stop` partials would remain.
 inline void consumer_level(int nslots, int stop, int L, long long *off, int *count)

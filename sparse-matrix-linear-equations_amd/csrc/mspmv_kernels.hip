@@ -615,6 +615,8 @@ struct TileArgs {
     const double *__restrict__ xr;     // MODE 2: the rows' own x (row R at xr[R * ld]) for x.(Ax) --
                                        // x itself unless the handle is a row range of x's rows
     const double *__restrict__ p_old;  // (unused by the single-RHS CG: p_old rides with r in x)
+    double *__restrict__ xsol;         // CG (MODE 1): the solution; iteration k applies x += alpha_{k-1} p_{k-1}
+                                       // to the tile's rows (cg1_lag_*)
     double *__restrict__ p_new;        // CG: the {r, p} buffer of the next iteration; p = r + beta p_old
                                        // is written for the tile's rows at p_new[2 R + 1] (cg_pstore)
     double *__restrict__ y;            // SpMV/SpMM: y / Y.   CG: Ap
@@ -1296,6 +1298,44 @@ __device__ __forceinline__ bool cg1_head(const TileArgs &a, double rs, double &b
     return true;
 }
 
+// Pipelined single-RHS CG, deferred solution update.  x += alpha_{k-1} p_{k-1} (AxpySingle,
+// single_strategy.hpp:143-144, the same expression) is applied by iteration k's SpMV to the rows of
+// its tile instead of by the update kernel of iteration k-1: the SpMV already holds p_{k-1} for
+// those rows (it rides in the {r, p} buffer it reads), so the update kernel no longer reads p and
+// x or writes x.  The last pending term is applied by k_cg1_xflush after the loop.  The operands of
+// the tile's first rows are loaded at entry (one row per thread); alpha_{k-1} is scal[0].alpha.
+struct CgLag {
+    double x, p, alpha;
+    int k;
+};
+
+template <int TB>
+__device__ __forceinline__ void cg1_lag_load(const TileArgs &a, int r0, int nrows, CgLag &g)
+{
+    const int i = threadIdx.x;
+    g.k = a.ctrl->iter_par[a.parity];  // the iteration cg1_head runs (not written by this launch)
+    g.alpha = a.scal[0].alpha;
+    g.x = g.p = 0.0;
+    if (i < nrows) {
+        g.x = a.xsol[r0 + i];
+        g.p = a.x[2 * (size_t)(r0 + i) + 1];
+    }
+}
+
+template <int TB>
+__device__ __forceinline__ void cg1_lag_store(const TileArgs &a, int r0, int nrows, const CgLag &g)
+{
+    if (g.k < 1)  // iteration 0: x = 0 and nothing is pending
+        return;
+    const int i = threadIdx.x;
+    if (i < nrows)
+        a.xsol[r0 + i] = g.x + g.alpha * g.p;
+    for (int j = i + TB; j < nrows; j += TB) {  // tiles of more rows than threads (empty rows)
+        const size_t R = (size_t)r0 + j;
+        a.xsol[R] = a.xsol[R] + g.alpha * a.x[2 * R + 1];
+    }
+}
+
 // Pipelined single-RHS CG tail of the SpMV: this tile's p.Ap partial, for the update kernel
 // to sum (folded by group tickets only beyond kConsumeTile tiles).
 template <typename SM>
@@ -1358,8 +1398,11 @@ k_spmv_tile(TileArgs a)
     // CG: the update's r.r partials are loaded first; summed (-> stop test, beta) once this
     // tile's stream and gathers are in flight.  Block-uniform, as is every branch on nnzt.
     PartRegs<CG ? kUpdateMaxBlocks / kBlock : 1> pin;
-    if constexpr (CG)
+    CgLag lag{};
+    if constexpr (CG) {
         part_load(a.part_in, a.n_part_in, pin);
+        cg1_lag_load<TB>(a, r0, nrows, lag);
+    }
     auto head = [&]() {  // the stop flag is tested before cg1_head records anything
         if (stopped)
             go = false;
@@ -1383,10 +1426,12 @@ k_spmv_tile(TileArgs a)
         });
         if (!go)
             return;
-        if constexpr (MODE == kModeCg)
+        if constexpr (MODE == kModeCg) {
+            cg1_lag_store<TB>(a, r0, nrows, lag);
             cg1_publish(a, sm, t, a.num_tiles, dot);
-        else if constexpr (MODE == kModeDot)
+        } else if constexpr (MODE == kModeDot) {
             dot_epilogue(a, sm, t, dot);
+        }
         return;
     }
     if (nblk > 0) {
@@ -1452,10 +1497,12 @@ k_spmv_tile(TileArgs a)
         o[5] = (unsigned long long)blockIdx.x;
     }
 #endif
-    if constexpr (MODE == kModeCg)
+    if constexpr (MODE == kModeCg) {
+        cg1_lag_store<TB>(a, r0, nrows, lag);
         cg1_publish(a, sm, t, a.num_tiles, dot);
-    else if constexpr (MODE == kModeDot)
+    } else if constexpr (MODE == kModeDot) {
         dot_epilogue(a, sm, t, dot);
+    }
 }
 
 // Single right-hand side, plans whose EVERY tile is a register node-block tile (FEM matrices such
@@ -2299,6 +2346,8 @@ __global__ __launch_bounds__(kBlock) void k_fold_dot(const double *part, int T, 
     }
     if (mode == kFoldCgAlpha) {
         __syncthreads();
+        if (tid == 0)
+            ctrl->x_pending = 0;  // the p update before this fold applied the deferred x term
         if (tid == 0 && ctrl->breakdown) {  // every column converged or broken: stop here
             int live = 0;
             for (int j = 0; j < L; ++j)
@@ -2395,6 +2444,12 @@ struct CgVecArgs {
     double *red_out;
     unsigned *gtickets;  // reduce_slots tickets
     int pcg;             // k_cg_update: SPAI-PCG (beta and rs_old come from R.Z, k_fold_dot)
+    // Single-GPU split CG: x += alpha p is deferred from the update to the next p update (which
+    // reads p anyway before overwriting it), so the update neither reads p nor reads / writes x.
+    // k_cg_update stores each column's masked alpha in scal[j].alpha and raises ctrl->x_pending;
+    // k_dist_pupdate applies the term; the fold after it clears the flag; k_cg_xflush applies the
+    // term still pending when the solve ends.  Same expression x + alpha p: bit-identical x.
+    int lazy_x;
 };
 
 // x = 0, r = p0 = b; rs_old_j = r_j.r_j, b_norm_j = sqrt(b_j.b_j) (no_pretreatment.hpp:61-79,
@@ -2493,23 +2548,36 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(CgVecArgs a)
     }
     const double2 nal = make_double2(-al.x, -al.y);
     double2 acc = make_double2(0.0, 0.0);
-    for (long long i = i0; i < npairs; i += stride) {
-        const double2 p = reinterpret_cast<const double2 *>(a.p)[i];
-        const double2 q = reinterpret_cast<const double2 *>(a.ap)[i];
-        double2 x = reinterpret_cast<double2 *>(a.x)[i];
-        double2 r = reinterpret_cast<double2 *>(a.r)[i];
-        x.x = x.x + al.x * p.x;
-        x.y = x.y + al.y * p.y;
-        r.x = r.x + nal.x * q.x;
-        r.y = r.y + nal.y * q.y;
-        reinterpret_cast<double2 *>(a.x)[i] = x;
-        reinterpret_cast<double2 *>(a.r)[i] = r;
-        acc.x += r.x * r.x;
-        acc.y += r.y * r.y;
+    if (a.lazy_x) {  // x += alpha p: deferred to the next p update (CgVecArgs::lazy_x)
+        for (long long i = i0; i < npairs; i += stride) {
+            const double2 q = reinterpret_cast<const double2 *>(a.ap)[i];
+            double2 r = reinterpret_cast<double2 *>(a.r)[i];
+            r.x = r.x + nal.x * q.x;
+            r.y = r.y + nal.y * q.y;
+            reinterpret_cast<double2 *>(a.r)[i] = r;
+            acc.x += r.x * r.x;
+            acc.y += r.y * r.y;
+        }
+    } else {
+        for (long long i = i0; i < npairs; i += stride) {
+            const double2 p = reinterpret_cast<const double2 *>(a.p)[i];
+            const double2 q = reinterpret_cast<const double2 *>(a.ap)[i];
+            double2 x = reinterpret_cast<double2 *>(a.x)[i];
+            double2 r = reinterpret_cast<double2 *>(a.r)[i];
+            x.x = x.x + al.x * p.x;
+            x.y = x.y + al.y * p.y;
+            r.x = r.x + nal.x * q.x;
+            r.y = r.y + nal.y * q.y;
+            reinterpret_cast<double2 *>(a.x)[i] = x;
+            reinterpret_cast<double2 *>(a.r)[i] = r;
+            acc.x += r.x * r.x;
+            acc.y += r.y * r.y;
+        }
     }
     if ((a.n_elems & 1) && blockIdx.x == 0 && tid == 0) {
         const long long i = a.n_elems - 1;
-        a.x[i] = a.x[i] + al.x * a.p[i];
+        if (!a.lazy_x)
+            a.x[i] = a.x[i] + al.x * a.p[i];
         const double r = a.r[i] + nal.x * a.ap[i];
         a.r[i] = r;
         acc.x += r * r;
@@ -2522,6 +2590,14 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(CgVecArgs a)
             a.red_out[tid] = s_out[tid];
     } else {
         if (tid == 0) {
+            if (a.lazy_x) {  // this iteration's alpha per column (as every block formed it above,
+                             // before the masks below change), for the deferred x += alpha p
+                for (int j = 0; j < L; ++j) {
+                    const double aj = a.conv[j] ? 0.0 : a.scal[j].rs_old / a.red_in[j];
+                    a.scal[j].alpha = (aj == aj && fabs(aj) < HUGE_VAL) ? aj : 0.0;
+                }
+                a.ctrl->x_pending = 1;
+            }
             const int iter = a.ctrl->iter;
             int nconv = 0;
             double maxrel = 0.0;
@@ -2587,17 +2663,37 @@ __global__ __launch_bounds__(kBlock) void k_dist_pupdate(CgVecArgs a, double *p)
         return;
     const long long stride = (long long)gridDim.x * kBlock;
     const long long i0 = (long long)blockIdx.x * kBlock + threadIdx.x;
+    const bool lag = a.lazy_x && a.ctrl->x_pending;  // the previous update's x += alpha p (lazy_x)
     if (L == 1) {
-        const double beta = a.scal[0].beta;
-        for (long long i = i0; i < a.n_elems; i += stride)
-            p[i] = a.r[i] + beta * p[i];
+        const double beta = a.scal[0].beta, alpha = a.scal[0].alpha;
+        for (long long i = i0; i < a.n_elems; i += stride) {
+            const double q = p[i];
+            if (lag)
+                a.x[i] = a.x[i] + alpha * q;
+            p[i] = a.r[i] + beta * q;
+        }
         return;
     }
     // column pairs: the stride (in pairs) is a multiple of L/2, so a thread keeps its pair
     constexpr int GL = L > 1 ? L / 2 : 1;
     const int cp = (int)(i0 % GL);
     const double2 beta = make_double2(a.scal[2 * cp].beta, a.scal[2 * cp + 1].beta);
+    const double2 alpha = make_double2(a.scal[2 * cp].alpha, a.scal[2 * cp + 1].alpha);
     const long long npairs = a.n_elems / 2;
+    if (lag) {
+        for (long long i = i0; i < npairs; i += stride) {
+            const double2 r = reinterpret_cast<const double2 *>(a.r)[i];
+            double2 q = reinterpret_cast<double2 *>(p)[i];
+            double2 x = reinterpret_cast<double2 *>(a.x)[i];
+            x.x = x.x + alpha.x * q.x;
+            x.y = x.y + alpha.y * q.y;
+            reinterpret_cast<double2 *>(a.x)[i] = x;
+            q.x = r.x + beta.x * q.x;
+            q.y = r.y + beta.y * q.y;
+            reinterpret_cast<double2 *>(p)[i] = q;
+        }
+        return;
+    }
     for (long long i = i0; i < npairs; i += stride) {
         const double2 r = reinterpret_cast<const double2 *>(a.r)[i];
         double2 q = reinterpret_cast<double2 *>(p)[i];
@@ -2605,6 +2701,20 @@ __global__ __launch_bounds__(kBlock) void k_dist_pupdate(CgVecArgs a, double *p)
         q.y = r.y + beta.y * q.y;
         reinterpret_cast<double2 *>(p)[i] = q;
     }
+}
+
+// After the split CG's loop: the deferred x += alpha p of the last update, if no p update applied
+// it (CgVecArgs::lazy_x).  p still holds that iteration's p: the p updates after the stop return at
+// once, and a stop in the fold (every column converged or broken) follows a p update that applied
+// the term and a fold that cleared the flag.
+template <int L>
+__global__ __launch_bounds__(kBlock) void k_cg_xflush(CgVecArgs a, const double *p)
+{
+    if (!a.ctrl->x_pending)
+        return;
+    const long long stride = (long long)gridDim.x * kBlock;
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < a.n_elems; i += stride)
+        a.x[i] = a.x[i] + a.scal[L == 1 ? 0 : (int)(i % L)].alpha * p[i];
 }
 
 // ---- IC(0) preconditioner apply: sync-free sparse triangular solves ---------------------------
@@ -2963,16 +3073,40 @@ int spmm_iptg_for(int L)
     return i ? i : (L >= 8 ? 16 : 8);
 }
 
+// Resident workgroups per CU of a kBlock-thread kernel from its own resources on gfx950: 160 KiB
+// of LDS per CU, 512 VGPRs per SIMD lane (granule 8), at most 8 waves per SIMD, 4 SIMDs.
+static int gfx950_blocks_per_cu(const void *fn)
+{
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, fn) != hipSuccess)
+        return 0;
+    const int waves_per_block = kBlock / 64;
+    const int vgpr = std::max(8, (fa.numRegs + 7) & ~7);
+    const int waves_simd = std::min(8, 512 / vgpr);
+    int by_waves = 4 * waves_simd / waves_per_block;
+    int by_lds = fa.sharedSizeBytes > 0 ? (int)(160 * 1024 / fa.sharedSizeBytes) : by_waves;
+    return std::max(0, std::min(by_waves, by_lds));
+}
+
 int spmv_tile_blocks_per_cu()
 {
     static const int occ = [] {
         const SpmvTuning &t = spmv_tuning();
-        int a = 0, b = 0;
-        if (t.ipt != 8 || t.tb != kBlock || t.tile_items || t.persist ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_spmv_tile<8, kModeSpmv, false>, kBlock, 0) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_spmv_tile<8, kModeCg, false>, kBlock, 0) != hipSuccess)
+        if (const char *e = getenv("MSPMV_TILE_SLOTS_PER_CU"))  // lab knob: 0 disables the stretch
+            return std::max(0, atoi(e));
+        if (t.ipt != 8 || t.tb != kBlock || t.tile_items || t.persist)
             return 0;
-        return std::min(a, b);
+        // from the kernels' own LDS / VGPR use (MSPMV_DEBUG_SLOTS prints the runtime's occupancy
+        // query beside it); the query is the fallback when the attributes are unavailable
+        int a = 0, b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_spmv_tile<8, kModeSpmv, false>, kBlock, 0) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_spmv_tile<8, kModeCg, false>, kBlock, 0) != hipSuccess)
+            a = b = 0;
+        const int c = std::min(gfx950_blocks_per_cu((const void *)k_spmv_tile<8, kModeSpmv, false>),
+                               gfx950_blocks_per_cu((const void *)k_spmv_tile<8, kModeCg, false>));
+        if (getenv("MSPMV_DEBUG_SLOTS"))
+            fprintf(stderr, "mspmv: tile slots per CU: occupancy query %d/%d, from attributes %d\n", a, b, c);
+        return c > 0 ? c : std::min(a, b);
     }();
     return occ;
 }
@@ -3428,8 +3562,9 @@ __global__ __launch_bounds__(kBlock) void k_cg1_init(Cg1Args a)
 }
 
 // Tail of iteration k (single_strategy.hpp:140-148): alpha = rs_k / p.Ap (every block sums the
-// SpMV's partials in the same order), x += alpha p, r += (-alpha) Ap, r.r partial per block.  A
-// non-finite alpha stops the solve before x and r change (the reference keeps going on NaN).
+// SpMV's partials in the same order), r += (-alpha) Ap, r.r partial per block; x += alpha p is
+// deferred to the next SpMV (cg1_lag_*), which takes alpha from scal[0].alpha.  A non-finite
+// alpha stops the solve before r changes (the reference keeps going on NaN).
 __global__ __launch_bounds__(kBlock) void k_cg1_update(Cg1Args a)
 {
     __shared__ double s_red[kBlock / 64];
@@ -3440,11 +3575,9 @@ __global__ __launch_bounds__(kBlock) void k_cg1_update(Cg1Args a)
     part_load(a.part_in, a.n_part_in, pin);
     const long long stride = (long long)gridDim.x * kBlock;
     const long long i0 = (long long)blockIdx.x * kBlock + tid;
-    double p = 0.0, q = 0.0, x = 0.0, r = 0.0;  // the first element's operands, in flight under the sum
+    double q = 0.0, r = 0.0;  // the first element's operands, in flight under the sum
     if (i0 < a.m) {
-        p = a.rp_next[2 * i0 + 1];
         q = a.ap[i0];
-        x = a.x[i0];
         r = a.rp[2 * i0];
     }
     const double pAp = part_sum(pin, s_red);
@@ -3457,18 +3590,16 @@ __global__ __launch_bounds__(kBlock) void k_cg1_update(Cg1Args a)
         }
         return;
     }
+    if (blockIdx.x == 0 && tid == 0)
+        a.scal[0].alpha = alpha;  // x += alpha p_k: the next SpMV's rows, or k_cg1_xflush
     const double nal = -alpha;
     double acc = 0.0;
     for (long long i = i0; i < a.m; i += stride) {
         if (i != i0) {
-            p = a.rp_next[2 * i + 1];
             q = a.ap[i];
-            x = a.x[i];
             r = a.rp[2 * i];
         }
-        x = x + alpha * p;
         r = r + nal * q;
-        a.x[i] = x;
         a.rp_next[2 * i] = r;
         acc += r * r;
     }
@@ -3496,6 +3627,24 @@ __global__ __launch_bounds__(kBlock) void k_cg1_finish(Cg1Args a)
         c->iters_out = k;
         c->done = 1;
     }
+}
+
+// After the loop (converged, max_iters or breakdown): the last deferred x += alpha p.  The solve
+// reported j + 1 = iters_out iterations; the update of iteration j ran (it stored alpha_j) and no
+// SpMV after it applied its term (the stop test that ended the solve returns before that, and
+// max_iters launches none).  p_j was written into the {r, p} buffer of parity (j + 1) & 1.  A
+// breakdown (non-finite alpha_j) leaves nothing pending: the update stopped before storing alpha_j
+// and iteration j's SpMV had applied alpha_{j-1} p_{j-1} already.
+__global__ __launch_bounds__(kBlock) void k_cg1_xflush(Cg1Args a)
+{
+    const CgControl *c = a.ctrl;
+    if (c->breakdown || c->iters_out < 1)
+        return;
+    const int j = c->iters_out - 1;
+    const double *rp = ((j + 1) & 1) ? a.rp_next : a.rp;  // rp: d_p0, rp_next: d_p1
+    const double alpha = a.scal[0].alpha;
+    for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < a.m; i += (long long)gridDim.x * kBlock)
+        a.x[i] = a.x[i] + alpha * rp[2 * i + 1];
 }
 
 int cg1_blocks(long long m)
@@ -3527,13 +3676,19 @@ hipError_t launch_cg1_init(mspmv_handle_s *h, const double *d_b, double *d_x, in
     return hipGetLastError();
 }
 
-hipError_t launch_cg1_finish(mspmv_handle_s *h, int parity, int nblk)
+hipError_t launch_cg1_finish(mspmv_handle_s *h, double *d_x, int parity, int nblk)
 {
     Cg1Args a = cg1_args(h, nullptr);
     a.part_in = h->d_partials_b;
     a.n_part_in = nblk;
     a.parity = parity;
     hipLaunchKernelGGL(k_cg1_finish, dim3(1), dim3(kBlock), 0, h->stream, a);
+    if (hipGetLastError() != hipSuccess)
+        return hipErrorLaunchFailure;
+    a.x = d_x;
+    a.rp = h->d_p0;
+    a.rp_next = h->d_p1;
+    hipLaunchKernelGGL(k_cg1_xflush, dim3(nblk), dim3(kBlock), 0, h->stream, a);
     return hipGetLastError();
 }
 
@@ -3570,6 +3725,7 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
     va.hist = h->d_hist;
     va.hist_cap = h->hist_cap;
     va.tol = tol;
+    va.lazy_x = 1;
     hipError_t e = launch_dist_vec(2, va, L, nblk, h->d_p0, h->stream);
     if (e != hipSuccess)
         return e;
@@ -3578,6 +3734,25 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
         return e;
     va.red_in = h->d_red;
     return dispatch_vec(false, va, L, nblk, h->stream);
+}
+
+// After the split iteration's loop: the x += alpha p still pending (CgVecArgs::lazy_x).
+hipError_t launch_cg_xflush(mspmv_handle_s *h, double *d_x, int L, int nblk)
+{
+    CgVecArgs va{};
+    va.n_elems = (long long)h->m * L;
+    va.x = d_x;
+    va.scal = h->d_scal;
+    va.ctrl = h->d_ctrl;
+    switch (L) {
+    case 1: hipLaunchKernelGGL((k_cg_xflush<1>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
+    case 2: hipLaunchKernelGGL((k_cg_xflush<2>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
+    case 4: hipLaunchKernelGGL((k_cg_xflush<4>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
+    case 8: hipLaunchKernelGGL((k_cg_xflush<8>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
+    case 16: hipLaunchKernelGGL((k_cg_xflush<16>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
 }
 
 // Multi-RHS CG always runs the split iteration; single-RHS the pipelined one unless
@@ -3600,6 +3775,7 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *
     double *rp_new = parity ? h->d_p0 : h->d_p1;  // receives p_k, then r_{k+1}
     TileArgs ta = make_args(h, plan, rp_old, h->d_ap, 1);
     ta.p_new = rp_new;
+    ta.xsol = d_x;
     ta.scal = h->d_scal;
     ta.ctrl = h->d_ctrl;
     ta.partials = h->d_partials;
