@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -99,6 +100,14 @@ struct mspmv_dist_s {
     mspmv_handle part[3] = {nullptr, nullptr, nullptr};
     int int_lo = 0, int_hi = 0;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // x ready, mid, halo, head, tail
+    // CG: K iterations (kernels, the interior's second stream, the RCCL exchange and all-reduces)
+    // captured once into a graph and replayed per batch while the key (buffers, plans, L, tolerance,
+    // history size, K) is unchanged.  Captured only after one eager batch has run on this object,
+    // so RCCL has set up its connections outside the capture.
+    hipGraph_t cg_graph = nullptr;
+    hipGraphExec_t cg_exec = nullptr;
+    std::vector<const void *> cg_key;
+    bool cg_warm = false;
 };
 
 extern "C" {
@@ -207,6 +216,10 @@ mspmv_status mspmv_dist_destroy(mspmv_dist d)
     dfree(d->d_hist);
     if (d->h_ctrl)
         (void)hipHostFree(d->h_ctrl);
+    if (d->cg_exec)
+        (void)hipGraphExecDestroy(d->cg_exec);
+    if (d->cg_graph)
+        (void)hipGraphDestroy(d->cg_graph);
     for (auto &ph : d->part)
         if (ph)
             mspmv_destroy(ph);
@@ -725,6 +738,61 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
     };
     // batches of K iterations, the control word of batch b inspected while b+1 is queued
     const int K = cg_batch_iters(d->n_own, d->local->nnz, L);
+    static const bool use_graph = [] {
+        const char *e = getenv("MSPMV_DIST_GRAPH");
+        return !e || atoi(e) != 0;
+    }();
+    const void *tk = nullptr;
+    static_assert(sizeof(tk) == sizeof(tolerance), "tolerance bits as a key word");
+    std::memcpy(&tk, &tolerance, sizeof tk);
+    const std::vector<const void *> key = {
+        d_X_own, d->d_pext, d->d_send, d->d_r, d->d_ap, d->d_partials, d->d_gtickets, d->d_scal, d->d_conv,
+        d->d_red, d->d_ctrl, va.hist, plan, pp[0], pp[1], pp[2], tk, reinterpret_cast<const void *>((intptr_t)L),
+        reinterpret_cast<const void *>((intptr_t)nblk), reinterpret_cast<const void *>((intptr_t)cap),
+        reinterpret_cast<const void *>((intptr_t)K)};
+    // one batch: the cached graph when it matches (capturing it now if this object has run an eager
+    // batch before), else the iterations enqueued one by one
+    auto batch = [&](int k) -> mspmv_status {
+        if (use_graph && k == K && d->cg_warm && (!d->cg_exec || d->cg_key != key)) {
+            if (d->cg_exec)
+                (void)hipGraphExecDestroy(d->cg_exec);
+            if (d->cg_graph)
+                (void)hipGraphDestroy(d->cg_graph);
+            d->cg_exec = nullptr;
+            d->cg_graph = nullptr;
+            d->cg_key.clear();
+            hipError_t e = hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed);
+            mspmv_status cst = e == hipSuccess ? MSPMV_OK : MSPMV_ERR_HIP;
+            for (int i = 0; i < K && cst == MSPMV_OK; ++i)
+                cst = iteration();
+            hipGraph_t g = nullptr;
+            const hipError_t e2 = e == hipSuccess ? hipStreamEndCapture(s, &g) : e;
+            d->cg_graph = g;
+            if (cst == MSPMV_OK && e2 == hipSuccess &&
+                hipGraphInstantiate(&d->cg_exec, g, nullptr, nullptr, 0) == hipSuccess) {
+                d->cg_key = key;
+                if (getenv("MSPMV_DEBUG_GRAPH"))
+                    fprintf(stderr, "mspmv: dist CG batch of %d iterations captured (rank %d)\n", K, d->rank);
+            } else {
+                fprintf(stderr, "mspmv: dist CG batch capture failed (rank %d): batches run eagerly\n", d->rank);
+                // capture unsupported here (or failed): this object runs its batches eagerly from now on
+                if (d->cg_graph)
+                    (void)hipGraphDestroy(d->cg_graph);
+                d->cg_graph = nullptr;
+                d->cg_exec = nullptr;
+                d->cg_warm = false;
+                (void)hipGetLastError();
+                if (cst != MSPMV_OK && cst != MSPMV_ERR_HIP)
+                    return cst;
+            }
+        }
+        if (use_graph && k == K && d->cg_exec && d->cg_key == key)
+            return hipGraphLaunch(d->cg_exec, s) == hipSuccess ? MSPMV_OK
+                                                               : fail_msg(MSPMV_ERR_HIP, "dist CG: graph launch failed");
+        for (int i = 0; i < k; ++i)
+            D_ST(iteration());
+        return MSPMV_OK;
+    };
     hipEvent_t evs[2] = {nullptr, nullptr};
     D_HIP(hipEventCreateWithFlags(&evs[0], hipEventDisableTiming));
     D_HIP(hipEventCreateWithFlags(&evs[1], hipEventDisableTiming));
@@ -733,8 +801,7 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
     while (st == MSPMV_OK) {
         const int k = std::min(K, max_iters - launched);
         if (k > 0) {
-            for (int i = 0; i < k && st == MSPMV_OK; ++i)
-                st = iteration();
+            st = batch(k);
             if (st != MSPMV_OK)
                 break;
             if (hipMemcpyAsync(&d->h_ctrl[slot], d->d_ctrl, sizeof(CgControl), hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -754,6 +821,7 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
                 break;
             }
             --pending;
+            d->cg_warm = true;  // a batch has run: RCCL's connections exist, later batches may be captured
             const bool done = d->h_ctrl[oldest].done != 0;
             oldest ^= 1;
             if (done)
