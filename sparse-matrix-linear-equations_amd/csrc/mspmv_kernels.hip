@@ -1386,7 +1386,7 @@ k_spmv_tile(TileArgs a)
     const unsigned long long lab_t0 = wall_clock64();
 #endif
     // CG: stop flag loaded now, tested after the stream and gathers are issued (see k_spmm_tile)
-    const int stopped = MODE != kModeSpmv ? a.ctrl->done : 0;
+    const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
     const int t = xcd_tile(blockIdx.x, a.num_tiles);
     const int2 b0 = a.bounds[t];
     const int2 b1 = a.bounds[t + 1];
@@ -1521,7 +1521,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_blk(TileArgs a)
     constexpr bool CG = MODE == kModeCg;
     __shared__ BlkSmem sm;
     const int tid = threadIdx.x;
-    const int stopped = MODE != kModeSpmv ? a.ctrl->done : 0;
+    const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
     const int t = xcd_tile(blockIdx.x, a.num_tiles);
     const int2 b0 = a.bounds[t];
     const int colbase = a.colbase[t];
@@ -1936,7 +1936,7 @@ k_spmm_tile(TileArgs a)
     // CG: the stop flag is loaded now and tested once the tile's stream is in flight, so the
     // flag's round trip does not delay every workgroup's first load (MODE 2 writes only the
     // scratch Ap and partials: a stopped solve only needs the work skipped, not fenced)
-    const int stopped = MODE != kModeSpmv ? a.ctrl->done : 0;
+    const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
     const int t = xcd_tile(blockIdx.x, a.num_tiles);
     const int2 b0 = a.bounds[t];
     const int2 b1 = a.bounds[t + 1];
@@ -2174,8 +2174,14 @@ __device__ __forceinline__ double2 rows8_sum2(const double2 (&p)[kBlkRows])
     return v;
 }
 
+// Waves per SIMD k_spmm_blk is compiled for (0: unconstrained, 96 VGPRs at L = 16 -> 5 waves);
+// a lab build can ask for more (-DMSPMV_SPMM_BLK_WAVES=6 or 7).
+#ifndef MSPMV_SPMM_BLK_WAVES
+#define MSPMV_SPMM_BLK_WAVES 0
+#endif
 template <int L, int MODE, bool NT>
-__global__ __launch_bounds__(kBlock) void k_spmm_blk(TileArgs a)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MSPMV_SPMM_BLK_WAVES > 0 ? MSPMV_SPMM_BLK_WAVES : 1))) void
+k_spmm_blk(TileArgs a)
 {
     static_assert(MODE != kModeCg, "multi-RHS CG runs the split iteration (MODE 2)");
     constexpr int GL = L / 2;      // lanes per panel row
@@ -2188,7 +2194,7 @@ __global__ __launch_bounds__(kBlock) void k_spmm_blk(TileArgs a)
     // VGPRs before the per-row pass skips, no faster at 96: the kernel waits on memory)
     constexpr int PB = MSPMV_SPMM_BLK_PB;
     __shared__ double2 s_red2[MODE == kModeDot ? kBlock / 64 : 1][GL];
-    const int stopped = MODE != kModeSpmv ? a.ctrl->done : 0;
+    const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
     const int tid = threadIdx.x, lane = tid & 63;
     const int g = lane / GL, c = lane % GL;
     const int t = xcd_tile(blockIdx.x, a.num_tiles);
@@ -2293,6 +2299,42 @@ constexpr unsigned char kConvBroken = 2;
 // What the fold's last block derives from the totals (k_fold_dot `mode`).
 enum : int { kFoldDot = 0, kFoldCgAlpha = 1, kFoldPcgAlpha = 2, kFoldPcgBeta = 3, kFoldPcgInit = 4 };
 
+// Split CG, after p.Ap of column j is known (one thread per column): the per-column breakdown
+// (no_pretreatment.hpp:109-120 has no guard: a zero RHS column gives alpha = 0/0 and a NaN column
+// that never converges).  The column is frozen (conv = kConvBroken: alpha = beta = 0 from here on,
+// x and r keep their last finite values, left out of the max-error history as the reference's NaN
+// is) and the other columns keep iterating.
+__device__ __forceinline__ void cg_alpha_column(int j, double pAp, const CgScalars *scal, const unsigned char *conv,
+                                                CgControl *ctrl)
+{
+    if (conv[j])
+        return;
+    const double alpha = scal[j].rs_old / pAp;
+    if (!(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
+        const_cast<unsigned char *>(conv)[j] = kConvBroken;
+        ctrl->breakdown = 1;
+    }
+}
+
+// ... then (after a barrier, thread 0): the deferred x term was applied by the p update before
+// this reduction (CgVecArgs::lazy_x), and every column converged or broken stops the solve here.
+template <int L>
+__device__ __forceinline__ void cg_alpha_finish(const unsigned char *conv, CgControl *ctrl)
+{
+    if (threadIdx.x != 0)
+        return;
+    ctrl->x_pending = 0;
+    if (ctrl->breakdown) {
+        int live = 0;
+        for (int j = 0; j < L; ++j)
+            live += conv[j] == 0;
+        if (live == 0) {
+            ctrl->done = 1;
+            ctrl->iters_out = ctrl->iter + 1;
+        }
+    }
+}
+
 // x.(A x) per column from the tile kernels' MODE 2 partials [T][L], in a fixed order: block g
 // folds tiles [g*q, g*q + q) (fold_cols), reduce_slots folds the block sums and its last block
 // writes dot_out.  The tile kernels thus end without any ticket or store drain (a ticket per
@@ -2321,17 +2363,8 @@ __global__ __launch_bounds__(kBlock) void k_fold_dot(const double *part, int T, 
     if (tid < L) {
         const double d = s_out[tid];
         dot_out[tid] = d;
-        if (mode == kFoldCgAlpha && !conv[tid]) {
-            // Per-column breakdown (no_pretreatment.hpp:109-120 has no guard: a zero RHS column
-            // gives alpha = 0/0 and a NaN column that never converges).  The column is frozen
-            // (conv = kConvBroken: alpha = beta = 0 from here on, x and r keep their last finite
-            // values, left out of the max-error history as the reference's NaN is) and the
-            // other columns keep iterating.
-            const double alpha = scal[tid].rs_old / d;
-            if (!(alpha == alpha && fabs(alpha) < HUGE_VAL)) {
-                const_cast<unsigned char *>(conv)[tid] = kConvBroken;
-                ctrl->breakdown = 1;
-            }
+        if (mode == kFoldCgAlpha) {
+            cg_alpha_column(tid, d, scal, conv, ctrl);
         } else if (mode == kFoldPcgAlpha) {  // sparse_approximate_inverse.hpp:131-138
             CgScalars &s = scal[tid];
             s.pAp = d;
@@ -2346,17 +2379,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_dot(const double *part, int T, 
     }
     if (mode == kFoldCgAlpha) {
         __syncthreads();
-        if (tid == 0)
-            ctrl->x_pending = 0;  // the p update before this fold applied the deferred x term
-        if (tid == 0 && ctrl->breakdown) {  // every column converged or broken: stop here
-            int live = 0;
-            for (int j = 0; j < L; ++j)
-                live += conv[j] == 0;
-            if (live == 0) {
-                ctrl->done = 1;
-                ctrl->iters_out = ctrl->iter + 1;
-            }
-        }
+        cg_alpha_finish<L>(conv, ctrl);
     }
 }
 
@@ -2860,6 +2883,8 @@ __global__ __launch_bounds__(kBlock) void k_trsv_tagged(const int *__restrict__ 
 
 // R.Z per column and the PCG scalars after it (PCGSolveMultiple): mode 0 (init, :96-104)
 // rs_old = R.Z; mode 1 (:171-185) beta = converged ? 0 : R.Z / rs_old, rs_old = R.Z.
+// Mode 2 (split CG with a plain SpMM, cg_dot_pass): p.Ap per column into red_out, then the
+// breakdown checks k_fold_dot makes in kFoldCgAlpha mode.
 template <int L>
 __global__ __launch_bounds__(kBlock) void k_pcg_dot(CgVecArgs a, int mode)
 {
@@ -2885,6 +2910,15 @@ __global__ __launch_bounds__(kBlock) void k_pcg_dot(CgVecArgs a, int mode)
     colpair_block_reduce<L>(acc, s_red2, a.partials + (size_t)blockIdx.x * L);
     if (!reduce_slots<L>(a.partials, a.gtickets, blockIdx.x, gridDim.x, s_colred, s_out, &s_last))
         return;
+    if (mode == 2) {  // split CG: p.Ap (a.r = p, a.p = Ap) -> red_out, breakdown per column
+        if (tid < L) {
+            a.red_out[tid] = s_out[tid];
+            cg_alpha_column(tid, s_out[tid], a.scal, a.conv, a.ctrl);
+        }
+        __syncthreads();
+        cg_alpha_finish<L>(a.conv, a.ctrl);
+        return;
+    }
     if (tid < L) {
         CgScalars &s = a.scal[tid];
         const double d = s_out[tid];
@@ -3708,6 +3742,19 @@ static hipError_t launch_fixup_ctrl(mspmv_handle_s *h, const TilePlan &plan, dou
 // that p.Ap.  For L >= 2 the fused iteration would gather two L-wide panel rows (r and
 // p_old) per nonzero, and the SpMM is gather-bound: measured 1.33 ms vs 0.62 + 0.14 ms split
 // on the nlpkkt120-sized L = 8 case.
+static hipError_t pcg_dot(const CgVecArgs &va, int L, int nblk, int mode, hipStream_t s);
+
+// Split CG: p.Ap from the SpMM's dot mode (x.(Ax) partials per tile) or from a separate pass over
+// p and Ap after the plain SpMM (MSPMV_CG_DOT=pass / fused; default: the pass).
+static bool cg_dot_pass(int L)
+{
+    static const int mode = [] {
+        const char *e = getenv("MSPMV_CG_DOT");
+        return e && std::string(e) == "fused" ? 0 : 1;
+    }();
+    return mode != 0 && L >= 1;
+}
+
 static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &plan, double *d_x, int L, int nblk,
                                             double tol)
 {
@@ -3729,9 +3776,26 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
     hipError_t e = launch_dist_vec(2, va, L, nblk, h->d_p0, h->stream);
     if (e != hipSuccess)
         return e;
-    if ((e = launch_spmm_dot(h, plan, h->d_p0, h->d_ap, L, h->d_ctrl, h->d_partials, h->d_gtickets, h->d_red,
-                             h->d_scal, h->d_conv)) != hipSuccess)
+    if (cg_dot_pass(L)) {
+        // the plain SpMM (its tile kernel holds fewer registers than the dot mode's, so more
+        // workgroups per CU, and never spills), stopped by the control word, then p.Ap in one
+        // streaming pass over p and Ap with the fold's breakdown checks (k_pcg_dot mode 2)
+        TileArgs ta = make_args(h, plan, h->d_p0, h->d_ap, L);
+        ta.ctrl = h->d_ctrl;
+        if ((e = launch_tile<kModeSpmv>(ta, L, h->stream, h->num_cus, stream_nt(h))) != hipSuccess)
+            return e;
+        if ((e = launch_fixup_ctrl(h, plan, h->d_ap, L)) != hipSuccess)
+            return e;
+        CgVecArgs vd = va;
+        vd.r = h->d_p0;
+        vd.p = h->d_ap;
+        vd.red_out = h->d_red;
+        if ((e = pcg_dot(vd, L, nblk, 2, h->stream)) != hipSuccess)
+            return e;
+    } else if ((e = launch_spmm_dot(h, plan, h->d_p0, h->d_ap, L, h->d_ctrl, h->d_partials, h->d_gtickets, h->d_red,
+                                    h->d_scal, h->d_conv)) != hipSuccess) {
         return e;
+    }
     va.red_in = h->d_red;
     return dispatch_vec(false, va, L, nblk, h->stream);
 }
