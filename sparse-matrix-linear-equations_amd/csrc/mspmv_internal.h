@@ -258,6 +258,8 @@ struct DistVecArgs {
     double *red_out;
     unsigned *gtickets;
     int pcg;
+    int lazy_x;  // (single-GPU split CG only: 0 here)
+    int rev;
 };
 // which: 0 init partial sums (b.b -> red_out), 1 init finish (red_in = all-reduced b.b),
 // 2 p update, 3 x/r update (alpha from red_in = all-reduced p.Ap; r.r -> red_out),

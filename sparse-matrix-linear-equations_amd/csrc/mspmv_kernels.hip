@@ -2473,7 +2473,18 @@ struct CgVecArgs {
     // k_dist_pupdate applies the term; the fold after it clears the flag; k_cg_xflush applies the
     // term still pending when the solve ends.  Same expression x + alpha p: bit-identical x.
     int lazy_x;
+    // Streaming passes of the split CG sweep their chunks of gridDim x kBlock elements last to
+    // first (rev = 1) or first to last, alternately, so a pass starts on the lines the previous
+    // pass touched last -- still in the 256 MiB Infinity Cache (every lane keeps its column pair).
+    int rev;
 };
+
+// Chunk c (of kBlock x gridDim elements, element i = c * stride + i0) visited at step k: first to
+// last, or last to first (CgVecArgs::rev).
+__device__ __forceinline__ long long sweep_index(long long k, long long nchunks, long long stride, long long i0, int rev)
+{
+    return (rev ? nchunks - 1 - k : k) * stride + i0;
+}
 
 // x = 0, r = p0 = b; rs_old_j = r_j.r_j, b_norm_j = sqrt(b_j.b_j) (no_pretreatment.hpp:61-79,
 // single_strategy.hpp:120-131).
@@ -2704,7 +2715,11 @@ __global__ __launch_bounds__(kBlock) void k_dist_pupdate(CgVecArgs a, double *p)
     const double2 alpha = make_double2(a.scal[2 * cp].alpha, a.scal[2 * cp + 1].alpha);
     const long long npairs = a.n_elems / 2;
     if (lag) {
-        for (long long i = i0; i < npairs; i += stride) {
+        const long long nch = (npairs + stride - 1) / stride;
+        for (long long k = 0; k < nch; ++k) {
+            const long long i = sweep_index(k, nch, stride, i0, a.rev);
+            if (i >= npairs)
+                continue;
             const double2 r = reinterpret_cast<const double2 *>(a.r)[i];
             double2 q = reinterpret_cast<double2 *>(p)[i];
             double2 x = reinterpret_cast<double2 *>(a.x)[i];
@@ -2898,8 +2913,13 @@ __global__ __launch_bounds__(kBlock) void k_pcg_dot(CgVecArgs a, int mode)
         return;
     const long long npairs = a.n_elems / 2;
     const long long stride = (long long)gridDim.x * kBlock;
+    const long long i0 = (long long)blockIdx.x * kBlock + tid;
+    const long long nch = (npairs + stride - 1) / stride;
     double2 acc = make_double2(0.0, 0.0);
-    for (long long i = (long long)blockIdx.x * kBlock + tid; i < npairs; i += stride) {
+    for (long long k = 0; k < nch; ++k) {
+        const long long i = sweep_index(k, nch, stride, i0, a.rev);
+        if (i >= npairs)
+            continue;
         const double2 r = reinterpret_cast<const double2 *>(a.r)[i];
         const double2 z = reinterpret_cast<const double2 *>(a.p)[i];
         acc.x += r.x * z.x;
@@ -3773,7 +3793,13 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
     va.hist_cap = h->hist_cap;
     va.tol = tol;
     va.lazy_x = 1;
+    static const int rev = [] {  // measured knob: alternate sweep directions (CgVecArgs::rev)
+        const char *e = getenv("MSPMV_CG_REV");
+        return e ? atoi(e) : 1;
+    }();
+    va.rev = rev;  // the p update (after the forward update) sweeps backwards
     hipError_t e = launch_dist_vec(2, va, L, nblk, h->d_p0, h->stream);
+    va.rev = 0;
     if (e != hipSuccess)
         return e;
     if (cg_dot_pass(L)) {
@@ -3790,6 +3816,7 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
         vd.r = h->d_p0;
         vd.p = h->d_ap;
         vd.red_out = h->d_red;
+        vd.rev = rev;  // ... the p.Ap pass backwards, so the update finds Ap's first lines cached
         if ((e = pcg_dot(vd, L, nblk, 2, h->stream)) != hipSuccess)
             return e;
     } else if ((e = launch_spmm_dot(h, plan, h->d_p0, h->d_ap, L, h->d_ctrl, h->d_partials, h->d_gtickets, h->d_red,
