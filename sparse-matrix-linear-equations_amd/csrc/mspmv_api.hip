@@ -163,16 +163,20 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
     const long long total = (long long)h->m + h->nnz;
     int step = tile, snap = tile / kSnapDiv;
     if (tile == tile_items_for(1)) {
-        // A grid a few tiles over one resident generation of workgroups takes two tile lifetimes
-        // (the parabolic_fem shape: 2,052 tiles on 2,048 slots).  Stretch the tiles into the
-        // snap slack so they fit one generation: MAXI (step + snap) is unchanged, rows entered by
-        // more than the smaller snap distance stay split (carries, k_fixup).
+        // A grid a few tiles over a whole number of resident generations of workgroups takes one
+        // tile lifetime more (the parabolic_fem shape: 2,052 tiles on 2,048 slots).  Stretch the
+        // tiles into the snap slack so they fit one generation fewer: MAXI (step + snap) is
+        // unchanged, rows entered by more than the smaller snap distance stay split (carries,
+        // k_fixup).
         const long long slots = (long long)h->num_cus * spmv_tile_blocks_per_cu();
         const long long t0 = (total + tile - 1) / tile;
-        const long long fit = slots > 0 ? (total + slots - 1) / slots : 0;
-        if (slots > 0 && t0 > slots && fit + 16 <= tile + tile / kSnapDiv) {
-            step = (int)fit;
-            snap = tile + tile / kSnapDiv - step;  // >= 16
+        if (slots > 0 && t0 > slots) {
+            const long long fewer = (t0 + slots - 1) / slots - 1;  // generations after stretching
+            const long long fit = (total + fewer * slots - 1) / (fewer * slots);
+            if (fit + 16 <= tile + tile / kSnapDiv) {
+                step = (int)fit;
+                snap = tile + tile / kSnapDiv - step;  // >= 16
+            }
         }
     }
     p.tile_items = step;

@@ -1372,7 +1372,10 @@ __device__ unsigned long long g_lab_stamps[kLabStampTiles * 6];
 #endif
 constexpr int spmv_tile_waves(int mode) { return mode == 1 && MSPMV_CG_WAVES > 0 ? MSPMV_CG_WAVES : 1; }
 
-template <int IPT, int MODE, bool NT, int TB = kBlock>
+// BLK = false: the plan has no node-block tiles (a.blk null), and the kernel is compiled without
+// their staging paths -- the pipelined CG's form then needs far fewer registers (their run arrays
+// set its VGPR count, so more workgroups fit per CU).
+template <int IPT, int MODE, bool NT, int TB = kBlock, bool BLK = true>
 __global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(spmv_tile_waves(MODE)))) void
 k_spmv_tile(TileArgs a)
 {
@@ -1412,13 +1415,13 @@ k_spmv_tile(TileArgs a)
     const int colbase = a.cols16 ? a.colbase[t] : -1;
     // node-block descriptors of this tile, loaded beside its bounds (entry 0 holds the count)
     uint4 bd = make_uint4(0u, 0u, 0u, 0u);
-    if (a.blk && (tid & 63) < a.blk_stride)
+    if (BLK && a.blk && (tid & 63) < a.blk_stride)
         bd = a.blk[(size_t)t * a.blk_stride + (tid & 63)];
-    const int nblk = a.blk ? (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u) : 0;
+    const int nblk = (BLK && a.blk) ? (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u) : 0;
     bool staged = false;
     // every run one chunk wide (block-uniform: each wave holds all descriptors): no LDS at all
-    const bool blk_reg = nblk > 0 && __ballot((tid & 63) < nblk && ((bd.x >> 16) & 255u) != 0) == 0;
-    if (blk_reg) {
+    const bool blk_reg = BLK && nblk > 0 && __ballot((tid & 63) < nblk && ((bd.x >> 16) & 255u) != 0) == 0;
+    if constexpr (BLK) if (blk_reg) {
         double dot = 0.0;
         blk_rows<MODE, NT, TB>(a, bd, nblk, r0, n0, colbase, beta, dot, [&]() {
             head();
@@ -1434,7 +1437,7 @@ k_spmv_tile(TileArgs a)
         }
         return;
     }
-    if (nblk > 0) {
+    if (BLK && nblk > 0) {
         blk_stage<CG, NT, TB>(a, bd, nblk, n0, colbase, sm.prod, beta, [&]() {
             head();
             return go;
@@ -2187,12 +2190,14 @@ k_spmm_blk(TileArgs a)
     constexpr int GL = L / 2;      // lanes per panel row
     constexpr int NGW = 64 / GL;   // column groups per wave = pattern columns per pass
 #ifndef MSPMV_SPMM_BLK_PB
-#define MSPMV_SPMM_BLK_PB 4
+#define MSPMV_SPMM_BLK_PB 0
 #endif
-    // passes whose gathers are in flight together (measured on the pwtk shape, L = 16: 2 and 8
-    // slower than 4; fused multiply-adds instead of the guarded mul + add, also slower, 96 -> 128
-    // VGPRs before the per-row pass skips, no faster at 96: the kernel waits on memory)
-    constexpr int PB = MSPMV_SPMM_BLK_PB;
+    // passes whose gathers are in flight together (measured on the pwtk shape: L = 16, 2 and 8
+    // slower than 4; L = 8 and 4, 2 faster than 4: 66.4 -> 60.2 and 50.0 -> 48.0 us, r02z; fused
+    // multiply-adds instead of the guarded mul + add, also slower, 96 -> 128 VGPRs before the
+    // per-row pass skips, no faster at 96: the kernel waits on memory; 6 waves per SIMD instead of
+    // 5, forced, no faster either: 82.4 vs 82.6 us at L = 16)
+    constexpr int PB = MSPMV_SPMM_BLK_PB > 0 ? MSPMV_SPMM_BLK_PB : (L >= 16 ? 4 : 2);
     __shared__ double2 s_red2[MODE == kModeDot ? kBlock / 64 : 1][GL];
     const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
     const int tid = threadIdx.x, lane = tid & 63;
@@ -3142,25 +3147,39 @@ static int gfx950_blocks_per_cu(const void *fn)
     return std::max(0, std::min(by_waves, by_lds));
 }
 
+// Slots of the striped single-RHS tile kernels at IPT items per thread: the SpMV and the pipelined
+// CG (its form without node blocks; FEM plans run the node-block kernels, whose tile counts are
+// not near a generation boundary), from the kernels' own LDS / VGPR use (MSPMV_DEBUG_SLOTS prints
+// the runtime's occupancy query beside it; the query is the fallback without attributes).
+template <int I>
+static int tile_slots_per_cu()
+{
+    const void *ks = (const void *)k_spmv_tile<I, kModeSpmv, false>;
+    const void *kc = (const void *)k_spmv_tile<I, kModeCg, false, kBlock, false>;
+    int a = 0, b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_spmv_tile<I, kModeSpmv, false>, kBlock, 0) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_spmv_tile<I, kModeCg, false, kBlock, false>, kBlock, 0) !=
+            hipSuccess)
+        a = b = 0;
+    const int c = std::min(gfx950_blocks_per_cu(ks), gfx950_blocks_per_cu(kc));
+    if (getenv("MSPMV_DEBUG_SLOTS"))
+        fprintf(stderr, "mspmv: tile slots per CU (IPT %d): occupancy query %d/%d, from attributes %d\n", I, a, b, c);
+    return c > 0 ? c : std::min(a, b);
+}
+
 int spmv_tile_blocks_per_cu()
 {
     static const int occ = [] {
         const SpmvTuning &t = spmv_tuning();
         if (const char *e = getenv("MSPMV_TILE_SLOTS_PER_CU"))  // lab knob: 0 disables the stretch
             return std::max(0, atoi(e));
-        if (t.ipt != 8 || t.tb != kBlock || t.tile_items || t.persist)
+        if (t.tb != kBlock || t.tile_items || t.persist)
             return 0;
-        // from the kernels' own LDS / VGPR use (MSPMV_DEBUG_SLOTS prints the runtime's occupancy
-        // query beside it); the query is the fallback when the attributes are unavailable
-        int a = 0, b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_spmv_tile<8, kModeSpmv, false>, kBlock, 0) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_spmv_tile<8, kModeCg, false>, kBlock, 0) != hipSuccess)
-            a = b = 0;
-        const int c = std::min(gfx950_blocks_per_cu((const void *)k_spmv_tile<8, kModeSpmv, false>),
-                               gfx950_blocks_per_cu((const void *)k_spmv_tile<8, kModeCg, false>));
-        if (getenv("MSPMV_DEBUG_SLOTS"))
-            fprintf(stderr, "mspmv: tile slots per CU: occupancy query %d/%d, from attributes %d\n", a, b, c);
-        return c > 0 ? c : std::min(a, b);
+        switch (t.ipt) {
+        case 4: return tile_slots_per_cu<4>();
+        case 8: return tile_slots_per_cu<8>();
+        default: return 0;
+        }
     }();
     return occ;
 }
@@ -3415,6 +3434,11 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_c
                 hipLaunchKernelGGL((k_spmv_tile<I, kModeSpmv, true, 64>), grid, dim3(64), 0, s, a);   \
             else                                                                                   \
                 hipLaunchKernelGGL((k_spmv_tile<I, kModeSpmv, false, 64>), grid, dim3(64), 0, s, a);  \
+        } else if (MODE == kModeCg && !a.blk) {                                                    \
+            if (nt)                                                                                \
+                hipLaunchKernelGGL((k_spmv_tile<I, MODE, true, kBlock, false>), grid, block, 0, s, a); \
+            else                                                                                   \
+                hipLaunchKernelGGL((k_spmv_tile<I, MODE, false, kBlock, false>), grid, block, 0, s, a); \
         } else if (nt)                                                                             \
             hipLaunchKernelGGL((k_spmv_tile<I, MODE, true>), grid, block, 0, s, a);                   \
         else                                                                                       \
