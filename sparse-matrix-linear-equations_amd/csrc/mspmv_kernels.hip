@@ -19,6 +19,7 @@
 #include "mspmv_internal.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1855,25 +1856,31 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
                 acc.y += v[u] * xv[u].y;
             }
         }
-        for (; k + 3 * Gp < e; k += 4 * Gp) {
-            const int c0 = s_col[k], c1 = s_col[k + Gp], c2 = s_col[k + 2 * Gp], c3 = s_col[k + 3 * Gp];
-            const double v0 = s_val[k], v1 = s_val[k + Gp], v2 = s_val[k + 2 * Gp], v3 = s_val[k + 3 * Gp];
-            const double2 x0 = panel(c0), x1 = panel(c1), x2 = panel(c2), x3 = panel(c3);
-            acc.x += v0 * x0.x;
-            acc.y += v0 * x0.y;
-            acc.x += v1 * x1.x;
-            acc.y += v1 * x1.y;
-            acc.x += v2 * x2.x;
-            acc.y += v2 * x2.y;
-            acc.x += v3 * x3.x;
-            acc.y += v3 * x3.y;
-        }
-        for (; k < e; k += Gp) {
-            const double v = s_val[k];
-            const double2 xv = panel(s_col[k]);
-            acc.x += v * xv.x;
-            acc.y += v * xv.y;
-        }
+        // the rest (< 8 per lane) as ONE batch, not a chain of single round trips: indices past
+        // the row clamp to its last nonzero and their products are skipped by a select (acc
+        // starts at +0.0 and never becomes -0.0, so adding +0.0 instead is the identity: the
+        // sums stay bit-identical)
+        auto rest = [&](auto nb) {
+            constexpr int NB = decltype(nb)::value;
+            double v[NB];
+            double2 xv[NB];
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+                const int kk = min(k + u * Gp, e - 1);
+                v[u] = s_val[kk];
+                xv[u] = panel(s_col[kk]);
+            }
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+                const bool on = k + u * Gp < e;
+                acc.x += on ? v[u] * xv[u].x : 0.0;
+                acc.y += on ? v[u] * xv[u].y : 0.0;
+            }
+        };
+        if (k + 3 * Gp < e)
+            rest(std::integral_constant<int, 8>{});
+        else if (k < e)
+            rest(std::integral_constant<int, 4>{});
         for (int off = Gp >> 1; off > 0; off >>= 1) {
             acc.x += __shfl_xor(acc.x, off * GL);
             acc.y += __shfl_xor(acc.y, off * GL);
