@@ -572,7 +572,7 @@ __global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *_
 // reads plus an 11-step search and two barriers for SpMV, IPTG/4 gather chunks for SpMM).
 __global__ void k_tile_modes(const int *__restrict__ row_offsets, const int2 *__restrict__ bounds,
                              const unsigned char *__restrict__ split, int num_tiles, int gl, int max_cost,
-                             int lanes, unsigned char *__restrict__ modes)
+                             int lanes, unsigned char *__restrict__ modes, int force_lg)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= num_tiles)
@@ -601,6 +601,10 @@ __global__ void k_tile_modes(const int *__restrict__ row_offsets, const int2 *__
             best_cost = cost;
             best = lg + 1;
         }
+    }
+    if (force_lg >= 0 && (gl << force_lg) <= 64) {  // lab knob (MSPMV_SPMM_LG): one group size for every tile
+        best = force_lg + 1;
+        best_cost = 0;
     }
     modes[t] = best_cost <= max_cost ? (unsigned char)best : (unsigned char)0;
 }
@@ -3281,8 +3285,12 @@ hipError_t launch_tile_modes(const int *d_row_offsets, const int2 *d_bounds, con
     // SpMM budget: twice the walk's gather chunks (4 steps each) plus its search
     const int cost = L == 1 ? tu.rg_cost : tu.spmm_rg_cost >= 0 ? tu.spmm_rg_cost : 2 * (4 * (spmm_iptg_for(L) / 4) + 2);
     const int lanes = L == 1 ? tu.tb : kBlock;  // threads sharing one tile
+    static const int force_lg = [] {
+        const char *e = getenv("MSPMV_SPMM_LG");
+        return e ? atoi(e) : -1;
+    }();
     hipLaunchKernelGGL(k_tile_modes, dim3((num_tiles + 255) / 256), dim3(256), 0, s, d_row_offsets, d_bounds, d_split,
-                       num_tiles, L == 1 ? 1 : L / 2, cost, lanes, d_modes);
+                       num_tiles, L == 1 ? 1 : L / 2, cost, lanes, d_modes, L == 1 ? -1 : force_lg);
     return hipGetLastError();
 }
 
