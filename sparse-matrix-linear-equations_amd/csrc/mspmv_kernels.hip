@@ -3742,8 +3742,14 @@ __global__ __launch_bounds__(kBlock) void k_cg1_xflush(Cg1Args a)
 
 int cg1_blocks(long long m)
 {
+    static const int cap = [] {  // lab knob: fewer update blocks (fewer r.r partials for every SpMV
+                                 // workgroup to load and sum, fewer p.Ap partial loads per block)
+        const char *e = getenv("MSPMV_CG1_BLOCKS");
+        const int v = e ? atoi(e) : 0;
+        return v > 0 && v <= kUpdateMaxBlocks ? v : kUpdateMaxBlocks;
+    }();
     const long long b = (m + kBlock - 1) / kBlock;  // one element per thread up to the cap
-    return (int)std::max<long long>(1, std::min<long long>(b, kUpdateMaxBlocks));
+    return (int)std::max<long long>(1, std::min<long long>(b, cap));
 }
 
 static Cg1Args cg1_args(mspmv_handle_s *h, double *d_x)
