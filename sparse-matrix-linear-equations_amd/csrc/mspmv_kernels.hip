@@ -2210,6 +2210,15 @@ k_spmm_blk(TileArgs a)
     // 5, forced, no faster either: 82.4 vs 82.6 us at L = 16)
     constexpr int PB = MSPMV_SPMM_BLK_PB > 0 ? MSPMV_SPMM_BLK_PB : (L >= 16 ? 4 : 2);
     __shared__ double2 s_red2[MODE == kModeDot ? kBlock / 64 : 1][GL];
+#ifndef MSPMV_SPMM_BLK_LDSV
+#define MSPMV_SPMM_BLK_LDSV 1
+#endif
+    // LDSV: each wave parks its run's values (row-major, [row][column]) and pattern columns in its
+    // own LDS slice, and a pass reads v[i][j] there (one broadcast read per (pass, row)) instead of
+    // holding the rows in registers and shuffling them (two bpermutes per (pass, row))
+    constexpr bool LDSV = MSPMV_SPMM_BLK_LDSV != 0;
+    __shared__ double s_v[LDSV ? kBlock / 64 : 1][LDSV ? kBlkRows : 1][64];
+    __shared__ int s_c[LDSV ? kBlock / 64 : 1][64];
     const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
     const int tid = threadIdx.x, lane = tid & 63;
     const int g = lane / GL, c = lane % GL;
@@ -2239,6 +2248,14 @@ k_spmm_blk(TileArgs a)
 #pragma unroll
         for (int i = 0; i < kBlkRows; ++i)
             vrow[i] = (i < h && lane < blk_len(d, i)) ? ld_stream<NT>(a.vals + n0 + vofs + start[i] + lane) : 0.0;
+        if constexpr (LDSV) {  // wave-private slice: the wave's LDS operations stay in order
+            s_c[wave][lane] = colj;
+#pragma unroll
+            for (int i = 0; i < kBlkRows; ++i)
+                if (i < h)
+                    s_v[wave][i][lane] = vrow[i];
+            __builtin_amdgcn_wave_barrier();
+        }
         const int ri = lane >> 3;  // the run row this lane's slot stores
         const bool store = (lane & 7) < GL && ri < h;
         double2 xx = make_double2(0.0, 0.0);  // dot mode: the stored row's own x, issued early
@@ -2253,7 +2270,7 @@ k_spmm_blk(TileArgs a)
 #pragma unroll
             for (int q = 0; q < PB; ++q) {
                 const int j = (pb + q) * NGW + g;
-                const int cq = __shfl(colj, j & 63);
+                const int cq = LDSV ? s_c[wave][j & 63] : __shfl(colj, j & 63);
                 xv[q] = j < wc ? *reinterpret_cast<const double2 *>(a.x + (size_t)cq * a.ld + 2 * c)
                                : make_double2(0.0, 0.0);
             }
@@ -2266,7 +2283,7 @@ k_spmm_blk(TileArgs a)
                     const int len = blk_len(d, i);
                     if (i >= h || jb >= len)  // wave-uniform: row i has no column in this pass
                         continue;
-                    const double v = __shfl(vrow[i], j & 63);
+                    const double v = LDSV ? s_v[wave][i][j & 63] : __shfl(vrow[i], j & 63);
                     const bool on = j < len;
                     acc[i].x += on ? v * xv[q].x : 0.0;
                     acc[i].y += on ? v * xv[q].y : 0.0;
