@@ -2203,12 +2203,11 @@ k_spmm_blk(TileArgs a)
 #ifndef MSPMV_SPMM_BLK_PB
 #define MSPMV_SPMM_BLK_PB 0
 #endif
-    // passes whose gathers are in flight together (measured on the pwtk shape: L = 16, 2 and 8
-    // slower than 4; L = 8 and 4, 2 faster than 4: 66.4 -> 60.2 and 50.0 -> 48.0 us, r02z; fused
-    // multiply-adds instead of the guarded mul + add, also slower, 96 -> 128 VGPRs before the
-    // per-row pass skips, no faster at 96: the kernel waits on memory; 6 waves per SIMD instead of
-    // 5, forced, no faster either: 82.4 vs 82.6 us at L = 16)
-    constexpr int PB = MSPMV_SPMM_BLK_PB > 0 ? MSPMV_SPMM_BLK_PB : (L >= 16 ? 4 : 2);
+    // passes whose gathers are in flight together, measured on the pwtk shape: with the values in
+    // registers (before LDSV) 4 was best at L = 16 and 2 at L = 4, 8 (r02z); with LDSV 2 is best at
+    // every width (L = 16: 72.4-73.1 vs 74.4-74.8 us at 4 and 89.4 at 8; L = 4: 40-41 vs 50-51 and
+    // 65 us; r02ah).  Fused multiply-adds instead of the guarded mul + add measured slower.
+    constexpr int PB = MSPMV_SPMM_BLK_PB > 0 ? MSPMV_SPMM_BLK_PB : 2;
     __shared__ double2 s_red2[MODE == kModeDot ? kBlock / 64 : 1][GL];
 #ifndef MSPMV_SPMM_BLK_LDSV
 #define MSPMV_SPMM_BLK_LDSV 1
