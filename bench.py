@@ -55,7 +55,13 @@ def pmc_traffic(kernel, bytes_launch):
     --pmc FETCH_SIZE / WRITE_SIZE passes of this same bench command), or None when no summary
     matches this kernel instantiation and workload size."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
+    import re
+
+    def tag_order(path):  # r01 < r01z < r02 < r02t < r02aa < r02ai: round, then session letters
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), key=tag_order, reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
