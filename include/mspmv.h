@@ -222,6 +222,11 @@ MSPMV_API mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, do
 MSPMV_API mspmv_status mspmv_time_spmm_batch_dev(int count, const mspmv_handle *hs, const double *const *d_X,
                                                  double *const *d_Y, int L, int reps, double *step_ms,
                                                  double *tile_kernel_ms, int *kernels_per_step);
+/* The practical HBM ceiling the roofline fraction is read against: a STREAM-like
+ * nontemporal read of a `bytes` buffer (>= 1 MiB; use >> 256 MiB so the Infinity Cache cannot hold
+ * it) on `device`, `reps` timed passes after one warm-up, HIP events around the timed region.
+ * *gbps = bytes x reps / time. */
+MSPMV_API mspmv_status mspmv_time_stream_read(int device, size_t bytes, int reps, double *gbps);
 /* Per-kernel average duration (ms) of the dominant (merge tile) kernel over the last
  * mspmv_time_spmm_dev call, and the number of kernels per SpMV/SpMM call. */
 MSPMV_API mspmv_status mspmv_last_kernel_ms(mspmv_handle h, double *tile_kernel_ms, int *kernels_per_call);

@@ -1352,6 +1352,53 @@ mspmv_status mspmv_dpcg_ic0_multi(mspmv_handle a, mspmv_ic0 m, const double *B, 
 }
 
 // ---- measurement ---------------------------------------------------------------------------
+mspmv_status mspmv_time_stream_read(int device, size_t bytes, int reps, double *gbps)
+{
+    if (!gbps || reps < 1 || bytes < (1u << 20))
+        return invalid("time_stream_read: gbps non-null, reps >= 1, bytes >= 1 MiB");
+    HIP_TRY(hipSetDevice(device));
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+    bytes &= ~(size_t)15;
+    double *buf = nullptr;
+    HIP_TRY(hipMalloc(&buf, bytes));
+    hipStream_t s = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipError_t e = hipMemset(buf, 0, bytes);
+    if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e == hipSuccess)
+        e = hipEventCreate(&e0);
+    if (e == hipSuccess)
+        e = hipEventCreate(&e1);
+    if (e == hipSuccess)
+        e = launch_stream_read(buf, bytes, cus, s);  // warm-up
+    if (e == hipSuccess)
+        e = hipEventRecord(e0, s);
+    for (int r = 0; r < reps && e == hipSuccess; ++r)
+        e = launch_stream_read(buf, bytes, cus, s);
+    if (e == hipSuccess)
+        e = hipEventRecord(e1, s);
+    if (e == hipSuccess)
+        e = hipEventSynchronize(e1);
+    float ms = 0.f;
+    if (e == hipSuccess)
+        e = hipEventElapsedTime(&ms, e0, e1);
+    if (e1)
+        (void)hipEventDestroy(e1);
+    if (e0)
+        (void)hipEventDestroy(e0);
+    if (s)
+        (void)hipStreamDestroy(s);
+    (void)hipFree(buf);
+    if (e != hipSuccess) {
+        set_error(std::string("time_stream_read: ") + hipGetErrorString(e));
+        return MSPMV_ERR_HIP;
+    }
+    *gbps = ms > 0.f ? (double)bytes * reps / (ms * 1e-3) / 1e9 : 0.0;
+    return MSPMV_OK;
+}
+
 mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y, int L, int reps,
                                  size_t flush_bytes, double *avg_ms)
 {

@@ -204,6 +204,8 @@ hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, in
 int tile_items_for(int L);
 // Resident single-RHS tile workgroups per CU at the default tile shape (0: non-default tuning).
 int spmv_tile_blocks_per_cu();
+// STREAM-like nontemporal read of `bytes` (16-B words) on stream s (mspmv_time_stream_read).
+hipError_t launch_stream_read(const double *p, size_t bytes, int num_cus, hipStream_t s);
 std::string spmv_kernel_name(const mspmv_handle_s *h);
 bool stream_nt(const mspmv_handle_s *h);
 bool supported_L(int L);

@@ -3048,6 +3048,34 @@ __global__ void k_flush(double *p, long long n, double v)
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
         p[i] = v;
 }
+// STREAM-like read of n2 16-byte words (the practical HBM ceiling the roofline is read against,
+// SURVEY 8(d)): grid-stride, four nontemporal 16-B loads in flight per thread per step.
+__global__ __launch_bounds__(kBlock) void k_stream_read(const double2 *p, long long n2, double *sink)
+{
+    double acc = 0.0;
+    const long long stride = (long long)gridDim.x * kBlock;
+    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + 3 * stride < n2; i += 4 * stride) {
+        const double2 a = ld_stream<true>(p + i), b = ld_stream<true>(p + i + stride);
+        const double2 c = ld_stream<true>(p + i + 2 * stride), d = ld_stream<true>(p + i + 3 * stride);
+        acc += (a.x + b.x) + (c.x + d.x) + (a.y + b.y) + (c.y + d.y);
+    }
+    for (; i < n2; i += stride) {
+        const double2 a = ld_stream<true>(p + i);
+        acc += a.x + a.y;
+    }
+    if (acc == -1.0)  // never (the buffer holds zeros): keeps the loads live without a store
+        *sink = acc;
+}
+
+hipError_t launch_stream_read(const double *p, size_t bytes, int num_cus, hipStream_t s)
+{
+    const long long n2 = (long long)(bytes / 16);
+    hipLaunchKernelGGL(k_stream_read, dim3((unsigned)std::max(1, num_cus * 8)), dim3(kBlock), 0, s,
+                       reinterpret_cast<const double2 *>(p), n2, const_cast<double *>(p));
+    return hipGetLastError();
+}
+
 __global__ void k_flush_read(const double *p, long long n, double *sink)
 {
     double acc = 0.0;

@@ -98,6 +98,7 @@ _SIGS = {
     "mspmv_dpcg_spai_multi": (_I, [_P, _P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
     "mspmv_dpcg_spai_multi_dev": (_I, [_P, _P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
     "mspmv_time_spmm_dev": (_I, [_P, _P, _P, _I, _I, _SZ, _PD]),
+    "mspmv_time_stream_read": (_I, [_I, _SZ, _I, _PD]),
     "mspmv_last_kernel_ms": (_I, [_P, _PD, _PI]),
     "mspmv_time_spmm_batch_dev": (_I, [_I, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P), _I, _I,
                                        _PD, _PD, _PI]),
@@ -161,6 +162,13 @@ def _check(status: int, where: str, allow=()):
 
 def device_count() -> int:
     return int(lib.mspmv_device_count())
+
+
+def time_stream_read(device: int = 0, nbytes: int = 1 << 30, reps: int = 20) -> float:
+    """GB/s of a STREAM-like nontemporal HBM read (the practical roofline ceiling)."""
+    g = ctypes.c_double(0.0)
+    _check(lib.mspmv_time_stream_read(device, nbytes, reps, ctypes.byref(g)), "time_stream_read")
+    return g.value
 
 
 def _ptr(a: np.ndarray) -> int:

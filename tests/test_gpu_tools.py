@@ -96,3 +96,13 @@ def test_precond_cli(tmp_path):
     its = {k: int(v[5]) for k, v in got.items()}
     assert all(v > 0 for v in its.values()) and its["IC0"] < its["NONE"] and its["SPAI"] < its["NONE"], its
     assert float(got["IC0"][1]) > 0 and float(got["NONE"][1]) == 0.0
+
+
+def test_stream_read_ceiling():
+    """mspmv_time_stream_read: the STREAM-like HBM read the bench reports beside the 8 TB/s spec
+    peak -- a plausible MI355X figure (above the SpMV's own rate floor, below the spec), and the
+    argument checks."""
+    gbps = mspmv.time_stream_read(0, 1 << 30, 5)
+    assert 2000.0 < gbps < 8200.0, gbps
+    with pytest.raises(mspmv.MspmvError):
+        mspmv.time_stream_read(0, 1024, 5)
