@@ -660,6 +660,9 @@ struct TileArgs {
     // SpMM: leading dimension of the x / y panels in doubles (L for whole panels; a column
     // chunk of a wider panel otherwise, mspmv_dspmm with L outside {1, 2, 4, 8, 16})
     int ld;
+    // single-RHS tile kernel: load the tile's row ends with its stream (1) instead of after the
+    // staging (0) -- one dependent round trip fewer per tile (SpmvTuning::early_re)
+    int early_re;
 };
 
 // Tile-kernel modes.
@@ -1401,6 +1404,7 @@ k_spmv_tile(TileArgs a)
     const int r0 = b0.x, n0 = b0.y;
     const int nrows = b1.x - r0;
     const int nnzt = b1.y - n0;
+    const int re_pre = a.early_re ? a.row_offsets[min(r0 + 1 + tid, a.m)] : 0;  // TileArgs::early_re
     double beta = 0.0;
     bool go = true;
     // CG: the update's r.r partials are loaded first; summed (-> stop test, beta) once this
@@ -1483,8 +1487,15 @@ k_spmv_tile(TileArgs a)
     const unsigned long long lab_t1 = wall_clock64();
 #endif
     int *rend = sm.rowend(nnzt);
-    for (int i = tid; i < nrows; i += TB)
-        rend[i] = a.row_offsets[r0 + 1 + i] - n0;
+    if (a.early_re) {
+        if (tid < nrows)
+            rend[tid] = re_pre - n0;
+        for (int i = tid + TB; i < nrows; i += TB)  // rare: more rows than threads
+            rend[i] = a.row_offsets[r0 + 1 + i] - n0;
+    } else {
+        for (int i = tid; i < nrows; i += TB)
+            rend[i] = a.row_offsets[r0 + 1 + i] - n0;
+    }
     tile_sync<TB>();
 #if MSPMV_LAB_ABLATE == 9
     const unsigned long long lab_t2 = wall_clock64();
@@ -3107,6 +3118,7 @@ struct SpmvTuning {
     int blkreg = 1;   // plans of register node-block tiles only run the LDS-free k_spmv_blk
     int runs = 0;     // ... or, for the plain SpMV, the persistent wave-pipelined k_spmv_runs
     int spmm_blk = 1; // SpMM (L >= 2) on such a plan runs k_spmm_blk instead of its own L-wide tiles
+    int early_re = 0; // single-RHS tile kernel: row ends issued with the stream (TileArgs::early_re)
     int dict = 1;     // single-RHS SpMV through per-tile column dictionaries (k_build_dict) when
                       // a tile's nonzeros repeat its distinct columns >= dict_ratio times (0: off)
 };
@@ -3144,6 +3156,8 @@ static const SpmvTuning &spmv_tuning()
             v.runs = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMM_BLK"))
             v.spmm_blk = atoi(e) != 0;
+        if (const char *e = getenv("MSPMV_SPMV_EARLY_RE"))
+            v.early_re = atoi(e);
         if (const char *e = getenv("MSPMV_SPMV_DICT"))
             v.dict = atoi(e) > 0 ? atoi(e) : 0;
         if (const char *e = getenv("MSPMV_TRSV_TAGGED"))
@@ -3364,6 +3378,7 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
     a.ndict = plan.d_ndict;
     a.idx16 = plan.d_idx16;
     a.ld = L;
+    a.early_re = L == 1 ? spmv_tuning().early_re : 0;
     return a;
 }
 
