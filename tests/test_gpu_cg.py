@@ -8,6 +8,8 @@ Tolerances (north_star "CG residual match within 1e-10 rel", read relative to ||
   * final x within 1e-8 relative, and the true residual ||b - A x||/||b|| of the same order
     as the oracle's.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -285,3 +287,51 @@ def test_cg_multi_breakdown_warns_in_facade(orc):
     with pytest.warns(RuntimeWarning, match="breakdown"):
         it = mspmv.CGSolveMultiple(a, B.reshape(-1), X, L, 3000, 1e-9)
     assert 0 < it < 3000 and np.all(X.reshape(n, L)[:, 1] == 0.0)
+
+
+_KNOB_CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import mspmv
+from test_gpu_cg import spd_cases
+a = spd_cases()[sys.argv[4]]()
+L = int(sys.argv[5])
+B = np.random.default_rng(11).uniform(0, 1, (a.num_rows, L))
+with mspmv.GpuCsr(a) as g:
+    X, it, h, st = g.cg_multi(B, 5000, 1e-9, hist_cap=5000)
+np.save(sys.argv[3] + "/X.npy", X)
+np.save(sys.argv[3] + "/h.npy", h)
+np.save(sys.argv[3] + "/m.npy", np.array([it, st]))
+print("KNOB OK")
+"""
+
+
+@pytest.mark.parametrize("env", [{"MSPMV_CG_DOT": "fused"}, {"MSPMV_CG_REV": "0"},
+                                 {"MSPMV_CG_DOT": "fused", "MSPMV_CG_REV": "0"}])
+@pytest.mark.parametrize("name,L", [("stencil27", 8), ("fem2d", 4), ("fem2d", 1)])
+def test_cg_split_forms_vs_oracle(tmp_path, orc, env, name, L):
+    """The split CG's alternative forms kept as knobs -- p.Ap from the SpMM's dot mode
+    (MSPMV_CG_DOT=fused) instead of the separate pass, forward-only sweeps (MSPMV_CG_REV=0) --
+    against the oracle's CGSolveMultiple like the default form (L = 1 runs split with
+    MSPMV_CG_SPLIT=1).  Each variant in its own process (the knobs are read once)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ, **env)
+    if L == 1:
+        e["MSPMV_CG_SPLIT"] = "1"
+    r = subprocess.run([sys.executable, "-c", _KNOB_CHILD, os.path.join(root, "sparse-matrix-linear-equations_amd"),
+                        os.path.join(root, "tests"), str(tmp_path), name, str(L)], env=e, capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "KNOB OK" in r.stdout, r.stdout + r.stderr[-3000:]
+    a = spd_cases()[name]()
+    B = np.random.default_rng(11).uniform(0, 1, (a.num_rows, L))
+    Xo, it_o, ho = orc.cg_multi(a, B, 5000, 1e-9, kernel=1, P=8, hist_cap=5000)
+    it, st = np.load(tmp_path / "m.npy")
+    assert st == 0 and iter_match(int(it), it_o, ho, 1e-9), (it, it_o)
+    hg = np.load(tmp_path / "h.npy")
+    k = min(len(hg), len(ho))
+    np.testing.assert_allclose(hg[:k], ho[:k], rtol=0, atol=1e-10)
+    Xg = np.load(tmp_path / "X.npy")
+    for j in range(L):
+        assert np.linalg.norm(Xg[:, j] - Xo[:, j]) <= 1e-8 * np.linalg.norm(Xo[:, j])
