@@ -284,7 +284,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
             return fail(MSPMV_ERR_HIP);
         }
         p.h_blk_reg.assign((size_t)T, 0);
-        int maxnd = 0;
+        int maxnd = 0, maxh = 0;
         for (int t = 0; t < T; ++t) {
             const uint4 *d = &hd[(size_t)t * kBlkPerTile];
             const int nd = (int)((d[0].y >> 8) & 255u);
@@ -292,6 +292,8 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
                 continue;
             ++p.num_tiles_blk;
             maxnd = std::max(maxnd, nd);
+            for (int i = 0; i < nd; ++i)
+                maxh = std::max(maxh, (int)(d[i].y & 15u));
             bool one = true;  // the kernel's own test: every chunk starts at pattern column 0
             for (int i = 0; i < nd; ++i)
                 one = one && ((d[i].x >> 16) & 255u) == 0;
@@ -300,6 +302,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
         }
         dev_free(p.d_blk);
         p.d_blk = nullptr;
+        p.blk_rows_max = maxh > 0 ? maxh : 8;
         if (p.num_tiles_blk > 0) {  // repack at the smallest stride that holds every tile's set
             p.blk_stride = maxnd <= 16 ? 16 : maxnd <= 32 ? 32 : 64;
             std::vector<uint4> packed((size_t)T * p.blk_stride, make_uint4(0u, 0u, 0u, 0u));

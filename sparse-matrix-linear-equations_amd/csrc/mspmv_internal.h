@@ -64,6 +64,7 @@ struct TilePlan {
     int blk_stride = 0;
     int num_tiles_blk = 0;              // tiles staged by node blocks
     int num_tiles_reg = 0;              // of those, tiles reduced in registers (h_blk_reg)
+    int blk_rows_max = 8;               // the tallest run (rows of one node) over the descriptors
     std::vector<unsigned char> h_blk_reg;  // [num_tiles] 1: every run one chunk wide (the SpMV reduces
                                            // such tiles in registers; mspmv_tile_modes reports 255)
 };

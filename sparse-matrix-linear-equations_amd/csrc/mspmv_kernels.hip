@@ -663,6 +663,7 @@ struct TileArgs {
     // single-RHS tile kernel: load the tile's row ends with its stream (1) instead of after the
     // staging (0) -- one dependent round trip fewer per tile (SpmvTuning::early_re)
     int early_re;
+    int blk_rows_max;  // node-block plans: the tallest run (TilePlan::blk_rows_max; k_spmm_blk's KR)
 };
 
 // Tile-kernel modes.
@@ -2204,7 +2205,9 @@ __device__ __forceinline__ double2 rows8_sum2(const double2 (&p)[kBlkRows])
 #ifndef MSPMV_SPMM_BLK_WAVES
 #define MSPMV_SPMM_BLK_WAVES 0
 #endif
-template <int L, int MODE, bool NT>
+// KR: the plan's tallest run (rows of one node, <= kBlkRows); KR = 6 (6-DOF FEM such as pwtk)
+// holds fewer accumulator and value registers than 8.
+template <int L, int MODE, bool NT, int KR = kBlkRows>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MSPMV_SPMM_BLK_WAVES > 0 ? MSPMV_SPMM_BLK_WAVES : 1))) void
 k_spmm_blk(TileArgs a)
 {
@@ -2244,24 +2247,24 @@ k_spmm_blk(TileArgs a)
         const uint4 d = blk_read(bd, di);
         const int vofs = d.x & 0xffff, wc = d.x >> 24;
         const int h = d.y & 15, p = (d.y >> 4) & 7, rofs = d.y >> 16;
-        int start[kBlkRows];
+        int start[KR];
         int pstart = 0, acc_s = 0;
 #pragma unroll
-        for (int i = 0; i < kBlkRows; ++i) {
+        for (int i = 0; i < KR; ++i) {
             start[i] = acc_s;
             pstart = i == p ? acc_s : pstart;
             acc_s += i < h ? blk_len(d, i) : 0;
         }
         // lane j: P[j] and the run's values in column j, one coalesced load per row
         const int colj = lane < wc ? colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + lane) : 0;
-        double vrow[kBlkRows];
+        double vrow[KR];
 #pragma unroll
-        for (int i = 0; i < kBlkRows; ++i)
+        for (int i = 0; i < KR; ++i)
             vrow[i] = (i < h && lane < blk_len(d, i)) ? ld_stream<NT>(a.vals + n0 + vofs + start[i] + lane) : 0.0;
         if constexpr (LDSV) {  // wave-private slice: the wave's LDS operations stay in order
             s_c[wave][lane] = colj;
 #pragma unroll
-            for (int i = 0; i < kBlkRows; ++i)
+            for (int i = 0; i < KR; ++i)
                 if (i < h)
                     s_v[wave][i][lane] = vrow[i];
             __builtin_amdgcn_wave_barrier();
@@ -2271,7 +2274,7 @@ k_spmm_blk(TileArgs a)
         double2 xx = make_double2(0.0, 0.0);  // dot mode: the stored row's own x, issued early
         if (MODE == kModeDot && store)
             xx = *reinterpret_cast<const double2 *>(a.xr + (size_t)(r0 + rofs + ri) * a.ld + 2 * c);
-        double2 acc[kBlkRows];
+        double2 acc[kBlkRows];  // rows KR.. stay 0.0 (compile-time constants: no registers)
 #pragma unroll
         for (int i = 0; i < kBlkRows; ++i)
             acc[i] = make_double2(0.0, 0.0);
@@ -2289,7 +2292,7 @@ k_spmm_blk(TileArgs a)
                 const int jb = (pb + q) * NGW;  // the pass's first pattern column (wave-uniform)
                 const int j = jb + g;
 #pragma unroll
-                for (int i = 0; i < kBlkRows; ++i) {
+                for (int i = 0; i < KR; ++i) {
                     const int len = blk_len(d, i);
                     if (i >= h || jb >= len)  // wave-uniform: row i has no column in this pass
                         continue;
@@ -3373,6 +3376,7 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
         a.blk = plan.d_blk;
         a.blk_stride = plan.blk_stride;
         a.all_reg = plan.d_blk && plan.num_tiles_reg == plan.num_tiles && spmv_tuning().blkreg && spmv_tuning().tb == kBlock;
+        a.blk_rows_max = plan.blk_rows_max;
     }
     a.dict = plan.d_dict;
     a.ndict = plan.d_ndict;
@@ -3453,10 +3457,19 @@ static void launch_spmm_L(const TileArgs &a, hipStream_t s, bool nt)
 {
     if constexpr (MODE != kModeCg) {
         if (a.all_reg) {  // a node-block plan (single-RHS tiles): every tile a register run tile
-            if (nt)
+#ifndef MSPMV_SPMM_BLK_KR6
+#define MSPMV_SPMM_BLK_KR6 1  // lab builds: 0 runs the 8-row kernel on every plan
+#endif
+            if (MSPMV_SPMM_BLK_KR6 && a.blk_rows_max <= 6) {
+                if (nt)
+                    hipLaunchKernelGGL((k_spmm_blk<LL, MODE, true, 6>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
+                else
+                    hipLaunchKernelGGL((k_spmm_blk<LL, MODE, false, 6>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
+            } else if (nt) {
                 hipLaunchKernelGGL((k_spmm_blk<LL, MODE, true>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
-            else
+            } else {
                 hipLaunchKernelGGL((k_spmm_blk<LL, MODE, false>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
+            }
             return;
         }
     }
