@@ -2243,10 +2243,11 @@ k_spmm_blk(TileArgs a)
     const int nd = (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u);
     const int wave = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
     double2 dot = make_double2(0.0, 0.0);
-    for (int di = wave; di < nd && !stopped; di += kBlock / 64) {  // wave-uniform
+    // lane j: P[j] and the run's values in column j of chunk di, one coalesced load per row
+    auto fetch = [&](int di, int &cj, double (&vr)[KR]) {
         const uint4 d = blk_read(bd, di);
         const int vofs = d.x & 0xffff, wc = d.x >> 24;
-        const int h = d.y & 15, p = (d.y >> 4) & 7, rofs = d.y >> 16;
+        const int h = d.y & 15, p = (d.y >> 4) & 7;
         int start[KR];
         int pstart = 0, acc_s = 0;
 #pragma unroll
@@ -2255,12 +2256,35 @@ k_spmm_blk(TileArgs a)
             pstart = i == p ? acc_s : pstart;
             acc_s += i < h ? blk_len(d, i) : 0;
         }
-        // lane j: P[j] and the run's values in column j, one coalesced load per row
-        const int colj = lane < wc ? colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + lane) : 0;
-        double vrow[KR];
+        cj = lane < wc ? colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + lane) : 0;
 #pragma unroll
         for (int i = 0; i < KR; ++i)
-            vrow[i] = (i < h && lane < blk_len(d, i)) ? ld_stream<NT>(a.vals + n0 + vofs + start[i] + lane) : 0.0;
+            vr[i] = (i < h && lane < blk_len(d, i)) ? ld_stream<NT>(a.vals + n0 + vofs + start[i] + lane) : 0.0;
+    };
+#ifndef MSPMV_SPMM_BLK_PF
+#define MSPMV_SPMM_BLK_PF 0
+#endif
+    // PF (with LDSV): the wave's next chunk's columns and values are loaded while this chunk's
+    // passes run (they land in registers the LDS slice has just been filled from)
+    constexpr bool PF = LDSV && MSPMV_SPMM_BLK_PF != 0;
+    int colj_n = 0;
+    double vrow_n[KR];
+    if (PF && wave < nd && !stopped)
+        fetch(wave, colj_n, vrow_n);
+    for (int di = wave; di < nd && !stopped; di += kBlock / 64) {  // wave-uniform
+        const uint4 d = blk_read(bd, di);
+        const int wc = d.x >> 24;
+        const int h = d.y & 15, rofs = d.y >> 16;
+        int colj;
+        double vrow[KR];
+        if constexpr (PF) {
+            colj = colj_n;
+#pragma unroll
+            for (int i = 0; i < KR; ++i)
+                vrow[i] = vrow_n[i];
+        } else {
+            fetch(di, colj, vrow);
+        }
         if constexpr (LDSV) {  // wave-private slice: the wave's LDS operations stay in order
             s_c[wave][lane] = colj;
 #pragma unroll
@@ -2268,6 +2292,8 @@ k_spmm_blk(TileArgs a)
                 if (i < h)
                     s_v[wave][i][lane] = vrow[i];
             __builtin_amdgcn_wave_barrier();
+            if (PF && di + kBlock / 64 < nd)
+                fetch(di + kBlock / 64, colj_n, vrow_n);
         }
         const int ri = lane >> 3;  // the run row this lane's slot stores
         const bool store = (lane & 7) < GL && ri < h;
