@@ -1925,7 +1925,10 @@ constexpr int spmm_waves_per_eu(int L, int IPTG, bool DICT = false)
     const int items = (kBlock / (L / 2)) * IPTG;
     const int lds = 16 * (items + items / kSnapDiv) + 6144 + (DICT ? kSpmmDictBytes : 0);  // + s_crow, s_cval, s_red2
     const int w = 163840 / lds;
-    return w < 1 ? 1 : w > 7 ? 7 : w;
+#ifndef MSPMV_SPMM_WAVES_CAP
+#define MSPMV_SPMM_WAVES_CAP 7
+#endif
+    return w < 1 ? 1 : w > MSPMV_SPMM_WAVES_CAP ? MSPMV_SPMM_WAVES_CAP : w;
 }
 
 // DICT: tiles with a column dictionary (multi-RHS plans, k_build_dict) gather each distinct
