@@ -738,10 +738,15 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
     };
     // batches of K iterations, the control word of batch b inspected while b+1 is queued
     const int K = cg_batch_iters(d->n_own, d->local->nnz, L);
-    static const bool use_graph = [] {
+    // MSPMV_DIST_GRAPH: 1 on, 0 off; unset: on for a single rank (tested bit-identical to eager),
+    // off for several ranks -- RCCL collectives replayed from a captured graph have only run at
+    // world 1 here (RCCL refuses two ranks on one device), so the driver's multi-GPU runs keep the
+    // eager enqueue unless asked
+    static const int graph_env = [] {
         const char *e = getenv("MSPMV_DIST_GRAPH");
-        return !e || atoi(e) != 0;
+        return e ? (atoi(e) != 0 ? 1 : 0) : -1;
     }();
+    const bool use_graph = graph_env >= 0 ? graph_env == 1 : d->nranks == 1;
     const void *tk = nullptr;
     static_assert(sizeof(tk) == sizeof(tolerance), "tolerance bits as a key word");
     std::memcpy(&tk, &tolerance, sizeof tk);
