@@ -236,12 +236,20 @@ def run_spmv_shapes(dev, cpu_seconds, do_cpu):
     fit the Infinity Cache, so hot and cold (flushed) kernel times are reported."""
     out = {}
     shapes = {"cant": (CANT, "configs[0]: cant-shaped banded, 64.2 nnz/row, band +-2,000"),
-              "rma10": (RMA10, "configs[1] second matrix: rma10-shaped banded, 50.7 nnz/row, band +-3,000")}
+              "rma10": (RMA10, "configs[1] second matrix: rma10-shaped banded, 50.7 nnz/row, band +-3,000"),
+              # SURVEY 8(d) skewed variant: pwtk's m and nnz with power-law row lengths (merge-path balance)
+              "powerlaw": (None, "skewed variant: pwtk's m and nnz, power-law row lengths (exponent 1.2, seed 3)")}
     for name, (sh, what) in shapes.items():
-        a = mspmv.CsrMatrix.synth_banded(sh["m"], sh["nnz"], sh["band"], seed=sh["seed"])
+        if sh is None:
+            a = mspmv.CsrMatrix.synth_powerlaw(PWTK["m"], PWTK["m"], PWTK["nnz"], 1.2, 3)
+        else:
+            a = mspmv.CsrMatrix.synth_banded(sh["m"], sh["nnz"], sh["band"], seed=sh["seed"])
         x, r = gpu_spmv_hot_cold(a, dev)
         r["workload"] = what
-        if name == "cant" and do_cpu:
+        if name == "powerlaw":
+            lens = np.diff(a.row_offsets)
+            r["row_length_max"], r["row_length_mean"] = int(lens.max()), round(float(lens.mean()), 1)
+        if name in ("cant", "powerlaw") and do_cpu:
             r["cpu_baselines"] = cpu_spmv_baselines(a, x, cpu_seconds)
             best = max(v["gflops"] for v in r["cpu_baselines"].values())
             r["gpu_cold_vs_best_cpu"] = round(r["gflops_cold"] / best, 1)
