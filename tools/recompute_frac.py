@@ -114,7 +114,7 @@ def main(src, dst):
             pmc_traffic.main(["", "--leg", ld, out(f"{leg}_pmc_traffic.json")])
         if leg in ("spmm16", "spmv_shapes"):
             L = 16 if leg == "spmm16" else 1
-            shapes = [k for k in (("cant", "pwtk") if leg == "spmm16" else ("cant", "rma10")) if k in lj]
+            shapes = [k for k in (("cant", "pwtk") if leg == "spmm16" else ("cant", "rma10", "powerlaw")) if k in lj]
             cold = sorted((r for r in rows if r["after_flush"] and r["kernel"].startswith(("k_spmm", "k_spmv"))),
                           key=lambda r: r["first_dispatch"])
             for name, r in zip(shapes, cold):
