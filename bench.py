@@ -534,7 +534,9 @@ def main():
         elif args.only == "cg_single":
             r = run_cg_single(dev, min(args.cpu_seconds, 10.0), do_cpu)
         else:
-            r = run_cg_multi(d, dev)[0]
+            r, large = run_cg_multi(d, dev)
+            if large:
+                r["spmv_nlpkkt120_size"] = large
         if d.rank == 0:
             print(json.dumps({"leg": args.only, **r}), flush=True)
         return

@@ -3379,8 +3379,12 @@ hipError_t launch_tile_modes(const int *d_row_offsets, const int2 *d_bounds, con
         const char *e = getenv("MSPMV_SPMM_LG");
         return e ? atoi(e) : -1;
     }();
+    static const int force_lg1 = [] {  // the same lab knob for the single-RHS tiles
+        const char *e = getenv("MSPMV_SPMV_LG");
+        return e ? atoi(e) : -1;
+    }();
     hipLaunchKernelGGL(k_tile_modes, dim3((num_tiles + 255) / 256), dim3(256), 0, s, d_row_offsets, d_bounds, d_split,
-                       num_tiles, L == 1 ? 1 : L / 2, cost, lanes, d_modes, L == 1 ? -1 : force_lg);
+                       num_tiles, L == 1 ? 1 : L / 2, cost, lanes, d_modes, L == 1 ? force_lg1 : force_lg);
     return hipGetLastError();
 }
 
