@@ -208,9 +208,10 @@ MSPMV_API mspmv_status mspmv_dpcg_ic0_multi_dev(mspmv_handle a, mspmv_ic0 m, con
 /* ---- measurement helpers (HIP events on the handle's stream) ------------------------ */
 /* Enqueue `reps` back-to-back SpMV (L == 1) or SpMM launches on device buffers and return
  * the average milliseconds per call measured by hipEvents on the handle's stream.
- * flush_bytes > 0 inserts a write of that many bytes to a scratch buffer before every
- * call (outside the timed events) to evict the 256 MiB Infinity Cache ("cold" protocol,
- * SURVEY 8(d)). */
+ * flush_bytes > 0 sweeps a scratch buffer of that many bytes before every call (outside the
+ * timed events) to evict the 256 MiB Infinity Cache ("cold" protocol): a
+ * nontemporal read sweep, so the caches hold clean unrelated lines (MSPMV_FLUSH=write: a write
+ * sweep, whose dirty lines the timed call would pay to write back). */
 MSPMV_API mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y, int L, int reps,
                                  size_t flush_bytes, double *avg_ms);
 /* Batch form for benchmarks: `reps` steps, each step one SpMM launch per handle (all handles
