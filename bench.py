@@ -120,6 +120,22 @@ class Dist:
         self.td.all_reduce(t, op=self.td.ReduceOp.MAX)
         return float(t.item())
 
+    def comm(self, dev):
+        """This rank's one RCCL communicator (mspmv.Comm, created on first use, collective), shared
+        by every sharded matrix of the run: no two communicators ever have collectives in flight."""
+        if getattr(self, "_comm", None) is None:
+            uid = self.bcast_bytes(mspmv.comm_unique_id() if self.rank == 0 else None)
+            self._comm = mspmv.Comm(uid, self.world, self.rank, dev)
+        return self._comm
+
+    def close_comm(self):
+        if getattr(self, "_comm", None) is not None:
+            try:
+                self._comm.close()
+            except RuntimeError as e:  # a sharded matrix left open by a failed leg: the process exit frees it
+                print(f"rank {self.rank}: {e}", file=sys.stderr)
+            self._comm = None
+
     def bcast_bytes(self, b):
         if not self.td:
             return b
@@ -128,12 +144,26 @@ class Dist:
         return obj[0]
 
 
+def host_cores():
+    """Host cores this process may run on: its CPU affinity (os.sched_getaffinity -- what the
+    reference's omp_get_num_procs() default counts), capped by the cgroup's CPU quota
+    when one is set (a GPU box's share of a larger machine)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(n, 256))  # cpu_spmv.cpp:370-371 sizes its carry arrays for <= 256 threads
+
+
 def cpu_baseline(a, x, seconds):
     """The reference's merge CsrMV on the host cores (bounded sample)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from _oracle import REF_SO, Oracle, RefLib
-    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
-    threads = max(1, min(threads, os.cpu_count() or 1))
+    threads = host_cores()
     if os.path.exists(REF_SO):
         ref = RefLib()
         kind = "reference"
@@ -185,7 +215,7 @@ def gpu_spmv_hot_cold(a, dev, seed=2):
 
 
 def _threads():
-    return max(1, min(int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1), os.cpu_count() or 1))
+    return host_cores()
 
 
 def _time_calls(fn, seconds):
@@ -287,7 +317,7 @@ def run_spmm16(dev, cpu_seconds, do_cpu):
             sys.path.insert(0, os.path.join(ROOT, "tests"))
             from _oracle import REF_SO, RefLib
             if os.path.exists(REF_SO):
-                threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1), os.cpu_count() or 1))
+                threads = host_cores()
                 ref = RefLib()
                 ref.merge_csrmm(a, X, threads)
                 calls, t0 = 0, time.perf_counter()
@@ -369,10 +399,9 @@ def run_cg_multi(d, dev):
                           "frac": round(nb / kern_ms / 1e6 / HBM_PEAK_GBS, 4)}
         mode = "1 GPU"
     else:
-        uid = d.bcast_bytes(mspmv.comm_unique_id() if d.rank == 0 else None)
         rb = mspmv.dist_partition(nk, d.world)
         loc = mspmv.local_rows(nk, rb, d.rank)
-        dc = mspmv.DistCsr(uid, d.world, d.rank, dev, rb, loc)
+        dc = mspmv.DistCsr(d.comm(dev), rb, loc)  # the rank's one communicator (Dist.comm)
         lo, hi = int(rb[d.rank]), int(rb[d.rank + 1])
         dB = mspmv.DeviceBuffer.from_array(np.ascontiguousarray(B[lo:hi]), dev)
         dX = mspmv.DeviceBuffer(8 * max(hi - lo, 1) * L, dev)
@@ -445,10 +474,10 @@ def run_sharded_headline(d, dev, args):
     rb = mspmv.dist_partition_offsets(ro, M, NNZ, world)
     lo, hi = int(rb[rank]), int(rb[rank + 1])
     dcs, dys, xps, infos, nnz_loc = [], [], [], [], 0
-    for i in range(args.batch):
-        uid = d.bcast_bytes(mspmv.comm_unique_id() if rank == 0 else None)
+    comm = d.comm(dev)  # ONE communicator (and stream) for every matrix of the batch: the exchanges are
+    for i in range(args.batch):  # one stream-ordered sequence, issued in the same order on every rank
         loc = mspmv.CsrMatrix.synth_fem_blocked_rows(M, NNZ, PWTK["block"], PWTK["half_band_nodes"], 1 + i, lo, hi)
-        dc = mspmv.DistCsr(uid, world, rank, dev, rb, loc)
+        dc = mspmv.DistCsr(comm, rb, loc)
         xp = dc.x_ext(1)
         mspmv.memcpy_h2d_ptr(xp, np.random.default_rng(2 + i).uniform(0.0, 1.0, M)[lo:hi])
         dcs.append(dc)
@@ -656,9 +685,22 @@ def main():
         except Exception as e:  # the headline line must still print
             result["cg_error"] = repr(e)[:300]
 
+    d.close_comm()
     if guard:
         if not guard.finish():  # the watchdog fired meanwhile and owns the exit
             return
+    if d.world > 1 and not args.no_cpu:
+        # north_star: the reference CPU path timed on the host cores "in the same run" at every N;
+        # rank 0, after the GPU legs (the other ranks wait at the barrier below)
+        if d.rank == 0:
+            a0 = mspmv.CsrMatrix.synth_fem_blocked(PWTK["m"], PWTK["nnz"], PWTK["block"], PWTK["half_band_nodes"],
+                                                   seed=1)
+            x0 = np.random.default_rng(2).uniform(0.0, 1.0, a0.num_cols)
+            _, cb = cpu_baseline(a0, x0, args.cpu_seconds)
+            cb["sample"] += "; one GPU's share of the sharded workload (a pwtk-shaped matrix), rank 0's host"
+            result["cpu_baseline"] = cb
+            result["speedup_vs_cpu"] = round(result["value"] / cb["value"], 1)
+        d.barrier()
     if d.rank == 0:
         print(json.dumps(result), flush=True)
     if d.td:

@@ -268,6 +268,10 @@ MSPMV_API mspmv_status mspmv_tile_modes(mspmv_handle h, int L, unsigned char *mo
  * "k_spmv_tile<8,0,true>" -- the name rocprofv3 reports.  Valid until the next call on this
  * thread. */
 MSPMV_API const char *mspmv_spmv_kernel_name(mspmv_handle h);
+/* The same for a plain SpMM with L right-hand sides (builds the plan for L if needed): e.g.
+ * "k_spmm_blk<16,0,false,6>" on a node-block plan, "k_spmm_tile<8,16,0,true>" elsewhere; widths
+ * outside 1, 2, 4, 8, 16 name their widest column chunk's kernel.  "" on error. */
+MSPMV_API const char *mspmv_spmm_kernel_name(mspmv_handle h, int L);
 
 /* ---- device memory helpers (so hosts need no HIP headers) ---------------------------- */
 MSPMV_API mspmv_status mspmv_device_malloc(int device, size_t bytes, void **d_ptr);

@@ -47,9 +47,23 @@ MSPMV_API mspmv_status mspmv_dist_localize(const int *row_begin, int nranks, int
 /* ---- communicator and sharded matrix ------------------------------------------------------ */
 /* Rank 0 creates the RCCL id and the host broadcasts it (torch.distributed, MPI, ...). */
 MSPMV_API mspmv_status mspmv_comm_unique_id(unsigned char id[MSPMV_UNIQUE_ID_BYTES]);
-/* Collective over all ranks: RCCL communicator init, localization of this rank's row block
- * (`local_rows`: num_rows = rows owned, num_cols = global columns, GLOBAL column ids), upload,
- * and the halo-exchange plan (request lists exchanged once with RCCL). */
+/* One communicator per rank (collective: RCCL init), shared by every sharded object on the rank.
+ * It owns ONE stream: every object created on it runs its local kernels and all of its collectives
+ * there, so a rank's collectives form one sequence in program order -- call the objects' collective
+ * functions in the same order on every rank.  (Several communicators with collectives in flight at
+ * once can deadlock under RCCL/NCCL; one communicator per rank rules that out.)  Destroy it after
+ * every object created on it (MSPMV_ERR_INVALID before). */
+typedef struct mspmv_comm_s *mspmv_comm;
+MSPMV_API mspmv_status mspmv_comm_create(const unsigned char id[MSPMV_UNIQUE_ID_BYTES], int nranks, int rank,
+                                         int device, mspmv_comm *out);
+MSPMV_API mspmv_status mspmv_comm_destroy(mspmv_comm c);
+/* Collective over all ranks of `c`: localization of this rank's row block (`local_rows`: num_rows =
+ * rows owned, num_cols = global columns, GLOBAL column ids), upload, and the halo-exchange plan
+ * (request lists exchanged once with RCCL). */
+MSPMV_API mspmv_status mspmv_dist_create_on(mspmv_comm c, const int *row_begin, const mspmv_csr_d *local_rows,
+                                            mspmv_dist *out);
+/* The same on a private communicator (mspmv_comm_create + mspmv_dist_create_on; destroyed with the
+ * object).  For one sharded object per rank; several objects on one rank share one mspmv_comm. */
 MSPMV_API mspmv_status mspmv_dist_create(const unsigned char id[MSPMV_UNIQUE_ID_BYTES], int nranks, int rank,
                                          int device, const int *row_begin, const mspmv_csr_d *local_rows,
                                          mspmv_dist *out);

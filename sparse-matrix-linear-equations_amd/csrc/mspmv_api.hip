@@ -384,7 +384,8 @@ static mspmv_status check_offsets_host(const int *ro, int m, int nnz)
     return MSPMV_OK;
 }
 
-static mspmv_status create_common(const mspmv_csr_d *a, int device, bool from_device, mspmv_handle *out)
+static mspmv_status create_common(const mspmv_csr_d *a, int device, bool from_device, mspmv_handle *out,
+                                  hipStream_t on_stream = nullptr)
 {
     ST_TRY(validate_host_csr(a));
     if (!out)
@@ -411,7 +412,10 @@ static mspmv_status create_common(const mspmv_csr_d *a, int device, bool from_de
     if (hipDeviceGetAttribute(&h->num_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
         h->num_cus < 1)
         h->num_cus = 256;
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (on_stream) {  // a stream owned by the caller (mspmv_comm: one stream per rank)
+        h->stream = on_stream;
+        h->own_stream = false;
+    } else if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         set_error("hipStreamCreate failed");
         return fail(MSPMV_ERR_HIP);
     }
@@ -508,6 +512,24 @@ const char *mspmv_spmv_kernel_name(mspmv_handle h)
     return name.c_str();
 }
 
+const char *mspmv_spmm_kernel_name(mspmv_handle h, int L)
+{
+    thread_local std::string name;
+    if (!h || L < 1)
+        return "";
+    // widths outside 1, 2, 4, 8, 16 run as column chunks (odd L on a zero-padded panel): the
+    // widest chunk's kernel
+    int w = 16;
+    const int lp = (L > 1 && (L & 1)) ? L + 1 : L;
+    while (w > lp)
+        w >>= 1;
+    const TilePlan *plan = nullptr;
+    if (get_plan(h, w, &plan) != MSPMV_OK)
+        return "";
+    name = spmm_kernel_name(h, *plan, w);
+    return name.c_str();
+}
+
 const char *mspmv_version(void) { return "mspmv 0.1.0 (gfx950, merge-path fp64)"; }
 
 int mspmv_device_count(void)
@@ -527,6 +549,15 @@ mspmv_status mspmv_csr_create_dev(const mspmv_csr_d *dev, int device, mspmv_hand
 {
     return create_common(dev, device, true, out);
 }
+
+}  // extern "C"
+
+mspmv_status mspmv::csr_create_on_stream(const mspmv_csr_d *host, int device, hipStream_t stream, mspmv_handle *out)
+{
+    return create_common(host, device, false, out, stream);
+}
+
+extern "C" {
 
 mspmv_status mspmv_destroy(mspmv_handle h)
 {
@@ -647,7 +678,17 @@ mspmv_status mspmv_set_cu_limit(mspmv_handle h, int num_cus)
         (void)hipStreamDestroy(h->stream);
     h->stream = s;
     h->own_stream = own;
-    h->num_cus = n;
+    if (n != h->num_cus) {
+        // the single-RHS plan's tile stretch is sized to num_cus x resident workgroups (build_plan):
+        // drop every cached plan so the next call plans for the CUs it will actually run on
+        for (auto &kv : h->plans)
+            free_plan(kv.second);
+        h->plans.clear();
+        h->num_cus = n;
+        const TilePlan *plan = nullptr;
+        ST_TRY(get_plan(h, 1, &plan));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+    }
     return MSPMV_OK;
 }
 

@@ -68,8 +68,22 @@ void dfree(T *&p)
 
 }  // namespace
 
-struct mspmv_dist_s {
+// One per rank: the RCCL communicator and the one stream every collective of every sharded object
+// on this rank is enqueued on (the objects' local handles run on it too).  All collectives of a rank
+// then form a single stream-ordered sequence, issued by one host thread in the program's order, so
+// every rank meets them in the same order and no two communicators can ever have collectives in
+// flight at once (RCCL/NCCL: concurrent operations on different communicators may deadlock).
+struct mspmv_comm_s {
     ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0, device = 0;
+    hipStream_t stream = nullptr;
+    int users = 0;  // sharded objects created on it (mspmv_comm_destroy refuses while > 0)
+};
+
+struct mspmv_dist_s {
+    mspmv_comm_s *cm = nullptr;
+    bool own_cm = false;  // mspmv_dist_create: a private communicator, destroyed with the object
+    ncclComm_t comm = nullptr;  // == cm->comm
     int nranks = 1, rank = 0, device = 0;
     int row_lo = 0, n_own = 0, n_halo = 0, n_send = 0;
     std::vector<int> row_begin;
@@ -228,9 +242,54 @@ mspmv_status mspmv_dist_destroy(mspmv_dist d)
             (void)hipEventDestroy(e);
     if (d->local)
         mspmv_destroy(d->local);
-    if (d->comm)
-        ncclCommDestroy(d->comm);
+    if (d->cm) {
+        --d->cm->users;
+        if (d->own_cm)
+            mspmv_comm_destroy(d->cm);
+    }
     delete d;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_comm_create(const unsigned char id[MSPMV_UNIQUE_ID_BYTES], int nranks, int rank, int device,
+                               mspmv_comm *out)
+{
+    if (!id || !out || nranks < 1 || rank < 0 || rank >= nranks)
+        return fail_msg(MSPMV_ERR_INVALID, "comm_create: bad arguments");
+    *out = nullptr;
+    D_HIP(hipSetDevice(device));
+    auto *c = new mspmv_comm_s();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail_msg(MSPMV_ERR_HIP, "comm_create: hipStreamCreate failed");
+    }
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    const ncclResult_t nr = ncclCommInitRank(&c->comm, nranks, u, rank);
+    if (nr != ncclSuccess) {
+        (void)hipStreamDestroy(c->stream);
+        delete c;
+        return fail_msg(MSPMV_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(nr));
+    }
+    *out = c;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_comm_destroy(mspmv_comm c)
+{
+    if (!c)
+        return MSPMV_OK;
+    if (c->users > 0)
+        return fail_msg(MSPMV_ERR_INVALID, "comm_destroy: sharded objects still use this communicator");
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    if (c->comm)
+        ncclCommDestroy(c->comm);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
     return MSPMV_OK;
 }
 
@@ -240,11 +299,34 @@ mspmv_status mspmv_dist_create(const unsigned char id[MSPMV_UNIQUE_ID_BYTES], in
     if (!id || !row_begin || !local_rows || !out || nranks < 1 || rank < 0 || rank >= nranks)
         return fail_msg(MSPMV_ERR_INVALID, "dist_create: bad arguments");
     *out = nullptr;
+    mspmv_comm c = nullptr;
+    D_ST(mspmv_comm_create(id, nranks, rank, device, &c));
+    mspmv_dist d = nullptr;
+    const mspmv_status st = mspmv_dist_create_on(c, row_begin, local_rows, &d);
+    if (st != MSPMV_OK) {
+        mspmv_comm_destroy(c);
+        return st;
+    }
+    d->own_cm = true;
+    *out = d;
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_dist_create_on(mspmv_comm c, const int *row_begin, const mspmv_csr_d *local_rows,
+                                  mspmv_dist *out)
+{
+    if (!c || !row_begin || !local_rows || !out)
+        return fail_msg(MSPMV_ERR_INVALID, "dist_create: bad arguments");
+    *out = nullptr;
+    const int nranks = c->nranks, rank = c->rank, device = c->device;
     const int lo = row_begin[rank], hi = row_begin[rank + 1];
     if (local_rows->num_rows != hi - lo || local_rows->num_cols != row_begin[nranks])
         return fail_msg(MSPMV_ERR_INVALID, "dist_create: local rows do not match row_begin (square matrix needed)");
     D_HIP(hipSetDevice(device));
     auto *d = new mspmv_dist_s();
+    d->cm = c;
+    ++c->users;
+    d->comm = c->comm;
     d->nranks = nranks;
     d->rank = rank;
     d->device = device;
@@ -255,13 +337,7 @@ mspmv_status mspmv_dist_create(const unsigned char id[MSPMV_UNIQUE_ID_BYTES], in
         mspmv_dist_destroy(d);
         return s;
     };
-    ncclUniqueId u;
-    std::memcpy(&u, id, sizeof(u));
-    ncclResult_t nr = ncclCommInitRank(&d->comm, nranks, u, rank);
-    if (nr != ncclSuccess) {
-        d->comm = nullptr;
-        return bail(fail_msg(MSPMV_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(nr)));
-    }
+    ncclResult_t nr = ncclSuccess;
     // localize this rank's rows
     const int nnz = local_rows->num_nonzeros;
     std::vector<int> lcols((size_t)std::max(nnz, 1));
@@ -280,15 +356,19 @@ mspmv_status mspmv_dist_create(const unsigned char id[MSPMV_UNIQUE_ID_BYTES], in
     mspmv_csr_d lc = *local_rows;
     lc.num_cols = d->n_own + n_halo;
     lc.column_indices = lcols.data();
-    if ((st = mspmv_csr_create(&lc, device, &d->local)) != MSPMV_OK)
+    // the local handle runs on the communicator's stream: this object's kernels and collectives, and
+    // every other object's on this rank, are one stream-ordered sequence
+    if ((st = csr_create_on_stream(&lc, device, c->stream, &d->local)) != MSPMV_OK)
         return bail(st);
     // interior rows: the longest contiguous run of rows that reference owned columns only (for a
     // banded / FEM matrix cut into row blocks, everything but the rows within the band of either
     // block end); split off only when it holds >= half the nonzeros and there is a halo at all
     // MSPMV_DIST_FORCE_SPLIT=1 (tests): split at the row thirds even without a halo, so one GPU
     // exercises the three-stream path (RCCL refuses two ranks on one device)
+    // and only without a halo: the middle third is not checked to read owned columns only, and it
+    // runs unordered with the exchange that fills the halo rows
     const char *force_env = getenv("MSPMV_DIST_FORCE_SPLIT");
-    const bool force = force_env && atoi(force_env) != 0 && d->n_own >= 3;
+    const bool force = force_env && atoi(force_env) != 0 && d->n_own >= 3 && n_halo == 0;
     if ((nranks > 1 && n_halo > 0) || force) {
         const int *ro = local_rows->row_offsets;
         int best_lo = 0, best_hi = 0, cur = 0;
@@ -787,8 +867,10 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
                 d->cg_exec = nullptr;
                 d->cg_warm = false;
                 (void)hipGetLastError();
-                if (cst != MSPMV_OK && cst != MSPMV_ERR_HIP)
-                    return cst;
+                // whatever failed inside the capture (HIP or RCCL), this batch still runs eagerly
+                // below: the other ranks enqueue theirs, so skipping it would misalign the
+                // collectives across ranks (a hang, not an error)
+                (void)cst;
             }
         }
         if (use_graph && k == K && d->cg_exec && d->cg_key == key)

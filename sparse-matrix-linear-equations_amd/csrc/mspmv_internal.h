@@ -208,6 +208,7 @@ int spmv_tile_blocks_per_cu();
 // STREAM-like nontemporal read of `bytes` (16-B words) on stream s (mspmv_time_stream_read).
 hipError_t launch_stream_read(const double *p, size_t bytes, int num_cus, hipStream_t s);
 std::string spmv_kernel_name(const mspmv_handle_s *h);
+std::string spmm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan, int L);
 bool stream_nt(const mspmv_handle_s *h);
 bool supported_L(int L);
 
@@ -281,6 +282,8 @@ hipError_t launch_fold_dot(int T, int L, double *partials, unsigned *gtickets, d
                            const unsigned char *conv, CgControl *ctrl, int fold_mode, hipStream_t s);
 // The tile plan a handle's kernels use for L right-hand sides (built on first use).
 mspmv_status plan_for(mspmv_handle_s *h, int L, const TilePlan **out);
+// mspmv_csr_create on a stream the caller owns (kept; the handle never destroys it)
+mspmv_status csr_create_on_stream(const mspmv_csr_d *host, int device, hipStream_t stream, mspmv_handle *out);
 // SPAI-preconditioned block CG (SPAISolveMultiple, work_2025/main/sparse_approximate_inverse.hpp:
 // 30-230) on A's handle h with the preconditioner's handle hm (same shape and device): init
 // (X = 0, R = B, Z = M R, P = Z, rs_old = R.Z) and one iteration (AP = A P -> alpha; X, R update

@@ -3225,12 +3225,28 @@ std::string spmv_kernel_name(const mspmv_handle_s *h)
            (stream_nt(h) ? "true" : "false") + (t.tb == 64 && !t.persist ? ",64>" : ">");
 }
 
+
 // SpMM tile depth: measured best 8 items per lane group for L <= 4 (fem-blocked pwtk shape,
 // L = 4: 55.6 vs 74.8 us at 16) and 16 for L >= 8 (nlpkkt120 shape, L = 8: 549 vs 741 us).
 int spmm_iptg_for(int L)
 {
     const int i = spmv_tuning().spmm_iptg;
     return i ? i : (L >= 8 ? 16 : 8);
+}
+
+// The kernel a plain SpMM of native width L (1, 2, 4, 8, 16) launches on `plan` (get_plan's
+// choice for L), spelled as rocprofv3 lists it: launch_spmm_L's dispatch, restated.
+std::string spmm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan, int L)
+{
+    if (L == 1)
+        return spmv_kernel_name(h);
+    const std::string nt = stream_nt(h) ? "true" : "false";
+    const SpmvTuning &t = spmv_tuning();
+    if (plan.d_blk && plan.num_tiles_reg == plan.num_tiles && t.blkreg && t.tb == kBlock && spmm_blk_enabled())
+        return "k_spmm_blk<" + std::to_string(L) + ",0," + nt + (plan.blk_rows_max <= 6 ? ",6>" : ",8>");
+    const int iptg = spmm_iptg_for(L);
+    const bool dict = L == 16 && iptg != 32 && plan.d_dict;
+    return "k_spmm_tile<" + std::to_string(L) + "," + std::to_string(iptg) + ",0," + nt + (dict ? ",true>" : ">");
 }
 
 // Resident workgroups per CU of a kBlock-thread kernel from its own resources on gfx950: 160 KiB
@@ -3408,7 +3424,10 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
         a.cols16 = plan.d_cols16;
         a.blk = plan.d_blk;
         a.blk_stride = plan.blk_stride;
-        a.all_reg = plan.d_blk && plan.num_tiles_reg == plan.num_tiles && spmv_tuning().blkreg && spmv_tuning().tb == kBlock;
+        // L > 1 runs the node-block plan only while k_spmm_blk is enabled (get_plan's gate): L = 2
+        // shares the single-RHS tile size, so without this the knob-off plan would still be all-reg
+        a.all_reg = plan.d_blk && plan.num_tiles_reg == plan.num_tiles && spmv_tuning().blkreg &&
+                    spmv_tuning().tb == kBlock && (L == 1 || spmm_blk_enabled());
         a.blk_rows_max = plan.blk_rows_max;
     }
     a.dict = plan.d_dict;

@@ -108,6 +108,7 @@ _SIGS = {
     "mspmv_plan_block_tiles": (_I, [_P, _I, _PI]),
     "mspmv_tile_modes": (_I, [_P, _I, _P]),
     "mspmv_spmv_kernel_name": (ctypes.c_char_p, [_P]),
+    "mspmv_spmm_kernel_name": (ctypes.c_char_p, [_P, _I]),
     "mspmv_device_malloc": (_I, [_I, _SZ, ctypes.POINTER(_P)]),
     "mspmv_device_free": (_I, [_P]),
     "mspmv_memcpy_h2d": (_I, [_P, _P, _SZ]),
@@ -123,6 +124,9 @@ _SIGS = {
     "mspmv_dist_localize": (_I, [_P, _I, _I, _P, _P, _P, _PI, _P, _I, _P]),
     "mspmv_comm_unique_id": (_I, [_P]),
     "mspmv_dist_create": (_I, [_P, _I, _I, _I, _P, ctypes.POINTER(_CsrD), ctypes.POINTER(_P)]),
+    "mspmv_comm_create": (_I, [_P, _I, _I, _I, ctypes.POINTER(_P)]),
+    "mspmv_comm_destroy": (_I, [_P]),
+    "mspmv_dist_create_on": (_I, [_P, _P, ctypes.POINTER(_CsrD), ctypes.POINTER(_P)]),
     "mspmv_dist_destroy": (_I, [_P]),
     "mspmv_dist_info": (_I, [_P, _PI, _PI, _PI]),
     "mspmv_dist_spmm_dev": (_I, [_P, _P, _P, _I]),
@@ -407,6 +411,10 @@ class GpuCsr:
     def kernel_name(self) -> str:
         """The single-RHS SpMV kernel instantiation used for this matrix (rocprofv3's name)."""
         return lib.mspmv_spmv_kernel_name(self.h).decode()
+
+    def spmm_kernel_name(self, L: int) -> str:
+        """The SpMM kernel instantiation launched for L right-hand sides (rocprofv3's spelling)."""
+        return lib.mspmv_spmm_kernel_name(self.h, L).decode()
 
     def plan_block_tiles(self, L: int = 1) -> int:
         """Tiles of the L-column plan staged by node blocks (mspmv_plan_block_tiles)."""
@@ -722,15 +730,48 @@ def comm_unique_id() -> bytes:
     return bytes(buf)
 
 
-class DistCsr:
-    """This rank's row block of a matrix sharded over `nranks` GPUs (collective create)."""
+class Comm:
+    """This rank's RCCL communicator and its one stream (mspmv_comm_create, collective): every
+    DistCsr created on it runs its kernels and collectives on that stream, so a rank's collectives
+    are one sequence in program order.  Close it after every DistCsr on it."""
 
-    def __init__(self, uid: bytes, nranks: int, rank: int, device: int, row_begin: np.ndarray, loc: CsrMatrix):
-        self.row_begin = np.ascontiguousarray(row_begin, np.int32)
+    def __init__(self, uid: bytes, nranks: int, rank: int, device: int):
         idb = (ctypes.c_ubyte * 128).from_buffer_copy(uid)
         h = ctypes.c_void_p()
-        _check(lib.mspmv_dist_create(idb, nranks, rank, device, _ptr(self.row_begin), ctypes.byref(loc._c()),
-                                     ctypes.byref(h)), "dist_create")
+        _check(lib.mspmv_comm_create(idb, nranks, rank, device, ctypes.byref(h)), "comm_create")
+        self.h, self.nranks, self.rank, self.device = h.value, nranks, rank, device
+
+    def close(self):
+        if getattr(self, "h", None):
+            _check(lib.mspmv_comm_destroy(self.h), "comm_destroy")
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class DistCsr:
+    """This rank's row block of a matrix sharded over `nranks` GPUs (collective create).  Either
+    on a shared Comm -- DistCsr(comm, row_begin, loc), the form for several matrices per rank -- or
+    on a private communicator: DistCsr(uid, nranks, rank, device, row_begin, loc)."""
+
+    def __init__(self, *args):
+        if len(args) == 3:
+            comm, row_begin, loc = args
+            self.row_begin = np.ascontiguousarray(row_begin, np.int32)
+            h = ctypes.c_void_p()
+            _check(lib.mspmv_dist_create_on(comm.h, _ptr(self.row_begin), ctypes.byref(loc._c()), ctypes.byref(h)),
+                   "dist_create_on")
+        else:
+            uid, nranks, rank, device, row_begin, loc = args
+            self.row_begin = np.ascontiguousarray(row_begin, np.int32)
+            idb = (ctypes.c_ubyte * 128).from_buffer_copy(uid)
+            h = ctypes.c_void_p()
+            _check(lib.mspmv_dist_create(idb, nranks, rank, device, _ptr(self.row_begin), ctypes.byref(loc._c()),
+                                         ctypes.byref(h)), "dist_create")
         self.h = h.value
         self.n_own = loc.num_rows
 

@@ -37,3 +37,12 @@ def gpu_available():
     if m.device_count() == 0:
         pytest.skip("no HIP device visible")
     return True
+
+
+def pytest_collection_modifyitems(config, items):
+    """Run test_gpu_fullsize.py (one test per BASELINE config at its full size) first, then the
+    rest in file order: a round-end run cut short still has covered every config."""
+    first = [it for it in items if it.fspath.basename == "test_gpu_fullsize.py"]
+    if first:
+        rest = [it for it in items if it.fspath.basename != "test_gpu_fullsize.py"]
+        items[:] = first + rest

@@ -281,3 +281,64 @@ def test_dist_cg_graph_matches_eager(tmp_path, split):
                 assert np.array_equal(e.view(np.uint8), gr.view(np.uint8)), (f, L, rep)
         it, st = np.load(res["1"] / f"m_{L}_0.npy")
         assert st == 0 and it > 24, (L, it)  # 8-iteration batches: the graph replayed several times
+
+
+def test_dist_shared_comm(orc):
+    """Several sharded matrices on ONE communicator (mspmv.Comm, the bench's N > 1 form): every
+    object's kernels and collectives run on the communicator's one stream, interleaved calls on two
+    matrices give each its own oracle result, the CG on each matches the oracle, and the
+    communicator refuses to close while a matrix still uses it."""
+    import mspmv
+    a1 = _matrix()
+    a2 = mspmv.CsrMatrix.synth_fem_blocked(36000, 36000 * 53, 6, 340, seed=3)
+    comm = mspmv.Comm(mspmv.comm_unique_id(), 1, 0, 0)
+    ds, Xs, dYs = [], [], []
+    for a in (a1, a2):
+        rb = mspmv.dist_partition(a, 1)
+        ds.append(mspmv.DistCsr(comm, rb, mspmv.local_rows(a, rb, 0)))
+        Xs.append(np.random.default_rng(a.num_rows).uniform(-1, 1, (a.num_rows, 4)))
+        dYs.append(mspmv.DeviceBuffer(8 * a.num_rows * 4))
+    with pytest.raises(mspmv.MspmvError):
+        comm.close()
+    dXs = [mspmv.DeviceBuffer.from_array(X) for X in Xs]
+    for _ in range(3):  # interleaved, no sync in between (the stream orders them)
+        for d, dX, dY in zip(ds, dXs, dYs):
+            d.spmm_dev(dX, dY, 4, sync=False)
+    ds[0].sync()
+    for a, X, dY in zip((a1, a2), Xs, dYs):
+        np.testing.assert_allclose(dY.download((a.num_rows, 4)), orc.csr_spmm_t(a, X), rtol=1e-13, atol=1e-13)
+    B = np.random.default_rng(9).uniform(0, 1, (a1.num_rows, 8))
+    dB, dX = mspmv.DeviceBuffer.from_array(B), mspmv.DeviceBuffer(8 * a1.num_rows * 8)
+    it, hist, st = ds[0].cg_dev(dB, dX, 8, 3000, 1e-9, hist_cap=3000)
+    Xo, it_o, ho = orc.cg_multi(a1, B, 3000, 1e-9, kernel=1, P=8, hist_cap=3000)
+    assert st == 0 and abs(it - it_o) <= 1
+    k = min(len(hist), len(ho))
+    np.testing.assert_allclose(hist[:k], ho[:k], rtol=0, atol=1e-10)
+    for d in ds:
+        d.close()
+    comm.close()
+
+
+_L2_CHILD = r"""
+import sys
+sys.path[:0] = [sys.argv[1]]
+import mspmv
+a = mspmv.CsrMatrix.synth_fem_blocked(21792, 1152443, 6, 170, seed=3)
+with mspmv.GpuCsr(a) as g:
+    print("NAMES", g.kernel_name(), g.spmm_kernel_name(2), g.spmm_kernel_name(16))
+"""
+
+
+@pytest.mark.parametrize("knob", ["1", "0"])
+def test_spmm_blk_knob_names_kernel(knob):
+    """MSPMV_SPMM_BLK=0 takes every L > 1 off the node-block SpMM -- L = 2 too, whose merge tiles
+    have the single-RHS tile size and so share that plan -- and mspmv_spmm_kernel_name reports the
+    kernel each width launches (the single-RHS SpMV keeps its node-block kernel either way)."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-c", _L2_CHILD, os.path.join(ROOT, "sparse-matrix-linear-equations_amd")],
+                       env=dict(os.environ, MSPMV_SPMM_BLK=knob), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    spmv, l2, l16 = r.stdout.split("NAMES", 1)[1].split()
+    assert spmv.startswith(("k_spmv_blk", "k_spmv_runs"))
+    want = "k_spmm_blk<" if knob == "1" else "k_spmm_tile<"
+    assert l2.startswith(want + "2,") and l16.startswith(want + "16,"), (l2, l16)
