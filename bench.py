@@ -644,8 +644,10 @@ def main():
             rd = mspmv.time_stream_read(dev, 1 << 30, 20)
             result["roofline"]["measured_read_GBps"] = round(rd, 1)
             result["roofline"]["frac_of_measured_read"] = round(achieved / rd, 4) if rd > 0 else None
-            result["roofline"]["measured_read_note"] = ("STREAM-like nontemporal read of 1 GiB (> the 256 MiB "
-                                                        "Infinity Cache), 20 passes, HIP events")
+            result["roofline"]["measured_read_note"] = ("nontemporal read of 1 GiB (> the 256 MiB Infinity Cache), "
+                                                        "one contiguous slice per workgroup, 4 workgroups per CU, "
+                                                        "20 passes, HIP events (the best of the read shapes in "
+                                                        "tools/read_ceiling.hip)")
         if hot_ms is not None:
             result["hot_single_matrix"] = {"ms_per_call": round(hot_ms, 5), "kernel_ms": round(hot_kern, 5),
                                            "GBps_vs_algorithmic": round(bytes_launch / (hot_kern * 1e-3) / 1e9, 1),

@@ -225,7 +225,8 @@ MSPMV_API mspmv_status mspmv_time_spmm_batch_dev(int count, const mspmv_handle *
                                                  double *tile_kernel_ms, int *kernels_per_step);
 /* The practical HBM ceiling the roofline fraction is read against: a STREAM-like
  * nontemporal read of a `bytes` buffer (>= 1 MiB; use >> 256 MiB so the Infinity Cache cannot hold
- * it) on `device`, `reps` timed passes after one warm-up, HIP events around the timed region.
+ * it) on `device`, one contiguous slice per workgroup (the fastest read shape measured: ~6.9 TB/s
+ * at 1 GiB), `reps` timed passes after one warm-up, HIP events around the timed region.
  * *gbps = bytes x reps / time. */
 MSPMV_API mspmv_status mspmv_time_stream_read(int device, size_t bytes, int reps, double *gbps);
 /* Per-kernel average duration (ms) of the dominant (merge tile) kernel over the last

@@ -384,10 +384,20 @@ static mspmv_status check_offsets_host(const int *ro, int m, int nnz)
     return MSPMV_OK;
 }
 
+// view_of: a row range of another handle on the same device -- a->row_offsets (host, rebased to 0)
+// are uploaded, the columns and values are the parent's from nonzero view_off on (not copied, not
+// owned; the parent validated them), a->column_indices / values are ignored.
 static mspmv_status create_common(const mspmv_csr_d *a, int device, bool from_device, mspmv_handle *out,
-                                  hipStream_t on_stream = nullptr)
+                                  hipStream_t on_stream = nullptr, const mspmv_handle_s *view_of = nullptr,
+                                  long long view_off = 0)
 {
-    ST_TRY(validate_host_csr(a));
+    if (view_of) {
+        if (!a || a->num_rows < 0 || a->num_nonzeros < 0 || !a->row_offsets || view_off < 0 ||
+            view_off + a->num_nonzeros > view_of->nnz || a->num_cols != view_of->n)
+            return invalid("row-range view outside its parent");
+    } else {
+        ST_TRY(validate_host_csr(a));
+    }
     if (!out)
         return invalid("null out handle");
     *out = nullptr;
@@ -423,13 +433,20 @@ static mspmv_status create_common(const mspmv_csr_d *a, int device, bool from_de
     // Column / value arrays are padded (zero column index, zero value) so the kernels' aligned
     // 16-byte group reads past the last nonzero stay inside the allocation.
     const size_t padded = (size_t)h->nnz + kNnzPad;
-    if ((st = dev_alloc(&h->d_row_offsets, (size_t)h->m + 1)) != MSPMV_OK ||
-        (st = dev_alloc(&h->d_cols, padded)) != MSPMV_OK || (st = dev_alloc(&h->d_vals, padded)) != MSPMV_OK)
+    if ((st = dev_alloc(&h->d_row_offsets, (size_t)h->m + 1)) != MSPMV_OK)
         return fail(st);
-    if (hipMemset(h->d_cols, 0, sizeof(int) * padded) != hipSuccess ||
-        hipMemset(h->d_vals, 0, sizeof(double) * padded) != hipSuccess) {
-        set_error("hipMemset of padded CSR arrays failed");
-        return fail(MSPMV_ERR_HIP);
+    if (view_of) {  // the parent's arrays (padded past its last nonzero, so past this range's too)
+        h->own_arrays = false;
+        h->d_cols = view_of->d_cols + view_off;
+        h->d_vals = view_of->d_vals + view_off;
+    } else {
+        if ((st = dev_alloc(&h->d_cols, padded)) != MSPMV_OK || (st = dev_alloc(&h->d_vals, padded)) != MSPMV_OK)
+            return fail(st);
+        if (hipMemset(h->d_cols, 0, sizeof(int) * padded) != hipSuccess ||
+            hipMemset(h->d_vals, 0, sizeof(double) * padded) != hipSuccess) {
+            set_error("hipMemset of padded CSR arrays failed");
+            return fail(MSPMV_ERR_HIP);
+        }
     }
     const hipMemcpyKind kind = from_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     std::vector<int> host_ro;
@@ -445,12 +462,13 @@ static mspmv_status create_common(const mspmv_csr_d *a, int device, bool from_de
     if ((st = check_offsets_host(ro, h->m, h->nnz)) != MSPMV_OK)
         return fail(st);
     if (hipMemcpy(h->d_row_offsets, a->row_offsets, sizeof(int) * (h->m + 1), kind) != hipSuccess ||
-        (h->nnz && hipMemcpy(h->d_cols, a->column_indices, sizeof(int) * (size_t)h->nnz, kind) != hipSuccess) ||
-        (h->nnz && hipMemcpy(h->d_vals, a->values, sizeof(double) * (size_t)h->nnz, kind) != hipSuccess)) {
+        (!view_of && h->nnz &&
+         hipMemcpy(h->d_cols, a->column_indices, sizeof(int) * (size_t)h->nnz, kind) != hipSuccess) ||
+        (!view_of && h->nnz && hipMemcpy(h->d_vals, a->values, sizeof(double) * (size_t)h->nnz, kind) != hipSuccess)) {
         set_error("CSR upload failed");
         return fail(MSPMV_ERR_HIP);
     }
-    if (h->nnz) {  // column range check on the device (a bad index would fault a gather)
+    if (h->nnz && !view_of) {  // column range check on the device (a bad index would fault a gather)
         int *d_bad = nullptr;
         if ((st = dev_alloc(&d_bad, 1)) != MSPMV_OK)
             return fail(st);
@@ -557,6 +575,19 @@ mspmv_status mspmv::csr_create_on_stream(const mspmv_csr_d *host, int device, hi
     return create_common(host, device, false, out, stream);
 }
 
+mspmv_status mspmv::csr_create_view(mspmv_handle parent, int row_lo, int row_hi, const int *host_row_offsets,
+                                    mspmv_handle *out)
+{
+    if (!parent || row_lo < 0 || row_hi < row_lo || row_hi > parent->m || !host_row_offsets)
+        return invalid("csr_create_view: bad row range");
+    const long long off = host_row_offsets[row_lo];
+    std::vector<int> ro((size_t)(row_hi - row_lo) + 1);
+    for (int r = row_lo; r <= row_hi; ++r)
+        ro[(size_t)(r - row_lo)] = (int)(host_row_offsets[r] - off);
+    const mspmv_csr_d v{row_hi - row_lo, parent->n, ro.back(), ro.data(), nullptr, nullptr};
+    return create_common(&v, parent->device, false, out, nullptr, parent, off);
+}
+
 extern "C" {
 
 mspmv_status mspmv_destroy(mspmv_handle h)
@@ -569,8 +600,10 @@ mspmv_status mspmv_destroy(mspmv_handle h)
     for (auto &kv : h->plans)
         free_plan(kv.second);
     dev_free(h->d_row_offsets);
-    dev_free(h->d_cols);
-    dev_free(h->d_vals);
+    if (h->own_arrays) {
+        dev_free(h->d_cols);
+        dev_free(h->d_vals);
+    }
     dev_free(h->d_r);
     dev_free(h->d_p0);
     dev_free(h->d_p1);

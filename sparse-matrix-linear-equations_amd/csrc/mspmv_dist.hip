@@ -391,16 +391,12 @@ mspmv_status mspmv_dist_create_on(mspmv_comm c, const int *row_begin, const mspm
         if (force || 2LL * (ro[best_hi] - ro[best_lo]) >= (long long)nnz) {
             d->int_lo = best_lo;
             d->int_hi = best_hi;
+            // the parts are row-range views of the local handle: their own row offsets, streams and
+            // plans, the local handle's columns and values (no second copy of the matrix)
             const int cut[4] = {0, best_lo, best_hi, d->n_own};
-            for (int q = 0; q < 3; ++q) {
-                std::vector<int> pro((size_t)(cut[q + 1] - cut[q]) + 1);
-                for (int r = cut[q]; r <= cut[q + 1]; ++r)
-                    pro[(size_t)(r - cut[q])] = ro[r] - ro[cut[q]];
-                mspmv_csr_d pc{cut[q + 1] - cut[q], lc.num_cols, ro[cut[q + 1]] - ro[cut[q]], pro.data(),
-                               lcols.data() + ro[cut[q]], local_rows->values + ro[cut[q]]};
-                if ((st = mspmv_csr_create(&pc, device, &d->part[q])) != MSPMV_OK)
+            for (int q = 0; q < 3; ++q)
+                if ((st = csr_create_view(d->local, cut[q], cut[q + 1], ro, &d->part[q])) != MSPMV_OK)
                     return bail(st);
-            }
             for (auto &e : d->ev)
                 if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
                     return bail(fail_msg(MSPMV_ERR_HIP, "dist_create: hipEventCreate"));

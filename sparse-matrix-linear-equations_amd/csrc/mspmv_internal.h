@@ -104,6 +104,7 @@ struct mspmv_handle_s {
     int num_cus = 256;
     hipStream_t stream = nullptr;
     bool own_stream = true;  // false: a shared CU-masked stream (mspmv_set_cu_limit)
+    bool own_arrays = true;  // false: d_cols / d_vals are a row range of another handle's (csr_create_view)
     int m = 0, n = 0, nnz = 0;
     int *d_row_offsets = nullptr;
     int *d_cols = nullptr;
@@ -284,6 +285,11 @@ hipError_t launch_fold_dot(int T, int L, double *partials, unsigned *gtickets, d
 mspmv_status plan_for(mspmv_handle_s *h, int L, const TilePlan **out);
 // mspmv_csr_create on a stream the caller owns (kept; the handle never destroys it)
 mspmv_status csr_create_on_stream(const mspmv_csr_d *host, int device, hipStream_t stream, mspmv_handle *out);
+// Rows [row_lo, row_hi) of `parent` as a handle of their own (own stream, row offsets and plans) whose
+// columns and values ARE the parent's (no copy; destroy it before the parent).  host_row_offsets: the
+// parent's row offsets on the host.
+mspmv_status csr_create_view(mspmv_handle parent, int row_lo, int row_hi, const int *host_row_offsets,
+                             mspmv_handle *out);
 // SPAI-preconditioned block CG (SPAISolveMultiple, work_2025/main/sparse_approximate_inverse.hpp:
 // 30-230) on A's handle h with the preconditioner's handle hm (same shape and device): init
 // (X = 0, R = B, Z = M R, P = Z, rs_old = R.Z) and one iteration (AP = A P -> alpha; X, R update

@@ -2210,11 +2210,20 @@ __device__ __forceinline__ double2 rows8_sum2(const double2 (&p)[kBlkRows])
 #endif
 // KR: the plan's tallest run (rows of one node, <= kBlkRows); KR = 6 (6-DOF FEM such as pwtk)
 // holds fewer accumulator and value registers than 8.
-template <int L, int MODE, bool NT, int KR = kBlkRows>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MSPMV_SPMM_BLK_WAVES > 0 ? MSPMV_SPMM_BLK_WAVES : 1))) void
+#if MSPMV_LAB_ABLATE == 10  // lab build only (tools/lab/stamps_blk.py): per-chunk phase stamps of k_spmm_blk
+constexpr int kLabBlkSlots = 1 << 16;  // (tile, wave, round) slots: 8 stamps each
+__device__ unsigned long long g_lab_blk[kLabBlkSlots * 8];
+#endif
+// TB = 64 (plain SpMM only): one wave per workgroup, workgroup b takes wave slot b % 4 of tile
+// b / 4 (XCD-contiguous over the 4 T slots), so a wave's slot frees as soon as ITS chunks are done
+// instead of when the tile's slowest wave is (a tile holds ~6 chunks over 4 waves: 2 rounds, 75 %
+// of the wave slots busy).
+template <int L, int MODE, bool NT, int KR = kBlkRows, int TB = kBlock>
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MSPMV_SPMM_BLK_WAVES > 0 ? MSPMV_SPMM_BLK_WAVES : 1))) void
 k_spmm_blk(TileArgs a)
 {
     static_assert(MODE != kModeCg, "multi-RHS CG runs the split iteration (MODE 2)");
+    static_assert(TB == kBlock || MODE == kModeSpmv, "one-wave workgroups run the plain SpMM only");
     constexpr int GL = L / 2;      // lanes per panel row
     constexpr int NGW = 64 / GL;   // column groups per wave = pattern columns per pass
 #ifndef MSPMV_SPMM_BLK_PB
@@ -2225,6 +2234,9 @@ k_spmm_blk(TileArgs a)
     // every width (L = 16: 72.4-73.1 vs 74.4-74.8 us at 4 and 89.4 at 8; L = 4: 40-41 vs 50-51 and
     // 65 us; r02ah).  Fused multiply-adds instead of the guarded mul + add measured slower.
     constexpr int PB = MSPMV_SPMM_BLK_PB > 0 ? MSPMV_SPMM_BLK_PB : 2;
+#ifndef MSPMV_SPMM_BLK_FMA
+#define MSPMV_SPMM_BLK_FMA 1  // lab builds: 0 keeps the guarded multiply + add on every pass
+#endif
     __shared__ double2 s_red2[MODE == kModeDot ? kBlock / 64 : 1][GL];
 #ifndef MSPMV_SPMM_BLK_LDSV
 #define MSPMV_SPMM_BLK_LDSV 1
@@ -2233,18 +2245,20 @@ k_spmm_blk(TileArgs a)
     // own LDS slice, and a pass reads v[i][j] there (one broadcast read per (pass, row)) instead of
     // holding the rows in registers and shuffling them (two bpermutes per (pass, row))
     constexpr bool LDSV = MSPMV_SPMM_BLK_LDSV != 0;
-    __shared__ double s_v[LDSV ? kBlock / 64 : 1][LDSV ? kBlkRows : 1][64];
-    __shared__ int s_c[LDSV ? kBlock / 64 : 1][64];
+    __shared__ double s_v[LDSV ? TB / 64 : 1][LDSV ? kBlkRows : 1][64];
+    __shared__ int s_c[LDSV ? TB / 64 : 1][64];
     const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
     const int tid = threadIdx.x, lane = tid & 63;
     const int g = lane / GL, c = lane % GL;
-    const int t = xcd_tile(blockIdx.x, a.num_tiles);
+    const int slot = TB == kBlock ? 0 : xcd_tile(blockIdx.x, a.num_tiles * (kBlock / 64));
+    const int t = TB == kBlock ? xcd_tile(blockIdx.x, a.num_tiles) : slot / (kBlock / 64);
     const int2 b0 = a.bounds[t];
     const int r0 = b0.x, n0 = b0.y;
     const int colbase = a.colbase[t];
     const uint4 bd = lane < a.blk_stride ? a.blk[(size_t)t * a.blk_stride + lane] : make_uint4(0u, 0u, 0u, 0u);
     const int nd = (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u);
-    const int wave = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const int wave = TB == kBlock ? __builtin_amdgcn_readfirstlane((int)(tid >> 6)) : 0;  // LDS slice
+    const int wslot = TB == kBlock ? wave : slot % (kBlock / 64);                         // chunk slot
     double2 dot = make_double2(0.0, 0.0);
     // lane j: P[j] and the run's values in column j of chunk di, one coalesced load per row
     auto fetch = [&](int di, int &cj, double (&vr)[KR]) {
@@ -2272,9 +2286,16 @@ k_spmm_blk(TileArgs a)
     constexpr bool PF = LDSV && MSPMV_SPMM_BLK_PF != 0;
     int colj_n = 0;
     double vrow_n[KR];
-    if (PF && wave < nd && !stopped)
-        fetch(wave, colj_n, vrow_n);
-    for (int di = wave; di < nd && !stopped; di += kBlock / 64) {  // wave-uniform
+    if (PF && wslot < nd && !stopped)
+        fetch(wslot, colj_n, vrow_n);
+    for (int di = wslot; di < nd && !stopped; di += kBlock / 64) {  // wave-uniform
+#if MSPMV_LAB_ABLATE == 10
+        const int lab_slot = (t * 4 + wslot) * 2 + (di >= kBlock / 64 ? 1 : 0);
+        unsigned long long *lab = g_lab_blk + (size_t)lab_slot * 8;
+        const bool lab_on = lab_slot < kLabBlkSlots && lane == 0 && di < 2 * (kBlock / 64) && MODE == kModeSpmv;
+        if (lab_on)
+            lab[0] = wall_clock64();
+#endif
         const uint4 d = blk_read(bd, di);
         const int wc = d.x >> 24;
         const int h = d.y & 15, rofs = d.y >> 16;
@@ -2288,6 +2309,17 @@ k_spmm_blk(TileArgs a)
         } else {
             fetch(di, colj, vrow);
         }
+#ifndef MSPMV_SPMM_BLK_XPF
+#define MSPMV_SPMM_BLK_XPF 1
+#endif
+        // X prefetch: one 8-B load per pattern column (lane j: row P[j]), issued behind the values,
+        // so the chunk's panel rows come into L2 while the values arrive.  A panel row a tile's XCD
+        // has not read yet (~1 in 5 of the gathers) would otherwise cost one Infinity-Cache round
+        // trip in nearly every pass round (a round's 8 rows rarely all hit): per-chunk stamps put
+        // the passes at 6 of 8.6 us per chunk (r03e).  Consumed (kept live) after the passes.
+        double xpf = 0.0;
+        if (MSPMV_SPMM_BLK_XPF && lane < wc)
+            xpf = a.x[(size_t)colj * a.ld];
         if constexpr (LDSV) {  // wave-private slice: the wave's LDS operations stay in order
             s_c[wave][lane] = colj;
 #pragma unroll
@@ -2295,6 +2327,10 @@ k_spmm_blk(TileArgs a)
                 if (i < h)
                     s_v[wave][i][lane] = vrow[i];
             __builtin_amdgcn_wave_barrier();
+#if MSPMV_LAB_ABLATE == 10
+            if (lab_on)
+                lab[1] = wall_clock64();
+#endif
             if (PF && di + kBlock / 64 < nd)
                 fetch(di + kBlock / 64, colj_n, vrow_n);
         }
@@ -2326,13 +2362,38 @@ k_spmm_blk(TileArgs a)
                     if (i >= h || jb >= len)  // wave-uniform: row i has no column in this pass
                         continue;
                     const double v = LDSV ? s_v[wave][i][j & 63] : __shfl(vrow[i], j & 63);
-                    const bool on = j < len;
-                    acc[i].x += on ? v * xv[q].x : 0.0;
-                    acc[i].y += on ? v * xv[q].y : 0.0;
+                    if (MSPMV_SPMM_BLK_FMA && jb + NGW <= len) {
+                        // every column of the pass is in row i (wave-uniform): one fused
+                        // multiply-add per component, no select (the node rows are summed by a
+                        // lane tree, so they are held to the reordering bound, which an FMA's
+                        // single rounding only tightens)
+                        acc[i].x = __builtin_fma(v, xv[q].x, acc[i].x);
+                        acc[i].y = __builtin_fma(v, xv[q].y, acc[i].y);
+                    } else {
+                        const bool on = j < len;
+                        acc[i].x += on ? v * xv[q].x : 0.0;
+                        acc[i].y += on ? v * xv[q].y : 0.0;
+                    }
                 }
             }
         }
+#if MSPMV_LAB_ABLATE == 10
+        if (lab_on) {
+            lab[2] = wall_clock64();
+            lab[5] = (unsigned long long)wc | ((unsigned long long)h << 8) | ((unsigned long long)nd << 16);
+        }
+#endif
+        if (MSPMV_SPMM_BLK_XPF)
+            asm volatile("" ::"v"(xpf));
         const double2 row = rows8_sum2<GL>(acc);
+#if MSPMV_LAB_ABLATE == 10
+        if (lab_on) {
+            lab[3] = wall_clock64();
+            unsigned hw;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            lab[4] = hw;
+        }
+#endif
         if (store) {
             *reinterpret_cast<double2 *>(a.y + (size_t)(r0 + rofs + ri) * a.ld + 2 * c) = row;
             if (MODE == kModeDot) {
@@ -3093,19 +3154,38 @@ __global__ void k_flush(double *p, long long n, double v)
 }
 // STREAM-like read of n2 16-byte words (the practical HBM ceiling the roofline is read against,
 // SURVEY 8(d)): grid-stride, four nontemporal 16-B loads in flight per thread per step.
+// The practical HBM read ceiling (bench `roofline.measured_read_GBps`): every workgroup streams ONE
+// contiguous slice of the buffer with nontemporal 16-B loads, two register stages of 8 loads per
+// lane in flight.  Measured on MI355X (tools/read_ceiling.hip, r03b), 1 GiB per launch: 6.89-6.90
+// TB/s for this shape at 4 or 8 workgroups per CU, against 5.5-5.6 TB/s for the grid-stride loop
+// used before (which every workgroup walks across the whole buffer) and 6.4-6.7 TB/s for LDS-DMA.
 __global__ __launch_bounds__(kBlock) void k_stream_read(const double2 *p, long long n2, double *sink)
 {
+    constexpr int U = 8;
+    const long long per = (n2 + gridDim.x - 1) / gridDim.x;
+    const long long b = (long long)blockIdx.x * per;
+    const long long e = b + per < n2 ? b + per : n2;
+    const long long step = (long long)kBlock * U;
+    auto ld = [&](long long i) { return i < e ? ld_stream<true>(p + i) : make_double2(0.0, 0.0); };
     double acc = 0.0;
-    const long long stride = (long long)gridDim.x * kBlock;
-    long long i = (long long)blockIdx.x * kBlock + threadIdx.x;
-    for (; i + 3 * stride < n2; i += 4 * stride) {
-        const double2 a = ld_stream<true>(p + i), b = ld_stream<true>(p + i + stride);
-        const double2 c = ld_stream<true>(p + i + 2 * stride), d = ld_stream<true>(p + i + 3 * stride);
-        acc += (a.x + b.x) + (c.x + d.x) + (a.y + b.y) + (c.y + d.y);
-    }
-    for (; i < n2; i += stride) {
-        const double2 a = ld_stream<true>(p + i);
-        acc += a.x + a.y;
+    double2 t0[U], t1[U];
+    long long i = b + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        t0[u] = ld(i + u * kBlock);
+    for (i += step; i < e + step; i += 2 * step) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            t1[u] = ld(i + u * kBlock);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            acc += t0[u].x + t0[u].y;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            t0[u] = ld(i + step + u * kBlock);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            acc += t1[u].x + t1[u].y;
     }
     if (acc == -1.0)  // never (the buffer holds zeros): keeps the loads live without a store
         *sink = acc;
@@ -3114,7 +3194,7 @@ __global__ __launch_bounds__(kBlock) void k_stream_read(const double2 *p, long l
 hipError_t launch_stream_read(const double *p, size_t bytes, int num_cus, hipStream_t s)
 {
     const long long n2 = (long long)(bytes / 16);
-    hipLaunchKernelGGL(k_stream_read, dim3((unsigned)std::max(1, num_cus * 8)), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL(k_stream_read, dim3((unsigned)std::max(1, num_cus * 4)), dim3(kBlock), 0, s,
                        reinterpret_cast<const double2 *>(p), n2, const_cast<double *>(p));
     return hipGetLastError();
 }
@@ -3150,6 +3230,7 @@ struct SpmvTuning {
     int blkreg = 1;   // plans of register node-block tiles only run the LDS-free k_spmv_blk
     int runs = 0;     // ... or, for the plain SpMV, the persistent wave-pipelined k_spmv_runs
     int spmm_blk = 1; // SpMM (L >= 2) on such a plan runs k_spmm_blk instead of its own L-wide tiles
+    int spmm_blk_tb = 256;  // k_spmm_blk workgroup size for the plain SpMM: 256 (one tile) or 64 (one wave)
     int early_re = 0; // single-RHS tile kernel: row ends issued with the stream (TileArgs::early_re)
     int dict = 1;     // single-RHS SpMV through per-tile column dictionaries (k_build_dict) when
                       // a tile's nonzeros repeat its distinct columns >= dict_ratio times (0: off)
@@ -3188,6 +3269,8 @@ static const SpmvTuning &spmv_tuning()
             v.runs = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMM_BLK"))
             v.spmm_blk = atoi(e) != 0;
+        if (const char *e = getenv("MSPMV_SPMM_BLK_TB"))
+            v.spmm_blk_tb = atoi(e) == 64 ? 64 : 256;
         if (const char *e = getenv("MSPMV_SPMV_EARLY_RE"))
             v.early_re = atoi(e);
         if (const char *e = getenv("MSPMV_SPMV_DICT"))
@@ -3243,7 +3326,8 @@ std::string spmm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan, int 
     const std::string nt = stream_nt(h) ? "true" : "false";
     const SpmvTuning &t = spmv_tuning();
     if (plan.d_blk && plan.num_tiles_reg == plan.num_tiles && t.blkreg && t.tb == kBlock && spmm_blk_enabled())
-        return "k_spmm_blk<" + std::to_string(L) + ",0," + nt + (plan.blk_rows_max <= 6 ? ",6>" : ",8>");
+        return "k_spmm_blk<" + std::to_string(L) + ",0," + nt + (plan.blk_rows_max <= 6 ? ",6" : ",8") +
+               (t.spmm_blk_tb == 64 ? ",64>" : ">");
     const int iptg = spmm_iptg_for(L);
     const bool dict = L == 16 && iptg != 32 && plan.d_dict;
     return "k_spmm_tile<" + std::to_string(L) + "," + std::to_string(iptg) + ",0," + nt + (dict ? ",true>" : ">");
@@ -3512,7 +3596,19 @@ static void launch_spmm_L(const TileArgs &a, hipStream_t s, bool nt)
 #ifndef MSPMV_SPMM_BLK_KR6
 #define MSPMV_SPMM_BLK_KR6 1  // lab builds: 0 runs the 8-row kernel on every plan
 #endif
-            if (MSPMV_SPMM_BLK_KR6 && a.blk_rows_max <= 6) {
+            if (MODE == kModeSpmv && spmv_tuning().spmm_blk_tb == 64) {
+                const dim3 g1((unsigned)a.num_tiles * (kBlock / 64));
+                if (a.blk_rows_max <= 6) {
+                    if (nt)
+                        hipLaunchKernelGGL((k_spmm_blk<LL, kModeSpmv, true, 6, 64>), g1, dim3(64), 0, s, a);
+                    else
+                        hipLaunchKernelGGL((k_spmm_blk<LL, kModeSpmv, false, 6, 64>), g1, dim3(64), 0, s, a);
+                } else if (nt) {
+                    hipLaunchKernelGGL((k_spmm_blk<LL, kModeSpmv, true, kBlkRows, 64>), g1, dim3(64), 0, s, a);
+                } else {
+                    hipLaunchKernelGGL((k_spmm_blk<LL, kModeSpmv, false, kBlkRows, 64>), g1, dim3(64), 0, s, a);
+                }
+            } else if (MSPMV_SPMM_BLK_KR6 && a.blk_rows_max <= 6) {
                 if (nt)
                     hipLaunchKernelGGL((k_spmm_blk<LL, MODE, true, 6>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
                 else
@@ -4380,6 +4476,12 @@ hipError_t launch_pcg_ic0_iteration(mspmv_handle_s *h, mspmv_ic0_s *ic, const Ti
 
 }  // namespace mspmv
 
+#if MSPMV_LAB_ABLATE == 10
+extern "C" __attribute__((visibility("default"))) int mspmv_lab_blk_stamps(unsigned long long *host, int slots)
+{
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mspmv::g_lab_blk), sizeof(unsigned long long) * 8 * slots);
+}
+#endif
 #if MSPMV_LAB_ABLATE == 9
 extern "C" __attribute__((visibility("default"))) int mspmv_lab_stamps(unsigned long long *host, int tiles)
 {

@@ -2,7 +2,12 @@
 # One GPU-box session: smoke -> GPU parity tests -> bench -> rocprofv3 kernel-trace summary.
 # Every GPU step has its own time limit; a crash / abort / timeout (anything but exit 0 or a
 # plain test failure, exit 1) ends the session so nothing else touches a possibly-faulted GPU.
-#   usage: tools/gpu_session.sh TAG [steps...]   steps: smoke tests bench prof pmc
+#   usage: tools/gpu_session.sh TAG [steps...]
+#   steps: smoke tests bench prof pmc readceil
+#          legs:LEG[,LEG]            tools/profile_legs.sh (kernel trace + FETCH/WRITE passes per bench leg)
+#          counters:LEG:REGEX        tools/pmc_passes.sh on `bench.py --only LEG` for kernels matching REGEX
+#          pytest:PATH                one test file / node id, -m gpu
+#          py:SCRIPT[:ARGS]          a lab script (python3 SCRIPT ARGS, 300 s limit)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 TAG=${1:-run}
@@ -42,6 +47,24 @@ for s in $STEPS; do
         timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write" -o bench \
             -- python3 bench.py --no-cpu --no-cg --no-extras >"$OUT/pmc_write.json" 2>"$OUT/pmc_write.err"
         rc=$?; echo "pmc write rc=$rc"; stop_unless_ok $rc pmc_write ;;
+    pytest:*)
+        timeout -k 10 900 python -m pytest ${s#pytest:} -m gpu -q -p no:cacheprovider -rf >"$OUT/pytest_sel.log" 2>&1
+        rc=$?; echo "pytest ${s#pytest:} rc=$rc"; tail -15 "$OUT/pytest_sel.log"; stop_unless_ok $rc pytest ;;
+    readceil)
+        [ -x tools/read_ceiling ] || /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o tools/read_ceiling tools/read_ceiling.hip
+        timeout -k 10 300 tools/read_ceiling >"$OUT/read_ceiling.txt" 2>&1
+        rc=$?; echo "readceil rc=$rc"; cat "$OUT/read_ceiling.txt"; stop_unless_ok $rc readceil ;;
+    legs:*)
+        timeout -k 10 900 bash tools/profile_legs.sh "$TAG" $(echo "${s#legs:}" | tr , ' ')
+        rc=$?; echo "legs rc=$rc"; stop_unless_ok $rc legs ;;
+    counters:*)
+        spec=${s#counters:}; leg=${spec%%:*}; re=${spec#*:}
+        timeout -k 10 1200 bash tools/pmc_passes.sh "$OUT/counters_$leg" "$re" -- python3 bench.py --only "$leg" --no-cpu
+        rc=$?; echo "counters $leg rc=$rc"; stop_unless_ok $rc counters ;;
+    py:*)
+        spec=${s#py:}; script=${spec%%:*}; args=""; [ "$spec" != "$script" ] && args=$(echo "${spec#*:}" | tr , ' ')
+        timeout -k 10 300 python3 -u "$script" $args >"$OUT/$(basename "$script" .py).txt" 2>&1
+        rc=$?; echo "py $script rc=$rc"; tail -40 "$OUT/$(basename "$script" .py).txt"; stop_unless_ok $rc py ;;
     *)
         echo "unknown step $s"; exit 2 ;;
     esac
