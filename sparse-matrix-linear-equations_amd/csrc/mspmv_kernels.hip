@@ -2203,27 +2203,29 @@ __device__ __forceinline__ double2 rows8_sum2(const double2 (&p)[kBlkRows])
     return v;
 }
 
-// Waves per SIMD k_spmm_blk is compiled for (0: unconstrained, 96 VGPRs at L = 16 -> 5 waves);
-// a lab build can ask for more (-DMSPMV_SPMM_BLK_WAVES=6 or 7).
+// Waves per SIMD k_spmm_blk is compiled for: 8 (<= 64 VGPRs; with the pass fence below the L = 16
+// kernel takes 60 and spills nothing).  Unconstrained the straight-line passes take 82 VGPRs (6
+// waves): pwtk L = 16 58.5 vs 51-52 us hot at 8 waves (r03g).  0 = unconstrained (lab builds).
 #ifndef MSPMV_SPMM_BLK_WAVES
-#define MSPMV_SPMM_BLK_WAVES 0
+#define MSPMV_SPMM_BLK_WAVES 8
 #endif
+// The instantiations that fit 64 VGPRs without spilling (plain SpMM, runs of <= 6 rows, L >= 4);
+// the others (L = 2, 8-row runs, dot mode) stay unconstrained rather than spill.
+constexpr int spmm_blk_waves(int L, int MODE, int KR)
+{
+    return MSPMV_SPMM_BLK_WAVES > 0 && MODE == 0 && KR <= 6 && L >= 4 ? MSPMV_SPMM_BLK_WAVES : 1;
+}
 // KR: the plan's tallest run (rows of one node, <= kBlkRows); KR = 6 (6-DOF FEM such as pwtk)
 // holds fewer accumulator and value registers than 8.
 #if MSPMV_LAB_ABLATE == 10  // lab build only (tools/lab/stamps_blk.py): per-chunk phase stamps of k_spmm_blk
 constexpr int kLabBlkSlots = 1 << 16;  // (tile, wave, round) slots: 8 stamps each
 __device__ unsigned long long g_lab_blk[kLabBlkSlots * 8];
 #endif
-// TB = 64 (plain SpMM only): one wave per workgroup, workgroup b takes wave slot b % 4 of tile
-// b / 4 (XCD-contiguous over the 4 T slots), so a wave's slot frees as soon as ITS chunks are done
-// instead of when the tile's slowest wave is (a tile holds ~6 chunks over 4 waves: 2 rounds, 75 %
-// of the wave slots busy).
-template <int L, int MODE, bool NT, int KR = kBlkRows, int TB = kBlock>
-__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(MSPMV_SPMM_BLK_WAVES > 0 ? MSPMV_SPMM_BLK_WAVES : 1))) void
+template <int L, int MODE, bool NT, int KR = kBlkRows>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(spmm_blk_waves(L, MODE, KR)))) void
 k_spmm_blk(TileArgs a)
 {
     static_assert(MODE != kModeCg, "multi-RHS CG runs the split iteration (MODE 2)");
-    static_assert(TB == kBlock || MODE == kModeSpmv, "one-wave workgroups run the plain SpMM only");
     constexpr int GL = L / 2;      // lanes per panel row
     constexpr int NGW = 64 / GL;   // column groups per wave = pattern columns per pass
 #ifndef MSPMV_SPMM_BLK_PB
@@ -2233,7 +2235,9 @@ k_spmm_blk(TileArgs a)
     // registers (before LDSV) 4 was best at L = 16 and 2 at L = 4, 8 (r02z); with LDSV 2 is best at
     // every width (L = 16: 72.4-73.1 vs 74.4-74.8 us at 4 and 89.4 at 8; L = 4: 40-41 vs 50-51 and
     // 65 us; r02ah).  Fused multiply-adds instead of the guarded mul + add measured slower.
-    constexpr int PB = MSPMV_SPMM_BLK_PB > 0 ? MSPMV_SPMM_BLK_PB : 2;
+    // straight-line passes (r03g, pwtk, hot): L = 16 PB 2 50.9-51.7 us vs PB 1 53.4-54.6; L = 8 PB 1
+    // 43.0-43.4 vs 43.6-45.6; L = 4 PB 1 37.3 vs 40.5-41.7
+    constexpr int PB = MSPMV_SPMM_BLK_PB > 0 ? MSPMV_SPMM_BLK_PB : (L >= 16 ? 2 : 1);
 #ifndef MSPMV_SPMM_BLK_FMA
 #define MSPMV_SPMM_BLK_FMA 1  // lab builds: 0 keeps the guarded multiply + add on every pass
 #endif
@@ -2245,20 +2249,18 @@ k_spmm_blk(TileArgs a)
     // own LDS slice, and a pass reads v[i][j] there (one broadcast read per (pass, row)) instead of
     // holding the rows in registers and shuffling them (two bpermutes per (pass, row))
     constexpr bool LDSV = MSPMV_SPMM_BLK_LDSV != 0;
-    __shared__ double s_v[LDSV ? TB / 64 : 1][LDSV ? kBlkRows : 1][64];
-    __shared__ int s_c[LDSV ? TB / 64 : 1][64];
+    __shared__ double s_v[LDSV ? kBlock / 64 : 1][LDSV ? kBlkRows : 1][64];
+    __shared__ int s_c[LDSV ? kBlock / 64 : 1][64];
     const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
     const int tid = threadIdx.x, lane = tid & 63;
     const int g = lane / GL, c = lane % GL;
-    const int slot = TB == kBlock ? 0 : xcd_tile(blockIdx.x, a.num_tiles * (kBlock / 64));
-    const int t = TB == kBlock ? xcd_tile(blockIdx.x, a.num_tiles) : slot / (kBlock / 64);
+    const int t = xcd_tile(blockIdx.x, a.num_tiles);
     const int2 b0 = a.bounds[t];
     const int r0 = b0.x, n0 = b0.y;
     const int colbase = a.colbase[t];
     const uint4 bd = lane < a.blk_stride ? a.blk[(size_t)t * a.blk_stride + lane] : make_uint4(0u, 0u, 0u, 0u);
     const int nd = (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u);
-    const int wave = TB == kBlock ? __builtin_amdgcn_readfirstlane((int)(tid >> 6)) : 0;  // LDS slice
-    const int wslot = TB == kBlock ? wave : slot % (kBlock / 64);                         // chunk slot
+    const int wave = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
     double2 dot = make_double2(0.0, 0.0);
     // lane j: P[j] and the run's values in column j of chunk di, one coalesced load per row
     auto fetch = [&](int di, int &cj, double (&vr)[KR]) {
@@ -2286,11 +2288,11 @@ k_spmm_blk(TileArgs a)
     constexpr bool PF = LDSV && MSPMV_SPMM_BLK_PF != 0;
     int colj_n = 0;
     double vrow_n[KR];
-    if (PF && wslot < nd && !stopped)
-        fetch(wslot, colj_n, vrow_n);
-    for (int di = wslot; di < nd && !stopped; di += kBlock / 64) {  // wave-uniform
+    if (PF && wave < nd && !stopped)
+        fetch(wave, colj_n, vrow_n);
+    for (int di = wave; di < nd && !stopped; di += kBlock / 64) {  // wave-uniform
 #if MSPMV_LAB_ABLATE == 10
-        const int lab_slot = (t * 4 + wslot) * 2 + (di >= kBlock / 64 ? 1 : 0);
+        const int lab_slot = (t * 4 + wave) * 2 + (di >= kBlock / 64 ? 1 : 0);
         unsigned long long *lab = g_lab_blk + (size_t)lab_slot * 8;
         const bool lab_on = lab_slot < kLabBlkSlots && lane == 0 && di < 2 * (kBlock / 64) && MODE == kModeSpmv;
         if (lab_on)
@@ -2309,23 +2311,11 @@ k_spmm_blk(TileArgs a)
         } else {
             fetch(di, colj, vrow);
         }
-#ifndef MSPMV_SPMM_BLK_XPF
-#define MSPMV_SPMM_BLK_XPF 1
-#endif
-        // X prefetch: one 8-B load per pattern column (lane j: row P[j]), issued behind the values,
-        // so the chunk's panel rows come into L2 while the values arrive.  A panel row a tile's XCD
-        // has not read yet (~1 in 5 of the gathers) would otherwise cost one Infinity-Cache round
-        // trip in nearly every pass round (a round's 8 rows rarely all hit): per-chunk stamps put
-        // the passes at 6 of 8.6 us per chunk (r03e).  Consumed (kept live) after the passes.
-        double xpf = 0.0;
-        if (MSPMV_SPMM_BLK_XPF && lane < wc)
-            xpf = a.x[(size_t)colj * a.ld];
         if constexpr (LDSV) {  // wave-private slice: the wave's LDS operations stay in order
             s_c[wave][lane] = colj;
 #pragma unroll
-            for (int i = 0; i < KR; ++i)
-                if (i < h)
-                    s_v[wave][i][lane] = vrow[i];
+            for (int i = 0; i < KR; ++i)  // rows >= h too (0.0 from fetch): the passes read every row
+                s_v[wave][i][lane] = vrow[i];
             __builtin_amdgcn_wave_barrier();
 #if MSPMV_LAB_ABLATE == 10
             if (lab_on)
@@ -2343,38 +2333,60 @@ k_spmm_blk(TileArgs a)
 #pragma unroll
         for (int i = 0; i < kBlkRows; ++i)
             acc[i] = make_double2(0.0, 0.0);
-        for (int pb = 0; pb * NGW < wc; pb += PB) {  // wave-uniform
-            double2 xv[PB];
+        // Straight-line passes: every LDS read and gather of a pass is unconditional, so a pass has
+        // ONE dependent LDS round trip (its column indices) and one gather round trip, not one per
+        // row (the per-row branches serialised six LDS round trips per pass: passes took 6 of a
+        // chunk's 8.6 us, r03e stamps).  Lanes past the chunk width hold column 0 (a valid panel
+        // row); rows >= h hold 0.0 (fetch) and are never stored.
+        int minlen = 64;
 #pragma unroll
-            for (int q = 0; q < PB; ++q) {
-                const int j = (pb + q) * NGW + g;
-                const int cq = LDSV ? s_c[wave][j & 63] : __shfl(colj, j & 63);
-                xv[q] = j < wc ? *reinterpret_cast<const double2 *>(a.x + (size_t)cq * a.ld + 2 * c)
-                               : make_double2(0.0, 0.0);
-            }
+        for (int i = 0; i < KR; ++i)
+            minlen = i < h ? min(minlen, blk_len(d, i)) : minlen;
+#ifndef MSPMV_SPMM_BLK_QFENCE
+#define MSPMV_SPMM_BLK_QFENCE 1
+#endif
+        int pb = 0;
+        if (MSPMV_SPMM_BLK_FMA) {
+            // groups of PB passes whose columns all lie in every row of the run: in-place fused
+            // multiply-adds, no select, no merge of paths (the accumulators stay in place)
+            for (; (pb + PB) * NGW <= minlen; pb += PB) {  // wave-uniform
+                int cq[PB];
 #pragma unroll
-            for (int q = 0; q < PB; ++q) {
-                const int jb = (pb + q) * NGW;  // the pass's first pattern column (wave-uniform)
-                const int j = jb + g;
+                for (int q = 0; q < PB; ++q)
+                    cq[q] = LDSV ? s_c[wave][((pb + q) * NGW + g) & 63] : __shfl(colj, ((pb + q) * NGW + g) & 63);
+                double2 xv[PB];
 #pragma unroll
-                for (int i = 0; i < KR; ++i) {
-                    const int len = blk_len(d, i);
-                    if (i >= h || jb >= len)  // wave-uniform: row i has no column in this pass
-                        continue;
-                    const double v = LDSV ? s_v[wave][i][j & 63] : __shfl(vrow[i], j & 63);
-                    if (MSPMV_SPMM_BLK_FMA && jb + NGW <= len) {
-                        // every column of the pass is in row i (wave-uniform): one fused
-                        // multiply-add per component, no select (the node rows are summed by a
-                        // lane tree, so they are held to the reordering bound, which an FMA's
-                        // single rounding only tightens)
+                for (int q = 0; q < PB; ++q)
+                    xv[q] = *reinterpret_cast<const double2 *>(a.x + (size_t)cq[q] * a.ld + 2 * c);
+#pragma unroll
+                for (int q = 0; q < PB; ++q) {
+                    const int j = (pb + q) * NGW + g;
+#pragma unroll
+                    for (int i = 0; i < KR; ++i) {
+                        const double v = LDSV ? s_v[wave][i][j & 63] : __shfl(vrow[i], j & 63);
                         acc[i].x = __builtin_fma(v, xv[q].x, acc[i].x);
                         acc[i].y = __builtin_fma(v, xv[q].y, acc[i].y);
-                    } else {
-                        const bool on = j < len;
-                        acc[i].x += on ? v * xv[q].x : 0.0;
-                        acc[i].y += on ? v * xv[q].y : 0.0;
                     }
+                    // pass q + 1's value reads stay behind pass q's FMAs: without the fence the
+                    // compiler hoists them and the kernel no longer fits 64 VGPRs (8 waves)
+                    if (MSPMV_SPMM_BLK_QFENCE)
+                        asm volatile("" ::: "memory");
                 }
+            }
+        }
+        // the remaining passes one at a time, each product kept or skipped by a select (the
+        // reference's products exactly: a non-finite panel entry in a column a shorter row lacks
+        // never reaches that row)
+        for (; pb * NGW < wc; ++pb) {  // wave-uniform
+            const int j = pb * NGW + g;
+            const int cq = LDSV ? s_c[wave][j & 63] : __shfl(colj, j & 63);
+            const double2 xv = *reinterpret_cast<const double2 *>(a.x + (size_t)cq * a.ld + 2 * c);
+#pragma unroll
+            for (int i = 0; i < KR; ++i) {
+                const double v = LDSV ? s_v[wave][i][j & 63] : __shfl(vrow[i], j & 63);
+                const bool on = i < h && j < blk_len(d, i);
+                acc[i].x += on ? v * xv.x : 0.0;
+                acc[i].y += on ? v * xv.y : 0.0;
             }
         }
 #if MSPMV_LAB_ABLATE == 10
@@ -2383,8 +2395,6 @@ k_spmm_blk(TileArgs a)
             lab[5] = (unsigned long long)wc | ((unsigned long long)h << 8) | ((unsigned long long)nd << 16);
         }
 #endif
-        if (MSPMV_SPMM_BLK_XPF)
-            asm volatile("" ::"v"(xpf));
         const double2 row = rows8_sum2<GL>(acc);
 #if MSPMV_LAB_ABLATE == 10
         if (lab_on) {
@@ -3230,7 +3240,6 @@ struct SpmvTuning {
     int blkreg = 1;   // plans of register node-block tiles only run the LDS-free k_spmv_blk
     int runs = 0;     // ... or, for the plain SpMV, the persistent wave-pipelined k_spmv_runs
     int spmm_blk = 1; // SpMM (L >= 2) on such a plan runs k_spmm_blk instead of its own L-wide tiles
-    int spmm_blk_tb = 256;  // k_spmm_blk workgroup size for the plain SpMM: 256 (one tile) or 64 (one wave)
     int early_re = 0; // single-RHS tile kernel: row ends issued with the stream (TileArgs::early_re)
     int dict = 1;     // single-RHS SpMV through per-tile column dictionaries (k_build_dict) when
                       // a tile's nonzeros repeat its distinct columns >= dict_ratio times (0: off)
@@ -3269,8 +3278,6 @@ static const SpmvTuning &spmv_tuning()
             v.runs = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMM_BLK"))
             v.spmm_blk = atoi(e) != 0;
-        if (const char *e = getenv("MSPMV_SPMM_BLK_TB"))
-            v.spmm_blk_tb = atoi(e) == 64 ? 64 : 256;
         if (const char *e = getenv("MSPMV_SPMV_EARLY_RE"))
             v.early_re = atoi(e);
         if (const char *e = getenv("MSPMV_SPMV_DICT"))
@@ -3326,8 +3333,7 @@ std::string spmm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan, int 
     const std::string nt = stream_nt(h) ? "true" : "false";
     const SpmvTuning &t = spmv_tuning();
     if (plan.d_blk && plan.num_tiles_reg == plan.num_tiles && t.blkreg && t.tb == kBlock && spmm_blk_enabled())
-        return "k_spmm_blk<" + std::to_string(L) + ",0," + nt + (plan.blk_rows_max <= 6 ? ",6" : ",8") +
-               (t.spmm_blk_tb == 64 ? ",64>" : ">");
+        return "k_spmm_blk<" + std::to_string(L) + ",0," + nt + (plan.blk_rows_max <= 6 ? ",6>" : ",8>");
     const int iptg = spmm_iptg_for(L);
     const bool dict = L == 16 && iptg != 32 && plan.d_dict;
     return "k_spmm_tile<" + std::to_string(L) + "," + std::to_string(iptg) + ",0," + nt + (dict ? ",true>" : ">");
@@ -3596,19 +3602,7 @@ static void launch_spmm_L(const TileArgs &a, hipStream_t s, bool nt)
 #ifndef MSPMV_SPMM_BLK_KR6
 #define MSPMV_SPMM_BLK_KR6 1  // lab builds: 0 runs the 8-row kernel on every plan
 #endif
-            if (MODE == kModeSpmv && spmv_tuning().spmm_blk_tb == 64) {
-                const dim3 g1((unsigned)a.num_tiles * (kBlock / 64));
-                if (a.blk_rows_max <= 6) {
-                    if (nt)
-                        hipLaunchKernelGGL((k_spmm_blk<LL, kModeSpmv, true, 6, 64>), g1, dim3(64), 0, s, a);
-                    else
-                        hipLaunchKernelGGL((k_spmm_blk<LL, kModeSpmv, false, 6, 64>), g1, dim3(64), 0, s, a);
-                } else if (nt) {
-                    hipLaunchKernelGGL((k_spmm_blk<LL, kModeSpmv, true, kBlkRows, 64>), g1, dim3(64), 0, s, a);
-                } else {
-                    hipLaunchKernelGGL((k_spmm_blk<LL, kModeSpmv, false, kBlkRows, 64>), g1, dim3(64), 0, s, a);
-                }
-            } else if (MSPMV_SPMM_BLK_KR6 && a.blk_rows_max <= 6) {
+            if (MSPMV_SPMM_BLK_KR6 && a.blk_rows_max <= 6) {
                 if (nt)
                     hipLaunchKernelGGL((k_spmm_blk<LL, MODE, true, 6>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
                 else
