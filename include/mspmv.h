@@ -273,6 +273,10 @@ MSPMV_API const char *mspmv_spmv_kernel_name(mspmv_handle h);
  * "k_spmm_blk<16,0,false,6>" on a node-block plan, "k_spmm_tile<8,16,0,true>" elsewhere; widths
  * outside 1, 2, 4, 8, 16 name their widest column chunk's kernel.  "" on error. */
 MSPMV_API const char *mspmv_spmm_kernel_name(mspmv_handle h, int L);
+/* The CG path the last solve on this handle ran: "k_cg_resident<RPT,NZR> x G" (single RHS, the
+ * matrix register/LDS-resident on every CU, one cooperative launch per solve), "pipelined (...)"
+ * (single RHS, two kernels per iteration), or the split multi-RHS / PCG forms.  "" before any. */
+MSPMV_API const char *mspmv_cg_kernel_name(mspmv_handle h);
 
 /* ---- device memory helpers (so hosts need no HIP headers) ---------------------------- */
 MSPMV_API mspmv_status mspmv_device_malloc(int device, size_t bytes, void **d_ptr);

@@ -521,6 +521,8 @@ extern "C" {
 
 const char *mspmv_last_error(void) { return g_err.c_str(); }
 
+const char *mspmv_cg_kernel_name(mspmv_handle h) { return h ? h->last_cg_kernel : ""; }
+
 const char *mspmv_spmv_kernel_name(mspmv_handle h)
 {
     thread_local std::string name;
@@ -628,6 +630,7 @@ mspmv_status mspmv_destroy(mspmv_handle h)
         (void)hipEventDestroy(h->ev0);
     if (h->ev1)
         (void)hipEventDestroy(h->ev1);
+    resident_free(h->rcg);
     if (h->stream && h->own_stream)
         (void)hipStreamDestroy(h->stream);
     delete h;
@@ -915,6 +918,54 @@ static mspmv_status ensure_cg_workspace(mspmv_handle_s *h, int L, int nblk, int 
     return MSPMV_OK;
 }
 
+// Register-resident single-RHS CG: one cooperative launch runs the whole solve.
+static mspmv_status cg_solve_resident(mspmv_handle_s *h, ResidentCg *rc, const double *d_b, double *d_x,
+                                      int max_iters, double tol, int *iters, double *hist, int use_cap)
+{
+    static char names[16][48];
+    static int nnames = 0;
+    const int saved_cap = h->hist_cap;
+    h->hist_cap = use_cap;
+    hipError_t e = hipMemsetAsync(h->d_ctrl, 0, sizeof(CgControl), h->stream);
+    if (e == hipSuccess)
+        e = launch_cg_resident(h, rc, d_b, d_x, max_iters, tol);
+    h->hist_cap = saved_cap;
+    if (e != hipSuccess) {
+        set_error(std::string("resident CG launch: ") + hipGetErrorString(e));
+        return MSPMV_ERR_HIP;
+    }
+    {
+        char buf[48];
+        snprintf(buf, sizeof buf, "k_cg_resident<%d,%d> x %d", rc->rpt, rc->nzr, rc->G);
+        int i = 0;
+        while (i < nnames && std::strcmp(names[i], buf) != 0)
+            ++i;
+        if (i == nnames && nnames < 16)
+            std::strcpy(names[nnames++], buf);
+        h->last_cg_kernel = i < 16 ? names[i] : "k_cg_resident";
+    }
+    CgControl fin{};
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    HIP_TRY(hipMemcpy(&fin, h->d_ctrl, sizeof(CgControl), hipMemcpyDeviceToHost));
+    const int it = fin.iters_out;
+    if (iters)
+        *iters = it;
+    if (hist && use_cap > 0) {
+        const int nh = std::min(it, use_cap);
+        if (nh > 0)
+            HIP_TRY(hipMemcpy(hist, h->d_hist, sizeof(double) * nh, hipMemcpyDeviceToHost));
+    }
+    if (fin.breakdown == 2) {
+        set_error("resident CG: a reduction hand-off never completed (solve stalled; workgroups not co-resident?)");
+        return MSPMV_ERR_STALL;
+    }
+    if (fin.breakdown) {
+        set_error("CG breakdown: p.Ap gave a non-finite alpha at iteration " + std::to_string(it));
+        return MSPMV_ERR_BREAKDOWN;
+    }
+    return MSPMV_OK;
+}
+
 // CG; SPAI-preconditioned CG with the preconditioner's handle hm; or IC(0)-preconditioned CG
 // with the factor ic.
 static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double *d_x, int L, int max_iters,
@@ -960,6 +1011,17 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
     const int cap = hist ? std::max(hist_cap, 0) : 0;
     ST_TRY(ensure_cg_workspace(h, L, nblk, std::max(plan->num_tiles, mplan ? mplan->num_tiles : 0), cap));
     const int use_cap = hist ? cap : 0;
+    if (pipelined && cg_resident_enabled()) {
+        // the whole solve as one register-resident launch, where the matrix fits (mspmv_cg_resident.hip)
+        ResidentCg *rc = nullptr;
+        ST_TRY(resident_prepare(h, &rc));
+        if (rc->ok)
+            return cg_solve_resident(h, rc, d_b, d_x, max_iters, tol, iters, hist, use_cap);
+    }
+    h->last_cg_kernel = pipelined ? "pipelined (k_spmv_tile MODE 1 + k_cg1_update)"
+                        : hm      ? "SPAI-PCG (split)"
+                        : ic      ? "IC0-PCG (split)"
+                                  : "split (p update, SpMM, p.Ap, update)";
     const int saved_cap = h->hist_cap;
     h->hist_cap = use_cap;  // kernels record only what the caller asked for
     HIP_TRY(hipMemsetAsync(h->d_ctrl, 0, sizeof(CgControl), h->stream));

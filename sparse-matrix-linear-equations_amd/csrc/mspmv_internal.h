@@ -91,6 +91,20 @@ struct CgControl {
     unsigned reserved;
 };
 
+// Register-resident single-RHS CG (mspmv_cg_resident.hip): the ELL layout of the matrix's row
+// blocks, one per CU, built once per handle when the matrix fits (ok).
+struct ResidentCg {
+    bool ok = false;
+    int G = 0, rpt = 0, nzr = 0;
+    int *d_rb = nullptr;
+    int *d_cols = nullptr;
+    double *d_vals = nullptr;
+    short *d_len = nullptr;
+    double *d_slots = nullptr;  // hand-off slots, reset to the empty pattern before every solve
+    size_t slot_bytes = 0;
+    unsigned *d_abort = nullptr;
+};
+
 }  // namespace mspmv
 
 // Every handle and IC(0) factor gets a process-unique generation number at creation, so a cached
@@ -137,6 +151,8 @@ struct mspmv_handle_s {
     int last_kernels_per_call = 1;
     void *d_flush = nullptr;
     size_t flush_cap = 0;
+    mspmv::ResidentCg *rcg = nullptr;  // register-resident CG layout (built on the first single-RHS CG)
+    const char *last_cg_kernel = "";   // the CG path the last solve ran (mspmv_cg_kernel_name)
 };
 
 // IC(0) factor on the device (mspmv_ic0_create): L and its transpose for the two sync-free
@@ -227,6 +243,13 @@ bool cg_split_iteration(int L);
 int cg1_blocks(long long m);
 hipError_t launch_cg1_init(mspmv_handle_s *h, const double *d_b, double *d_x, int nblk);
 hipError_t launch_cg1_finish(mspmv_handle_s *h, double *d_x, int parity, int nblk);
+// Register-resident single-RHS CG (one cooperative launch for the whole solve; MSPMV_CG_RESIDENT=0
+// turns it off): the layout is built on first use; r->ok false when the matrix does not fit.
+bool cg_resident_enabled();
+mspmv_status resident_prepare(mspmv_handle_s *h, ResidentCg **out);
+void resident_free(ResidentCg *r);
+hipError_t launch_cg_resident(mspmv_handle_s *h, ResidentCg *r, const double *d_b, double *d_x, int max_iters,
+                              double tol);
 // Split (multi-RHS) CG: the last deferred x += alpha p after the loop (a no-op when none is pending).
 hipError_t launch_cg_xflush(mspmv_handle_s *h, double *d_x, int L, int nblk);
 // Offset (doubles) and count of the partials level a consumer sums: levels of a fan-in

@@ -29,13 +29,22 @@ namespace mspmv {
 // ------------------------------------------------------------------------------------------
 // helpers
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ int xcd_tile(int b, int T)
+__device__ __forceinline__ int xcd_tile(int b, int T, int K = 1)
 {
     // Blocks are dealt round-robin over the 8 XCDs; give XCD k (= b % 8, a label only) the
     // contiguous tile range [k*q + min(k,r), +q + (k<r)).  Bijective for any T.
+    // K > 1: that range is cut into K contiguous sub-ranges walked side by side (the XCD's i-th
+    // block takes sub-range i % K, position i / K), so the resident workgroups stream from K
+    // places per XCD instead of one window.  Bijective for any T, K >= 1.
     const int q = T >> 3, r = T & 7;
     const int k = b & 7, i = b >> 3;
-    return k * q + (k < r ? k : r) + i;
+    const int base = k * q + (k < r ? k : r);
+    if (K <= 1)
+        return base + i;
+    const int cnt = q + (k < r ? 1 : 0);
+    const int q2 = cnt / K, r2 = cnt - q2 * K;
+    const int s = i % K, pos = i / K;
+    return base + s * q2 + (s < r2 ? s : r2) + pos;
 }
 
 // Streamed-once matrix arrays: nontemporal loads (don't displace x / X from the caches).
@@ -664,6 +673,7 @@ struct TileArgs {
     // staging (0) -- one dependent round trip fewer per tile (SpmvTuning::early_re)
     int early_re;
     int blk_rows_max;  // node-block plans: the tallest run (TilePlan::blk_rows_max; k_spmm_blk's KR)
+    int tstreams;      // tile order: contiguous tile streams per XCD walked side by side (xcd_tile's K)
 };
 
 // Tile-kernel modes.
@@ -1399,7 +1409,7 @@ k_spmv_tile(TileArgs a)
 #endif
     // CG: stop flag loaded now, tested after the stream and gathers are issued (see k_spmm_tile)
     const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
-    const int t = xcd_tile(blockIdx.x, a.num_tiles);
+    const int t = xcd_tile(blockIdx.x, a.num_tiles, a.tstreams);
     const int2 b0 = a.bounds[t];
     const int2 b1 = a.bounds[t + 1];
     const int r0 = b0.x, n0 = b0.y;
@@ -1542,7 +1552,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_blk(TileArgs a)
     __shared__ BlkSmem sm;
     const int tid = threadIdx.x;
     const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
-    const int t = xcd_tile(blockIdx.x, a.num_tiles);
+    const int t = xcd_tile(blockIdx.x, a.num_tiles, a.tstreams);
     const int2 b0 = a.bounds[t];
     const int colbase = a.colbase[t];
     const uint4 bd =
@@ -1966,7 +1976,7 @@ k_spmm_tile(TileArgs a)
     // flag's round trip does not delay every workgroup's first load (MODE 2 writes only the
     // scratch Ap and partials: a stopped solve only needs the work skipped, not fenced)
     const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
-    const int t = xcd_tile(blockIdx.x, a.num_tiles);
+    const int t = xcd_tile(blockIdx.x, a.num_tiles, a.tstreams);
     const int2 b0 = a.bounds[t];
     const int2 b1 = a.bounds[t + 1];
     const int r0 = b0.x, n0 = b0.y;
@@ -2254,7 +2264,7 @@ k_spmm_blk(TileArgs a)
     const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
     const int tid = threadIdx.x, lane = tid & 63;
     const int g = lane / GL, c = lane % GL;
-    const int t = xcd_tile(blockIdx.x, a.num_tiles);
+    const int t = xcd_tile(blockIdx.x, a.num_tiles, a.tstreams);
     const int2 b0 = a.bounds[t];
     const int r0 = b0.x, n0 = b0.y;
     const int colbase = a.colbase[t];
@@ -3525,6 +3535,11 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
     a.idx16 = plan.d_idx16;
     a.ld = L;
     a.early_re = L == 1 ? spmv_tuning().early_re : 0;
+    static const int tstreams = [] {  // lab knob: MSPMV_TILE_STREAMS=K (xcd_tile)
+        const char *e = getenv("MSPMV_TILE_STREAMS");
+        return e ? std::max(1, atoi(e)) : 1;
+    }();
+    a.tstreams = tstreams;
     return a;
 }
 

@@ -109,6 +109,7 @@ _SIGS = {
     "mspmv_tile_modes": (_I, [_P, _I, _P]),
     "mspmv_spmv_kernel_name": (ctypes.c_char_p, [_P]),
     "mspmv_spmm_kernel_name": (ctypes.c_char_p, [_P, _I]),
+    "mspmv_cg_kernel_name": (ctypes.c_char_p, [_P]),
     "mspmv_device_malloc": (_I, [_I, _SZ, ctypes.POINTER(_P)]),
     "mspmv_device_free": (_I, [_P]),
     "mspmv_memcpy_h2d": (_I, [_P, _P, _SZ]),
@@ -411,6 +412,10 @@ class GpuCsr:
     def kernel_name(self) -> str:
         """The single-RHS SpMV kernel instantiation used for this matrix (rocprofv3's name)."""
         return lib.mspmv_spmv_kernel_name(self.h).decode()
+
+    def cg_kernel_name(self) -> str:
+        """The CG path the last solve on this matrix ran (mspmv_cg_kernel_name)."""
+        return lib.mspmv_cg_kernel_name(self.h).decode()
 
     def spmm_kernel_name(self, L: int) -> str:
         """The SpMM kernel instantiation launched for L right-hand sides (rocprofv3's spelling)."""
