@@ -1838,6 +1838,17 @@ __global__ __launch_bounds__(kBlock) void k_spmv_persist(TileArgs a, int tpb)
 // Gp = 1 is the row-by-row CSR-order sum of the reference's row-split SpMM, bit for bit.
 // DICT: s_col holds each nonzero's position in the tile's column dictionary and the panel rows
 // are read from s_panel (parked there by k_spmm_tile) -- the same operands, the same sums.
+// Dot mode (MODE 2) of the row-group SpMM tiles: the x.(Ax) contribution of the tile's whole rows
+// is taken after the row loop, from the Ap rows the workgroup has just stored and the rows' own x
+// (both contiguous nrows x L slices, L2-resident: x[R] is a column of row R), instead of holding
+// each row's x and the running dot in registers through the gathers -- the dot mode then needs
+// no more registers than the plain SpMM, so it keeps the plain kernel's occupancy.  Lab builds:
+// -DMSPMV_SPMM_DOT_TAIL=0 restores the in-loop form.
+#ifndef MSPMV_SPMM_DOT_TAIL
+#define MSPMV_SPMM_DOT_TAIL 1
+#endif
+constexpr bool kSpmmDotTail = MSPMV_SPMM_DOT_TAIL != 0;
+
 template <int L, int MODE, bool DICT = false>
 __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_col, const double *s_val,
                                                 const int *rend, int t, int r0, int nrows, int nnzt,
@@ -1860,9 +1871,10 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
     for (int r = tid / W; r < nseg; r += kBlock / W) {  // uniform within a group
         const int s0 = r == 0 ? 0 : rend[r - 1];
         const int e = r < nrows ? rend[r] : nnzt;
-        // MODE 2: the row's own x, issued ahead of the row's gathers (used after them)
+        // MODE 2 without the tail pass (kSpmmDotTail): the row's own x, issued ahead of the row's
+        // gathers (used after them)
         double2 xx = make_double2(0.0, 0.0);
-        if (MODE == kModeDot && sub == 0)
+        if (MODE == kModeDot && !kSpmmDotTail && sub == 0)
             xx = *reinterpret_cast<const double2 *>(a.xr + (size_t)(r0 + r) * a.ld + 2 * lane);
         double2 acc = make_double2(0.0, 0.0);
         int k = s0 + sub;
@@ -1917,7 +1929,7 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
                 *reinterpret_cast<double2 *>(a.y + off) = acc;
             else  // the trailing partial row -> carry (k_fixup adds it in tile order)
                 *reinterpret_cast<double2 *>(a.carry_val + (size_t)t * L + 2 * lane) = acc;
-            if (MODE == kModeDot) {
+            if (MODE == kModeDot && !kSpmmDotTail) {
                 dot.x += xx.x * acc.x;
                 dot.y += xx.y * acc.y;
             }
@@ -2045,10 +2057,11 @@ k_spmm_tile(TileArgs a)
         return;
 
     double2 dot = make_double2(0.0, 0.0);
-    if (DICT && nd > 0) {
-        spmm_group_rows<L, MODE, true>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, dot, rmode - 1, s_panel);
-    } else if (rmode != 0) {
-        spmm_group_rows<L, MODE>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, dot, rmode - 1);
+    if (rmode != 0) {
+        if (DICT && nd > 0)
+            spmm_group_rows<L, MODE, true>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, dot, rmode - 1, s_panel);
+        else
+            spmm_group_rows<L, MODE>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, dot, rmode - 1);
     } else {
     const int ipt = (items + NG - 1) / NG;
     const int d0 = min(g * ipt, items);
@@ -2061,7 +2074,7 @@ k_spmm_tile(TileArgs a)
     auto write_row = [&](int row, double2 val) {
         const size_t off = (size_t)(r0 + row) * a.ld + 2 * lane;
         *reinterpret_cast<double2 *>(a.y + off) = val;
-        if (MODE == kModeDot) {
+        if (MODE == kModeDot && !kSpmmDotTail) {
             const double2 xx = *reinterpret_cast<const double2 *>(a.xr + off);
             dot.x += xx.x * val.x;
             dot.y += xx.y * val.y;
@@ -2150,7 +2163,7 @@ k_spmm_tile(TileArgs a)
             acc.y += c.y;
         }
         *reinterpret_cast<double2 *>(a.carry_val + (size_t)t * L + 2 * lane) = acc;
-        if (MODE == kModeDot) {
+        if (MODE == kModeDot && !kSpmmDotTail) {
             const size_t off = (size_t)(r0 + nrows) * a.ld + 2 * lane;
             const double2 xx = *reinterpret_cast<const double2 *>(a.xr + off);
             dot.x += xx.x * acc.x;
@@ -2159,6 +2172,26 @@ k_spmm_tile(TileArgs a)
     }
     }  // merge walk
 
+    if (MODE == kModeDot && kSpmmDotTail) {
+        // the tile's whole Ap rows, stored above by its own waves (either path): drained, then
+        // visible to the workgroup after the barrier (one CU, and no wave read these lines before).
+        // Pair e = (row e / GL, columns 2 (e % GL) + {0, 1}); kBlock % GL == 0, so a thread always
+        // takes its own column pair `lane`, as the in-loop dot does.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        // The trailing partial row (a carry, k_fixup adds it later) counts by linearity: its x
+        // times the carry this tile stored.
+        const int npair = (nrows + (a.split[t + 1] ? 1 : 0)) * GL;
+        for (int e = tid; e < npair; e += kBlock) {
+            const int row = e / GL;
+            const size_t off = (size_t)(r0 + row) * a.ld + 2 * lane;
+            const double2 ap = *reinterpret_cast<const double2 *>(
+                row < nrows ? a.y + off : a.carry_val + (size_t)t * L + 2 * lane);
+            const double2 xx = *reinterpret_cast<const double2 *>(a.xr + off);
+            dot.x += xx.x * ap.x;
+            dot.y += xx.y * ap.y;
+        }
+    }
     if (MODE != kModeSpmv) {
         // Reduce the per-lane column partials over the groups (lanes with equal tid % GL).
 #pragma unroll
