@@ -264,6 +264,12 @@ MSPMV_API mspmv_status mspmv_plan_block_tiles(mspmv_handle h, int L, int *tiles_
  * lanes per row (times L/2 column-pair lanes for L > 1).  g = 1 sums each row sequentially in
  * CSR order -> bit-identical to SpmvGold / the row-split SpMM for rows the tile holds whole. */
 MSPMV_API mspmv_status mspmv_tile_modes(mspmv_handle h, int L, unsigned char *modes);
+/* Threads that share one tile of the plan the plain L-column product runs on (*lanes): 256, or 64
+ * for a single-RHS matrix whose rows are skewed (most workgroup tiles would be merge walks), which
+ * the plain SpMV runs on one-wave tiles of 512 merge items.  A merge-walk tile gives each of its
+ * lanes (L = 1) ceil(items / lanes) consecutive merge items -- what mspmv_tile_plan's readers
+ * need to tell the rows summed sequentially from the split ones. */
+MSPMV_API mspmv_status mspmv_tile_lanes(mspmv_handle h, int L, int *lanes);
 /* The single-RHS SpMV kernel instantiation launched for this matrix (tuning read once from
  * the MSPMV_SPMV_* environment; nontemporal matrix loads above 128 MiB), e.g.
  * "k_spmv_tile<8,0,true>" -- the name rocprofv3 reports.  Valid until the next call on this

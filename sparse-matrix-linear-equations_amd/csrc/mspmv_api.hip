@@ -104,7 +104,7 @@ static void free_plan(TilePlan &p)
 // Build (once) the tile plan for L right-hand sides, validating on the host every bound the
 // kernels rely on (monotone boundaries, <= 1.25 * tile_items merge items per tile) before any
 // tile kernel can run on it.
-static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out);
+static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes = 0);
 
 // The in-tile reduction modes of a plan for L right-hand sides, built on first use.
 static mspmv_status ensure_modes(mspmv_handle_s *h, TilePlan &p, int L)
@@ -115,7 +115,7 @@ static mspmv_status ensure_modes(mspmv_handle_s *h, TilePlan &p, int L)
     mspmv_status st = dev_alloc(&m, (size_t)std::max(p.num_tiles, 1));
     if (st != MSPMV_OK)
         return st;
-    hipError_t e = launch_tile_modes(h->d_row_offsets, p.d_bounds, p.d_split, p.num_tiles, L, m, h->stream);
+    hipError_t e = launch_tile_modes(h->d_row_offsets, p.d_bounds, p.d_split, p.num_tiles, L, m, h->stream, p.lanes);
     if (e == hipSuccess)
         e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) {
@@ -127,27 +127,33 @@ static mspmv_status ensure_modes(mspmv_handle_s *h, TilePlan &p, int L)
     return MSPMV_OK;
 }
 
-static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out)
+static mspmv_status spmv_plan(mspmv_handle_s *h, const TilePlan **out);
+
+// plain: the caller runs the plain product (y = A x / Y = A X), whose single-RHS form may take a
+// one-wave plan of its own (spmv_plan); CG, dot-mode and sharded callers use the workgroup plan.
+static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out, bool plain = false)
 {
+    if (plain && L == 1)
+        return spmv_plan(h, out);
     if (L > 1 && spmm_blk_enabled()) {
         // a matrix of node blocks only (every single-RHS tile a register run tile: FEM node rows)
         // multiplies L columns on that plan with k_spmm_blk -- one panel-row gather per (run,
         // column) -- instead of its own L-wide merge tiles
-        auto one = h->plans.find(tile_items_for(1));
+        auto one = h->plans.find(plan_key(1));
         if (one != h->plans.end() && one->second.d_blk && one->second.num_tiles_reg == one->second.num_tiles) {
             ST_TRY(ensure_modes(h, one->second, L));
             *out = &one->second;
             return MSPMV_OK;
         }
     }
-    const int tile = tile_items_for(L);
-    auto it = h->plans.find(tile);
+    const int key = plan_key(L);
+    auto it = h->plans.find(key);
     if (it == h->plans.end()) {
         const TilePlan *np = nullptr;
         mspmv_status st = build_plan(h, L, &np);
         if (st != MSPMV_OK)
             return st;
-        it = h->plans.find(tile);
+        it = h->plans.find(key);
     }
     mspmv_status st = ensure_modes(h, it->second, L);
     if (st != MSPMV_OK)
@@ -156,13 +162,17 @@ static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out)
     return MSPMV_OK;
 }
 
-static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
+static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes)
 {
-    const int tile = tile_items_for(L);
+    // lanes: 64 builds the one-wave single-RHS plan (tile = 64 x items per thread, keyed by that
+    // size); 0 the default plan for L
+    const bool onewave = L == 1 && lanes == 64 && tile_items_for(1) != 64 * spmv_items_per_thread();
+    const int tile = onewave ? 64 * spmv_items_per_thread() : tile_items_for(L);
     TilePlan p;
+    p.lanes = (L == 1 && (onewave || tile_items_for(1) == 64 * spmv_items_per_thread())) ? 64 : kBlock;
     const long long total = (long long)h->m + h->nnz;
     int step = tile, snap = tile / kSnapDiv;
-    if (tile == tile_items_for(1)) {
+    if (tile == tile_items_for(1) && p.lanes == kBlock) {
         // A grid a few tiles over a whole number of resident generations of workgroups takes one
         // tile lifetime more (the parabolic_fem shape: 2,052 tiles on 2,048 slots).  Stretch the
         // tiles into the snap slack so they fit one generation fewer: MAXI (step + snap) is
@@ -243,7 +253,8 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
     // the single-RHS kernels' 16-bit column stream; keyed on the tile size, not L, because the
     // L = 2 SpMM shares the single-RHS plan.  (The SpMM itself keeps int32 columns: it is gather
     // bound, and the 16-bit stream measured 0% at L = 4/8 and 7% slower at L = 16.)
-    if (tile == tile_items_for(1) && T > 0 && h->nnz > 0 && spmv_cols16_enabled()) {
+    const bool single = tile == tile_items_for(1) || onewave;  // a single-RHS plan
+    if (single && T > 0 && h->nnz > 0 && spmv_cols16_enabled()) {
         if ((st = dev_alloc(&p.d_colbase, (size_t)T)) != MSPMV_OK ||
             (st = dev_alloc(&p.d_cols16, (size_t)h->nnz + kNnzPad)) != MSPMV_OK)
             return fail(st);
@@ -269,7 +280,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
         }
     }
     // node blocks: single-RHS plan on the 16-bit stream only (the runs' pattern columns are read there)
-    if (tile == tile_items_for(1) && p.d_cols16 && spmv_blocks_enabled()) {
+    if (tile == tile_items_for(1) && !onewave && p.lanes == kBlock && p.d_cols16 && spmv_blocks_enabled()) {
         if ((st = dev_alloc(&p.d_blk, (size_t)T * kBlkPerTile)) != MSPMV_OK)
             return fail(st);
         e = launch_build_blocks(h->d_row_offsets, h->d_cols, p.d_bounds, p.d_split, p.d_colbase, T, p.d_blk,
@@ -318,7 +329,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
         }
     }
     // multi-RHS: only the L = 16 plan (k_spmm_tile's DICT path runs at L = 16 only)
-    const bool multi = tile != tile_items_for(1);
+    const bool multi = !single;
     const bool want = multi ? L == 16 && tile != tile_items_for(8) && spmm_dict_enabled() : spmv_dict_enabled();
     if (T > 0 && h->nnz > 0 && want) {
         if ((st = dev_alloc(&p.d_dict, (size_t)h->nnz + kNnzPad)) != MSPMV_OK ||
@@ -350,8 +361,46 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out)
             p.d_idx16 = nullptr;
         }
     }
-    auto res = h->plans.emplace(tile, p);
+    auto res = h->plans.emplace(p.lanes == 64 ? -tile : tile, p);  // one-wave plans: negative keys (plan_key)
     *out = &res.first->second;
+    return MSPMV_OK;
+}
+
+// The plan the plain single-RHS SpMV runs on.  Decided once per handle on first use: a matrix
+// whose workgroup plan is mostly merge-walk tiles (row lengths uneven inside most tiles: skewed,
+// power-law rows) runs one-wave tiles instead (k_spmv_tile<.., 64>: 512 merge items, wave
+// barriers only), so a tile's hub-row closing and its walkers' latencies stall one wave, not four.
+// Measured on the skewed pwtk-sized variant 100.1 -> 78.3 us; on row-group plans (banded, FEM,
+// stencils) one-wave tiles lost 1-15 % (r03r), so those keep the workgroup plan.
+static mspmv_status spmv_plan(mspmv_handle_s *h, const TilePlan **out)
+{
+    const TilePlan *wg = nullptr;
+    ST_TRY(get_plan(h, 1, &wg));
+    if (h->spmv_onewave < 0) {
+        const int mode = spmv_onewave_mode();
+        bool want = mode == 1 && wg->lanes == kBlock;
+        if (mode < 0 && wg->lanes == kBlock && wg->num_tiles >= 64 && !wg->d_blk) {
+            std::vector<unsigned char> hm((size_t)wg->num_tiles);
+            HIP_TRY(hipMemcpy(hm.data(), wg->d_modes[0], hm.size(), hipMemcpyDeviceToHost));
+            long long walk = 0;
+            for (unsigned char v : hm)
+                walk += v == 0;
+            want = 2 * walk >= (long long)wg->num_tiles;  // most tiles merge walks
+        }
+        if (want) {
+            const TilePlan *np = nullptr;
+            const int key = -64 * spmv_items_per_thread();  // build_plan's key for one-wave plans
+            if (h->plans.find(key) == h->plans.end())
+                ST_TRY(build_plan(h, 1, &np, 64));
+            ST_TRY(ensure_modes(h, h->plans.find(key)->second, 1));
+        }
+        h->spmv_onewave = want ? 1 : 0;
+    }
+    if (h->spmv_onewave == 1) {
+        *out = &h->plans.find(-64 * spmv_items_per_thread())->second;
+        return MSPMV_OK;
+    }
+    *out = wg;
     return MSPMV_OK;
 }
 
@@ -528,6 +577,9 @@ const char *mspmv_spmv_kernel_name(mspmv_handle h)
     thread_local std::string name;
     if (!h)
         return "";
+    const TilePlan *plan = nullptr;  // settles the handle's plain-SpMV plan (one-wave or not)
+    if (h->m > 0 && spmv_plan(h, &plan) != MSPMV_OK)
+        return "";
     name = spmv_kernel_name(h);
     return name.c_str();
 }
@@ -544,7 +596,7 @@ const char *mspmv_spmm_kernel_name(mspmv_handle h, int L)
     while (w > lp)
         w >>= 1;
     const TilePlan *plan = nullptr;
-    if (get_plan(h, w, &plan) != MSPMV_OK)
+    if (get_plan(h, w, &plan, true) != MSPMV_OK)
         return "";
     name = spmm_kernel_name(h, *plan, w);
     return name.c_str();
@@ -720,6 +772,7 @@ mspmv_status mspmv_set_cu_limit(mspmv_handle h, int num_cus)
         for (auto &kv : h->plans)
             free_plan(kv.second);
         h->plans.clear();
+        h->spmv_onewave = -1;
         h->num_cus = n;
         const TilePlan *plan = nullptr;
         ST_TRY(get_plan(h, 1, &plan));
@@ -789,7 +842,7 @@ mspmv_status mspmv_dspmm_dev(mspmv_handle h, const double *d_X, double *d_Y, int
         return MSPMV_OK;
     if (supported_L(L)) {
         const TilePlan *plan = nullptr;
-        ST_TRY(get_plan(h, L, &plan));
+        ST_TRY(get_plan(h, L, &plan, true));
         int nk = 0;
         HIP_TRY(launch_spmm(h, *plan, d_X, d_Y, L, &nk));
         return MSPMV_OK;
@@ -1549,7 +1602,7 @@ mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y,
     if (L > 1 && (!aligned16(d_X) || !aligned16(d_Y)))
         return invalid("multi-vector panels must be 16-byte aligned");
     const TilePlan *plan = nullptr;
-    ST_TRY(get_plan(h, L, &plan));
+    ST_TRY(get_plan(h, L, &plan, true));
     if (flush_bytes && flush_bytes > h->flush_cap) {
         if (h->d_flush)
             (void)hipFree(h->d_flush);
@@ -1627,7 +1680,7 @@ mspmv_status mspmv_time_spmm_batch_dev(int count, const mspmv_handle *hs, const 
     std::vector<const TilePlan *> plans(count);
     int kps = 0;
     for (int i = 0; i < count; ++i) {
-        ST_TRY(get_plan(hs[i], L, &plans[i]));
+        ST_TRY(get_plan(hs[i], L, &plans[i], true));
         kps += (plans[i]->num_tiles ? 1 : 0) + (plans[i]->num_carries ? 1 : 0);
     }
     hipStream_t s = hs[0]->stream;
@@ -1714,7 +1767,7 @@ mspmv_status mspmv_tile_plan(mspmv_handle h, int L, int *num_tiles, int *tile_it
     if (!supported_L(L))
         return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
     const TilePlan *plan = nullptr;
-    ST_TRY(get_plan(h, L, &plan));
+    ST_TRY(get_plan(h, L, &plan, true));
     if (num_tiles)
         *num_tiles = plan->num_tiles;
     if (tile_items)
@@ -1734,7 +1787,7 @@ mspmv_status mspmv_tile_modes(mspmv_handle h, int L, unsigned char *modes)
     if (!modes)
         return invalid("null modes");
     const TilePlan *plan = nullptr;
-    ST_TRY(get_plan(h, L, &plan));
+    ST_TRY(get_plan(h, L, &plan, true));
     if (plan->num_tiles)
         HIP_TRY(hipMemcpy(modes, plan->d_modes[l_index(L)], plan->num_tiles, hipMemcpyDeviceToHost));
     // node-block tiles reduced in registers (lane tree, not the plan's mode): L = 1 on any plan
@@ -1746,11 +1799,24 @@ mspmv_status mspmv_tile_modes(mspmv_handle h, int L, unsigned char *modes)
     return MSPMV_OK;
 }
 
+mspmv_status mspmv_tile_lanes(mspmv_handle h, int L, int *lanes)
+{
+    ST_TRY(check_handle(h));
+    if (!lanes)
+        return invalid("null out pointer");
+    if (!supported_L(L))
+        return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
+    const TilePlan *plan = nullptr;
+    ST_TRY(get_plan(h, L, &plan, true));
+    *lanes = L == 1 ? plan->lanes : kBlock;
+    return MSPMV_OK;
+}
+
 mspmv_status mspmv_tile_streams(mspmv_handle h, int *tiles_cols16, int *tiles_dict)
 {
     ST_TRY(check_handle(h));
     const TilePlan *plan = nullptr;
-    ST_TRY(get_plan(h, 1, &plan));
+    ST_TRY(get_plan(h, 1, &plan, true));
     if (tiles_cols16)
         *tiles_cols16 = plan->d_cols16 ? plan->num_tiles16 : 0;
     if (tiles_dict)
@@ -1766,7 +1832,7 @@ mspmv_status mspmv_plan_block_tiles(mspmv_handle h, int L, int *tiles_blk)
     if (!supported_L(L))
         return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
     const TilePlan *plan = nullptr;
-    ST_TRY(get_plan(h, L, &plan));
+    ST_TRY(get_plan(h, L, &plan, true));
     *tiles_blk = plan->d_blk ? plan->num_tiles_blk : 0;
     return MSPMV_OK;
 }
@@ -1779,7 +1845,7 @@ mspmv_status mspmv_plan_dict_tiles(mspmv_handle h, int L, int *tiles_dict)
     if (!supported_L(L))
         return (set_error("L must be one of 1, 2, 4, 8, 16"), MSPMV_ERR_UNSUPPORTED);
     const TilePlan *plan = nullptr;
-    ST_TRY(get_plan(h, L, &plan));
+    ST_TRY(get_plan(h, L, &plan, true));
     *tiles_dict = plan->d_dict && (L == 1 || L == 16) ? plan->num_tiles_dict : 0;
     return MSPMV_OK;
 }

@@ -32,6 +32,7 @@ constexpr int kUpdateMaxBlocks = 1024;
 // coordinates ("split") and the tile before them writes a carry that a small fix-up
 // kernel adds in tile order.  Every tile holds at most tile_items + tile_items/kSnapDiv items.
 struct TilePlan {
+    int lanes = kBlock;                 // threads sharing one tile: 256, or 64 (one-wave plain-SpMV plan)
     int tile_items = 0;
     int snap = 0;
     int num_tiles = 0;
@@ -153,6 +154,9 @@ struct mspmv_handle_s {
     size_t flush_cap = 0;
     mspmv::ResidentCg *rcg = nullptr;  // register-resident CG layout (built on the first single-RHS CG)
     const char *last_cg_kernel = "";   // the CG path the last solve ran (mspmv_cg_kernel_name)
+    // plain single-RHS SpMV on one-wave tiles (a plan of its own, TilePlan::lanes = 64): -1 not
+    // decided yet, 0 no, 1 yes (mspmv_api.hip spmv_plan: skewed rows, most tiles merge walks)
+    int spmv_onewave = -1;
 };
 
 // IC(0) factor on the device (mspmv_ic0_create): L and its transpose for the two sync-free
@@ -180,7 +184,14 @@ void set_error(const std::string &msg);
 hipError_t launch_merge_coords(const int *d_row_offsets, int m, int nnz, long long diag_step, int num_parts,
                                int2 *d_out, hipStream_t s);
 hipError_t launch_tile_modes(const int *d_row_offsets, const int2 *d_bounds, const unsigned char *d_split,
-                             int num_tiles, int L, unsigned char *d_modes, hipStream_t s);
+                             int num_tiles, int L, unsigned char *d_modes, hipStream_t s, int lanes = kBlock);
+// Items per thread of the single-RHS tiles (the nominal tile is lanes x this)
+int spmv_items_per_thread();
+// Threads per single-RHS tile of the default plan (256; the MSPMV_SPMV_TB=64 lab knob makes it 64)
+int spmv_tile_lanes();
+// Whether single-RHS plans may run on one-wave tiles when their rows are skewed (MSPMV_SPMV_ONEWAVE:
+// -1 auto (default), 0 never, 1 every plain SpMV)
+int spmv_onewave_mode();
 inline int l_index(int L) { return L == 1 ? 0 : L == 2 ? 1 : L == 4 ? 2 : L == 8 ? 3 : 4; }
 hipError_t launch_snap(const int *d_row_offsets, int m, int2 *d_bounds, unsigned char *d_split, int num_tiles,
                        int snap, hipStream_t s);
@@ -220,6 +231,9 @@ hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const 
 hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L, int ld = 0);
 // Nominal tile size (merge items per tile) used for L right-hand sides.
 int tile_items_for(int L);
+// Map key of the default plan for L (one-wave plans are keyed by minus their tile size: 512 is also
+// the L = 16 tile size)
+inline int plan_key(int L) { return L == 1 && spmv_tile_lanes() == 64 ? -tile_items_for(1) : tile_items_for(L); }
 // Resident single-RHS tile workgroups per CU at the default tile shape (0: non-default tuning).
 int spmv_tile_blocks_per_cu();
 // STREAM-like nontemporal read of `bytes` (16-B words) on stream s (mspmv_time_stream_read).

@@ -389,7 +389,8 @@ __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ c
         __syncthreads();
     }
     const int lines_direct = s_scan[0];
-    if (ratio == 0 || nz == 0 || (ratio > 0 && 2 * lines_direct < nz)) {
+    // ratio >= 100 (MSPMV_SPMV_DICT=100, lab A/B): every tile takes its dictionary
+    if (ratio == 0 || nz == 0 || (ratio > 0 && ratio < 100 && 2 * lines_direct < nz)) {
         if (tid == 0)
             ndict[t] = 0;
         return;
@@ -452,7 +453,7 @@ __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ c
         __syncthreads();
     }
     const int lines_dict = s_scan[0];
-    const bool use = ratio > 0 ? 4 * lines_dict <= 3 * lines_direct : (nu <= dmax && 2 * nu <= nz);
+    const bool use = ratio >= 100 ? true : ratio > 0 ? 4 * lines_dict <= 3 * lines_direct : (nu <= dmax && 2 * nu <= nz);
     if (tid == 0)
         ndict[t] = use ? nu : 0;
     if (!use)
@@ -674,6 +675,7 @@ struct TileArgs {
     int early_re;
     int blk_rows_max;  // node-block plans: the tallest run (TilePlan::blk_rows_max; k_spmm_blk's KR)
     int tstreams;      // tile order: contiguous tile streams per XCD walked side by side (xcd_tile's K)
+    int tb;            // threads sharing one tile (the plan's lanes: 256, or 64 for one-wave SpMV plans)
 };
 
 // Tile-kernel modes.
@@ -768,6 +770,76 @@ __device__ __forceinline__ void stage_store(const StageRegs<NJ, CG> &st, int nnz
             s_prod[pslot(k)] = st.v[j] * x;
     }
 }
+// Grouped staging (plain SpMV on the 16-bit stream; MSPMV_SPMV_GROUP = W, 2 or 4, 0 = striped):
+// thread tid takes the ABSOLUTE nonzero groups q0 + tid + TB u of W consecutive nonzeros (q0 =
+// n0 / W), each one aligned W*8-B value load (W/2 16-B loads) and one aligned W*2-B column load --
+// 2/W of the striped form's column loads and 1/2 of its value loads for the same bytes (the stream
+// instructions, not its bytes, are what the tile kernel spends here: the nlpkkt120-size SpMV ran
+// 5 % faster with pairs, r03q).  Elements of a group outside the tile gather x[colbase] (always a
+// valid column) and are not stored.  A tile with a group more than NP * TB (a start off the
+// W-grid at the nominal size) issues one extra round (block-uniform).
+#ifndef MSPMV_SPMV_GROUP
+#define MSPMV_SPMV_GROUP 2  // lab builds: 0 = striped staging, 4 = quads (nlpkkt120 size 245 vs 223 us, r03r)
+#endif
+typedef unsigned v2u_t __attribute__((ext_vector_type(2)));
+template <int NP, int W>
+struct GroupRegs {
+    unsigned c[NP][W / 2];  // two 16-bit column offsets per word
+    double2 v[NP][W / 2];
+    double x[NP][W];
+};
+template <int NP, int W, bool NT, int TB>
+__device__ __forceinline__ void group_issue(const TileArgs &a, int n0, int nnzt, int colbase, int ubase,
+                                            GroupRegs<NP, W> &st)
+{
+    const int q0 = n0 / W, qlast = (n0 + nnzt - 1) / W;
+    const double2 *v2 = reinterpret_cast<const double2 *>(a.vals);
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+        const int q = min(q0 + (int)threadIdx.x + TB * (ubase + u), qlast);
+        if constexpr (W == 2) {
+            st.c[u][0] = ld_stream<NT>(reinterpret_cast<const unsigned *>(a.cols16) + q);
+        } else {
+            const v2u_t *c4 = reinterpret_cast<const v2u_t *>(a.cols16);
+            const v2u_t cc = NT ? __builtin_nontemporal_load(c4 + q) : c4[q];
+            st.c[u][0] = cc.x;
+            st.c[u][1] = cc.y;
+        }
+#pragma unroll
+        for (int h = 0; h < W / 2; ++h)
+            st.v[u][h] = ld_stream<NT>(v2 + (size_t)q * (W / 2) + h);
+    }
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+        const int q = min(q0 + (int)threadIdx.x + TB * (ubase + u), qlast);
+        const int k0 = W * q - n0;
+#pragma unroll
+        for (int e = 0; e < W; ++e) {
+            const int off = (int)((st.c[u][e >> 1] >> (16 * (e & 1))) & 0xffffu);
+            const bool in = k0 + e >= 0 && k0 + e < nnzt;
+            st.x[u][e] = a.x[colbase + (in ? off : 0)];
+        }
+    }
+}
+template <int NP, int W, int TB>
+__device__ __forceinline__ void group_store(const GroupRegs<NP, W> &st, int n0, int nnzt, int ubase, double *s_prod)
+{
+    const int q0 = n0 / W, qlast = (n0 + nnzt - 1) / W;
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+        const int q = q0 + (int)threadIdx.x + TB * (ubase + u);
+        if (q > qlast)
+            continue;
+        const int k0 = W * q - n0;
+#pragma unroll
+        for (int e = 0; e < W; ++e) {
+            const double v = (e & 1) ? st.v[u][e >> 1].y : st.v[u][e >> 1].x;
+            if (k0 + e >= 0 && k0 + e < nnzt)
+                s_prod[pslot(k0 + e)] = v * st.x[u][e];
+        }
+    }
+}
+
 template <int NJ, bool CG, bool NT>
 __device__ __forceinline__ void stage_products(const TileArgs &a, int n0, int nnzt, double beta, double *s_prod)
 {
@@ -1474,6 +1546,20 @@ k_spmv_tile(TileArgs a)
         }
     }
     if (staged) {
+    } else if (MSPMV_SPMV_GROUP > 0 && MODE == kModeSpmv && colbase >= 0 && nnzt > 0 && nnzt <= TILE) {
+        constexpr int W = MSPMV_SPMV_GROUP > 0 ? MSPMV_SPMV_GROUP : 2;
+        constexpr int NP = (TILE / TB + W - 1) / W;
+        GroupRegs<NP, W> st;
+        group_issue<NP, W, NT, TB>(a, n0, nnzt, colbase, 0, st);
+        head();
+        if (go) {
+            group_store<NP, W, TB>(st, n0, nnzt, 0, sm.prod);
+            if ((n0 + nnzt - 1) / W - n0 / W + 1 > NP * TB) {  // a start off the W-grid at the nominal size
+                GroupRegs<1, W> ex;
+                group_issue<1, W, NT, TB>(a, n0, nnzt, colbase, NP, ex);
+                group_store<1, W, TB>(ex, n0, nnzt, NP, sm.prod);
+            }
+        }
     } else if (nnzt > 0 && nnzt <= TILE) {  // the common case: no snapped-in extra nonzeros
         StageRegs<IPT, CG> st;
         stage_issue<IPT, CG, NT, TB>(a, n0, nnzt, colbase, st);
@@ -3350,12 +3436,25 @@ bool stream_nt(const mspmv_handle_s *h)
 std::string spmv_kernel_name(const mspmv_handle_s *h)
 {
     const SpmvTuning &t = spmv_tuning();
-    const auto it = h->plans.find(tile_items_for(1));
-    if (it != h->plans.end() && it->second.d_blk && it->second.num_tiles_reg == it->second.num_tiles && t.blkreg &&
-        t.tb == kBlock && !t.persist)
+    const auto it = h->plans.find(plan_key(1));
+    if (h->spmv_onewave != 1 && it != h->plans.end() && it->second.d_blk &&
+        it->second.num_tiles_reg == it->second.num_tiles && t.blkreg && t.tb == kBlock && !t.persist)
         return std::string(t.runs ? "k_spmv_runs<" : "k_spmv_blk<0,") + (stream_nt(h) ? "true>" : "false>");
+    const bool one = !t.persist && (t.tb == 64 || h->spmv_onewave == 1);
     return std::string(t.persist ? "k_spmv_persist<" : "k_spmv_tile<") + std::to_string(t.ipt) + ",0," +
-           (stream_nt(h) ? "true" : "false") + (t.tb == 64 && !t.persist ? ",64>" : ">");
+           (stream_nt(h) ? "true" : "false") + (one ? ",64>" : ">");
+}
+
+int spmv_items_per_thread() { return spmv_tuning().ipt; }
+int spmv_tile_lanes() { return spmv_tuning().tb; }
+
+int spmv_onewave_mode()
+{
+    static const int m = [] {
+        const char *e = getenv("MSPMV_SPMV_ONEWAVE");
+        return e ? (atoi(e) < 0 ? -1 : atoi(e) != 0) : -1;
+    }();
+    return spmv_tuning().tb == 64 || spmv_tuning().persist ? 0 : m;
 }
 
 
@@ -3516,14 +3615,14 @@ hipError_t launch_snap(const int *d_row_offsets, int m, int2 *d_bounds, unsigned
 }
 
 hipError_t launch_tile_modes(const int *d_row_offsets, const int2 *d_bounds, const unsigned char *d_split,
-                             int num_tiles, int L, unsigned char *d_modes, hipStream_t s)
+                             int num_tiles, int L, unsigned char *d_modes, hipStream_t s, int lanes_in)
 {
     if (num_tiles == 0)
         return hipSuccess;
     const SpmvTuning &tu = spmv_tuning();
     // SpMM budget: twice the walk's gather chunks (4 steps each) plus its search
     const int cost = L == 1 ? tu.rg_cost : tu.spmm_rg_cost >= 0 ? tu.spmm_rg_cost : 2 * (4 * (spmm_iptg_for(L) / 4) + 2);
-    const int lanes = L == 1 ? tu.tb : kBlock;  // threads sharing one tile
+    const int lanes = L == 1 ? lanes_in : kBlock;  // threads sharing one tile
     static const int force_lg = [] {
         const char *e = getenv("MSPMV_SPMM_LG");
         return e ? atoi(e) : -1;
@@ -3573,6 +3672,7 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
         return e ? std::max(1, atoi(e)) : 1;
     }();
     a.tstreams = tstreams;
+    a.tb = L == 1 ? plan.lanes : kBlock;
     return a;
 }
 
@@ -3706,7 +3806,7 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_c
                 launch_spmv_persist<I, MODE, true>(a, s, num_cus, tu.bpc);                         \
             else                                                                                   \
                 launch_spmv_persist<I, MODE, false>(a, s, num_cus, tu.bpc);                        \
-        } else if (MODE == kModeSpmv && tu.tb == 64) {                                             \
+        } else if (MODE == kModeSpmv && a.tb == 64) {                                              \
             if (nt)                                                                                \
                 hipLaunchKernelGGL((k_spmv_tile<I, kModeSpmv, true, 64>), grid, dim3(64), 0, s, a);   \
             else                                                                                   \

@@ -107,6 +107,7 @@ _SIGS = {
     "mspmv_plan_dict_tiles": (_I, [_P, _I, _PI]),
     "mspmv_plan_block_tiles": (_I, [_P, _I, _PI]),
     "mspmv_tile_modes": (_I, [_P, _I, _P]),
+    "mspmv_tile_lanes": (_I, [_P, _I, _PI]),
     "mspmv_spmv_kernel_name": (ctypes.c_char_p, [_P]),
     "mspmv_spmm_kernel_name": (ctypes.c_char_p, [_P, _I]),
     "mspmv_cg_kernel_name": (ctypes.c_char_p, [_P]),
@@ -395,8 +396,10 @@ class GpuCsr:
         bounds = np.ctypeslib.as_array(b).view(np.int32).reshape(nt.value + 1, 2).copy()
         modes = np.zeros(max(nt.value, 1), np.uint8)
         _check(lib.mspmv_tile_modes(self.h, L, _ptr(modes)), "tile_modes")
+        lanes = ctypes.c_int()
+        _check(lib.mspmv_tile_lanes(self.h, L, ctypes.byref(lanes)), "tile_lanes")
         return {"num_tiles": nt.value, "tile_items": ti.value, "num_carries": nc.value, "bounds": bounds,
-                "modes": modes[: nt.value]}
+                "modes": modes[: nt.value], "lanes": lanes.value}
 
     def tile_streams(self):
         """(tiles on 16-bit column offsets, tiles gathering through column dictionaries)."""

@@ -4,9 +4,10 @@ import numpy as np
 EPS = 2.0 ** -53
 
 
-def groups_per_tile(L):
-    """Merge walkers per 256-thread tile: one per thread (L == 1) or one per L/2 lanes."""
-    return 256 if L == 1 else 256 // (L // 2)
+def groups_per_tile(L, lanes=256):
+    """Merge walkers per tile: one per thread (L == 1; 256 threads, or 64 on a one-wave plan) or
+    one per L/2 lanes of a 256-thread tile."""
+    return lanes if L == 1 else 256 // (L // 2)
 
 
 def unsplit_rows(a, plan, L):
@@ -20,7 +21,7 @@ def unsplit_rows(a, plan, L):
     """
     bounds = plan["bounds"]
     modes = plan.get("modes")
-    ng = groups_per_tile(L)
+    ng = groups_per_tile(L, plan.get("lanes", 256))
     ro = a.row_offsets.astype(np.int64)
     mask = np.zeros(a.num_rows, bool)
     for t in range(plan["num_tiles"]):

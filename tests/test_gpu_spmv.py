@@ -122,6 +122,28 @@ def test_tile_modes_cover_both_reductions(orc):
                 assert nb >= n - 2 * plan["num_tiles"]   # all rows held whole by a tile
 
 
+def test_skewed_rows_run_one_wave_tiles(orc):
+    """Plain SpMV plan choice (spmv_plan): a power-law matrix, whose workgroup tiles are mostly
+    merge walks, runs one-wave tiles (64 lanes, 512 merge items); a banded one keeps 256-thread
+    tiles.  Parity with 64 walkers per walk tile, and the CG on the skewed handle still runs its
+    own workgroup plan."""
+    skew = mspmv.CsrMatrix.synth_powerlaw(60000, 60000, 1800000, exponent=1.2, seed=7)
+    band = mspmv.CsrMatrix.synth_banded(20000, 1000000, 800, seed=5)
+    for a, lanes in ((skew, 64), (band, 256)):
+        x = np.random.default_rng(11).uniform(-1, 1, a.num_cols)
+        with mspmv.GpuCsr(a) as g:
+            y = g.spmv(x)
+            plan = g.tile_plan(1)
+            assert plan["lanes"] == lanes, (plan["lanes"], lanes)
+            assert g.kernel_name().endswith(",64>") == (lanes == 64), g.kernel_name()
+            if lanes == 64:
+                assert (plan["modes"] == 0).any()
+            check_parity(a, y, orc.spmv_gold(a, x), x, plan, 1)
+            # the L = 2 SpMM shares the workgroup single-RHS tile size: unaffected by the choice
+            X = np.random.default_rng(12).uniform(-1, 1, (a.num_cols, 2))
+            check_parity(a, g.spmm(X), orc.csr_spmm_t(a, X), X, g.tile_plan(2), 2)
+
+
 @pytest.mark.parametrize("name", ["cant_small", "powerlaw", "fem2d", "powerlaw_rect"])
 @pytest.mark.parametrize("L", [1, 2, 4, 8, 16])
 def test_spmm_synthetic(orc, name, L):

@@ -13,6 +13,6 @@ done
 wait
 for n in "$@"; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/lab/libmspmv_abl$n.so /tmp/abl_$n.o \
-     $C/build/mspmv_api.o $C/build/mspmv_dist.o $C/build/mspmv_synth.o $C/build/mspmv_io.o $C/build/mspmv_spai.o $C/build/mspmv_ic0.o \
+     $C/build/mspmv_api.o $C/build/mspmv_dist.o $C/build/mspmv_cg_resident.o $C/build/mspmv_synth.o $C/build/mspmv_io.o $C/build/mspmv_spai.o $C/build/mspmv_ic0.o \
      -fopenmp -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 done
