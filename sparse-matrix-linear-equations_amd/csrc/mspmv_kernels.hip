@@ -1008,6 +1008,82 @@ __device__ __forceinline__ double rows8_sum(const double (&p)[kBlkRows])
     return v;
 }
 
+// rows8_sum over the 32 lanes of a half-wave: row i's total lands in lanes 4i .. 4i + 3 of the
+// half (i = (lane & 31) >> 2).  Shuffles with xor <= 16 never cross the halves, so the two halves
+// fold two different runs with the same 10 shuffles.
+__device__ __forceinline__ double rows8_sum32(const double (&p)[kBlkRows])
+{
+    const int lane = threadIdx.x & 63;
+    const bool b4 = lane & 16, b3 = lane & 8, b2 = lane & 4;
+    double q4[4], q2[2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        q4[k] = (b4 ? p[k + 4] : p[k]) + __shfl_xor(b4 ? p[k] : p[k + 4], 16);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        q2[k] = (b3 ? q4[k + 2] : q4[k]) + __shfl_xor(b3 ? q4[k] : q4[k + 2], 8);
+    double v = (b2 ? q2[1] : q2[0]) + __shfl_xor(b2 ? q2[0] : q2[1], 4);
+    v += __shfl_xor(v, 2);
+    v += __shfl_xor(v, 1);
+    return v;
+}
+
+// Plain SpMV form of blk_rows with column PAIRS (MSPMV_BLK_PAIR): each half-wave owns one run per
+// round and its lane l owns pattern columns 2l and 2l + 1, so a row of the run arrives in ONE
+// 16-B load per lane (half the value-load instructions of column-owner lanes; the loads may be
+// 8-B aligned only -- gfx9's unaligned access mode), and one rows8_sum32 folds both halves' runs
+// (half the shuffles).  A lane's two products are added before the half-wave tree: a fixed order,
+// so rows stay reproducible and within the reordering bound (mode 255).
+#ifndef MSPMV_BLK_PAIR
+#define MSPMV_BLK_PAIR 1  // lab builds: 0 keeps column-owner lanes (pwtk shape 24.98 vs 22.6-23.1 us, r03t)
+#endif
+template <bool NT, int KR>
+__device__ __forceinline__ void blk_rows_pair(const TileArgs &a, const uint4 &bd, int nd, int r0, int n0,
+                                              int colbase)
+{
+    constexpr int NW = kBlock / 64;
+    const int lane = threadIdx.x & 63;
+    const int half = lane >> 5, hl = lane & 31;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    for (int round = 0; round * 2 * NW < nd; ++round) {
+        const int di = wave + NW * (2 * round + half);
+        const bool valid = di < nd;
+        const int src = min(di, nd - 1);  // descriptor lane (every wave holds all of them in bd)
+        const uint4 d = make_uint4((unsigned)__shfl((int)bd.x, src), (unsigned)__shfl((int)bd.y, src),
+                                   (unsigned)__shfl((int)bd.z, src), (unsigned)__shfl((int)bd.w, src));
+        const int vofs = d.x & 0xffff, wc = d.x >> 24;
+        const int h = d.y & 15, p = (d.y >> 4) & 7, rofs = d.y >> 16;
+        double2 v[KR];
+        bool in0[KR], in1[KR];
+        int start = 0, pstart = 0;
+#pragma unroll
+        for (int i = 0; i < KR; ++i) {
+            pstart = i == p ? start : pstart;
+            const int len = blk_len(d, i);
+            in0[i] = valid && i < h && 2 * hl < len;
+            in1[i] = valid && i < h && 2 * hl + 1 < len;
+            v[i] = make_double2(0.0, 0.0);
+            if (in0[i])
+                v[i] = ld_stream<NT>(reinterpret_cast<const double2 *>(a.vals + n0 + vofs + start + 2 * hl));
+            start += i < h ? len : 0;
+        }
+        int c0 = 0, c1 = 0;  // column 0 of x: always valid to gather
+        if (valid && 2 * hl < wc)
+            c0 = colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + 2 * hl);
+        if (valid && 2 * hl + 1 < wc)
+            c1 = colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + 2 * hl + 1);
+        const double x0 = a.x[c0], x1 = a.x[c1];
+        double pr[kBlkRows];
+#pragma unroll
+        for (int i = 0; i < kBlkRows; ++i)
+            pr[i] = i < KR ? (in0[i] ? v[i].x * x0 : 0.0) + (in1[i] ? v[i].y * x1 : 0.0) : 0.0;
+        const double sum = rows8_sum32(pr);
+        const int myrow = hl >> 2;
+        if (valid && (hl & 3) == 0 && myrow < h)
+            a.y[r0 + rofs + myrow] = sum;
+    }
+}
+
 // Node-block tiles whose runs are at most 64 columns wide (one chunk each: FEM node rows) skip
 // LDS altogether: lane j of the run's wave holds the products of pattern column j in every row
 // of the run, rows8_sum folds them across the wave, and lane 8i stores row i (y; CG: p for the
@@ -1631,7 +1707,7 @@ struct BlkSmem {
     int last;
 };
 
-template <int MODE, bool NT>
+template <int MODE, bool NT, int KR = kBlkRows>
 __global__ __launch_bounds__(kBlock) void k_spmv_blk(TileArgs a)
 {
     constexpr bool CG = MODE == kModeCg;
@@ -1649,6 +1725,11 @@ __global__ __launch_bounds__(kBlock) void k_spmv_blk(TileArgs a)
     PartRegs<CG ? kUpdateMaxBlocks / kBlock : 1> pin;
     if constexpr (CG)
         part_load(a.part_in, a.n_part_in, pin);
+    if constexpr (MODE == kModeSpmv && MSPMV_BLK_PAIR && KR <= 6) {  // taller runs: 73 VGPRs, column owners
+        if (!stopped)
+            blk_rows_pair<NT, KR>(a, bd, nblk, b0.x, b0.y, colbase);
+        return;
+    }
     blk_rows<MODE, NT, kBlock>(a, bd, nblk, b0.x, b0.y, colbase, beta, dot, [&]() {
         if (stopped)
             go = false;
@@ -3439,7 +3520,8 @@ std::string spmv_kernel_name(const mspmv_handle_s *h)
     const auto it = h->plans.find(plan_key(1));
     if (h->spmv_onewave != 1 && it != h->plans.end() && it->second.d_blk &&
         it->second.num_tiles_reg == it->second.num_tiles && t.blkreg && t.tb == kBlock && !t.persist)
-        return std::string(t.runs ? "k_spmv_runs<" : "k_spmv_blk<0,") + (stream_nt(h) ? "true>" : "false>");
+        return std::string(t.runs ? "k_spmv_runs<" : "k_spmv_blk<0,") + (stream_nt(h) ? "true" : "false") +
+               (t.runs ? ">" : MSPMV_BLK_PAIR && it->second.blk_rows_max <= 6 ? ",6>" : ",8>");
     const bool one = !t.persist && (t.tb == 64 || h->spmv_onewave == 1);
     return std::string(t.persist ? "k_spmv_persist<" : "k_spmv_tile<") + std::to_string(t.ipt) + ",0," +
            (stream_nt(h) ? "true" : "false") + (one ? ",64>" : ">");
@@ -3790,6 +3872,13 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_c
                 launch_spmv_runs<true>(a, s, num_cus);
             else
                 launch_spmv_runs<false>(a, s, num_cus);
+            break;
+        }
+        if (MSPMV_BLK_PAIR && MODE == kModeSpmv && a.all_reg && !tu.persist && a.blk_rows_max <= 6) {
+            if (nt)  // runs of <= 6 rows (6-DOF FEM): the pair form's value arrays sized to them
+                hipLaunchKernelGGL((k_spmv_blk<kModeSpmv, true, 6>), grid, block, 0, s, a);
+            else
+                hipLaunchKernelGGL((k_spmv_blk<kModeSpmv, false, 6>), grid, block, 0, s, a);
             break;
         }
         if (a.all_reg && !tu.persist && MODE != kModeCg) {
