@@ -2459,7 +2459,7 @@ k_spmm_blk(TileArgs a)
     // own LDS slice, and a pass reads v[i][j] there (one broadcast read per (pass, row)) instead of
     // holding the rows in registers and shuffling them (two bpermutes per (pass, row))
     constexpr bool LDSV = MSPMV_SPMM_BLK_LDSV != 0;
-    __shared__ double s_v[LDSV ? kBlock / 64 : 1][LDSV ? kBlkRows : 1][64];
+    __shared__ __attribute__((aligned(16))) double s_v[LDSV ? kBlock / 64 : 1][LDSV ? kBlkRows : 1][64];
     __shared__ int s_c[LDSV ? kBlock / 64 : 1][64];
     const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
     const int tid = threadIdx.x, lane = tid & 63;
@@ -2496,6 +2496,12 @@ k_spmm_blk(TileArgs a)
     // PF (with LDSV): the wave's next chunk's columns and values are loaded while this chunk's
     // passes run (they land in registers the LDS slice has just been filled from)
     constexpr bool PF = LDSV && MSPMV_SPMM_BLK_PF != 0;
+#ifndef MSPMV_SPMM_BLK_V2
+#define MSPMV_SPMM_BLK_V2 0  // measured slower: pwtk L = 16 cold 52.8-53.4 vs 50.2-50.8 us (r03v)
+#endif
+    // V2 (with LDSV, without PF): the run's values arrive as column pairs, two rows per load
+    // instruction (the node-block SpMV's blk_rows_pair finding: load instructions, not bytes)
+    constexpr bool V2 = LDSV && !PF && MSPMV_SPMM_BLK_V2 != 0 && KR % 2 == 0;
     int colj_n = 0;
     double vrow_n[KR];
     if (PF && wave < nd && !stopped)
@@ -2518,10 +2524,48 @@ k_spmm_blk(TileArgs a)
 #pragma unroll
             for (int i = 0; i < KR; ++i)
                 vrow[i] = vrow_n[i];
-        } else {
+        } else if constexpr (!V2) {
             fetch(di, colj, vrow);
         }
-        if constexpr (LDSV) {  // wave-private slice: the wave's LDS operations stay in order
+        if constexpr (LDSV && V2) {
+            // column pairs: half h2 of the wave loads rows h2, h2 + 2, ... of the run, lane hl its
+            // columns 2 hl and 2 hl + 1 -- one 16-B load per lane for two rows (8-B aligned at worst),
+            // stored into the slice as one 16-B LDS write; rows >= h and columns past a row hold 0.0
+            const int vofs = d.x & 0xffff, p = (d.y >> 4) & 7;
+            const int h2 = lane >> 5, hl = lane & 31;
+            int start[KR];
+            int pstart = 0, acc_s = 0;
+#pragma unroll
+            for (int i = 0; i < KR; ++i) {
+                start[i] = acc_s;
+                pstart = i == p ? acc_s : pstart;
+                acc_s += i < h ? blk_len(d, i) : 0;
+            }
+            colj = lane < wc ? colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + lane) : 0;
+            double2 vp[KR / 2];
+#pragma unroll
+            for (int ii = 0; ii < KR / 2; ++ii) {
+                const int i = 2 * ii + h2;
+                int len = 0;
+#pragma unroll
+                for (int r = 0; r < KR; ++r)  // row i's length and start (i differs between the halves)
+                    len = r == i ? blk_len(d, r) : len;
+                int st0 = 0;
+#pragma unroll
+                for (int r = 0; r < KR; ++r)
+                    st0 = r == i ? start[r] : st0;
+                vp[ii] = make_double2(0.0, 0.0);
+                if (i < h && 2 * hl < len)
+                    vp[ii] = ld_stream<NT>(reinterpret_cast<const double2 *>(a.vals + n0 + vofs + st0 + 2 * hl));
+                if (!(i < h && 2 * hl + 1 < len))
+                    vp[ii].y = 0.0;
+            }
+            s_c[wave][lane] = colj;
+#pragma unroll
+            for (int ii = 0; ii < KR / 2; ++ii)
+                *reinterpret_cast<double2 *>(&s_v[wave][2 * ii + h2][2 * hl]) = vp[ii];
+            __builtin_amdgcn_wave_barrier();
+        } else if constexpr (LDSV) {  // wave-private slice: the wave's LDS operations stay in order
             s_c[wave][lane] = colj;
 #pragma unroll
             for (int i = 0; i < KR; ++i)  // rows >= h too (0.0 from fetch): the passes read every row
