@@ -18,7 +18,7 @@ import sys
 
 
 def short_name(name):
-    n = name.replace("void ", "").replace("mspmv::", "").split("(")[0]
+    n = name.replace("void ", "").replace("mspmv::", "").replace("(anonymous namespace)::", "").split("(")[0]
     return n.replace(" ", "")
 
 
@@ -33,7 +33,7 @@ def grid_stats(trace_csv):
     prev = ""
     for r in recs:
         k = short_name(r["Kernel_Name"])
-        key = (k, int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]), int(prev == "k_flush"))
+        key = (k, int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"]), int(prev in ("k_flush", "k_flush_read")))
         prev = k.split("<")[0]
         groups[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0)
         first.setdefault(key, int(r["Dispatch_Id"]))

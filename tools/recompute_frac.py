@@ -70,6 +70,11 @@ def cg_loop_times(trace, iterations):
         k = short_name(r["Kernel_Name"])
         calls[k] = calls.get(k, 0) + 1
     loop = {k for k, c in calls.items() if c >= iterations}
+    if not loop:  # the register-resident CG: the whole solve is ONE cooperative launch (the last one is timed)
+        res = [r for r in recs if short_name(r["Kernel_Name"]).startswith("k_cg_resident")]
+        if res:
+            dur = (int(res[-1]["End_Timestamp"]) - int(res[-1]["Start_Timestamp"])) / 1000.0
+            return dur / iterations, dur / iterations, [short_name(res[-1]["Kernel_Name"])]
     lrecs = [r for r in recs if short_name(r["Kernel_Name"]) in loop]
     busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in lrecs) / 1000.0
     half = lrecs[len(lrecs) // 2:]
