@@ -2127,6 +2127,9 @@ constexpr int spmm_waves_per_eu(int L, int IPTG, bool DICT = false)
 // (pwtk shape): L = 16 130 -> 102 us; at L = 4 and 8 it lost (47 -> 55, 63 -> 67 us; the
 // 27-point nlpkkt120 size at L = 8 505 -> 590 us: the extra dependent round trip and the
 // occupancy the 16 KB panel costs outweigh 64-B gathers), so only L = 16 plans build one.
+#ifndef MSPMV_SPMM_GROUP4
+#define MSPMV_SPMM_GROUP4 0  // measured even: CG multi L = 8 0.915-0.920 vs 0.914 ms/iteration (r03z)
+#endif
 template <int L, int IPTG, int MODE, bool NT, bool DICT = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(spmm_waves_per_eu(L, IPTG, DICT)))) void
 k_spmm_tile(TileArgs a)
@@ -2179,7 +2182,37 @@ k_spmm_tile(TileArgs a)
     // Every round's loads are issued before any is stored to LDS (indices clamped into the
     // tile), the first round of row ends with them: one memory round trip per tile, not STG.
     const int re0 = a.row_offsets[min(r0 + 1 + min(tid, max(nrows - 1, 0)), a.m)];  // clamped: always issued
-    if (nnzt > 0) {  // block-uniform
+    if (MSPMV_SPMM_GROUP4 && !DICT && nnzt > 0) {  // block-uniform
+        // grouped staging: thread tid takes the absolute groups of 4 consecutive nonzeros q0 + tid +
+        // 256 u (q0 = n0 / 4): one 16-B column load and two 16-B value loads per group instead of
+        // four 4-B and four 8-B loads (the single-RHS pair staging's finding: load instructions)
+        constexpr int NR = (MAXI / 4 + 1 + kBlock - 1) / kBlock;
+        const int q0 = n0 >> 2, qlast = (n0 + nnzt - 1) >> 2;
+        int4 c4[NR];
+        double2 v4[NR][2];
+#pragma unroll
+        for (int u = 0; u < NR; ++u) {
+            const int q = min(q0 + tid + kBlock * u, qlast);
+            c4[u] = ld_stream<NT>(reinterpret_cast<const int4 *>(a.cols) + q);
+            v4[u][0] = ld_stream<NT>(reinterpret_cast<const double2 *>(a.vals) + 2 * (size_t)q);
+            v4[u][1] = ld_stream<NT>(reinterpret_cast<const double2 *>(a.vals) + 2 * (size_t)q + 1);
+        }
+#pragma unroll
+        for (int u = 0; u < NR; ++u) {
+            const int q = q0 + tid + kBlock * u;
+            if (q > qlast)
+                continue;
+            const int k0 = 4 * q - n0;
+            const int cc[4] = {c4[u].x, c4[u].y, c4[u].z, c4[u].w};
+            const double vv[4] = {v4[u][0].x, v4[u][0].y, v4[u][1].x, v4[u][1].y};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (k0 + e >= 0 && k0 + e < nnzt) {
+                    s_col[k0 + e] = cc[e];
+                    s_val[k0 + e] = vv[e];
+                }
+        }
+    } else if (nnzt > 0) {  // block-uniform
         int cst[STG];
         double vst[STG];
         if (DICT && nd > 0) {
