@@ -2919,6 +2919,39 @@ __device__ __forceinline__ long long sweep_index(long long k, long long nchunks,
     return (rev ? nchunks - 1 - k : k) * stride + i0;
 }
 
+// The pairs a thread of a streaming CG kernel visits, in order.  Grid-stride chunks (the whole grid
+// sweeps one chunk after another, rev: last chunk first) or, with MSPMV_VEC_SLICE, one contiguous
+// slice per workgroup walked 256 pairs at a time (rev: from the slice's end) -- the layout of the
+// measured read ceiling (tools/read_ceiling.hip).  Slices are a multiple of GL pairs long, so a
+// thread keeps its column pair (tid % GL) either way.
+#ifndef MSPMV_VEC_SLICE
+#define MSPMV_VEC_SLICE 0  // measured even: CG multi L = 8 0.920-0.921 vs 0.916-0.919 ms/iteration (r03aa)
+#endif
+template <int GL, typename F>
+__device__ __forceinline__ void for_pairs(long long npairs, int rev, F &&f)
+{
+    if (MSPMV_VEC_SLICE) {
+        long long per = (npairs + gridDim.x - 1) / gridDim.x;
+        per = (per + GL - 1) / GL * GL;
+        const long long lo = min(npairs, (long long)blockIdx.x * per), hi = min(npairs, lo + per);
+        const long long nch = (hi - lo + kBlock - 1) / kBlock;
+        for (long long k = 0; k < nch; ++k) {
+            const long long i = lo + (rev ? nch - 1 - k : k) * kBlock + threadIdx.x;
+            if (i < hi)
+                f(i);
+        }
+    } else {
+        const long long stride = (long long)gridDim.x * kBlock;
+        const long long i0 = (long long)blockIdx.x * kBlock + threadIdx.x;
+        const long long nch = (npairs + stride - 1) / stride;
+        for (long long k = 0; k < nch; ++k) {
+            const long long i = sweep_index(k, nch, stride, i0, rev);
+            if (i < npairs)
+                f(i);
+        }
+    }
+}
+
 // x = 0, r = p0 = b; rs_old_j = r_j.r_j, b_norm_j = sqrt(b_j.b_j) (no_pretreatment.hpp:61-79,
 // single_strategy.hpp:120-131).
 template <int L>
@@ -3016,7 +3049,8 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(CgVecArgs a)
     const double2 nal = make_double2(-al.x, -al.y);
     double2 acc = make_double2(0.0, 0.0);
     if (a.lazy_x) {  // x += alpha p: deferred to the next p update (CgVecArgs::lazy_x)
-        for (long long i = i0; i < npairs; i += stride) {
+        (void)stride;
+        for_pairs<GL>(npairs, 0, [&](long long i) {
             const double2 q = reinterpret_cast<const double2 *>(a.ap)[i];
             double2 r = reinterpret_cast<double2 *>(a.r)[i];
             r.x = r.x + nal.x * q.x;
@@ -3024,7 +3058,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(CgVecArgs a)
             reinterpret_cast<double2 *>(a.r)[i] = r;
             acc.x += r.x * r.x;
             acc.y += r.y * r.y;
-        }
+        });
     } else {
         for (long long i = i0; i < npairs; i += stride) {
             const double2 p = reinterpret_cast<const double2 *>(a.p)[i];
@@ -3148,11 +3182,7 @@ __global__ __launch_bounds__(kBlock) void k_dist_pupdate(CgVecArgs a, double *p)
     const double2 alpha = make_double2(a.scal[2 * cp].alpha, a.scal[2 * cp + 1].alpha);
     const long long npairs = a.n_elems / 2;
     if (lag) {
-        const long long nch = (npairs + stride - 1) / stride;
-        for (long long k = 0; k < nch; ++k) {
-            const long long i = sweep_index(k, nch, stride, i0, a.rev);
-            if (i >= npairs)
-                continue;
+        for_pairs<GL>(npairs, a.rev, [&](long long i) {
             const double2 r = reinterpret_cast<const double2 *>(a.r)[i];
             double2 q = reinterpret_cast<double2 *>(p)[i];
             double2 x = reinterpret_cast<double2 *>(a.x)[i];
@@ -3162,7 +3192,7 @@ __global__ __launch_bounds__(kBlock) void k_dist_pupdate(CgVecArgs a, double *p)
             q.x = r.x + beta.x * q.x;
             q.y = r.y + beta.y * q.y;
             reinterpret_cast<double2 *>(p)[i] = q;
-        }
+        });
         return;
     }
     for (long long i = i0; i < npairs; i += stride) {
@@ -3347,17 +3377,15 @@ __global__ __launch_bounds__(kBlock) void k_pcg_dot(CgVecArgs a, int mode)
     const long long npairs = a.n_elems / 2;
     const long long stride = (long long)gridDim.x * kBlock;
     const long long i0 = (long long)blockIdx.x * kBlock + tid;
-    const long long nch = (npairs + stride - 1) / stride;
     double2 acc = make_double2(0.0, 0.0);
-    for (long long k = 0; k < nch; ++k) {
-        const long long i = sweep_index(k, nch, stride, i0, a.rev);
-        if (i >= npairs)
-            continue;
+    (void)stride;
+    (void)i0;
+    for_pairs<GL>(npairs, a.rev, [&](long long i) {
         const double2 r = reinterpret_cast<const double2 *>(a.r)[i];
         const double2 z = reinterpret_cast<const double2 *>(a.p)[i];
         acc.x += r.x * z.x;
         acc.y += r.y * z.y;
-    }
+    });
     if ((a.n_elems & 1) && blockIdx.x == 0 && tid == 0)
         acc.x += a.r[a.n_elems - 1] * a.p[a.n_elems - 1];
     colpair_block_reduce<L>(acc, s_red2, a.partials + (size_t)blockIdx.x * L);
