@@ -92,6 +92,7 @@ static void free_plan(TilePlan &p)
         dev_free(m);
     dev_free(p.d_carry_tiles);
     dev_free(p.d_carry_rows);
+    dev_free(p.d_carry_runs);
     dev_free(p.d_carry_val);
     dev_free(p.d_colbase);
     dev_free(p.d_cols16);
@@ -242,9 +243,21 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         if ((st = dev_alloc(&p.d_carry_tiles, ct.size())) != MSPMV_OK ||
             (st = dev_alloc(&p.d_carry_rows, cr.size())) != MSPMV_OK)
             return fail(st);
+        // runs of consecutive carries of one row (a hub row split over many tiles: hundreds), each
+        // summed by one wave of the fix-up
+        std::vector<int> runs;
+        for (size_t i = 0; i < cr.size(); ++i)
+            if (i == 0 || cr[i] != cr[i - 1])
+                runs.push_back((int)i);
+        p.num_carry_runs = (int)runs.size();
+        runs.push_back((int)cr.size());
+        if ((st = dev_alloc(&p.d_carry_runs, runs.size())) != MSPMV_OK)
+            return fail(st);
         e = hipMemcpy(p.d_carry_tiles, ct.data(), sizeof(int) * ct.size(), hipMemcpyHostToDevice);
         if (e == hipSuccess)
             e = hipMemcpy(p.d_carry_rows, cr.data(), sizeof(int) * cr.size(), hipMemcpyHostToDevice);
+        if (e == hipSuccess)
+            e = hipMemcpy(p.d_carry_runs, runs.data(), sizeof(int) * runs.size(), hipMemcpyHostToDevice);
         if (e != hipSuccess) {
             set_error(std::string("tile plan upload: ") + hipGetErrorString(e));
             return fail(MSPMV_ERR_HIP);
@@ -1631,10 +1644,10 @@ mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y,
             e = launch_spmm_dot(h, *plan, d_X, d_Y, L, h->d_ctrl, h->d_partials, h->d_gtickets, h->d_red);
         else if (e == hipSuccess)
             e = launch_spmm_tile_only(h, *plan, d_X, d_Y, L);
+        if (e == hipSuccess && !time_dot)  // the product is complete only after the carries: timed with it
+            e = launch_fixup(h, *plan, d_Y, L);
         if (e == hipSuccess)
             e = hipEventRecord(ev[2 * i + 1], h->stream);
-        if (e == hipSuccess)
-            e = launch_fixup(h, *plan, d_Y, L);
     }
     if (e == hipSuccess)
         e = hipEventRecord(ev[2 * reps], h->stream);

@@ -45,6 +45,8 @@ struct TilePlan {
     int *d_carry_tiles = nullptr;       // [num_carries] tile ids, ascending
     int *d_carry_rows = nullptr;        // [num_carries] row each carry belongs to
     double *d_carry_val = nullptr;      // [num_tiles * L_max]
+    int num_carry_runs = 0;             // maximal runs of consecutive carries of one row
+    int *d_carry_runs = nullptr;        // [num_carry_runs + 1] first carry of each run, then num_carries
     int carry_L = 0;                    // capacity (columns) of d_carry_val
     // Single-RHS plans: 16-bit column offsets.  A tile whose columns span < 65536 stores
     // col - colbase[t] in cols16 (2 B per nonzero instead of 4 in the HBM stream); colbase[t]

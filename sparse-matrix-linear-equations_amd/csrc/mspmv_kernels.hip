@@ -1372,7 +1372,7 @@ __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT, TB> 
             } else if (MODE == kModeDot) {
                 dot += ox * v;
             }
-        } else {  // the trailing partial row -> carry (k_fixup adds it in tile order)
+        } else {  // the trailing partial row -> carry (k_fixup adds the row's carries in a fixed order)
             a.carry_val[t] = v;
             if (MODE == kModeCg)
                 dot += (ox + beta * op) * v;
@@ -2094,7 +2094,7 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
             const size_t off = (size_t)(r0 + r) * a.ld + 2 * lane;
             if (r < nrows)
                 *reinterpret_cast<double2 *>(a.y + off) = acc;
-            else  // the trailing partial row -> carry (k_fixup adds it in tile order)
+            else  // the trailing partial row -> carry (k_fixup adds the row's carries in a fixed order)
                 *reinterpret_cast<double2 *>(a.carry_val + (size_t)t * L + 2 * lane) = acc;
             if (MODE == kModeDot && !kSpmmDotTail) {
                 dot.x += xx.x * acc.x;
@@ -2818,23 +2818,40 @@ __global__ __launch_bounds__(kBlock) void k_fold_dot(const double *part, int T, 
 
 // Rows split between tiles: y[R] = (carry_a + carry_a+1 + ...) + y[R], carries in tile order.
 // One thread per (carry, column); the first carry of each row's run sums the run.
-__global__ void k_fixup(const int *__restrict__ carry_tiles, const int *__restrict__ carry_rows, int nc,
-                        const double *__restrict__ carry_val, double *__restrict__ Y, int L,
-                        const CgControl *ctrl, int ld)
+// Carries of split rows (tiles that end inside a row), added after the tile kernel.  One wave per
+// (run of consecutive carries of one row, column j): lane l sums carries l, l + 64, ... of the run in
+// order, a fixed xor butterfly folds the wave, lane 0 adds the total to the row the completing tile
+// wrote.  Fixed order, so reproducible; a hub row split over hundreds of tiles (the skewed variant's
+// dense row: 425 one-wave tiles) costs one wave round trip instead of a serial loop over its carries
+// (85 us before, r03u).
+__global__ void k_fixup(const int *__restrict__ carry_tiles, const int *__restrict__ carry_rows,
+                        const int *__restrict__ carry_runs, int nruns, const double *__restrict__ carry_val,
+                        double *__restrict__ Y, int L, const CgControl *ctrl, int ld)
 {
     if (ctrl && ctrl->done)
         return;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    const int i = idx / L, j = idx % L;
-    if (i >= nc)
+    const int w = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6), lane = threadIdx.x & 63;
+    const int run = w / L, j = w % L;
+    if (run >= nruns)  // wave-uniform
         return;
-    const int R = carry_rows[i];
-    if (i > 0 && carry_rows[i - 1] == R)
-        return;
-    double sum = carry_val[(size_t)carry_tiles[i] * L + j];
-    for (int u = i + 1; u < nc && carry_rows[u] == R; ++u)
+    const int i0 = carry_runs[run], i1 = carry_runs[run + 1];
+    double sum = 0.0;
+    for (int u = i0 + lane; u < i1; u += 64)
         sum += carry_val[(size_t)carry_tiles[u] * L + j];
-    Y[(size_t)R * ld + j] = sum + Y[(size_t)R * ld + j];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        sum += __shfl_xor(sum, off);
+    if (lane == 0) {
+        const int R = carry_rows[i0];
+        Y[(size_t)R * ld + j] = sum + Y[(size_t)R * ld + j];
+    }
+}
+
+static void fixup_launch(const TilePlan &plan, double *d_Y, int L, const CgControl *ctrl, int ld, hipStream_t s)
+{
+    const long long waves = (long long)plan.num_carry_runs * L;
+    hipLaunchKernelGGL(k_fixup, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, plan.d_carry_tiles,
+                       plan.d_carry_rows, plan.d_carry_runs, plan.num_carry_runs, plan.d_carry_val, d_Y, L, ctrl, ld);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -4053,9 +4070,7 @@ hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, in
         ld = L;
     if (plan.num_carries == 0)
         return hipSuccess;
-    const int n = plan.num_carries * L;
-    hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, h->stream, plan.d_carry_tiles,
-                       plan.d_carry_rows, plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)nullptr, ld);
+    fixup_launch(plan, d_Y, L, nullptr, ld, h->stream);
     return hipGetLastError();
 }
 
@@ -4352,9 +4367,7 @@ static hipError_t launch_fixup_ctrl(mspmv_handle_s *h, const TilePlan &plan, dou
 {
     if (plan.num_carries == 0)
         return hipSuccess;
-    const int n = plan.num_carries * L;
-    hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, h->stream, plan.d_carry_tiles, plan.d_carry_rows,
-                       plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)h->d_ctrl, L);
+    fixup_launch(plan, d_Y, L, h->d_ctrl, L, h->stream);
     return hipGetLastError();
 }
 
@@ -4551,9 +4564,7 @@ hipError_t launch_spmm_dot_tiles(mspmv_handle_s *h, const TilePlan &plan, const 
     if (e != hipSuccess)
         return e;
     if (plan.num_carries) {
-        const int n = plan.num_carries * L;
-        hipLaunchKernelGGL(k_fixup, dim3((n + 255) / 256), dim3(256), 0, s, plan.d_carry_tiles, plan.d_carry_rows,
-                           plan.num_carries, plan.d_carry_val, d_Y, L, (const CgControl *)ctrl, L);
+        fixup_launch(plan, d_Y, L, ctrl, L, s);
         e = hipGetLastError();
     }
     return e;
