@@ -173,7 +173,11 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
     p.lanes = (L == 1 && (onewave || tile_items_for(1) == 64 * spmv_items_per_thread())) ? 64 : kBlock;
     const long long total = (long long)h->m + h->nnz;
     int step = tile, snap = tile / kSnapDiv;
-    if (tile == tile_items_for(1) && p.lanes == kBlock) {
+    static const bool stretch_on = [] {  // lab knob: MSPMV_SPMV_STRETCH=0 keeps nominal tiles
+        const char *e = getenv("MSPMV_SPMV_STRETCH");
+        return !e || atoi(e) != 0;
+    }();
+    if (tile == tile_items_for(1) && p.lanes == kBlock && stretch_on) {
         // A grid a few tiles over a whole number of resident generations of workgroups takes one
         // tile lifetime more (the parabolic_fem shape: 2,052 tiles on 2,048 slots).  Stretch the
         // tiles into the snap slack so they fit one generation fewer: MAXI (step + snap) is
