@@ -147,7 +147,9 @@ def main(src, dst):
     lines += ["", "hot rows include the untimed warm-up launches; cold rows are the launches right after bench's "
               "512 MiB flush kernel.  CG: span = the timed solve's first-to-last loop-kernel time / iterations "
               "(bench divides wall time, which adds the host call); kernel-busy = the loop kernels' summed "
-              "durations per iteration."]
+              "durations per iteration.  spmm16 / spmv_shapes: since r03ab the bench's cold time is the "
+              "tile kernel AND its carry fix-up (plus the event gap of the second launch); the trace column "
+              "is the tile kernel alone."]
     open(out("frac_check.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
