@@ -343,6 +343,29 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
                 set_error("node blocks: upload failed");
                 return fail(MSPMV_ERR_HIP);
             }
+            if (p.num_tiles_reg == T) {  // the pair form's one-gather-per-pair test (all-register plans)
+                int *d_ok = nullptr;
+                int ok = 1;
+                if ((st = dev_alloc(&d_ok, 1)) != MSPMV_OK)
+                    return fail(st);
+                e = hipMemcpy(d_ok, &ok, sizeof(int), hipMemcpyHostToDevice);
+                if (e == hipSuccess)
+                    e = launch_blk_pairs_check(h->d_cols, p.d_bounds, p.d_blk, p.blk_stride, T, d_ok, h->stream);
+                if (e == hipSuccess)
+                    e = hipMemcpyAsync(&ok, d_ok, sizeof(int), hipMemcpyDeviceToHost, h->stream);
+                if (e == hipSuccess)
+                    e = hipStreamSynchronize(h->stream);
+                dev_free(d_ok);
+                if (e != hipSuccess) {
+                    set_error(std::string("node-block pairs: ") + hipGetErrorString(e));
+                    return fail(MSPMV_ERR_HIP);
+                }
+                static const bool pg_on = [] {  // lab knob: MSPMV_BLK_PAIRGATHER=0 gathers per column
+                    const char *v = getenv("MSPMV_BLK_PAIRGATHER");
+                    return !v || atoi(v) != 0;
+                }();
+                p.blk_pairs = ok && pg_on;
+            }
         }
     }
     // multi-RHS: only the L = 16 plan (k_spmm_tile's DICT path runs at L = 16 only)

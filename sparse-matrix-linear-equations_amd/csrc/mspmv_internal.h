@@ -68,6 +68,7 @@ struct TilePlan {
     int num_tiles_blk = 0;              // tiles staged by node blocks
     int num_tiles_reg = 0;              // of those, tiles reduced in registers (h_blk_reg)
     int blk_rows_max = 8;               // the tallest run (rows of one node) over the descriptors
+    int blk_pairs = 0;                  // every run pattern pairs consecutive columns (k_blk_pairs_check)
     std::vector<unsigned char> h_blk_reg;  // [num_tiles] 1: every run one chunk wide (the SpMV reduces
                                            // such tiles in registers; mspmv_tile_modes reports 255)
 };
@@ -210,6 +211,8 @@ constexpr int kBlkPerTile = 64;  // == kBlkMax in the kernels: descriptor capaci
 hipError_t launch_build_blocks(const int *d_row_offsets, const int *d_cols, const int2 *d_bounds,
                                const unsigned char *d_split, const int *d_colbase, int num_tiles, uint4 *d_blk,
                                hipStream_t s);
+hipError_t launch_blk_pairs_check(const int *d_cols, const int2 *d_bounds, const uint4 *d_blk, int stride,
+                                  int num_tiles, int *d_ok, hipStream_t s);
 hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_tiles, int max_items, int *d_dict,
                              int *d_ndict, unsigned short *d_idx16, hipStream_t s, bool multi);
 bool spmm_dict_enabled();

@@ -676,6 +676,8 @@ struct TileArgs {
     int blk_rows_max;  // node-block plans: the tallest run (TilePlan::blk_rows_max; k_spmm_blk's KR)
     int tstreams;      // tile order: contiguous tile streams per XCD walked side by side (xcd_tile's K)
     int tb;            // threads sharing one tile (the plan's lanes: 256, or 64 for one-wave SpMV plans)
+    int blk_pairs;     // node-block plans whose run patterns pair consecutive columns (TilePlan::blk_pairs)
+    int n;             // columns (x holds n entries)
 };
 
 // Tile-kernel modes.
@@ -1068,11 +1070,25 @@ __device__ __forceinline__ void blk_rows_pair(const TileArgs &a, const uint4 &bd
             start += i < h ? len : 0;
         }
         int c0 = 0, c1 = 0;  // column 0 of x: always valid to gather
-        if (valid && 2 * hl < wc)
-            c0 = colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + 2 * hl);
-        if (valid && 2 * hl + 1 < wc)
-            c1 = colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + 2 * hl + 1);
-        const double x0 = a.x[c0], x1 = a.x[c1];
+        double x0, x1;
+        if (a.blk_pairs) {
+            // the plan checked P[2j + 1] == P[2j] + 1 (k_blk_pairs_check): one column offset and ONE
+            // 16-B gather (8-B aligned at worst) per lane; the last column sits at n - 1 at most, so the
+            // load starts at n - 2 at most and picks its half
+            if (valid && 2 * hl < wc)
+                c0 = colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + 2 * hl);
+            const int base = min(c0, a.n - 2);
+            const double2 xx = *reinterpret_cast<const double2 *>(a.x + base);
+            x0 = base == c0 ? xx.x : xx.y;
+            x1 = xx.y;  // used only where 2 hl + 1 < wc, i.e. column c0 + 1 <= n - 1 and base == c0
+        } else {
+            if (valid && 2 * hl < wc)
+                c0 = colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + 2 * hl);
+            if (valid && 2 * hl + 1 < wc)
+                c1 = colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + 2 * hl + 1);
+            x0 = a.x[c0];
+            x1 = a.x[c1];
+        }
         double pr[kBlkRows];
 #pragma unroll
         for (int i = 0; i < kBlkRows; ++i)
@@ -3782,6 +3798,45 @@ hipError_t launch_build_blocks(const int *d_row_offsets, const int *d_cols, cons
     return hipGetLastError();
 }
 
+// Plan time: do the run patterns of every node-block tile come in pairs of consecutive columns
+// (P[2j + 1] == P[2j] + 1)?  FEM nodes with an even number of unknowns do (pwtk: 6 per node).
+// One thread per tile (descriptors packed at `stride`); *ok is cleared by any pair that is not.
+__global__ void k_blk_pairs_check(const int *__restrict__ cols, const int2 *__restrict__ bounds,
+                                  const uint4 *__restrict__ blk, int stride, int num_tiles, int *ok)
+{
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= num_tiles)
+        return;
+    const int n0 = bounds[t].y;
+    const int nd = (int)((blk[(size_t)t * stride].y >> 8) & 255u);
+    bool good = true;
+    for (int di = 0; di < nd && good; ++di) {
+        const uint4 d = blk[(size_t)t * stride + di];
+        const int vofs = d.x & 0xffff, wc = d.x >> 24, h = d.y & 15, p = (d.y >> 4) & 7;
+        int start = 0, pstart = 0;
+        for (int i = 0; i < h; ++i) {
+            if (i == p)
+                pstart = start;
+            start += blk_len(d, i);
+        }
+        const int *c = cols + n0 + vofs + pstart;
+        for (int j = 0; 2 * j + 1 < wc && good; ++j)
+            good = c[2 * j + 1] == c[2 * j] + 1;
+    }
+    if (!good)
+        atomicAnd(ok, 0);
+}
+
+hipError_t launch_blk_pairs_check(const int *d_cols, const int2 *d_bounds, const uint4 *d_blk, int stride,
+                                  int num_tiles, int *d_ok, hipStream_t s)
+{
+    if (num_tiles <= 0)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_blk_pairs_check, dim3((num_tiles + 255) / 256), dim3(256), 0, s, d_cols, d_bounds, d_blk,
+                       stride, num_tiles, d_ok);
+    return hipGetLastError();
+}
+
 bool spmm_dict_enabled()
 {
     static const bool on = [] {
@@ -3877,6 +3932,8 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
     }();
     a.tstreams = tstreams;
     a.tb = L == 1 ? plan.lanes : kBlock;
+    a.blk_pairs = L == 1 && plan.blk_pairs && h->n >= 2;
+    a.n = h->n;
     return a;
 }
 
