@@ -780,6 +780,9 @@ __device__ __forceinline__ void stage_store(const StageRegs<NJ, CG> &st, int nnz
 // 5 % faster with pairs, r03q).  Elements of a group outside the tile gather x[colbase] (always a
 // valid column) and are not stored.  A tile with a group more than NP * TB (a start off the
 // W-grid at the nominal size) issues one extra round (block-uniform).
+#ifndef MSPMV_SPMV_XPAIR
+#define MSPMV_SPMV_XPAIR 0  // lab: one 16-B x load per consecutive pair -- nlpkkt120 size 261-262 vs 220-224 us (r03af)
+#endif
 #ifndef MSPMV_SPMV_GROUP
 #define MSPMV_SPMV_GROUP 2  // lab builds: 0 = striped staging, 4 = quads (nlpkkt120 size 245 vs 223 us, r03r)
 #endif
@@ -815,6 +818,24 @@ __device__ __forceinline__ void group_issue(const TileArgs &a, int n0, int nnzt,
     for (int u = 0; u < NP; ++u) {
         const int q = min(q0 + (int)threadIdx.x + TB * (ubase + u), qlast);
         const int k0 = W * q - n0;
+        if (W == 2 && MSPMV_SPMV_XPAIR) {
+            // a pair whose columns are consecutive (stencil / FEM runs) takes both x values from ONE
+            // 16-B load (8-B aligned at worst, clamped to start at n - 2); the second gather is issued
+            // only for the lanes whose columns are not -- when at least half the wave's pairs are
+            const int c0 = colbase + ((k0 >= 0) ? (int)(st.c[u][0] & 0xffffu) : 0);
+            const int c1 = colbase + ((k0 + 1 < nnzt) ? (int)(st.c[u][0] >> 16) : 0);
+            const bool adj = c1 == c0 + 1;
+            if (__popcll(__ballot(adj)) >= 32) {  // wave-uniform
+                const int base = min(c0, a.n - 2);
+                const double2 xx = *reinterpret_cast<const double2 *>(a.x + base);
+                st.x[u][0] = base == c0 ? xx.x : xx.y;
+                st.x[u][1] = (adj && base == c0) ? xx.y : a.x[c1];
+                continue;
+            }
+            st.x[u][0] = a.x[c0];
+            st.x[u][1] = a.x[c1];
+            continue;
+        }
 #pragma unroll
         for (int e = 0; e < W; ++e) {
             const int off = (int)((st.c[u][e >> 1] >> (16 * (e & 1))) & 0xffffu);
