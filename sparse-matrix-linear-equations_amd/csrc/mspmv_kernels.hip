@@ -1690,8 +1690,8 @@ k_spmv_tile(TileArgs a)
     }
     if (!go)
         return;
-    // Row ends after the staging: measured faster here than issuing them with the stream
-    // (+0.9 us on the pwtk shape), unlike the multi-RHS kernel.
+    // Row ends: issued with the stream by default (TileArgs::early_re; with the pair staging 1-2 %
+    // faster, r03ah/r03ai -- with the old striped staging it had measured +0.9 us on pwtk), or here.
 #if MSPMV_LAB_ABLATE == 9
     __syncthreads();
     const unsigned long long lab_t1 = wall_clock64();
@@ -3609,7 +3609,8 @@ struct SpmvTuning {
     int blkreg = 1;   // plans of register node-block tiles only run the LDS-free k_spmv_blk
     int runs = 0;     // ... or, for the plain SpMV, the persistent wave-pipelined k_spmv_runs
     int spmm_blk = 1; // SpMM (L >= 2) on such a plan runs k_spmm_blk instead of its own L-wide tiles
-    int early_re = 0; // single-RHS tile kernel: row ends issued with the stream (TileArgs::early_re)
+    int early_re = 1; // single-RHS tile kernel: row ends issued with the stream (TileArgs::early_re); with
+                      // the pair staging it measured 1-2 % faster (nlpkkt120 size, cant, pipelined CG: r03ah/r03ai)
     int dict = 1;     // single-RHS SpMV through per-tile column dictionaries (k_build_dict) when
                       // a tile's nonzeros repeat its distinct columns >= dict_ratio times (0: off)
 };
