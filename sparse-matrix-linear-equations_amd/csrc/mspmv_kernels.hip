@@ -917,6 +917,65 @@ __device__ __forceinline__ void dict_stage(const TileArgs &a, double *s_prod, in
     }
 }
 
+// dict_stage with the pair staging's loads (MSPMV_SPMV_DICT_PAIR): thread tid takes the absolute
+// nonzero pairs n0/2 + tid + TB u -- one 16-B value load and one 4-B load of two dictionary
+// positions per pair; the same products into the same slots, so results are unchanged.
+#ifndef MSPMV_SPMV_DICT_PAIR
+#define MSPMV_SPMV_DICT_PAIR 0  // lab: measured even or slower on cant / rma10 / scattered band (r03aj)
+#endif
+template <int NP, bool NT, int TB>
+__device__ __forceinline__ void dict_stage_pair(const TileArgs &a, double *s_prod, int nd, int n0, int nnzt)
+{
+    constexpr int DJ = 3;
+    const int tid = threadIdx.x;
+    const int q0 = n0 >> 1, qlast = (n0 + nnzt - 1) >> 1;
+    unsigned ix[NP];
+    double2 v[NP];
+    int dc[DJ];
+    double dx[DJ];
+#pragma unroll
+    for (int u = 0; u < DJ; ++u)
+        dc[u] = ld_stream<NT>(a.dict + n0 + min(tid + u * TB, nd - 1));
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+        const int q = min(q0 + tid + TB * u, qlast);
+        ix[u] = ld_stream<NT>(reinterpret_cast<const unsigned *>(a.idx16) + q);
+        v[u] = ld_stream<NT>(reinterpret_cast<const double2 *>(a.vals) + q);
+    }
+#pragma unroll
+    for (int u = 0; u < DJ; ++u)
+        dx[u] = a.x[dc[u]];
+    double *s_x = s_prod;  // nd <= nnzt: the dictionary's x fits the product slots
+#pragma unroll
+    for (int u = 0; u < DJ; ++u)
+        if (tid + u * TB < nd)
+            s_x[tid + u * TB] = dx[u];
+    for (int d = tid + DJ * TB; d < nd; d += TB)  // rare: > DJ * TB distinct columns
+        s_x[d] = a.x[a.dict[n0 + d]];
+    tile_sync<TB>();
+    double pr[NP][2];
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+        const int q = min(q0 + tid + TB * u, qlast);
+        const int k0 = 2 * q - n0;
+        // positions of elements outside the tile belong to a neighbour's dictionary: read slot 0
+        pr[u][0] = v[u].x * s_x[k0 >= 0 ? (int)(ix[u] & 0xffffu) : 0];
+        pr[u][1] = v[u].y * s_x[k0 + 1 < nnzt ? (int)(ix[u] >> 16) : 0];
+    }
+    tile_sync<TB>();
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+        const int q = q0 + tid + TB * u;
+        if (q > qlast)
+            continue;
+        const int k0 = 2 * q - n0;
+        if (k0 >= 0)
+            s_prod[pslot(k0)] = pr[u][0];
+        if (k0 + 1 < nnzt)
+            s_prod[pslot(k0 + 1)] = pr[u][1];
+    }
+}
+
 // Node-block staging (k_build_blocks): wave w takes the tile's run chunks w, w + 4, ..., two per
 // round.  Per chunk, lane l owns pattern column j = j0 + l: one 16-bit column offset of row P,
 // one gather (x, or CG's {r, p}), and the values of that column in every row of the run that is
@@ -1651,7 +1710,9 @@ k_spmv_tile(TileArgs a)
     } else if constexpr (MODE == kModeSpmv) {
         const int nd = a.dict ? a.ndict[t] : 0;  // > 0: this tile gathers through its dictionary
         if (nd > 0) {
-            if (nnzt <= TILE)
+            if (MSPMV_SPMV_DICT_PAIR && nnzt <= TILE && ((n0 + nnzt - 1) >> 1) - (n0 >> 1) + 1 <= (TILE / TB + 1) / 2 * TB)
+                dict_stage_pair<(TILE / TB + 1) / 2, NT, TB>(a, sm.prod, nd, n0, nnzt);
+            else if (nnzt <= TILE)
                 dict_stage<IPT, NT, TB>(a, sm.prod, nd, n0, nnzt);
             else
                 dict_stage<MAXJ, NT, TB>(a, sm.prod, nd, n0, nnzt);
