@@ -105,7 +105,9 @@ static void free_plan(TilePlan &p)
 // Build (once) the tile plan for L right-hand sides, validating on the host every bound the
 // kernels rely on (monotone boundaries, <= 1.25 * tile_items merge items per tile) before any
 // tile kernel can run on it.
-static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes = 0);
+static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes = 0, int wide_tile = 0);
+// Map key of a wide node-block plan (build_plan's wide_tile): apart from every other plan's key
+static int wide_key(int tile) { return 1 << 24 | tile; }
 
 // The in-tile reduction modes of a plan for L right-hand sides, built on first use.
 static mspmv_status ensure_modes(mspmv_handle_s *h, TilePlan &p, int L)
@@ -163,12 +165,14 @@ static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out, boo
     return MSPMV_OK;
 }
 
-static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes)
+static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes, int wide_tile)
 {
     // lanes: 64 builds the one-wave single-RHS plan (tile = 64 x items per thread, keyed by that
-    // size); 0 the default plan for L
+    // size); wide_tile > 0 a single-RHS node-block plan of wider tiles (two rounds of runs per
+    // workgroup allowed; spmv_plan); 0 the default plan for L
     const bool onewave = L == 1 && lanes == 64 && tile_items_for(1) != 64 * spmv_items_per_thread();
-    const int tile = onewave ? 64 * spmv_items_per_thread() : tile_items_for(L);
+    const bool wide = L == 1 && wide_tile > 0 && !onewave;
+    const int tile = onewave ? 64 * spmv_items_per_thread() : wide ? wide_tile : tile_items_for(L);
     TilePlan p;
     p.lanes = (L == 1 && (onewave || tile_items_for(1) == 64 * spmv_items_per_thread())) ? 64 : kBlock;
     const long long total = (long long)h->m + h->nnz;
@@ -177,7 +181,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         const char *e = getenv("MSPMV_SPMV_STRETCH");
         return !e || atoi(e) != 0;
     }();
-    if (tile == tile_items_for(1) && p.lanes == kBlock && stretch_on) {
+    if (tile == tile_items_for(1) && p.lanes == kBlock && stretch_on && !wide) {
         // A grid a few tiles over a whole number of resident generations of workgroups takes one
         // tile lifetime more (the parabolic_fem shape: 2,052 tiles on 2,048 slots).  Stretch the
         // tiles into the snap slack so they fit one generation fewer: MAXI (step + snap) is
@@ -270,7 +274,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
     // the single-RHS kernels' 16-bit column stream; keyed on the tile size, not L, because the
     // L = 2 SpMM shares the single-RHS plan.  (The SpMM itself keeps int32 columns: it is gather
     // bound, and the 16-bit stream measured 0% at L = 4/8 and 7% slower at L = 16.)
-    const bool single = tile == tile_items_for(1) || onewave;  // a single-RHS plan
+    const bool single = tile == tile_items_for(1) || onewave || wide;  // a single-RHS plan
     if (single && T > 0 && h->nnz > 0 && spmv_cols16_enabled()) {
         if ((st = dev_alloc(&p.d_colbase, (size_t)T)) != MSPMV_OK ||
             (st = dev_alloc(&p.d_cols16, (size_t)h->nnz + kNnzPad)) != MSPMV_OK)
@@ -297,11 +301,11 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         }
     }
     // node blocks: single-RHS plan on the 16-bit stream only (the runs' pattern columns are read there)
-    if (tile == tile_items_for(1) && !onewave && p.lanes == kBlock && p.d_cols16 && spmv_blocks_enabled()) {
+    if ((tile == tile_items_for(1) || wide) && !onewave && p.lanes == kBlock && p.d_cols16 && spmv_blocks_enabled()) {
         if ((st = dev_alloc(&p.d_blk, (size_t)T * kBlkPerTile)) != MSPMV_OK)
             return fail(st);
         e = launch_build_blocks(h->d_row_offsets, h->d_cols, p.d_bounds, p.d_split, p.d_colbase, T, p.d_blk,
-                                h->stream);
+                                h->stream, wide ? 16 : 8);
         std::vector<uint4> hd((size_t)T * kBlkPerTile);
         if (e == hipSuccess)
             e = hipMemcpyAsync(hd.data(), p.d_blk, sizeof(uint4) * hd.size(), hipMemcpyDeviceToHost, h->stream);
@@ -370,7 +374,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
     }
     // multi-RHS: only the L = 16 plan (k_spmm_tile's DICT path runs at L = 16 only)
     const bool multi = !single;
-    const bool want = multi ? L == 16 && tile != tile_items_for(8) && spmm_dict_enabled() : spmv_dict_enabled();
+    const bool want = multi ? L == 16 && tile != tile_items_for(8) && spmm_dict_enabled() : spmv_dict_enabled() && !wide;
     if (T > 0 && h->nnz > 0 && want) {
         if ((st = dev_alloc(&p.d_dict, (size_t)h->nnz + kNnzPad)) != MSPMV_OK ||
             (st = dev_alloc(&p.d_ndict, (size_t)T)) != MSPMV_OK ||
@@ -401,7 +405,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
             p.d_idx16 = nullptr;
         }
     }
-    auto res = h->plans.emplace(p.lanes == 64 ? -tile : tile, p);  // one-wave plans: negative keys (plan_key)
+    auto res = h->plans.emplace(wide ? wide_key(tile) : p.lanes == 64 ? -tile : tile, p);  // one-wave: negative keys
     *out = &res.first->second;
     return MSPMV_OK;
 }
@@ -435,9 +439,35 @@ static mspmv_status spmv_plan(mspmv_handle_s *h, const TilePlan **out)
             ST_TRY(ensure_modes(h, h->plans.find(key)->second, 1));
         }
         h->spmv_onewave = want ? 1 : 0;
+        // node-block plans (every tile a register run tile whose pattern columns pair up): wider tiles
+        // fill more of a workgroup's eight half-wave run slots (MSPMV_BLK_TILE merge items, 0 = off)
+        static const int wide_tile = [] {
+            const char *v = getenv("MSPMV_BLK_TILE");
+            return v ? std::max(0, atoi(v)) : kBlkWideTile;
+        }();
+        if (!want && wide_tile > wg->tile_items && wide_tile <= 8192 && wg->d_blk &&
+            wg->num_tiles_reg == wg->num_tiles && wg->blk_pairs) {
+            const TilePlan *np = nullptr;
+            if (h->plans.find(wide_key(wide_tile)) == h->plans.end())
+                ST_TRY(build_plan(h, 1, &np, 0, wide_tile));
+            TilePlan &wp = h->plans.find(wide_key(wide_tile))->second;
+            if (wp.d_blk && wp.num_tiles_reg == wp.num_tiles && wp.blk_pairs &&
+                wp.blk_rows_max <= wg->blk_rows_max) {
+                ST_TRY(ensure_modes(h, wp, 1));
+                h->spmv_onewave = 2;
+            }
+        }
     }
     if (h->spmv_onewave == 1) {
         *out = &h->plans.find(-64 * spmv_items_per_thread())->second;
+        return MSPMV_OK;
+    }
+    if (h->spmv_onewave == 2) {
+        static const int wide_tile2 = [] {
+            const char *v = getenv("MSPMV_BLK_TILE");
+            return v ? std::max(0, atoi(v)) : kBlkWideTile;
+        }();
+        *out = &h->plans.find(wide_key(wide_tile2))->second;
         return MSPMV_OK;
     }
     *out = wg;

@@ -158,7 +158,8 @@ struct mspmv_handle_s {
     mspmv::ResidentCg *rcg = nullptr;  // register-resident CG layout (built on the first single-RHS CG)
     const char *last_cg_kernel = "";   // the CG path the last solve ran (mspmv_cg_kernel_name)
     // plain single-RHS SpMV on one-wave tiles (a plan of its own, TilePlan::lanes = 64): -1 not
-    // decided yet, 0 no, 1 yes (mspmv_api.hip spmv_plan: skewed rows, most tiles merge walks)
+    // decided yet, 0 no, 1 yes (mspmv_api.hip spmv_plan: skewed rows, most tiles merge walks); 2: a wide
+    // node-block plan of its own (MSPMV_BLK_TILE)
     int spmv_onewave = -1;
 };
 
@@ -208,9 +209,14 @@ bool spmv_blocks_enabled();
 // SpMM (L >= 2) through the single-RHS node-block plan (k_spmm_blk) when all its tiles are register tiles.
 bool spmm_blk_enabled();
 constexpr int kBlkPerTile = 64;  // == kBlkMax in the kernels: descriptor capacity of a tile
+// Merge items per tile of the plain SpMV's wide node-block plan (spmv_plan; 0 = off)
+#ifndef MSPMV_BLK_WIDE_TILE
+#define MSPMV_BLK_WIDE_TILE 0  // lab: 2560 / 3072 / 4096 measured 0.78 / 0.79 / 0.82-0.83 vs 0.82-0.84 (r03an)
+#endif
+constexpr int kBlkWideTile = MSPMV_BLK_WIDE_TILE;
 hipError_t launch_build_blocks(const int *d_row_offsets, const int *d_cols, const int2 *d_bounds,
                                const unsigned char *d_split, const int *d_colbase, int num_tiles, uint4 *d_blk,
-                               hipStream_t s);
+                               hipStream_t s, int max_chunks = 8);
 hipError_t launch_blk_pairs_check(const int *d_cols, const int2 *d_bounds, const uint4 *d_blk, int stride,
                                   int num_tiles, int *d_ok, hipStream_t s);
 hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_tiles, int max_items, int *d_dict,

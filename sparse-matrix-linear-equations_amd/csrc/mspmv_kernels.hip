@@ -503,7 +503,8 @@ __device__ __forceinline__ int blk_len(const uint4 &d, int i)
 // the 16-bit column stream, fits in kBlkMax chunks, and its runs pay (below).
 __global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *__restrict__ cols,
                                const int2 *__restrict__ bounds, const unsigned char *__restrict__ split,
-                               const int *__restrict__ colbase, int num_tiles, uint4 *__restrict__ blk)
+                               const int *__restrict__ colbase, int num_tiles, uint4 *__restrict__ blk,
+                               int max_chunks)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= num_tiles)
@@ -566,7 +567,7 @@ __global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *_
     // for the first's sums.  2-D Kronecker FEM matrices with 3, 4 and 6 unknowns per node (15-30
     // columns, ~11-20 runs per tile) ran 3.1x, 2.0x and 1.2x slower on node blocks than striped;
     // the pwtk shape (53 columns, ~7 runs per tile) 1.14x faster.
-    if (5 * sum_w > 3 * (n1 - n0) || sum_w < 32 * nruns || nd > 8)
+    if (5 * sum_w > 3 * (n1 - n0) || sum_w < 32 * nruns || nd > max_chunks)
         return;
     d0.y |= (unsigned)nd << 8;
     out[0] = d0;
@@ -3871,13 +3872,13 @@ bool spmm_blk_enabled() { return spmv_tuning().spmm_blk != 0 && spmv_tuning().bl
 
 hipError_t launch_build_blocks(const int *d_row_offsets, const int *d_cols, const int2 *d_bounds,
                                const unsigned char *d_split, const int *d_colbase, int num_tiles, uint4 *d_blk,
-                               hipStream_t s)
+                               hipStream_t s, int max_chunks)
 {
     static_assert(kBlkMax == kBlkPerTile, "descriptor capacity");
     if (num_tiles <= 0)
         return hipSuccess;
     hipLaunchKernelGGL(k_build_blocks, dim3((num_tiles + 127) / 128), dim3(128), 0, s, d_row_offsets, d_cols, d_bounds,
-                       d_split, d_colbase, num_tiles, d_blk);
+                       d_split, d_colbase, num_tiles, d_blk, max_chunks);
     return hipGetLastError();
 }
 
