@@ -335,6 +335,41 @@ def run_spmm16(dev, cpu_seconds, do_cpu):
     return out
 
 
+def resident_phases(g, db, dx, thr, stamp_iters=256):
+    """Where an iteration of the register-resident CG goes (configs[3]'s kernel keeps the matrix in
+    VGPRs/LDS, so its 'bytes per iteration' are a speed figure, not HBM traffic): one extra solve with
+    wall_clock64() stamps (100 MHz) at the phase boundaries of every workgroup (mspmv_cg_resident_stamps),
+    medians over workgroups and iterations 1..stamp_iters-1:
+      spmv    iteration start -> the workgroup's rows of Ap done (p gathers + row sums)
+      handoff1 the LAST workgroup's Ap done -> this workgroup has the p.Ap total (the reduction hand-off
+               itself; time waiting for slower workgroups is 'skew1')
+      update  p.Ap total -> the workgroup's r update done
+      handoff2 the last workgroup's r done -> this workgroup has the r.r total ('skew2' likewise)
+    The stamped solve runs beside no other work; its stamps add a barrier per phase, so its
+    iteration time is quoted next to the unstamped one."""
+    its, st = g.cg_resident_stamps(db, dx, 10000, thr, stamp_iters)
+    k = min(its, stamp_iters)
+    if k < 3:
+        return None
+    t = st[1:k].astype(np.int64)          # [iters][G][5], skip iteration 0 (cold)
+    us = 0.01                             # one tick of the 100 MHz clock in microseconds
+    last1 = t[:, :, 1].max(axis=1, keepdims=True)
+    last3 = t[:, :, 3].max(axis=1, keepdims=True)
+    med = lambda a: round(float(np.median(a)) * us, 3)
+    out = {"stamped_iterations": int(k - 1), "workgroups": int(t.shape[1]),
+           "spmv_us": med(t[:, :, 1] - t[:, :, 0]),
+           "skew1_us": med(last1[:, 0:1] - t[:, :, 1]),
+           "handoff1_us": med(t[:, :, 2] - last1),
+           "update_us": med(t[:, :, 3] - t[:, :, 2]),
+           "skew2_us": med(last3[:, 0:1] - t[:, :, 3]),
+           "handoff2_us": med(t[:, :, 4] - last3),
+           "spmv_max_us": round(float(np.median((t[:, :, 1] - t[:, :, 0]).max(axis=1))) * us, 3)}
+    out["iteration_us"] = med(t[1:, :, 0] - t[:-1, :, 0])
+    out["note"] = ("medians over workgroups x iterations of wall_clock64 phase stamps; handoff = last "
+                   "publisher -> total received; skew = own publish -> last publisher")
+    return out
+
+
 def run_cg_single(dev, cpu_seconds, do_cpu):
     """configs[3]: CGSolveSingle on a parabolic_fem-shaped SPD matrix."""
     pf = mspmv.CsrMatrix.synth_stencil(0, PARABOLIC_FEM["m"], PARABOLIC_FEM["width"],
@@ -348,13 +383,20 @@ def run_cg_single(dev, cpu_seconds, do_cpu):
         t0 = time.perf_counter()
         it, _, st = g.cg_dev(db, dx, 1, 10000, thr)
         el = time.perf_counter() - t0
+        kernel = g.cg_kernel_name()
+        phases = resident_phases(g, db, dx, thr) if kernel.startswith("k_cg_resident") else None
+        db.free()
+        dx.free()
     ips = it / el
     out = {"workload": f"CGSolveSingle, parabolic_fem-shaped SPD (7-pt FEM, diag shift {PARABOLIC_FEM['shift']}) "
                        f"m={n} nnz={pf.num_nonzeros}, srand(42) RHS, tol = 1e-5*||b|| (cpu_singlecg quirk)",
            "iterations": it, "seconds": round(el, 5), "iters_per_s": round(ips, 1),
            "us_per_iter": round(el / max(it, 1) * 1e6, 2),
            "achieved_GBps": round(cg_iter_bytes(n, pf.num_nonzeros) * ips / 1e9, 1),
-           "roofline_frac": round(cg_iter_bytes(n, pf.num_nonzeros) * ips / 1e9 / HBM_PEAK_GBS, 4), "status": st}
+           "roofline_frac": round(cg_iter_bytes(n, pf.num_nonzeros) * ips / 1e9 / HBM_PEAK_GBS, 4), "status": st,
+           "kernel": kernel}
+    if phases:
+        out["resident_phases"] = phases
     if do_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from _oracle import Oracle

@@ -135,6 +135,17 @@ MSPMV_API mspmv_status mspmv_dcg_single(mspmv_handle h, const double *b, double 
                               int *iters, double *resid_hist, int hist_cap);
 MSPMV_API mspmv_status mspmv_dcg_single_dev(mspmv_handle h, const double *d_b, double *d_x, int max_iters, double tolerance,
                                   int *iters, double *resid_hist, int hist_cap);
+/* Diagnostic (measurement of configs[3]'s kernel): one register-resident single-RHS solve, as
+ * mspmv_dcg_single_dev on device vectors, that also records wall_clock64() (a constant 100 MHz
+ * clock) at five phase boundaries of every workgroup's iterations k < stamp_iters:
+ * stamps[(k * G + w) * 5 + i], i = 0 iteration start, 1 the workgroup's rows of Ap done, 2 the
+ * p.Ap total received, 3 the workgroup's r update done, 4 the r.r total received (entries of
+ * iterations not run stay 0).  stamps holds stamp_iters * G * 5 values; *workgroups = G.
+ * MSPMV_ERR_UNSUPPORTED when the matrix does not take the resident path.  No reference
+ * counterpart (CGSolveSingle has no instrumentation). */
+MSPMV_API mspmv_status mspmv_cg_resident_stamps(mspmv_handle h, const double *d_b, double *d_x, int max_iters,
+                                                double tolerance, int *iters, unsigned long long *stamps,
+                                                int stamp_iters, int *workgroups);
 /* Block multi-RHS CG, CGSolveMultiple (work_2025/main/no_pretreatment.hpp:32-197): L
  * lock-step recurrences on interleaved n x L panels, per-column converged masks
  * (alpha = beta = 0 once converged), stop when all columns converged.  Breakdown is per

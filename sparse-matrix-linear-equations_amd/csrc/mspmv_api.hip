@@ -105,9 +105,7 @@ static void free_plan(TilePlan &p)
 // Build (once) the tile plan for L right-hand sides, validating on the host every bound the
 // kernels rely on (monotone boundaries, <= 1.25 * tile_items merge items per tile) before any
 // tile kernel can run on it.
-static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes = 0, int wide_tile = 0);
-// Map key of a wide node-block plan (build_plan's wide_tile): apart from every other plan's key
-static int wide_key(int tile) { return 1 << 24 | tile; }
+static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes = 0);
 
 // The in-tile reduction modes of a plan for L right-hand sides, built on first use.
 static mspmv_status ensure_modes(mspmv_handle_s *h, TilePlan &p, int L)
@@ -165,28 +163,22 @@ static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out, boo
     return MSPMV_OK;
 }
 
-static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes, int wide_tile)
+static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes)
 {
-    // lanes: 64 builds the one-wave single-RHS plan (tile = 64 x items per thread, keyed by that
-    // size); wide_tile > 0 a single-RHS node-block plan of wider tiles (two rounds of runs per
-    // workgroup allowed; spmv_plan); 0 the default plan for L
-    const bool onewave = L == 1 && lanes == 64 && tile_items_for(1) != 64 * spmv_items_per_thread();
-    const bool wide = L == 1 && wide_tile > 0 && !onewave;
-    const int tile = onewave ? 64 * spmv_items_per_thread() : wide ? wide_tile : tile_items_for(L);
+    // lanes: 64 builds the one-wave single-RHS plan (tile = 64 x items per thread, keyed by minus
+    // that size); 0 the default plan for L
+    const bool onewave = L == 1 && lanes == 64;
+    const int tile = onewave ? 64 * spmv_items_per_thread() : tile_items_for(L);
     TilePlan p;
-    p.lanes = (L == 1 && (onewave || tile_items_for(1) == 64 * spmv_items_per_thread())) ? 64 : kBlock;
+    p.lanes = onewave ? 64 : kBlock;
     const long long total = (long long)h->m + h->nnz;
     int step = tile, snap = tile / kSnapDiv;
-    static const bool stretch_on = [] {  // lab knob: MSPMV_SPMV_STRETCH=0 keeps nominal tiles
-        const char *e = getenv("MSPMV_SPMV_STRETCH");
-        return !e || atoi(e) != 0;
-    }();
-    if (tile == tile_items_for(1) && p.lanes == kBlock && stretch_on && !wide) {
+    if (L == 1 && !onewave) {
         // A grid a few tiles over a whole number of resident generations of workgroups takes one
         // tile lifetime more (the parabolic_fem shape: 2,052 tiles on 2,048 slots).  Stretch the
         // tiles into the snap slack so they fit one generation fewer: MAXI (step + snap) is
         // unchanged, rows entered by more than the smaller snap distance stay split (carries,
-        // k_fixup).
+        // k_fixup).  (Measured against nominal tiles in round 3: kept.)
         const long long slots = (long long)h->num_cus * spmv_tile_blocks_per_cu();
         const long long t0 = (total + tile - 1) / tile;
         if (slots > 0 && t0 > slots) {
@@ -274,8 +266,8 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
     // the single-RHS kernels' 16-bit column stream; keyed on the tile size, not L, because the
     // L = 2 SpMM shares the single-RHS plan.  (The SpMM itself keeps int32 columns: it is gather
     // bound, and the 16-bit stream measured 0% at L = 4/8 and 7% slower at L = 16.)
-    const bool single = tile == tile_items_for(1) || onewave || wide;  // a single-RHS plan
-    if (single && T > 0 && h->nnz > 0 && spmv_cols16_enabled()) {
+    const bool single = L == 1;  // a single-RHS plan
+    if (single && T > 0 && h->nnz > 0) {
         if ((st = dev_alloc(&p.d_colbase, (size_t)T)) != MSPMV_OK ||
             (st = dev_alloc(&p.d_cols16, (size_t)h->nnz + kNnzPad)) != MSPMV_OK)
             return fail(st);
@@ -301,11 +293,11 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         }
     }
     // node blocks: single-RHS plan on the 16-bit stream only (the runs' pattern columns are read there)
-    if ((tile == tile_items_for(1) || wide) && !onewave && p.lanes == kBlock && p.d_cols16 && spmv_blocks_enabled()) {
+    if (single && !onewave && p.d_cols16 && spmv_blocks_enabled()) {
         if ((st = dev_alloc(&p.d_blk, (size_t)T * kBlkPerTile)) != MSPMV_OK)
             return fail(st);
         e = launch_build_blocks(h->d_row_offsets, h->d_cols, p.d_bounds, p.d_split, p.d_colbase, T, p.d_blk,
-                                h->stream, wide ? 16 : 8);
+                                h->stream, kBlkPlanChunks);
         std::vector<uint4> hd((size_t)T * kBlkPerTile);
         if (e == hipSuccess)
             e = hipMemcpyAsync(hd.data(), p.d_blk, sizeof(uint4) * hd.size(), hipMemcpyDeviceToHost, h->stream);
@@ -317,6 +309,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         }
         p.h_blk_reg.assign((size_t)T, 0);
         int maxnd = 0, maxh = 0;
+        std::vector<unsigned char> reg((size_t)T, 0);
         for (int t = 0; t < T; ++t) {
             const uint4 *d = &hd[(size_t)t * kBlkPerTile];
             const int nd = (int)((d[0].y >> 8) & 255u);
@@ -326,11 +319,19 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
             maxnd = std::max(maxnd, nd);
             for (int i = 0; i < nd; ++i)
                 maxh = std::max(maxh, (int)(d[i].y & 15u));
-            bool one = true;  // the kernel's own test: every chunk starts at pattern column 0
+            bool one = true;  // the kernels' own test: every chunk starts at pattern column 0
             for (int i = 0; i < nd; ++i)
                 one = one && ((d[i].x >> 16) & 255u) == 0;
-            p.h_blk_reg[(size_t)t] = one;
+            reg[(size_t)t] = one;
             p.num_tiles_reg += one;
+        }
+        // the plain SpMV runs the column-pair node-block kernel (its register fallback taking the
+        // other tiles) when most tiles are register run tiles; otherwise k_spmv_tile, whose register
+        // path takes the run tiles of one round (<= kBlkTileChunks chunks)
+        p.blk_spmv = p.num_tiles_reg > 0 && 2LL * p.num_tiles_reg >= T;
+        for (int t = 0; t < T; ++t) {
+            const int nd = (int)((hd[(size_t)t * kBlkPerTile].y >> 8) & 255u);
+            p.h_blk_reg[(size_t)t] = p.blk_spmv || (reg[(size_t)t] && nd <= kBlkTileChunks);
         }
         dev_free(p.d_blk);
         p.d_blk = nullptr;
@@ -347,34 +348,11 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
                 set_error("node blocks: upload failed");
                 return fail(MSPMV_ERR_HIP);
             }
-            if (p.num_tiles_reg == T) {  // the pair form's one-gather-per-pair test (all-register plans)
-                int *d_ok = nullptr;
-                int ok = 1;
-                if ((st = dev_alloc(&d_ok, 1)) != MSPMV_OK)
-                    return fail(st);
-                e = hipMemcpy(d_ok, &ok, sizeof(int), hipMemcpyHostToDevice);
-                if (e == hipSuccess)
-                    e = launch_blk_pairs_check(h->d_cols, p.d_bounds, p.d_blk, p.blk_stride, T, d_ok, h->stream);
-                if (e == hipSuccess)
-                    e = hipMemcpyAsync(&ok, d_ok, sizeof(int), hipMemcpyDeviceToHost, h->stream);
-                if (e == hipSuccess)
-                    e = hipStreamSynchronize(h->stream);
-                dev_free(d_ok);
-                if (e != hipSuccess) {
-                    set_error(std::string("node-block pairs: ") + hipGetErrorString(e));
-                    return fail(MSPMV_ERR_HIP);
-                }
-                static const bool pg_on = [] {  // lab knob: MSPMV_BLK_PAIRGATHER=0 gathers per column
-                    const char *v = getenv("MSPMV_BLK_PAIRGATHER");
-                    return !v || atoi(v) != 0;
-                }();
-                p.blk_pairs = ok && pg_on;
-            }
         }
     }
     // multi-RHS: only the L = 16 plan (k_spmm_tile's DICT path runs at L = 16 only)
     const bool multi = !single;
-    const bool want = multi ? L == 16 && tile != tile_items_for(8) && spmm_dict_enabled() : spmv_dict_enabled() && !wide;
+    const bool want = multi ? L == 16 && tile != tile_items_for(8) : true;
     if (T > 0 && h->nnz > 0 && want) {
         if ((st = dev_alloc(&p.d_dict, (size_t)h->nnz + kNnzPad)) != MSPMV_OK ||
             (st = dev_alloc(&p.d_ndict, (size_t)T)) != MSPMV_OK ||
@@ -405,7 +383,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
             p.d_idx16 = nullptr;
         }
     }
-    auto res = h->plans.emplace(wide ? wide_key(tile) : p.lanes == 64 ? -tile : tile, p);  // one-wave: negative keys
+    auto res = h->plans.emplace(p.lanes == 64 ? -tile : tile, p);  // one-wave: negative keys
     *out = &res.first->second;
     return MSPMV_OK;
 }
@@ -421,9 +399,8 @@ static mspmv_status spmv_plan(mspmv_handle_s *h, const TilePlan **out)
     const TilePlan *wg = nullptr;
     ST_TRY(get_plan(h, 1, &wg));
     if (h->spmv_onewave < 0) {
-        const int mode = spmv_onewave_mode();
-        bool want = mode == 1 && wg->lanes == kBlock;
-        if (mode < 0 && wg->lanes == kBlock && wg->num_tiles >= 64 && !wg->d_blk) {
+        bool want = false;
+        if (wg->lanes == kBlock && wg->num_tiles >= 64 && !wg->d_blk) {
             std::vector<unsigned char> hm((size_t)wg->num_tiles);
             HIP_TRY(hipMemcpy(hm.data(), wg->d_modes[0], hm.size(), hipMemcpyDeviceToHost));
             long long walk = 0;
@@ -439,38 +416,8 @@ static mspmv_status spmv_plan(mspmv_handle_s *h, const TilePlan **out)
             ST_TRY(ensure_modes(h, h->plans.find(key)->second, 1));
         }
         h->spmv_onewave = want ? 1 : 0;
-        // node-block plans (every tile a register run tile whose pattern columns pair up): wider tiles
-        // fill more of a workgroup's eight half-wave run slots (MSPMV_BLK_TILE merge items, 0 = off)
-        static const int wide_tile = [] {
-            const char *v = getenv("MSPMV_BLK_TILE");
-            return v ? std::max(0, atoi(v)) : kBlkWideTile;
-        }();
-        if (!want && wide_tile > wg->tile_items && wide_tile <= 8192 && wg->d_blk &&
-            wg->num_tiles_reg == wg->num_tiles && wg->blk_pairs) {
-            const TilePlan *np = nullptr;
-            if (h->plans.find(wide_key(wide_tile)) == h->plans.end())
-                ST_TRY(build_plan(h, 1, &np, 0, wide_tile));
-            TilePlan &wp = h->plans.find(wide_key(wide_tile))->second;
-            if (wp.d_blk && wp.num_tiles_reg == wp.num_tiles && wp.blk_pairs &&
-                wp.blk_rows_max <= wg->blk_rows_max) {
-                ST_TRY(ensure_modes(h, wp, 1));
-                h->spmv_onewave = 2;
-            }
-        }
     }
-    if (h->spmv_onewave == 1) {
-        *out = &h->plans.find(-64 * spmv_items_per_thread())->second;
-        return MSPMV_OK;
-    }
-    if (h->spmv_onewave == 2) {
-        static const int wide_tile2 = [] {
-            const char *v = getenv("MSPMV_BLK_TILE");
-            return v ? std::max(0, atoi(v)) : kBlkWideTile;
-        }();
-        *out = &h->plans.find(wide_key(wide_tile2))->second;
-        return MSPMV_OK;
-    }
-    *out = wg;
+    *out = h->spmv_onewave == 1 ? &h->plans.find(-64 * spmv_items_per_thread())->second : wg;
     return MSPMV_OK;
 }
 
@@ -640,7 +587,7 @@ extern "C" {
 
 const char *mspmv_last_error(void) { return g_err.c_str(); }
 
-const char *mspmv_cg_kernel_name(mspmv_handle h) { return h ? h->last_cg_kernel : ""; }
+const char *mspmv_cg_kernel_name(mspmv_handle h) { return h ? h->last_cg_kernel.c_str() : ""; }
 
 const char *mspmv_spmv_kernel_name(mspmv_handle h)
 {
@@ -837,6 +784,10 @@ mspmv_status mspmv_set_cu_limit(mspmv_handle h, int num_cus)
     h->stream = s;
     h->own_stream = own;
     if (n != h->num_cus) {
+        // the register-resident CG layout is one workgroup per CU of the whole device: a CU-limited
+        // stream cannot hold it (and one built while limited is "does not fit") -- rebuilt on demand
+        resident_free(h->rcg);
+        h->rcg = nullptr;
         // the single-RHS plan's tile stretch is sized to num_cus x resident workgroups (build_plan):
         // drop every cached plan so the next call plans for the CUs it will actually run on
         for (auto &kv : h->plans)
@@ -1041,32 +992,23 @@ static mspmv_status ensure_cg_workspace(mspmv_handle_s *h, int L, int nblk, int 
     return MSPMV_OK;
 }
 
-// Register-resident single-RHS CG: one cooperative launch runs the whole solve.
+// Register-resident single-RHS CG: one launch runs the whole solve.  d_stamps: the diagnostic
+// phase stamps (mspmv_cg_resident_stamps), null in ordinary solves.
 static mspmv_status cg_solve_resident(mspmv_handle_s *h, ResidentCg *rc, const double *d_b, double *d_x,
-                                      int max_iters, double tol, int *iters, double *hist, int use_cap)
+                                      int max_iters, double tol, int *iters, double *hist, int use_cap,
+                                      unsigned long long *d_stamps = nullptr, int stamp_iters = 0)
 {
-    static char names[16][48];
-    static int nnames = 0;
     const int saved_cap = h->hist_cap;
     h->hist_cap = use_cap;
     hipError_t e = hipMemsetAsync(h->d_ctrl, 0, sizeof(CgControl), h->stream);
     if (e == hipSuccess)
-        e = launch_cg_resident(h, rc, d_b, d_x, max_iters, tol);
+        e = launch_cg_resident(h, rc, d_b, d_x, max_iters, tol, d_stamps, stamp_iters);
     h->hist_cap = saved_cap;
     if (e != hipSuccess) {
         set_error(std::string("resident CG launch: ") + hipGetErrorString(e));
         return MSPMV_ERR_HIP;
     }
-    {
-        char buf[48];
-        snprintf(buf, sizeof buf, "k_cg_resident<%d,%d> x %d", rc->rpt, rc->nzr, rc->G);
-        int i = 0;
-        while (i < nnames && std::strcmp(names[i], buf) != 0)
-            ++i;
-        if (i == nnames && nnames < 16)
-            std::strcpy(names[nnames++], buf);
-        h->last_cg_kernel = i < 16 ? names[i] : "k_cg_resident";
-    }
+    h->last_cg_kernel = rc->name;
     CgControl fin{};
     HIP_TRY(hipStreamSynchronize(h->stream));
     HIP_TRY(hipMemcpy(&fin, h->d_ctrl, sizeof(CgControl), hipMemcpyDeviceToHost));
@@ -1086,6 +1028,20 @@ static mspmv_status cg_solve_resident(mspmv_handle_s *h, ResidentCg *rc, const d
         set_error("CG breakdown: p.Ap gave a non-finite alpha at iteration " + std::to_string(it));
         return MSPMV_ERR_BREAKDOWN;
     }
+    return MSPMV_OK;
+}
+
+// The resident layout of h when the next single-RHS solve may use it: built for this handle's
+// current CU count (all of the device's CUs), matrix fits.  nullptr otherwise.
+static mspmv_status resident_for(mspmv_handle_s *h, ResidentCg **out)
+{
+    *out = nullptr;
+    if (!cg_resident_enabled())
+        return MSPMV_OK;
+    ResidentCg *rc = nullptr;
+    ST_TRY(resident_prepare(h, &rc));
+    if (rc->ok && rc->G == h->num_cus)
+        *out = rc;
     return MSPMV_OK;
 }
 
@@ -1134,11 +1090,11 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
     const int cap = hist ? std::max(hist_cap, 0) : 0;
     ST_TRY(ensure_cg_workspace(h, L, nblk, std::max(plan->num_tiles, mplan ? mplan->num_tiles : 0), cap));
     const int use_cap = hist ? cap : 0;
-    if (pipelined && cg_resident_enabled()) {
+    if (pipelined) {
         // the whole solve as one register-resident launch, where the matrix fits (mspmv_cg_resident.hip)
         ResidentCg *rc = nullptr;
-        ST_TRY(resident_prepare(h, &rc));
-        if (rc->ok)
+        ST_TRY(resident_for(h, &rc));
+        if (rc)
             return cg_solve_resident(h, rc, d_b, d_x, max_iters, tol, iters, hist, use_cap);
     }
     h->last_cg_kernel = pipelined ? "pipelined (k_spmv_tile MODE 1 + k_cg1_update)"
@@ -1414,6 +1370,45 @@ mspmv_status mspmv_dcg_single_dev(mspmv_handle h, const double *d_b, double *d_x
     return cg_solve_dev(h, d_b, d_x, 1, max_iters, tolerance, iters, resid_hist, hist_cap);
 }
 
+mspmv_status mspmv_cg_resident_stamps(mspmv_handle h, const double *d_b, double *d_x, int max_iters, double tolerance,
+                                      int *iters, unsigned long long *stamps, int stamp_iters, int *workgroups)
+{
+    ST_TRY(check_handle(h));
+    if (!d_b || !d_x || !stamps || stamp_iters < 1 || max_iters < 0)
+        return invalid("cg_resident_stamps: vectors, stamps and stamp_iters >= 1 required");
+    if (!aligned16(d_b) || !aligned16(d_x))
+        return invalid("CG vectors must be 16-byte aligned");
+    if (h->m < 1 || h->m != h->n)
+        return invalid("CG needs a non-empty square matrix");
+    HIP_TRY(hipSetDevice(h->device));
+    const TilePlan *plan = nullptr;
+    ST_TRY(get_plan(h, 1, &plan));
+    ST_TRY(ensure_cg_workspace(h, 1, cg1_blocks(h->m), plan->num_tiles, 0));
+    ResidentCg *rc = nullptr;
+    ST_TRY(resident_for(h, &rc));
+    if (!rc)
+        return (set_error("cg_resident_stamps: this matrix does not take the register-resident CG"),
+                MSPMV_ERR_UNSUPPORTED);
+    const size_t n = (size_t)stamp_iters * rc->G * 5;
+    unsigned long long *d_st = nullptr;
+    ST_TRY(dev_alloc(&d_st, n));
+    mspmv_status st = MSPMV_OK;
+    if (hipMemsetAsync(d_st, 0, sizeof(unsigned long long) * n, h->stream) != hipSuccess) {
+        set_error("cg_resident_stamps: memset failed");
+        st = MSPMV_ERR_HIP;
+    }
+    if (st == MSPMV_OK)
+        st = cg_solve_resident(h, rc, d_b, d_x, max_iters, tolerance, iters, nullptr, 0, d_st, stamp_iters);
+    if (st == MSPMV_OK && hipMemcpy(stamps, d_st, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error("cg_resident_stamps: download failed");
+        st = MSPMV_ERR_HIP;
+    }
+    dev_free(d_st);
+    if (workgroups)
+        *workgroups = rc->G;
+    return st;
+}
+
 mspmv_status mspmv_dcg_single(mspmv_handle h, const double *b, double *x, int max_iters, double tolerance,
                               int *iters, double *resid_hist, int hist_cap)
 {
@@ -1682,30 +1677,37 @@ mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y,
         h->flush_cap = flush_bytes;
         HIP_TRY(launch_flush(h->d_flush, flush_bytes, h->stream, true));  // defined contents (+1.0)
     }
-    // A/B lab hook: MSPMV_TIME_DOT=1 times the CG's MODE 2 SpMM (x.(AX) partials + fold) instead
-    static const bool time_dot = getenv("MSPMV_TIME_DOT") != nullptr;
-    if (time_dot) {
-        ST_TRY(ensure_cg_workspace(h, L, cg_update_blocks((long long)h->m * L), plan->num_tiles, 0));
-        HIP_TRY(hipMemsetAsync(h->d_ctrl, 0, sizeof(CgControl), h->stream));
-    }
+    // Per launch: the tile kernel's first workgroup start to the last kernel's end (the carry fix-up's,
+    // when the plan splits rows: the product is complete only after it), recorded by the kernels
+    // themselves (set_launch_events -> hipExtLaunchKernel), so the dispatch gap after the flush is not
+    // in the per-launch time.  ev[2 reps] closes the whole region (flushes included) for avg_ms.
     std::vector<hipEvent_t> ev((size_t)reps * 2 + 2, nullptr);
     for (auto &e : ev)
         HIP_TRY(hipEventCreate(&e));
     hipError_t e = hipSuccess;
-    for (int i = 0; i < reps && e == hipSuccess; ++i) {
+    const bool fix = plan->num_carries > 0;
+    if (plan->num_tiles > 0) {
         if (flush_bytes)
             e = launch_flush(h->d_flush, flush_bytes, h->stream, false);
         if (e == hipSuccess)
-            e = hipEventRecord(ev[2 * i], h->stream);
-        if (e == hipSuccess && time_dot)
-            e = launch_spmm_dot(h, *plan, d_X, d_Y, L, h->d_ctrl, h->d_partials, h->d_gtickets, h->d_red);
-        else if (e == hipSuccess)
-            e = launch_spmm_tile_only(h, *plan, d_X, d_Y, L);
-        if (e == hipSuccess && !time_dot)  // the product is complete only after the carries: timed with it
-            e = launch_fixup(h, *plan, d_Y, L);
-        if (e == hipSuccess)
-            e = hipEventRecord(ev[2 * i + 1], h->stream);
+            e = hipEventRecord(ev[2 * reps + 1], h->stream);  // start of the whole region
     }
+    for (int i = 0; i < reps && e == hipSuccess && plan->num_tiles > 0; ++i) {
+        if (flush_bytes && i > 0)
+            e = launch_flush(h->d_flush, flush_bytes, h->stream, false);
+        if (e == hipSuccess) {
+            set_launch_events(ev[2 * i], fix ? nullptr : ev[2 * i + 1]);
+            e = launch_spmm_tile_only(h, *plan, d_X, d_Y, L);
+        }
+        if (e == hipSuccess && fix) {
+            set_launch_events(nullptr, ev[2 * i + 1]);
+            e = launch_fixup(h, *plan, d_Y, L);
+        }
+        set_launch_events(nullptr, nullptr);
+    }
+    if (plan->num_tiles == 0)
+        for (int i = 0; i < 2 * reps + 2 && e == hipSuccess; ++i)
+            e = hipEventRecord(ev[(size_t)i], h->stream);
     if (e == hipSuccess)
         e = hipEventRecord(ev[2 * reps], h->stream);
     if (e == hipSuccess)
@@ -1718,7 +1720,7 @@ mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y,
     }
     float total = 0.f;
     if (e == hipSuccess)
-        e = hipEventElapsedTime(&total, ev[0], ev[2 * reps]);
+        e = hipEventElapsedTime(&total, ev[2 * reps + 1], ev[2 * reps]);
     for (auto &x : ev)
         (void)hipEventDestroy(x);
     if (e != hipSuccess) {
@@ -1787,11 +1789,16 @@ mspmv_status mspmv_time_spmm_batch_dev(int count, const mspmv_handle *hs, const 
             for (int i = 0; i < count && e == hipSuccess; ++i) {
                 hipStream_t own = hs[i]->stream;
                 hs[i]->stream = s;
-                e = hipEventRecord(ev[k++], s);
-                if (e == hipSuccess)
+                if (plans[i]->num_tiles > 0) {  // the tile kernel's own start / end (set_launch_events)
+                    set_launch_events(ev[k], ev[k + 1]);
                     e = launch_spmm_tile_only(hs[i], *plans[i], d_X[i], d_Y[i], L);
-                if (e == hipSuccess)
-                    e = hipEventRecord(ev[k++], s);
+                    set_launch_events(nullptr, nullptr);
+                } else {
+                    e = hipEventRecord(ev[k], s);
+                    if (e == hipSuccess)
+                        e = hipEventRecord(ev[k + 1], s);
+                }
+                k += 2;
                 if (e == hipSuccess)
                     e = launch_fixup(hs[i], *plans[i], d_Y[i], L);
                 hs[i]->stream = own;

@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
 
 #define RES_HIP_TRY(expr)                                                                          \
@@ -71,7 +72,12 @@ struct ResArgs {
     int max_iters;
     double tol;
     int G;
+    // diagnostic solves only (mspmv_cg_resident_stamps): wall_clock64() of every workgroup at the
+    // phase boundaries of iterations k < stamp_iters, [k][w][kResStamps]; null in every other solve
+    unsigned long long *stamps;
+    int stamp_iters;
 };
+constexpr int kResStamps = 5;  // iteration start | Ap done | p.Ap summed | r done | r.r summed
 
 __device__ __forceinline__ void st_sc1(double *p, double v)
 {
@@ -113,12 +119,25 @@ __device__ __forceinline__ double res_block_sum(double v, double *s_red)
 
 // Publish this workgroup's partial for one phase: every wave's payload stores (sc1) drain, the
 // workgroup meets, one lane stores the partial (sc1) -- the flag of the hand-off.
+// A NaN partial is published as the canonical quiet NaN: a payload equal to kSlotEmpty (b memset
+// to 0xFF) would otherwise read as "not published yet" and the solve would stall instead of
+// reporting the breakdown.
 __device__ __forceinline__ void res_publish(double part, double *slot, double *s_red)
 {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its payload is out
-    const double t = res_block_sum(part, s_red);       // (contains the workgroup barrier)
-    if (threadIdx.x == 0)
+    double t = res_block_sum(part, s_red);             // (contains the workgroup barrier)
+    if (threadIdx.x == 0) {
+        if (t != t)
+            t = __longlong_as_double(0x7ff8000000000000ll);
         st_sc1(slot, t);
+    }
+}
+
+// Diagnostic phase stamp (thread 0, stamped solves only): a plain vector store of wall_clock64().
+__device__ __forceinline__ void res_stamp(const ResArgs &a, int k, int w, int phase)
+{
+    if (a.stamps && threadIdx.x == 0 && k < a.stamp_iters)
+        a.stamps[((size_t)k * a.G + w) * kResStamps + phase] = wall_clock64();
 }
 
 // Wave 0 polls the G slots of one phase until none holds the empty pattern (s_sleep between
@@ -244,6 +263,7 @@ __global__ __launch_bounds__(kRB) void k_cg_resident(ResArgs a)
             double *nxt = (k & 1) ? a.pair0 : a.pair1;
             double *slot_a = a.slots + (size_t)(1 + 2 * (k % kResRing)) * G;
             double *slot_b = slot_a + G;
+            res_stamp(a, k, w, 0);
             // Ap = A p_k (OmpCsrSpmv, row by row in CSR order), p_k own rows, p.Ap partial
             double Ap[RPT];
             double dot = 0.0;
@@ -272,12 +292,16 @@ __global__ __launch_bounds__(kRB) void k_cg_resident(ResArgs a)
                     dot += p[s] * acc;
                 }
             }
+            if (a.stamps)
+                __syncthreads();  // stamped solves: the phase ends when every wave's rows are done
+            res_stamp(a, k, w, 1);
             res_publish(dot, slot_a + w, s_red);
             if (!res_wait_sum<NSL>(slot_a, G, a.abort_word, &s_tot, &s_ok)) {
                 iters = k;
                 brk = 2;
                 break;
             }
+            res_stamp(a, k, w, 2);
             const double alpha = rs / s_tot;
             if (!(alpha == alpha && fabs(alpha) < HUGE_VAL)) {  // breakdown: stop before x and r change
                 iters = k + 1;
@@ -296,12 +320,16 @@ __global__ __launch_bounds__(kRB) void k_cg_resident(ResArgs a)
                     rr += r[s] * r[s];
                 }
             }
+            if (a.stamps)
+                __syncthreads();
+            res_stamp(a, k, w, 3);
             res_publish(rr, slot_b + w, s_red);
             if (!res_wait_sum<NSL>(slot_b, G, a.abort_word, &s_tot, &s_ok)) {
                 iters = k;
                 brk = 2;
                 break;
             }
+            res_stamp(a, k, w, 4);
             const double rs_new = s_tot;
             const double rel = sqrt(rs_new) / b_norm;
             if (w == 0 && t == 0 && a.hist && k < a.hist_cap)
@@ -371,7 +399,12 @@ hipError_t res_launch_t(const ResArgs &a, hipStream_t s, bool check_only, int *o
     auto go = [&](const void *kern) -> hipError_t {
         if (check_only)
             return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, kern, kRB, 0);
-        return hipLaunchCooperativeKernel(kern, dim3(a.G), dim3(kRB), args, 0, s);
+        // A plain launch: the grid is one workgroup per CU and the occupancy check above admitted
+        // one, so every workgroup is resident -- the residency a cooperative launch would check,
+        // without its per-launch host cost and its separate queue (whose teardown at process exit
+        // crashed under rocprofv3: r03u).  Every spin in the kernel is bounded, so a grid that is
+        // not co-resident after all ends in MSPMV_ERR_STALL, never a hang.
+        return hipLaunchKernel(kern, dim3(a.G), dim3(kRB), args, 0, s);
     };
     if (nsl <= 4)
         return go((const void *)k_cg_resident<RPT, NZR, 4>);
@@ -440,24 +473,21 @@ void resident_free(ResidentCg *r)
 
 // Build (once per handle) the resident layout if the matrix fits: every row block <= RPT x 1024
 // rows and every row <= NZR nonzeros for one instantiated shape, one 1024-thread workgroup
-// resident per CU.  r->ok = false otherwise (the caller runs the pipelined CG).
-mspmv_status resident_prepare(mspmv_handle_s *h, ResidentCg **out)
+// resident per CU.  r->ok = false otherwise (the caller runs the pipelined CG).  The layout is
+// attached to the handle only once it is complete; any failure while building it (allocation,
+// fill) leaves a not-ok layout attached and returns MSPMV_OK, so this solve and every later one
+// take the pipelined CG alike instead of the first one failing.
+static bool resident_build(mspmv_handle_s *h, ResidentCg *r)
 {
-    *out = nullptr;
-    if (h->rcg) {
-        *out = h->rcg;
-        return MSPMV_OK;
-    }
-    auto *r = new ResidentCg();
-    h->rcg = r;
-    *out = r;
     int total = 0;
-    RES_HIP_TRY(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, h->device));
+    if (hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess)
+        return false;
     if (h->num_cus != total || h->m < 1 || h->m != h->n)  // CU-limited streams: residency is not the device's
-        return MSPMV_OK;
+        return false;
     const int G = total;
     std::vector<int> ro((size_t)h->m + 1);
-    RES_HIP_TRY(hipMemcpy(ro.data(), h->d_row_offsets, sizeof(int) * ro.size(), hipMemcpyDeviceToHost));
+    if (hipMemcpy(ro.data(), h->d_row_offsets, sizeof(int) * ro.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        return false;
     // merge-path balanced row blocks: block j starts at the last row i with i + ro[i] <= j (m + nnz) / G
     std::vector<int> rb((size_t)G + 1);
     const long long tot = (long long)h->m + h->nnz;
@@ -487,35 +517,61 @@ mspmv_status resident_prepare(mspmv_handle_s *h, ResidentCg **out)
             best = i;
     }
     if (best < 0)
-        return MSPMV_OK;
+        return false;
     const int rpt = kResShapes[best].rpt, nzr = kResShapes[best].nzr;
     ResArgs probe{};
     probe.G = G;
     int occ = 0;
     if (res_dispatch(rpt, nzr, probe, h->stream, true, &occ) != hipSuccess || occ < 1)
-        return MSPMV_OK;
+        return false;
     const size_t ell = (size_t)G * rpt * nzr * kRB;
-    RES_HIP_TRY(hipMalloc(&r->d_rb, sizeof(int) * rb.size()));
-    RES_HIP_TRY(hipMalloc(&r->d_cols, sizeof(int) * ell));
-    RES_HIP_TRY(hipMalloc(&r->d_vals, sizeof(double) * ell));
-    RES_HIP_TRY(hipMalloc(&r->d_len, sizeof(short) * (size_t)G * rpt * kRB));
-    r->slot_bytes = sizeof(double) * (size_t)(1 + 2 * kResRing) * G;  // a multiple of 16 (G even)
+    r->slot_bytes = sizeof(double) * (size_t)(1 + 2 * kResRing) * G;
     r->slot_bytes = (r->slot_bytes + 15) & ~(size_t)15;
-    RES_HIP_TRY(hipMalloc(&r->d_slots, r->slot_bytes));
-    RES_HIP_TRY(hipMalloc(&r->d_abort, 16));
-    RES_HIP_TRY(hipMemcpyAsync(r->d_rb, rb.data(), sizeof(int) * rb.size(), hipMemcpyHostToDevice, h->stream));
-    RES_HIP_TRY(res_fill(rpt, nzr, h->d_row_offsets, h->d_cols, h->d_vals, r->d_rb, G, r->d_cols, r->d_vals, r->d_len,
-                     h->stream));
-    RES_HIP_TRY(hipStreamSynchronize(h->stream));
+    if (hipMalloc(&r->d_rb, sizeof(int) * rb.size()) != hipSuccess ||
+        hipMalloc(&r->d_cols, sizeof(int) * ell) != hipSuccess ||
+        hipMalloc(&r->d_vals, sizeof(double) * ell) != hipSuccess ||
+        hipMalloc(&r->d_len, sizeof(short) * (size_t)G * rpt * kRB) != hipSuccess ||
+        hipMalloc(&r->d_slots, r->slot_bytes) != hipSuccess || hipMalloc(&r->d_abort, 16) != hipSuccess)
+        return false;
+    if (hipMemcpyAsync(r->d_rb, rb.data(), sizeof(int) * rb.size(), hipMemcpyHostToDevice, h->stream) != hipSuccess ||
+        res_fill(rpt, nzr, h->d_row_offsets, h->d_cols, h->d_vals, r->d_rb, G, r->d_cols, r->d_vals, r->d_len,
+                 h->stream) != hipSuccess ||
+        hipStreamSynchronize(h->stream) != hipSuccess)
+        return false;
     r->G = G;
     r->rpt = rpt;
     r->nzr = nzr;
-    r->ok = true;
+    char buf[64];
+    snprintf(buf, sizeof buf, "k_cg_resident<%d,%d> x %d", rpt, nzr, G);
+    r->name = buf;
+    return true;
+}
+
+mspmv_status resident_prepare(mspmv_handle_s *h, ResidentCg **out)
+{
+    *out = h->rcg;
+    if (h->rcg)
+        return MSPMV_OK;
+    auto *r = new ResidentCg();
+    if (!resident_build(h, r)) {
+        // a layout that does not fit or could not be built: release what was allocated, clear any
+        // sticky error of the failed call, and remember "not resident" for this handle
+        for (void *p : {(void *)r->d_rb, (void *)r->d_cols, (void *)r->d_vals, (void *)r->d_len, (void *)r->d_slots,
+                        (void *)r->d_abort})
+            if (p)
+                (void)hipFree(p);
+        *r = ResidentCg();
+        (void)hipGetLastError();
+    } else {
+        r->ok = true;
+    }
+    h->rcg = r;
+    *out = r;
     return MSPMV_OK;
 }
 
 hipError_t launch_cg_resident(mspmv_handle_s *h, ResidentCg *r, const double *d_b, double *d_x, int max_iters,
-                              double tol)
+                              double tol, unsigned long long *d_stamps, int stamp_iters)
 {
     hipError_t e = hipMemsetAsync(r->d_slots, 0xFF, r->slot_bytes, h->stream);  // every slot empty
     if (e == hipSuccess)
@@ -540,6 +596,8 @@ hipError_t launch_cg_resident(mspmv_handle_s *h, ResidentCg *r, const double *d_
     a.max_iters = max_iters;
     a.tol = tol;
     a.G = r->G;
+    a.stamps = d_stamps;
+    a.stamp_iters = d_stamps ? stamp_iters : 0;
     return res_dispatch(r->rpt, r->nzr, a, h->stream, false, nullptr);
 }
 

@@ -54,7 +54,7 @@ struct TilePlan {
     int *d_colbase = nullptr;           // [num_tiles]
     unsigned short *d_cols16 = nullptr; // [nnz + kNnzPad]
     int num_tiles16 = 0;                // tiles on the 16-bit stream
-    // Single-RHS plans, MSPMV_SPMV_DICT=1: per-tile column dictionaries (k_build_dict).  Tile t's
+    // Single-RHS plans: per-tile column dictionaries (k_build_dict) where they pay.  Tile t's
     // distinct columns ascending in dict[n0 ..] (ndict[t] of them), each nonzero's position in
     // that list in idx16[k].  Null when not built.
     int *d_dict = nullptr;              // [nnz + kNnzPad]
@@ -68,9 +68,10 @@ struct TilePlan {
     int num_tiles_blk = 0;              // tiles staged by node blocks
     int num_tiles_reg = 0;              // of those, tiles reduced in registers (h_blk_reg)
     int blk_rows_max = 8;               // the tallest run (rows of one node) over the descriptors
-    int blk_pairs = 0;                  // every run pattern pairs consecutive columns (k_blk_pairs_check)
-    std::vector<unsigned char> h_blk_reg;  // [num_tiles] 1: every run one chunk wide (the SpMV reduces
-                                           // such tiles in registers; mspmv_tile_modes reports 255)
+    bool blk_spmv = false;              // the plain SpMV runs k_spmv_blk (most tiles register run tiles;
+                                        // the rest take its register fallback)
+    std::vector<unsigned char> h_blk_reg;  // [num_tiles] 1: the plain SpMV reduces the tile in registers
+                                           // (a reordered sum: mspmv_tile_modes reports 255)
 };
 
 // Device-resident CG scalars (one set per right-hand side column).
@@ -107,6 +108,7 @@ struct ResidentCg {
     double *d_slots = nullptr;  // hand-off slots, reset to the empty pattern before every solve
     size_t slot_bytes = 0;
     unsigned *d_abort = nullptr;
+    std::string name;  // "k_cg_resident<RPT,NZR> x G" (mspmv_cg_kernel_name)
 };
 
 }  // namespace mspmv
@@ -156,10 +158,9 @@ struct mspmv_handle_s {
     void *d_flush = nullptr;
     size_t flush_cap = 0;
     mspmv::ResidentCg *rcg = nullptr;  // register-resident CG layout (built on the first single-RHS CG)
-    const char *last_cg_kernel = "";   // the CG path the last solve ran (mspmv_cg_kernel_name)
+    std::string last_cg_kernel;        // the CG path the last solve ran (mspmv_cg_kernel_name)
     // plain single-RHS SpMV on one-wave tiles (a plan of its own, TilePlan::lanes = 64): -1 not
-    // decided yet, 0 no, 1 yes (mspmv_api.hip spmv_plan: skewed rows, most tiles merge walks); 2: a wide
-    // node-block plan of its own (MSPMV_BLK_TILE)
+    // decided yet, 0 no, 1 yes (mspmv_api.hip spmv_plan: skewed rows, most tiles merge walks)
     int spmv_onewave = -1;
 };
 
@@ -191,44 +192,30 @@ hipError_t launch_tile_modes(const int *d_row_offsets, const int2 *d_bounds, con
                              int num_tiles, int L, unsigned char *d_modes, hipStream_t s, int lanes = kBlock);
 // Items per thread of the single-RHS tiles (the nominal tile is lanes x this)
 int spmv_items_per_thread();
-// Threads per single-RHS tile of the default plan (256; the MSPMV_SPMV_TB=64 lab knob makes it 64)
-int spmv_tile_lanes();
-// Whether single-RHS plans may run on one-wave tiles when their rows are skewed (MSPMV_SPMV_ONEWAVE:
-// -1 auto (default), 0 never, 1 every plain SpMV)
-int spmv_onewave_mode();
 inline int l_index(int L) { return L == 1 ? 0 : L == 2 ? 1 : L == 4 ? 2 : L == 8 ? 3 : 4; }
 hipError_t launch_snap(const int *d_row_offsets, int m, int2 *d_bounds, unsigned char *d_split, int num_tiles,
                        int snap, hipStream_t s);
 // Per-tile 16-bit column offsets (TilePlan::d_colbase / d_cols16); whether plans get them.
 hipError_t launch_pack_cols16(const int *d_cols, const int2 *d_bounds, int num_tiles, int *d_colbase,
                               unsigned short *d_cols16, hipStream_t s);
-bool spmv_cols16_enabled();
-bool spmv_dict_enabled();
 // Node blocks (runs of rows sharing one column list) for the single-RHS plan; needs cols16.
 bool spmv_blocks_enabled();
 // SpMM (L >= 2) through the single-RHS node-block plan (k_spmm_blk) when all its tiles are register tiles.
 bool spmm_blk_enabled();
 constexpr int kBlkPerTile = 64;  // == kBlkMax in the kernels: descriptor capacity of a tile
-// Merge items per tile of the plain SpMV's wide node-block plan (spmv_plan; 0 = off)
-#ifndef MSPMV_BLK_WIDE_TILE
-#define MSPMV_BLK_WIDE_TILE 0  // lab: 2560 / 3072 / 4096 measured 0.78 / 0.79 / 0.82-0.83 vs 0.82-0.84 (r03an)
-#endif
-constexpr int kBlkWideTile = MSPMV_BLK_WIDE_TILE;
+// Chunks per tile k_build_blocks may describe for the plain SpMV's column-pair kernel (two rounds of
+// its eight half-wave run slots), and the one-round limit of k_spmv_tile's node-block paths.
+constexpr int kBlkPlanChunks = 16;
+constexpr int kBlkTileChunks = 8;
 hipError_t launch_build_blocks(const int *d_row_offsets, const int *d_cols, const int2 *d_bounds,
                                const unsigned char *d_split, const int *d_colbase, int num_tiles, uint4 *d_blk,
                                hipStream_t s, int max_chunks = 8);
-hipError_t launch_blk_pairs_check(const int *d_cols, const int2 *d_bounds, const uint4 *d_blk, int stride,
-                                  int num_tiles, int *d_ok, hipStream_t s);
 hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_tiles, int max_items, int *d_dict,
                              int *d_ndict, unsigned short *d_idx16, hipStream_t s, bool multi);
-bool spmm_dict_enabled();
 // Multi-RHS column dictionaries: the distinct panel rows a tile parks in LDS, 8 KB per workgroup
 // (L = 16: 64 rows), which keeps 7 workgroups per CU; 16 KB (5 per CU) measured 105 vs 102 us and
 // 24 KB 119 us on the pwtk shape.
-#ifndef MSPMV_SPMM_DICT_BYTES
-#define MSPMV_SPMM_DICT_BYTES 8192  // lab builds override (tools/lab/build_variant.sh)
-#endif
-constexpr int kSpmmDictBytes = MSPMV_SPMM_DICT_BYTES;
+constexpr int kSpmmDictBytes = 8192;
 constexpr int spmm_dict_max(int L) { return kSpmmDictBytes / (8 * L); }
 // y = A x (L == 1) or Y = A X (row-major panels), tile kernel + optional carry fix-up.
 hipError_t launch_spmm(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
@@ -244,7 +231,7 @@ hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, in
 int tile_items_for(int L);
 // Map key of the default plan for L (one-wave plans are keyed by minus their tile size: 512 is also
 // the L = 16 tile size)
-inline int plan_key(int L) { return L == 1 && spmv_tile_lanes() == 64 ? -tile_items_for(1) : tile_items_for(L); }
+inline int plan_key(int L) { return tile_items_for(L); }
 // Resident single-RHS tile workgroups per CU at the default tile shape (0: non-default tuning).
 int spmv_tile_blocks_per_cu();
 // STREAM-like nontemporal read of `bytes` (16-B words) on stream s (mspmv_time_stream_read).
@@ -252,6 +239,9 @@ hipError_t launch_stream_read(const double *p, size_t bytes, int num_cus, hipStr
 std::string spmv_kernel_name(const mspmv_handle_s *h);
 std::string spmm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan, int L);
 bool stream_nt(const mspmv_handle_s *h);
+// Kernel-boundary timing: the next product launch records start / stop at its own first workgroup's
+// start and last workgroup's end (null: none).  Consumed by that launch.
+void set_launch_events(hipEvent_t start, hipEvent_t stop);
 bool supported_L(int L);
 
 // CG pieces
@@ -268,13 +258,15 @@ bool cg_split_iteration(int L);
 int cg1_blocks(long long m);
 hipError_t launch_cg1_init(mspmv_handle_s *h, const double *d_b, double *d_x, int nblk);
 hipError_t launch_cg1_finish(mspmv_handle_s *h, double *d_x, int parity, int nblk);
-// Register-resident single-RHS CG (one cooperative launch for the whole solve; MSPMV_CG_RESIDENT=0
+// Register-resident single-RHS CG (one launch for the whole solve; MSPMV_CG_RESIDENT=0
 // turns it off): the layout is built on first use; r->ok false when the matrix does not fit.
 bool cg_resident_enabled();
 mspmv_status resident_prepare(mspmv_handle_s *h, ResidentCg **out);
 void resident_free(ResidentCg *r);
+// d_stamps (diagnostic solves, mspmv_cg_resident_stamps): [stamp_iters][G][5] wall_clock64() phase
+// stamps of every workgroup; null otherwise.
 hipError_t launch_cg_resident(mspmv_handle_s *h, ResidentCg *r, const double *d_b, double *d_x, int max_iters,
-                              double tol);
+                              double tol, unsigned long long *d_stamps = nullptr, int stamp_iters = 0);
 // Split (multi-RHS) CG: the last deferred x += alpha p after the loop (a no-op when none is pending).
 hipError_t launch_cg_xflush(mspmv_handle_s *h, double *d_x, int L, int nblk);
 // Offset (doubles) and count of the partials level a consumer sums: levels of a fan-in

@@ -18,6 +18,8 @@
 //     sees one contiguous band of x / X.
 #include "mspmv_internal.h"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <type_traits>
 #include <cmath>
@@ -45,6 +47,23 @@ __device__ __forceinline__ int xcd_tile(int b, int T, int K = 1)
     const int q2 = cnt / K, r2 = cnt - q2 * K;
     const int s = i % K, pos = i / K;
     return base + s * q2 + (s < r2 ? s : r2) + pos;
+}
+
+// Kernel-boundary timing events (mspmv_time_spmm_dev): the next product launch through ggl() records
+// `start` when its first workgroup starts and `stop` when its last one ends (hipExtLaunchKernel), so
+// a cold timing excludes the dispatch gap after the cache flush that stream events around the launch
+// included (cant: 21.2 us by stream events against 15.4 us in the trace).
+static thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
+void set_launch_events(hipEvent_t start, hipEvent_t stop)
+{
+    t_ev_start = start;
+    t_ev_stop = stop;
+}
+template <typename... KArgs, typename... Args>
+static void ggl(void (*kernel)(KArgs...), dim3 grid, dim3 block, hipStream_t s, Args... args)
+{
+    hipExtLaunchKernelGGL(kernel, grid, block, 0, s, t_ev_start, t_ev_stop, 0, args...);
+    t_ev_start = t_ev_stop = nullptr;
 }
 
 // Streamed-once matrix arrays: nontemporal loads (don't displace x / X from the caches).
@@ -488,11 +507,19 @@ __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ c
 // plan's stride being the smallest of 16, 32, 64 that holds every tile's set):
 //   x: vofs (nonzero offset of the run's first row in the tile, bits 0-15) | j0 (first pattern
 //      column of this chunk, 16-23) | wc (chunk width <= 64, 24-31)
-//   y: h (rows, 1..8, bits 0-3) | p (row holding P, 4-6) | nd (descriptor count, in entry 0 only,
-//      8-15; 0 = the tile stages the plain way) | rofs (the run's first row in the tile, 16-31)
+//   y: h (rows, 1..8, bits 0-3) | p (row holding P, 4-6) | pairs (bit 7: the chunk's pattern columns
+//      come in consecutive pairs, P[j0 + 2i + 1] == P[j0 + 2i] + 1, at least one pair) | nd (descriptor
+//      count, in entry 0 only, 8-15; 0 = the tile stages the plain way) | rofs (the run's first row in
+//      the tile, 16-31)
 //   z, w: the h row lengths, 8 bits each (rows of a run are <= 255 long)
 constexpr int kBlkMax = 64;  // descriptors a tile may have (the plan stores them at a stride of 16, 32 or 64)
 constexpr int kBlkRows = 8;
+// Rows per run: at most 6, the column-pair SpMV kernel's value registers (k_spmv_blk<.., 6>); a node
+// of 7 or 8 unknowns becomes two runs (a 6-DOF FEM node, pwtk's, is one).
+constexpr int kBlkRunRows = 6;
+// (kBlkTileChunks, mspmv_internal.h: the chunks of a tile the LDS-staged and column-owner paths of
+// k_spmv_tile take -- one round of its four waves, more measured slower than striped staging; tiles
+// of up to kBlkPlanChunks run only in the column-pair kernel, which loops over rounds.)
 
 __device__ __forceinline__ int blk_len(const uint4 &d, int i)
 {
@@ -523,7 +550,7 @@ __global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *_
         int p = g, plen = row_offsets[g + 1] - gs;
         unsigned lens[2] = {0u, 0u};
         int h = 0;
-        for (; r < r1 && h < kBlkRows; ++r, ++h) {
+        for (; r < r1 && h < kBlkRunRows; ++r, ++h) {
             const int s = row_offsets[r], len = row_offsets[r + 1] - s;
             if (len > 255)
                 return;
@@ -544,13 +571,18 @@ __global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *_
         sum_w += plen;
         ++nruns;
         const int vofs = gs - n0;
+        const int ps = row_offsets[p];
         for (int j0 = 0; j0 < plen || (j0 == 0 && plen == 0); j0 += 64) {
             if (nd == kBlkMax || j0 > 255)
                 return;
             const int wc = min(64, plen - j0);
+            bool pairs = wc >= 2;  // one 16-B x load per column pair (k_spmv_blk's pair form)
+            for (int q = j0; q + 1 < j0 + wc && pairs; q += 2)
+                pairs = cols[ps + q + 1] == cols[ps + q] + 1;
             const uint4 dd = make_uint4((unsigned)vofs | ((unsigned)j0 << 16) | ((unsigned)wc << 24),
-                                        (unsigned)h | ((unsigned)(p - g) << 4) | ((unsigned)(g - r0) << 16), lens[0],
-                                        lens[1]);
+                                        (unsigned)h | ((unsigned)(p - g) << 4) | (pairs ? 0x80u : 0u) |
+                                            ((unsigned)(g - r0) << 16),
+                                        lens[0], lens[1]);
             if (nd == 0)
                 d0 = dd;
             else
@@ -583,7 +615,7 @@ __global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *_
 // reads plus an 11-step search and two barriers for SpMV, IPTG/4 gather chunks for SpMM).
 __global__ void k_tile_modes(const int *__restrict__ row_offsets, const int2 *__restrict__ bounds,
                              const unsigned char *__restrict__ split, int num_tiles, int gl, int max_cost,
-                             int lanes, unsigned char *__restrict__ modes, int force_lg)
+                             int lanes, unsigned char *__restrict__ modes)
 {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= num_tiles)
@@ -612,10 +644,6 @@ __global__ void k_tile_modes(const int *__restrict__ row_offsets, const int2 *__
             best_cost = cost;
             best = lg + 1;
         }
-    }
-    if (force_lg >= 0 && (gl << force_lg) <= 64) {  // lab knob (MSPMV_SPMM_LG): one group size for every tile
-        best = force_lg + 1;
-        best_cost = 0;
     }
     modes[t] = best_cost <= max_cost ? (unsigned char)best : (unsigned char)0;
 }
@@ -675,9 +703,8 @@ struct TileArgs {
     // staging (0) -- one dependent round trip fewer per tile (SpmvTuning::early_re)
     int early_re;
     int blk_rows_max;  // node-block plans: the tallest run (TilePlan::blk_rows_max; k_spmm_blk's KR)
-    int tstreams;      // tile order: contiguous tile streams per XCD walked side by side (xcd_tile's K)
     int tb;            // threads sharing one tile (the plan's lanes: 256, or 64 for one-wave SpMV plans)
-    int blk_pairs;     // node-block plans whose run patterns pair consecutive columns (TilePlan::blk_pairs)
+    int blk_spmv;      // the plain SpMV runs k_spmv_blk on this plan (TilePlan::blk_spmv; mixed plans too)
     int n;             // columns (x holds n entries)
 };
 
@@ -773,7 +800,7 @@ __device__ __forceinline__ void stage_store(const StageRegs<NJ, CG> &st, int nnz
             s_prod[pslot(k)] = st.v[j] * x;
     }
 }
-// Grouped staging (plain SpMV on the 16-bit stream; MSPMV_SPMV_GROUP = W, 2 or 4, 0 = striped):
+// Grouped staging (plain SpMV on the 16-bit stream, W = 2: pairs):
 // thread tid takes the ABSOLUTE nonzero groups q0 + tid + TB u of W consecutive nonzeros (q0 =
 // n0 / W), each one aligned W*8-B value load (W/2 16-B loads) and one aligned W*2-B column load --
 // 2/W of the striped form's column loads and 1/2 of its value loads for the same bytes (the stream
@@ -781,12 +808,9 @@ __device__ __forceinline__ void stage_store(const StageRegs<NJ, CG> &st, int nnz
 // 5 % faster with pairs, r03q).  Elements of a group outside the tile gather x[colbase] (always a
 // valid column) and are not stored.  A tile with a group more than NP * TB (a start off the
 // W-grid at the nominal size) issues one extra round (block-uniform).
-#ifndef MSPMV_SPMV_XPAIR
-#define MSPMV_SPMV_XPAIR 0  // lab: one 16-B x load per consecutive pair -- nlpkkt120 size 261-262 vs 220-224 us (r03af)
-#endif
-#ifndef MSPMV_SPMV_GROUP
-#define MSPMV_SPMV_GROUP 2  // lab builds: 0 = striped staging, 4 = quads (nlpkkt120 size 245 vs 223 us, r03r)
-#endif
+// Measured and not kept (r03af, r03r): quads (W = 4) 245 vs 223 us and one 16-B x load per
+// consecutive pair 261 vs 220 us at the nlpkkt120 size.
+constexpr int kGroupW = 2;
 typedef unsigned v2u_t __attribute__((ext_vector_type(2)));
 template <int NP, int W>
 struct GroupRegs {
@@ -819,24 +843,6 @@ __device__ __forceinline__ void group_issue(const TileArgs &a, int n0, int nnzt,
     for (int u = 0; u < NP; ++u) {
         const int q = min(q0 + (int)threadIdx.x + TB * (ubase + u), qlast);
         const int k0 = W * q - n0;
-        if (W == 2 && MSPMV_SPMV_XPAIR) {
-            // a pair whose columns are consecutive (stencil / FEM runs) takes both x values from ONE
-            // 16-B load (8-B aligned at worst, clamped to start at n - 2); the second gather is issued
-            // only for the lanes whose columns are not -- when at least half the wave's pairs are
-            const int c0 = colbase + ((k0 >= 0) ? (int)(st.c[u][0] & 0xffffu) : 0);
-            const int c1 = colbase + ((k0 + 1 < nnzt) ? (int)(st.c[u][0] >> 16) : 0);
-            const bool adj = c1 == c0 + 1;
-            if (__popcll(__ballot(adj)) >= 32) {  // wave-uniform
-                const int base = min(c0, a.n - 2);
-                const double2 xx = *reinterpret_cast<const double2 *>(a.x + base);
-                st.x[u][0] = base == c0 ? xx.x : xx.y;
-                st.x[u][1] = (adj && base == c0) ? xx.y : a.x[c1];
-                continue;
-            }
-            st.x[u][0] = a.x[c0];
-            st.x[u][1] = a.x[c1];
-            continue;
-        }
 #pragma unroll
         for (int e = 0; e < W; ++e) {
             const int off = (int)((st.c[u][e >> 1] >> (16 * (e & 1))) & 0xffffu);
@@ -915,65 +921,6 @@ __device__ __forceinline__ void dict_stage(const TileArgs &a, double *s_prod, in
         const int k = tid + j * TB;
         if (k < nnzt)
             s_prod[pslot(k)] = pr[j];
-    }
-}
-
-// dict_stage with the pair staging's loads (MSPMV_SPMV_DICT_PAIR): thread tid takes the absolute
-// nonzero pairs n0/2 + tid + TB u -- one 16-B value load and one 4-B load of two dictionary
-// positions per pair; the same products into the same slots, so results are unchanged.
-#ifndef MSPMV_SPMV_DICT_PAIR
-#define MSPMV_SPMV_DICT_PAIR 0  // lab: measured even or slower on cant / rma10 / scattered band (r03aj)
-#endif
-template <int NP, bool NT, int TB>
-__device__ __forceinline__ void dict_stage_pair(const TileArgs &a, double *s_prod, int nd, int n0, int nnzt)
-{
-    constexpr int DJ = 3;
-    const int tid = threadIdx.x;
-    const int q0 = n0 >> 1, qlast = (n0 + nnzt - 1) >> 1;
-    unsigned ix[NP];
-    double2 v[NP];
-    int dc[DJ];
-    double dx[DJ];
-#pragma unroll
-    for (int u = 0; u < DJ; ++u)
-        dc[u] = ld_stream<NT>(a.dict + n0 + min(tid + u * TB, nd - 1));
-#pragma unroll
-    for (int u = 0; u < NP; ++u) {
-        const int q = min(q0 + tid + TB * u, qlast);
-        ix[u] = ld_stream<NT>(reinterpret_cast<const unsigned *>(a.idx16) + q);
-        v[u] = ld_stream<NT>(reinterpret_cast<const double2 *>(a.vals) + q);
-    }
-#pragma unroll
-    for (int u = 0; u < DJ; ++u)
-        dx[u] = a.x[dc[u]];
-    double *s_x = s_prod;  // nd <= nnzt: the dictionary's x fits the product slots
-#pragma unroll
-    for (int u = 0; u < DJ; ++u)
-        if (tid + u * TB < nd)
-            s_x[tid + u * TB] = dx[u];
-    for (int d = tid + DJ * TB; d < nd; d += TB)  // rare: > DJ * TB distinct columns
-        s_x[d] = a.x[a.dict[n0 + d]];
-    tile_sync<TB>();
-    double pr[NP][2];
-#pragma unroll
-    for (int u = 0; u < NP; ++u) {
-        const int q = min(q0 + tid + TB * u, qlast);
-        const int k0 = 2 * q - n0;
-        // positions of elements outside the tile belong to a neighbour's dictionary: read slot 0
-        pr[u][0] = v[u].x * s_x[k0 >= 0 ? (int)(ix[u] & 0xffffu) : 0];
-        pr[u][1] = v[u].y * s_x[k0 + 1 < nnzt ? (int)(ix[u] >> 16) : 0];
-    }
-    tile_sync<TB>();
-#pragma unroll
-    for (int u = 0; u < NP; ++u) {
-        const int q = q0 + tid + TB * u;
-        if (q > qlast)
-            continue;
-        const int k0 = 2 * q - n0;
-        if (k0 >= 0)
-            s_prod[pslot(k0)] = pr[u][0];
-        if (k0 + 1 < nnzt)
-            s_prod[pslot(k0 + 1)] = pr[u][1];
     }
 }
 
@@ -1111,15 +1058,13 @@ __device__ __forceinline__ double rows8_sum32(const double (&p)[kBlkRows])
     return v;
 }
 
-// Plain SpMV form of blk_rows with column PAIRS (MSPMV_BLK_PAIR): each half-wave owns one run per
+// Plain SpMV form of blk_rows with column PAIRS: each half-wave owns one run per
 // round and its lane l owns pattern columns 2l and 2l + 1, so a row of the run arrives in ONE
 // 16-B load per lane (half the value-load instructions of column-owner lanes; the loads may be
 // 8-B aligned only -- gfx9's unaligned access mode), and one rows8_sum32 folds both halves' runs
 // (half the shuffles).  A lane's two products are added before the half-wave tree: a fixed order,
 // so rows stay reproducible and within the reordering bound (mode 255).
-#ifndef MSPMV_BLK_PAIR
-#define MSPMV_BLK_PAIR 1  // lab builds: 0 keeps column-owner lanes (pwtk shape 24.98 vs 22.6-23.1 us, r03t)
-#endif
+// (column-owner lanes instead: pwtk shape 24.98 vs 22.6-23.1 us, r03t)
 template <bool NT, int KR>
 __device__ __forceinline__ void blk_rows_pair(const TileArgs &a, const uint4 &bd, int nd, int r0, int n0,
                                               int colbase)
@@ -1152,10 +1097,10 @@ __device__ __forceinline__ void blk_rows_pair(const TileArgs &a, const uint4 &bd
         }
         int c0 = 0, c1 = 0;  // column 0 of x: always valid to gather
         double x0, x1;
-        if (a.blk_pairs) {
-            // the plan checked P[2j + 1] == P[2j] + 1 (k_blk_pairs_check): one column offset and ONE
-            // 16-B gather (8-B aligned at worst) per lane; the last column sits at n - 1 at most, so the
-            // load starts at n - 2 at most and picks its half
+        if ((d.y >> 7) & 1u) {  // uniform per half-wave (its run)
+            // the plan checked P[2j + 1] == P[2j] + 1 for this chunk (k_build_blocks, so n >= 2): one
+            // column offset and ONE 16-B gather (8-B aligned at worst) per lane; the last column sits at
+            // n - 1 at most, so the load starts at n - 2 at most and picks its half
             if (valid && 2 * hl < wc)
                 c0 = colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + 2 * hl);
             const int base = min(c0, a.n - 2);
@@ -1624,24 +1569,11 @@ __device__ __forceinline__ void cg1_publish(const TileArgs &a, SM &sm, int slot,
 // (UpdatePSingle, single_strategy.hpp:89-97, fused into the SpMV), writes p for its rows, Ap, and
 // p.Ap by linearity.  TB = 64 (one-wave workgroups, SpMV only): every wave owns its tile, so no
 // workgroup barrier ties a wave's progress to its siblings' gather latencies.
-#if MSPMV_LAB_ABLATE == 9  // lab build only (tools/lab/stamps.py): per-tile phase stamps
-constexpr int kLabStampTiles = 1 << 17;
-__device__ unsigned long long g_lab_stamps[kLabStampTiles * 6];
-#endif
-// Waves per SIMD the pipelined CG's tile kernel is compiled for (MODE 1): unconstrained it takes
-// 92 VGPRs (5 waves, 5 workgroups per CU); a lab build can ask the compiler for more
-// (-DMSPMV_CG_WAVES=7 or 8) at the price of fewer loads in flight per wave.
-#ifndef MSPMV_CG_WAVES
-#define MSPMV_CG_WAVES 0
-#endif
-constexpr int spmv_tile_waves(int mode) { return mode == 1 && MSPMV_CG_WAVES > 0 ? MSPMV_CG_WAVES : 1; }
-
 // BLK = false: the plan has no node-block tiles (a.blk null), and the kernel is compiled without
 // their staging paths -- the pipelined CG's form then needs far fewer registers (their run arrays
 // set its VGPR count, so more workgroups fit per CU).
 template <int IPT, int MODE, bool NT, int TB = kBlock, bool BLK = true>
-__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(spmv_tile_waves(MODE)))) void
-k_spmv_tile(TileArgs a)
+__global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
 {
     static_assert(TB == kBlock || MODE == kModeSpmv, "one-wave tiles run the plain SpMV only");
     constexpr bool CG = MODE == kModeCg;
@@ -1649,12 +1581,9 @@ k_spmv_tile(TileArgs a)
     constexpr int MAXJ = SpmvSmem<IPT, TB>::MAXJ;
     __shared__ SpmvSmem<IPT, TB> sm;
     const int tid = threadIdx.x;
-#if MSPMV_LAB_ABLATE == 9
-    const unsigned long long lab_t0 = wall_clock64();
-#endif
     // CG: stop flag loaded now, tested after the stream and gathers are issued (see k_spmm_tile)
     const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
-    const int t = xcd_tile(blockIdx.x, a.num_tiles, a.tstreams);
+    const int t = xcd_tile(blockIdx.x, a.num_tiles);
     const int2 b0 = a.bounds[t];
     const int2 b1 = a.bounds[t + 1];
     const int r0 = b0.x, n0 = b0.y;
@@ -1682,7 +1611,9 @@ k_spmv_tile(TileArgs a)
     uint4 bd = make_uint4(0u, 0u, 0u, 0u);
     if (BLK && a.blk && (tid & 63) < a.blk_stride)
         bd = a.blk[(size_t)t * a.blk_stride + (tid & 63)];
-    const int nblk = (BLK && a.blk) ? (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u) : 0;
+    int nblk = (BLK && a.blk) ? (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u) : 0;
+    if (nblk > kBlkTileChunks)  // more than one round of runs: striped staging here (k_spmv_blk takes them)
+        nblk = 0;
     bool staged = false;
     // every run one chunk wide (block-uniform: each wave holds all descriptors): no LDS at all
     const bool blk_reg = BLK && nblk > 0 && __ballot((tid & 63) < nblk && ((bd.x >> 16) & 255u) != 0) == 0;
@@ -1711,9 +1642,7 @@ k_spmv_tile(TileArgs a)
     } else if constexpr (MODE == kModeSpmv) {
         const int nd = a.dict ? a.ndict[t] : 0;  // > 0: this tile gathers through its dictionary
         if (nd > 0) {
-            if (MSPMV_SPMV_DICT_PAIR && nnzt <= TILE && ((n0 + nnzt - 1) >> 1) - (n0 >> 1) + 1 <= (TILE / TB + 1) / 2 * TB)
-                dict_stage_pair<(TILE / TB + 1) / 2, NT, TB>(a, sm.prod, nd, n0, nnzt);
-            else if (nnzt <= TILE)
+            if (nnzt <= TILE)
                 dict_stage<IPT, NT, TB>(a, sm.prod, nd, n0, nnzt);
             else
                 dict_stage<MAXJ, NT, TB>(a, sm.prod, nd, n0, nnzt);
@@ -1721,8 +1650,8 @@ k_spmv_tile(TileArgs a)
         }
     }
     if (staged) {
-    } else if (MSPMV_SPMV_GROUP > 0 && MODE == kModeSpmv && colbase >= 0 && nnzt > 0 && nnzt <= TILE) {
-        constexpr int W = MSPMV_SPMV_GROUP > 0 ? MSPMV_SPMV_GROUP : 2;
+    } else if (MODE == kModeSpmv && colbase >= 0 && nnzt > 0 && nnzt <= TILE) {
+        constexpr int W = kGroupW;
         constexpr int NP = (TILE / TB + W - 1) / W;
         GroupRegs<NP, W> st;
         group_issue<NP, W, NT, TB>(a, n0, nnzt, colbase, 0, st);
@@ -1754,10 +1683,6 @@ k_spmv_tile(TileArgs a)
         return;
     // Row ends: issued with the stream by default (TileArgs::early_re; with the pair staging 1-2 %
     // faster, r03ah/r03ai -- with the old striped staging it had measured +0.9 us on pwtk), or here.
-#if MSPMV_LAB_ABLATE == 9
-    __syncthreads();
-    const unsigned long long lab_t1 = wall_clock64();
-#endif
     int *rend = sm.rowend(nnzt);
     if (a.early_re) {
         if (tid < nrows)
@@ -1769,25 +1694,10 @@ k_spmv_tile(TileArgs a)
             rend[i] = a.row_offsets[r0 + 1 + i] - n0;
     }
     tile_sync<TB>();
-#if MSPMV_LAB_ABLATE == 9
-    const unsigned long long lab_t2 = wall_clock64();
-#endif
     double dot = 0.0;
     double xr, pr;
     row_operands<MODE>(a, r0, nrows, xr, pr);
     reduce_tile<IPT, MODE, TB>(a, sm, t, r0, n0, nrows, nnzt, a.rmode[t], a.split[t + 1] != 0, beta, dot, xr, pr);
-#if MSPMV_LAB_ABLATE == 9
-    __syncthreads();
-    if (tid == 0 && MODE == kModeSpmv && t < kLabStampTiles) {
-        unsigned long long *o = g_lab_stamps + (size_t)t * 6;
-        o[0] = lab_t0;
-        o[1] = lab_t1;
-        o[2] = lab_t2;
-        o[3] = wall_clock64();
-        o[4] = (unsigned long long)__smid();
-        o[5] = (unsigned long long)blockIdx.x;
-    }
-#endif
     if constexpr (MODE == kModeCg) {
         cg1_lag_store<TB>(a, r0, nrows, lag);
         cg1_publish(a, sm, t, a.num_tiles, dot);
@@ -1796,10 +1706,72 @@ k_spmv_tile(TileArgs a)
     }
 }
 
-// Single right-hand side, plans whose EVERY tile is a register node-block tile (FEM matrices such
-// as pwtk): the tile kernel without any LDS staging (only the CG / dot-mode epilogue's 2 KB), so
-// occupancy is set by registers alone -- 8 workgroups (32 waves) per CU instead of the 7 that
-// k_spmv_tile's 22.6 KB of LDS allow.  Same per-tile work as k_spmv_tile's blk_rows path.
+// Register fallback of the plain node-block SpMV for the tiles of a mixed plan that are not register
+// run tiles (rows outside any run pattern, patterns wider than 64 columns, split boundaries): groups
+// of G lanes take the tile's row segments round-robin (its whole rows, then the trailing partial row
+// of a split boundary), lane j of a group sums products j, j + G, ... of its segment in order with
+// four loads in flight, a fixed xor butterfly folds the group and its lane 0 stores the row (the
+// trailing partial row: the tile's carry, which k_fixup adds).  No LDS, so the kernel keeps its
+// register-only occupancy.  G is the smallest power of two with 4 G >= the tile's mean segment
+// length.  Reproducible, and within the 2 (len+1) eps (|A||x|)_i reordering bound of the CSR-order
+// sum (mspmv_tile_modes reports these tiles as 255).
+template <bool NT>
+__device__ __forceinline__ void tile_rows_reg(const TileArgs &a, int t, int r0, int n0, int colbase)
+{
+    const int2 b1 = a.bounds[t + 1];
+    const int nrows = b1.x - r0, nnzt = b1.y - n0;
+    const int nseg = nrows + (a.split[t + 1] ? 1 : 0);
+    if (nseg == 0)
+        return;
+    const int mean = (nnzt + nseg - 1) / nseg;
+    int lg = 0;
+    while (lg < 6 && (4 << lg) < mean)
+        ++lg;
+    const int G = 1 << lg;
+    const int lane = threadIdx.x & (G - 1);
+    auto col = [&](int k) {
+        return colbase >= 0 ? colbase + (int)ld_stream<NT>(a.cols16 + n0 + k) : ld_stream<NT>(a.cols + n0 + k);
+    };
+    for (int r = (int)threadIdx.x >> lg; r < nseg; r += kBlock >> lg) {  // uniform within a group
+        const int s0 = r == 0 ? 0 : a.row_offsets[r0 + r] - n0;
+        const int e = r < nrows ? a.row_offsets[r0 + r + 1] - n0 : nnzt;
+        double v = 0.0;
+        int k = s0 + lane;
+        for (; k + 3 * G < e; k += 4 * G) {
+            int c[4];
+            double w[4], xv[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                c[u] = col(k + u * G);
+                w[u] = ld_stream<NT>(a.vals + n0 + k + u * G);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                xv[u] = a.x[c[u]];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                v += w[u] * xv[u];
+        }
+        for (; k < e; k += G)
+            v += ld_stream<NT>(a.vals + n0 + k) * a.x[col(k)];
+        for (int off = G >> 1; off > 0; off >>= 1)
+            v += __shfl_xor(v, off);
+        if (lane == 0) {
+            if (r < nrows)
+                a.y[r0 + r] = v;
+            else
+                a.carry_val[t] = v;
+        }
+    }
+}
+
+// Single right-hand side, node-block plans (FEM matrices such as pwtk): the tile kernel without any
+// LDS staging (only the CG / dot-mode epilogue's 2 KB), so occupancy is set by registers alone -- 8
+// workgroups (32 waves) per CU instead of the 7 that k_spmv_tile's 22.6 KB of LDS allow.  Plain SpMV
+// (MODE 0, column pairs): register run tiles through blk_rows_pair, every other tile of the plan
+// through tile_rows_reg, so a plan whose tiles are mostly node blocks runs here whole (blk_spmv).
+// Dot mode: plans whose EVERY tile is a register run tile, the per-tile work of k_spmv_tile's
+// blk_rows path.
 struct BlkSmem {
     double red[kBlock / 64];
     double cval[kBlock];
@@ -1813,7 +1785,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_blk(TileArgs a)
     __shared__ BlkSmem sm;
     const int tid = threadIdx.x;
     const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
-    const int t = xcd_tile(blockIdx.x, a.num_tiles, a.tstreams);
+    const int t = xcd_tile(blockIdx.x, a.num_tiles);
     const int2 b0 = a.bounds[t];
     const int colbase = a.colbase[t];
     const uint4 bd =
@@ -1824,9 +1796,16 @@ __global__ __launch_bounds__(kBlock) void k_spmv_blk(TileArgs a)
     PartRegs<CG ? kUpdateMaxBlocks / kBlock : 1> pin;
     if constexpr (CG)
         part_load(a.part_in, a.n_part_in, pin);
-    if constexpr (MODE == kModeSpmv && MSPMV_BLK_PAIR && KR <= 6) {  // taller runs: 73 VGPRs, column owners
-        if (!stopped)
+    if constexpr (MODE == kModeSpmv && KR <= 6) {  // taller runs: 73 VGPRs, column owners
+        if (stopped)
+            return;
+        // a register run tile: every chunk starts at pattern column 0 (wave-uniform: each wave holds
+        // all descriptors)
+        const bool reg = nblk > 0 && __ballot((tid & 63) < nblk && ((bd.x >> 16) & 255u) != 0) == 0;
+        if (reg)
             blk_rows_pair<NT, KR>(a, bd, nblk, b0.x, b0.y, colbase);
+        else
+            tile_rows_reg<NT>(a, t, b0.x, b0.y, a.cols16 ? colbase : -1);
         return;
     }
     blk_rows<MODE, NT, kBlock>(a, bd, nblk, b0.x, b0.y, colbase, beta, dot, [&]() {
@@ -1844,259 +1823,6 @@ __global__ __launch_bounds__(kBlock) void k_spmv_blk(TileArgs a)
         dot_epilogue(a, sm, t, dot);
 }
 
-// Single right-hand side, node-block plans (every tile a register run tile), persistent and
-// wave-pipelined.  The unit of work is one run chunk (k_build_blocks' descriptor: <= 8 rows of a
-// node x <= 64 pattern columns); wave w of workgroup b owns chunks w and w + 4 of the tiles
-// xcd_tile(b), xcd_tile(b + G), ... (G = gridDim.x, a multiple of 8, so they stay on one XCD).
-// At entry lane j of the wave loads unit j's descriptor, tile bounds and column base (one memory
-// round trip for the wave's whole run of <= 32 tiles); the units then go through a three-stage
-// register pipeline: unit u's x gathers are issued, then unit u + 2's values and 16-bit columns,
-// then unit u's products and row sums run -- so two chunks' streams are always in flight per
-// wave, with no metadata round trip, barrier or workgroup dispatch between them.  Per chunk the
-// arithmetic is blk_rows' (the same products summed by the same rows8_sum tree), so y is
-// bit-identical to k_spmv_blk's.
-constexpr int kRunsMaxTiles = 32;  // tiles per workgroup: 2 units each in one wave's 64 lanes
-
-struct RunMeta {  // lane j: unit j
-    uint4 d;
-    int n0, r0, colbase, ok;
-};
-
-struct RunStage {
-    double v[kBlkRows];
-    double x;
-    int c;
-};
-
-__device__ __forceinline__ uint4 run_desc(const RunMeta &m, int j)
-{
-    return make_uint4((unsigned)__builtin_amdgcn_readlane((int)m.d.x, j),
-                      (unsigned)__builtin_amdgcn_readlane((int)m.d.y, j),
-                      (unsigned)__builtin_amdgcn_readlane((int)m.d.z, j),
-                      (unsigned)__builtin_amdgcn_readlane((int)m.d.w, j));
-}
-
-template <bool NT>
-__device__ __forceinline__ void run_issue(const TileArgs &a, const RunMeta &m, int j, RunStage &s)
-{
-    const int lane = threadIdx.x & 63;
-    s.c = 0;
-    if (!__builtin_amdgcn_readlane(m.ok, j))  // an empty unit (the tile has fewer chunks)
-        return;
-    const uint4 d = run_desc(m, j);
-    const int n0 = __builtin_amdgcn_readlane(m.n0, j), colbase = __builtin_amdgcn_readlane(m.colbase, j);
-    const int vofs = d.x & 0xffff, wc = d.x >> 24;
-    const int h = d.y & 15, p = (d.y >> 4) & 7;
-    int start = 0, pstart = 0;
-#pragma unroll
-    for (int i = 0; i < kBlkRows; ++i) {
-        pstart = i == p ? start : pstart;
-        const int len = blk_len(d, i);
-        if (i < h && lane < len)
-            s.v[i] = ld_stream<NT>(a.vals + n0 + vofs + start + lane);
-        start += i < h ? len : 0;
-    }
-    if (lane < wc)
-        s.c = colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + lane);
-}
-
-__device__ __forceinline__ void run_gather(const TileArgs &a, const RunMeta &m, int j, RunStage &s)
-{
-    const int wc = __builtin_amdgcn_readlane(m.ok, j) ? (int)((unsigned)__builtin_amdgcn_readlane((int)m.d.x, j) >> 24) : 0;
-    s.x = 0.0;
-    if ((threadIdx.x & 63) < wc)
-        s.x = a.x[s.c];
-}
-
-__device__ __forceinline__ void run_finish(const TileArgs &a, const RunMeta &m, int j, const RunStage &s)
-{
-    if (!__builtin_amdgcn_readlane(m.ok, j))
-        return;
-    const int lane = threadIdx.x & 63;
-    const uint4 d = run_desc(m, j);
-    const int h = d.y & 15, rofs = d.y >> 16;
-    double pr[kBlkRows];
-#pragma unroll
-    for (int i = 0; i < kBlkRows; ++i)
-        pr[i] = (i < h && lane < blk_len(d, i)) ? s.v[i] * s.x : 0.0;
-    const double sum = rows8_sum(pr);
-    const int myrow = lane >> 3;
-    if ((lane & 7) == 0 && myrow < h)
-        a.y[__builtin_amdgcn_readlane(m.r0, j) + rofs + myrow] = sum;
-}
-
-template <bool NT>
-__global__ __launch_bounds__(kBlock) void k_spmv_runs(TileArgs a)
-{
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int G = gridDim.x, b = blockIdx.x, T = a.num_tiles;
-    const int U = 2 * ((T - b + G - 1) / G);  // the host keeps this <= 2 * kRunsMaxTiles
-    RunMeta m{};
-    if (lane < U) {
-        const int t = xcd_tile(b + (lane >> 1) * G, T);
-        const uint4 *bt = a.blk + (size_t)t * a.blk_stride;
-        const int di = w + 4 * (lane & 1);  // < 8 <= blk_stride: always inside the tile's set
-        const uint4 d0 = bt[0], dc = bt[di];
-        const int2 b0 = a.bounds[t];
-        m.colbase = a.colbase[t];
-        m.d = di == 0 ? d0 : dc;
-        m.ok = di < (int)((d0.y >> 8) & 255u);
-        m.n0 = b0.y;
-        m.r0 = b0.x;
-    }
-    RunStage A, B, C;
-    run_issue<NT>(a, m, 0, A);
-    run_issue<NT>(a, m, 1, B);  // U >= 2
-    for (int u = 0; u < U; u += 3) {
-        run_gather(a, m, u, A);
-        if (u + 2 < U)
-            run_issue<NT>(a, m, u + 2, C);
-        run_finish(a, m, u, A);
-        if (u + 1 >= U)
-            break;
-        run_gather(a, m, u + 1, B);
-        if (u + 3 < U)
-            run_issue<NT>(a, m, u + 3, A);
-        run_finish(a, m, u + 1, B);
-        if (u + 2 >= U)
-            break;
-        run_gather(a, m, u + 2, C);
-        if (u + 4 < U)
-            run_issue<NT>(a, m, u + 4, B);
-        run_finish(a, m, u + 2, C);
-    }
-}
-
-// Single right-hand side, persistent and software-pipelined.  Workgroup v (XCD-grouped) walks
-// the contiguous tile run [v*tpb, min((v+1)*tpb, T)); its bounds, reduction modes and tail
-// flags are staged in LDS once.  Two register stages (A, B) ping-pong, so no register copy of
-// an in-flight load ever forces a wait: while tile i's x gathers, products and in-tile
-// reduction run, the (col, val) stream and first row ends of tile i+1 are already in flight
-// (issued right after tile i's gathers, so waiting for the gathers -- the older loads -- never
-// waits for the prefetch).  The chain per tile is then gather latency + LDS reduction, with
-// the HBM stream of the next tile underneath it, instead of stream + gather + reduction.
-constexpr int kMaxTpb = 255;
-
-template <int IPT>
-struct PipeStage {
-    int c[IPT];
-    double v[IPT];
-    int re;  // this thread's row end (row tid of the tile), relative to nothing
-};
-
-// Issue one tile's stream: cols first (the gathers wait on them), then vals, then the first
-// round of row ends.  Always issued, clamped into the tile (an empty tile reads its start
-// element, which the kNnzPad padding keeps in bounds), so every path has the same count.
-template <int IPT, bool NT>
-__device__ __forceinline__ void pipe_issue(const TileArgs &a, int m, int2 b0, int2 b1, PipeStage<IPT> &st)
-{
-    const int nz = b1.y - b0.y, nr = b1.x - b0.x;
-    const int tid = threadIdx.x;
-#pragma unroll
-    for (int j = 0; j < IPT; ++j)
-        st.c[j] = ld_stream<NT>(a.cols + b0.y + max(min(tid + j * kBlock, nz - 1), 0));
-#pragma unroll
-    for (int j = 0; j < IPT; ++j)
-        st.v[j] = ld_stream<NT>(a.vals + b0.y + max(min(tid + j * kBlock, nz - 1), 0));
-    st.re = a.row_offsets[min(b0.x + 1 + max(min(tid, nr - 1), 0), m)];
-}
-
-template <int IPT, int MODE, bool NT>
-__device__ __forceinline__ void pipe_tile(const TileArgs &a, SpmvSmem<IPT> &sm, const int2 *s_b,
-                                          const unsigned char *s_mode, int m, int i, int ntl, int t,
-                                          PipeStage<IPT> &cur, PipeStage<IPT> &nxt, double beta, double &dot)
-{
-    constexpr bool CG = MODE == kModeCg;
-    constexpr int TILE = SpmvSmem<IPT>::TILE;
-    const int tid = threadIdx.x;
-    const int2 b0 = s_b[i], b1 = s_b[i + 1], b2 = s_b[min(i + 2, ntl)];
-    const int r0 = b0.x, n0 = b0.y;
-    const int nrows = b1.x - r0;
-    const int nnzt = b1.y - n0;
-    // (1) this tile's gathers (cur.c arrived: only loads issued before it are waited for)
-    double xv[IPT], pv[IPT];
-#pragma unroll
-    for (int j = 0; j < IPT; ++j)
-        xv[j] = a.x[cur.c[j]];
-    if (CG) {
-#pragma unroll
-        for (int j = 0; j < IPT; ++j)
-            pv[j] = a.p_old[cur.c[j]];
-    }
-    double xr, pr;  // CG / dot epilogue operands: issued before the prefetch, so waits stay counted
-    row_operands<MODE>(a, r0, nrows, xr, pr);
-    // (2) the next tile's stream, under this tile's gather wait and reduction
-    pipe_issue<IPT, NT>(a, m, b1, b2, nxt);
-    // (3) products and row ends to LDS
-#pragma unroll
-    for (int j = 0; j < IPT; ++j) {
-        const int k = tid + j * kBlock;
-        double x = xv[j];
-        if (CG)
-            x = x + beta * pv[j];
-        if (k < nnzt)
-            sm.prod[pslot(k)] = cur.v[j] * x;
-    }
-    if (nnzt > TILE) {  // rare: nonzeros snapped in beyond the nominal tile (direct loads)
-        for (int k = TILE + tid; k < nnzt; k += kBlock) {
-            const int col = a.cols[n0 + k];
-            double x = a.x[col];
-            if (CG)
-                x = x + beta * a.p_old[col];
-            sm.prod[pslot(k)] = a.vals[n0 + k] * x;
-        }
-    }
-    int *rend = sm.rowend(nnzt);
-    if (tid < nrows)
-        rend[tid] = cur.re - n0;
-    for (int r = kBlock + tid; r < nrows; r += kBlock)  // rare: > 256 rows in the tile
-        rend[r] = a.row_offsets[r0 + 1 + r] - n0;
-    __syncthreads();
-    const unsigned char mt = s_mode[i];
-    reduce_tile<IPT, MODE>(a, sm, t, r0, n0, nrows, nnzt, mt & 0x7f, (mt & 0x80) != 0, beta, dot, xr, pr);
-}
-
-template <int IPT, int MODE, bool NT>
-__global__ __launch_bounds__(kBlock) void k_spmv_persist(TileArgs a, int tpb)
-{
-    static_assert(MODE != kModeCg, "the pipelined CG head runs in the one-tile kernel only");
-    __shared__ SpmvSmem<IPT> sm;
-    __shared__ int2 s_b[kMaxTpb + 1];
-    __shared__ unsigned char s_mode[kMaxTpb + 1];  // reduction mode | 0x80 when the tile has a tail
-    const int tid = threadIdx.x;
-    if (MODE != kModeSpmv && a.ctrl->done)
-        return;
-    const int T = a.num_tiles;
-    const int v = xcd_tile(blockIdx.x, gridDim.x);
-    const int t_begin = min(v * tpb, T), t_end = min(t_begin + tpb, T);
-    const int ntl = t_end - t_begin;
-    const double beta = MODE == kModeCg ? a.scal[0].beta : 0.0;
-    if (tid <= ntl) {
-        s_b[tid] = a.bounds[t_begin + tid];
-        if (tid < ntl)
-            s_mode[tid] = (unsigned char)(a.rmode[t_begin + tid] | (a.split[t_begin + tid + 1] ? 0x80 : 0));
-    }
-    __syncthreads();
-    double dot = 0.0;
-    if (ntl > 0) {
-        PipeStage<IPT> A, B;
-        pipe_issue<IPT, NT>(a, a.m, s_b[0], s_b[1], A);
-        int i = 0;
-        for (; i + 1 < ntl; i += 2) {
-            pipe_tile<IPT, MODE, NT>(a, sm, s_b, s_mode, a.m, i, ntl, t_begin + i, A, B, beta, dot);
-            pipe_tile<IPT, MODE, NT>(a, sm, s_b, s_mode, a.m, i + 1, ntl, t_begin + i + 1, B, A, beta, dot);
-        }
-        if (i < ntl)
-            pipe_tile<IPT, MODE, NT>(a, sm, s_b, s_mode, a.m, i, ntl, t_begin + i, A, B, beta, dot);
-    }
-    if (MODE == kModeDot) {  // one partial per tile: the run's sum at its first tile, zeros after
-        dot_epilogue(a, sm, t_begin, dot);
-        for (int i = 1 + tid; i < ntl; i += kBlock)
-            a.partials[t_begin + i] = 0.0;
-    }
-}
-
 // Row-group reduction of one multi-RHS tile (mode lgp + 1): a row group is GL column-pair
 // lanes x Gp = 2^lgp nonzero lanes.  Lane (c, j) of a group sums, for its columns 2c, 2c+1,
 // the products of nonzeros j, j+Gp, ... of the row in order from 0.0 (four panel-row gathers
@@ -2108,17 +1834,12 @@ __global__ __launch_bounds__(kBlock) void k_spmv_persist(TileArgs a, int tpb)
 // is taken after the row loop, from the Ap rows the workgroup has just stored and the rows' own x
 // (both contiguous nrows x L slices, L2-resident: x[R] is a column of row R), instead of holding
 // each row's x and the running dot in registers through the gathers -- the dot mode then needs
-// no more registers than the plain SpMM, so it keeps the plain kernel's occupancy.  Lab builds:
-// -DMSPMV_SPMM_DOT_TAIL=0 restores the in-loop form.
-#ifndef MSPMV_SPMM_DOT_TAIL
-#define MSPMV_SPMM_DOT_TAIL 1
-#endif
-constexpr bool kSpmmDotTail = MSPMV_SPMM_DOT_TAIL != 0;
+// no more registers than the plain SpMM, so it keeps the plain kernel's occupancy.
 
-template <int L, int MODE, bool DICT = false>
+template <int L, bool DICT = false>
 __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_col, const double *s_val,
-                                                const int *rend, int t, int r0, int nrows, int nnzt,
-                                                double2 &dot, int lgp, const double2 *s_panel = nullptr)
+                                                const int *rend, int t, int r0, int nrows, int nnzt, int lgp,
+                                                const double2 *s_panel = nullptr)
 {
     constexpr int GL = L / 2;
     const int Gp = 1 << lgp;
@@ -2137,11 +1858,6 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
     for (int r = tid / W; r < nseg; r += kBlock / W) {  // uniform within a group
         const int s0 = r == 0 ? 0 : rend[r - 1];
         const int e = r < nrows ? rend[r] : nnzt;
-        // MODE 2 without the tail pass (kSpmmDotTail): the row's own x, issued ahead of the row's
-        // gathers (used after them)
-        double2 xx = make_double2(0.0, 0.0);
-        if (MODE == kModeDot && !kSpmmDotTail && sub == 0)
-            xx = *reinterpret_cast<const double2 *>(a.xr + (size_t)(r0 + r) * a.ld + 2 * lane);
         double2 acc = make_double2(0.0, 0.0);
         int k = s0 + sub;
         // batches of 8 panel-row gathers in flight per lane (the SpMM is gather-latency bound:
@@ -2195,10 +1911,6 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
                 *reinterpret_cast<double2 *>(a.y + off) = acc;
             else  // the trailing partial row -> carry (k_fixup adds the row's carries in a fixed order)
                 *reinterpret_cast<double2 *>(a.carry_val + (size_t)t * L + 2 * lane) = acc;
-            if (MODE == kModeDot && !kSpmmDotTail) {
-                dot.x += xx.x * acc.x;
-                dot.y += xx.y * acc.y;
-            }
         }
     }
 }
@@ -2213,10 +1925,7 @@ constexpr int spmm_waves_per_eu(int L, int IPTG, bool DICT = false)
     const int items = (kBlock / (L / 2)) * IPTG;
     const int lds = 16 * (items + items / kSnapDiv) + 6144 + (DICT ? kSpmmDictBytes : 0);  // + s_crow, s_cval, s_red2
     const int w = 163840 / lds;
-#ifndef MSPMV_SPMM_WAVES_CAP
-#define MSPMV_SPMM_WAVES_CAP 7
-#endif
-    return w < 1 ? 1 : w > MSPMV_SPMM_WAVES_CAP ? MSPMV_SPMM_WAVES_CAP : w;
+    return w < 1 ? 1 : w > 7 ? 7 : w;
 }
 
 // DICT: tiles with a column dictionary (multi-RHS plans, k_build_dict) gather each distinct
@@ -2226,9 +1935,8 @@ constexpr int spmm_waves_per_eu(int L, int IPTG, bool DICT = false)
 // (pwtk shape): L = 16 130 -> 102 us; at L = 4 and 8 it lost (47 -> 55, 63 -> 67 us; the
 // 27-point nlpkkt120 size at L = 8 505 -> 590 us: the extra dependent round trip and the
 // occupancy the 16 KB panel costs outweigh 64-B gathers), so only L = 16 plans build one.
-#ifndef MSPMV_SPMM_GROUP4
-#define MSPMV_SPMM_GROUP4 0  // measured even: CG multi L = 8 0.915-0.920 vs 0.914 ms/iteration (r03z)
-#endif
+// (Grouped staging, 4 nonzeros per lane: measured even, CG multi L = 8 0.915-0.920 vs 0.914 ms per
+// iteration, r03z -- not kept.)
 template <int L, int IPTG, int MODE, bool NT, bool DICT = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(spmm_waves_per_eu(L, IPTG, DICT)))) void
 k_spmm_tile(TileArgs a)
@@ -2257,7 +1965,7 @@ k_spmm_tile(TileArgs a)
     // flag's round trip does not delay every workgroup's first load (MODE 2 writes only the
     // scratch Ap and partials: a stopped solve only needs the work skipped, not fenced)
     const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
-    const int t = xcd_tile(blockIdx.x, a.num_tiles, a.tstreams);
+    const int t = xcd_tile(blockIdx.x, a.num_tiles);
     const int2 b0 = a.bounds[t];
     const int2 b1 = a.bounds[t + 1];
     const int r0 = b0.x, n0 = b0.y;
@@ -2281,37 +1989,7 @@ k_spmm_tile(TileArgs a)
     // Every round's loads are issued before any is stored to LDS (indices clamped into the
     // tile), the first round of row ends with them: one memory round trip per tile, not STG.
     const int re0 = a.row_offsets[min(r0 + 1 + min(tid, max(nrows - 1, 0)), a.m)];  // clamped: always issued
-    if (MSPMV_SPMM_GROUP4 && !DICT && nnzt > 0) {  // block-uniform
-        // grouped staging: thread tid takes the absolute groups of 4 consecutive nonzeros q0 + tid +
-        // 256 u (q0 = n0 / 4): one 16-B column load and two 16-B value loads per group instead of
-        // four 4-B and four 8-B loads (the single-RHS pair staging's finding: load instructions)
-        constexpr int NR = (MAXI / 4 + 1 + kBlock - 1) / kBlock;
-        const int q0 = n0 >> 2, qlast = (n0 + nnzt - 1) >> 2;
-        int4 c4[NR];
-        double2 v4[NR][2];
-#pragma unroll
-        for (int u = 0; u < NR; ++u) {
-            const int q = min(q0 + tid + kBlock * u, qlast);
-            c4[u] = ld_stream<NT>(reinterpret_cast<const int4 *>(a.cols) + q);
-            v4[u][0] = ld_stream<NT>(reinterpret_cast<const double2 *>(a.vals) + 2 * (size_t)q);
-            v4[u][1] = ld_stream<NT>(reinterpret_cast<const double2 *>(a.vals) + 2 * (size_t)q + 1);
-        }
-#pragma unroll
-        for (int u = 0; u < NR; ++u) {
-            const int q = q0 + tid + kBlock * u;
-            if (q > qlast)
-                continue;
-            const int k0 = 4 * q - n0;
-            const int cc[4] = {c4[u].x, c4[u].y, c4[u].z, c4[u].w};
-            const double vv[4] = {v4[u][0].x, v4[u][0].y, v4[u][1].x, v4[u][1].y};
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-                if (k0 + e >= 0 && k0 + e < nnzt) {
-                    s_col[k0 + e] = cc[e];
-                    s_val[k0 + e] = vv[e];
-                }
-        }
-    } else if (nnzt > 0) {  // block-uniform
+    if (nnzt > 0) {  // block-uniform
         int cst[STG];
         double vst[STG];
         if (DICT && nd > 0) {
@@ -2358,9 +2036,9 @@ k_spmm_tile(TileArgs a)
     double2 dot = make_double2(0.0, 0.0);
     if (rmode != 0) {
         if (DICT && nd > 0)
-            spmm_group_rows<L, MODE, true>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, dot, rmode - 1, s_panel);
+            spmm_group_rows<L, true>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, rmode - 1, s_panel);
         else
-            spmm_group_rows<L, MODE>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, dot, rmode - 1);
+            spmm_group_rows<L>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, rmode - 1);
     } else {
     const int ipt = (items + NG - 1) / NG;
     const int d0 = min(g * ipt, items);
@@ -2371,13 +2049,7 @@ k_spmm_tile(TileArgs a)
     const bool need_cin = (cx < ex) && (cy > (cx == 0 ? 0 : s_rowend[cx - 1]));
 
     auto write_row = [&](int row, double2 val) {
-        const size_t off = (size_t)(r0 + row) * a.ld + 2 * lane;
-        *reinterpret_cast<double2 *>(a.y + off) = val;
-        if (MODE == kModeDot && !kSpmmDotTail) {
-            const double2 xx = *reinterpret_cast<const double2 *>(a.xr + off);
-            dot.x += xx.x * val.x;
-            dot.y += xx.y * val.y;
-        }
+        *reinterpret_cast<double2 *>(a.y + (size_t)(r0 + row) * a.ld + 2 * lane) = val;
     };
 
     double2 run = make_double2(0.0, 0.0);
@@ -2462,16 +2134,10 @@ k_spmm_tile(TileArgs a)
             acc.y += c.y;
         }
         *reinterpret_cast<double2 *>(a.carry_val + (size_t)t * L + 2 * lane) = acc;
-        if (MODE == kModeDot && !kSpmmDotTail) {
-            const size_t off = (size_t)(r0 + nrows) * a.ld + 2 * lane;
-            const double2 xx = *reinterpret_cast<const double2 *>(a.xr + off);
-            dot.x += xx.x * acc.x;
-            dot.y += xx.y * acc.y;
-        }
     }
     }  // merge walk
 
-    if (MODE == kModeDot && kSpmmDotTail) {
+    if (MODE == kModeDot) {
         // the tile's whole Ap rows, stored above by its own waves (either path): drained, then
         // visible to the workgroup after the barrier (one CU, and no wave read these lines before).
         // Pair e = (row e / GL, columns 2 (e % GL) + {0, 1}); kBlock % GL == 0, so a thread always
@@ -2547,22 +2213,12 @@ __device__ __forceinline__ double2 rows8_sum2(const double2 (&p)[kBlkRows])
 
 // Waves per SIMD k_spmm_blk is compiled for: 8 (<= 64 VGPRs; with the pass fence below the L = 16
 // kernel takes 60 and spills nothing).  Unconstrained the straight-line passes take 82 VGPRs (6
-// waves): pwtk L = 16 58.5 vs 51-52 us hot at 8 waves (r03g).  0 = unconstrained (lab builds).
-#ifndef MSPMV_SPMM_BLK_WAVES
-#define MSPMV_SPMM_BLK_WAVES 8
-#endif
-// The instantiations that fit 64 VGPRs without spilling (plain SpMM, runs of <= 6 rows, L >= 4);
-// the others (L = 2, 8-row runs, dot mode) stay unconstrained rather than spill.
-constexpr int spmm_blk_waves(int L, int MODE, int KR)
-{
-    return MSPMV_SPMM_BLK_WAVES > 0 && MODE == 0 && KR <= 6 && L >= 4 ? MSPMV_SPMM_BLK_WAVES : 1;
-}
+// waves): pwtk L = 16 58.5 vs 51-52 us hot at 8 waves (r03g).  The instantiations that fit 64 VGPRs
+// without spilling (plain SpMM, runs of <= 6 rows, L >= 4); the others (L = 2, 8-row runs, dot
+// mode) stay unconstrained rather than spill.
+constexpr int spmm_blk_waves(int L, int MODE, int KR) { return MODE == 0 && KR <= 6 && L >= 4 ? 8 : 1; }
 // KR: the plan's tallest run (rows of one node, <= kBlkRows); KR = 6 (6-DOF FEM such as pwtk)
 // holds fewer accumulator and value registers than 8.
-#if MSPMV_LAB_ABLATE == 10  // lab build only (tools/lab/stamps_blk.py): per-chunk phase stamps of k_spmm_blk
-constexpr int kLabBlkSlots = 1 << 16;  // (tile, wave, round) slots: 8 stamps each
-__device__ unsigned long long g_lab_blk[kLabBlkSlots * 8];
-#endif
 template <int L, int MODE, bool NT, int KR = kBlkRows>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(spmm_blk_waves(L, MODE, KR)))) void
 k_spmm_blk(TileArgs a)
@@ -2570,33 +2226,23 @@ k_spmm_blk(TileArgs a)
     static_assert(MODE != kModeCg, "multi-RHS CG runs the split iteration (MODE 2)");
     constexpr int GL = L / 2;      // lanes per panel row
     constexpr int NGW = 64 / GL;   // column groups per wave = pattern columns per pass
-#ifndef MSPMV_SPMM_BLK_PB
-#define MSPMV_SPMM_BLK_PB 0
-#endif
     // passes whose gathers are in flight together, measured on the pwtk shape: with the values in
     // registers (before LDSV) 4 was best at L = 16 and 2 at L = 4, 8 (r02z); with LDSV 2 is best at
     // every width (L = 16: 72.4-73.1 vs 74.4-74.8 us at 4 and 89.4 at 8; L = 4: 40-41 vs 50-51 and
     // 65 us; r02ah).  Fused multiply-adds instead of the guarded mul + add measured slower.
     // straight-line passes (r03g, pwtk, hot): L = 16 PB 2 50.9-51.7 us vs PB 1 53.4-54.6; L = 8 PB 1
     // 43.0-43.4 vs 43.6-45.6; L = 4 PB 1 37.3 vs 40.5-41.7
-    constexpr int PB = MSPMV_SPMM_BLK_PB > 0 ? MSPMV_SPMM_BLK_PB : (L >= 16 ? 2 : 1);
-#ifndef MSPMV_SPMM_BLK_FMA
-#define MSPMV_SPMM_BLK_FMA 1  // lab builds: 0 keeps the guarded multiply + add on every pass
-#endif
+    constexpr int PB = L >= 16 ? 2 : 1;
     __shared__ double2 s_red2[MODE == kModeDot ? kBlock / 64 : 1][GL];
-#ifndef MSPMV_SPMM_BLK_LDSV
-#define MSPMV_SPMM_BLK_LDSV 1
-#endif
-    // LDSV: each wave parks its run's values (row-major, [row][column]) and pattern columns in its
-    // own LDS slice, and a pass reads v[i][j] there (one broadcast read per (pass, row)) instead of
-    // holding the rows in registers and shuffling them (two bpermutes per (pass, row))
-    constexpr bool LDSV = MSPMV_SPMM_BLK_LDSV != 0;
-    __shared__ __attribute__((aligned(16))) double s_v[LDSV ? kBlock / 64 : 1][LDSV ? kBlkRows : 1][64];
-    __shared__ int s_c[LDSV ? kBlock / 64 : 1][64];
+    // each wave parks its run's values (row-major, [row][column]) and pattern columns in its own LDS
+    // slice, and a pass reads v[i][j] there (one broadcast read per (pass, row)) instead of holding
+    // the rows in registers and shuffling them (two bpermutes per (pass, row)): r02ag
+    __shared__ __attribute__((aligned(16))) double s_v[kBlock / 64][kBlkRows][64];
+    __shared__ int s_c[kBlock / 64][64];
     const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
     const int tid = threadIdx.x, lane = tid & 63;
     const int g = lane / GL, c = lane % GL;
-    const int t = xcd_tile(blockIdx.x, a.num_tiles, a.tstreams);
+    const int t = xcd_tile(blockIdx.x, a.num_tiles);
     const int2 b0 = a.bounds[t];
     const int r0 = b0.x, n0 = b0.y;
     const int colbase = a.colbase[t];
@@ -2622,93 +2268,19 @@ k_spmm_blk(TileArgs a)
         for (int i = 0; i < KR; ++i)
             vr[i] = (i < h && lane < blk_len(d, i)) ? ld_stream<NT>(a.vals + n0 + vofs + start[i] + lane) : 0.0;
     };
-#ifndef MSPMV_SPMM_BLK_PF
-#define MSPMV_SPMM_BLK_PF 0
-#endif
-    // PF (with LDSV): the wave's next chunk's columns and values are loaded while this chunk's
-    // passes run (they land in registers the LDS slice has just been filled from)
-    constexpr bool PF = LDSV && MSPMV_SPMM_BLK_PF != 0;
-#ifndef MSPMV_SPMM_BLK_V2
-#define MSPMV_SPMM_BLK_V2 0  // measured slower: pwtk L = 16 cold 52.8-53.4 vs 50.2-50.8 us (r03v)
-#endif
-    // V2 (with LDSV, without PF): the run's values arrive as column pairs, two rows per load
-    // instruction (the node-block SpMV's blk_rows_pair finding: load instructions, not bytes)
-    constexpr bool V2 = LDSV && !PF && MSPMV_SPMM_BLK_V2 != 0 && KR % 2 == 0;
-    int colj_n = 0;
-    double vrow_n[KR];
-    if (PF && wave < nd && !stopped)
-        fetch(wave, colj_n, vrow_n);
     for (int di = wave; di < nd && !stopped; di += kBlock / 64) {  // wave-uniform
-#if MSPMV_LAB_ABLATE == 10
-        const int lab_slot = (t * 4 + wave) * 2 + (di >= kBlock / 64 ? 1 : 0);
-        unsigned long long *lab = g_lab_blk + (size_t)lab_slot * 8;
-        const bool lab_on = lab_slot < kLabBlkSlots && lane == 0 && di < 2 * (kBlock / 64) && MODE == kModeSpmv;
-        if (lab_on)
-            lab[0] = wall_clock64();
-#endif
         const uint4 d = blk_read(bd, di);
         const int wc = d.x >> 24;
         const int h = d.y & 15, rofs = d.y >> 16;
-        int colj;
-        double vrow[KR];
-        if constexpr (PF) {
-            colj = colj_n;
-#pragma unroll
-            for (int i = 0; i < KR; ++i)
-                vrow[i] = vrow_n[i];
-        } else if constexpr (!V2) {
+        {  // wave-private slice: the wave's LDS operations stay in order
+            int colj;
+            double vrow[KR];
             fetch(di, colj, vrow);
-        }
-        if constexpr (LDSV && V2) {
-            // column pairs: half h2 of the wave loads rows h2, h2 + 2, ... of the run, lane hl its
-            // columns 2 hl and 2 hl + 1 -- one 16-B load per lane for two rows (8-B aligned at worst),
-            // stored into the slice as one 16-B LDS write; rows >= h and columns past a row hold 0.0
-            const int vofs = d.x & 0xffff, p = (d.y >> 4) & 7;
-            const int h2 = lane >> 5, hl = lane & 31;
-            int start[KR];
-            int pstart = 0, acc_s = 0;
-#pragma unroll
-            for (int i = 0; i < KR; ++i) {
-                start[i] = acc_s;
-                pstart = i == p ? acc_s : pstart;
-                acc_s += i < h ? blk_len(d, i) : 0;
-            }
-            colj = lane < wc ? colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + lane) : 0;
-            double2 vp[KR / 2];
-#pragma unroll
-            for (int ii = 0; ii < KR / 2; ++ii) {
-                const int i = 2 * ii + h2;
-                int len = 0;
-#pragma unroll
-                for (int r = 0; r < KR; ++r)  // row i's length and start (i differs between the halves)
-                    len = r == i ? blk_len(d, r) : len;
-                int st0 = 0;
-#pragma unroll
-                for (int r = 0; r < KR; ++r)
-                    st0 = r == i ? start[r] : st0;
-                vp[ii] = make_double2(0.0, 0.0);
-                if (i < h && 2 * hl < len)
-                    vp[ii] = ld_stream<NT>(reinterpret_cast<const double2 *>(a.vals + n0 + vofs + st0 + 2 * hl));
-                if (!(i < h && 2 * hl + 1 < len))
-                    vp[ii].y = 0.0;
-            }
-            s_c[wave][lane] = colj;
-#pragma unroll
-            for (int ii = 0; ii < KR / 2; ++ii)
-                *reinterpret_cast<double2 *>(&s_v[wave][2 * ii + h2][2 * hl]) = vp[ii];
-            __builtin_amdgcn_wave_barrier();
-        } else if constexpr (LDSV) {  // wave-private slice: the wave's LDS operations stay in order
             s_c[wave][lane] = colj;
 #pragma unroll
             for (int i = 0; i < KR; ++i)  // rows >= h too (0.0 from fetch): the passes read every row
                 s_v[wave][i][lane] = vrow[i];
             __builtin_amdgcn_wave_barrier();
-#if MSPMV_LAB_ABLATE == 10
-            if (lab_on)
-                lab[1] = wall_clock64();
-#endif
-            if (PF && di + kBlock / 64 < nd)
-                fetch(di + kBlock / 64, colj_n, vrow_n);
         }
         const int ri = lane >> 3;  // the run row this lane's slot stores
         const bool store = (lane & 7) < GL && ri < h;
@@ -2728,36 +2300,30 @@ k_spmm_blk(TileArgs a)
 #pragma unroll
         for (int i = 0; i < KR; ++i)
             minlen = i < h ? min(minlen, blk_len(d, i)) : minlen;
-#ifndef MSPMV_SPMM_BLK_QFENCE
-#define MSPMV_SPMM_BLK_QFENCE 1
-#endif
         int pb = 0;
-        if (MSPMV_SPMM_BLK_FMA) {
-            // groups of PB passes whose columns all lie in every row of the run: in-place fused
-            // multiply-adds, no select, no merge of paths (the accumulators stay in place)
-            for (; (pb + PB) * NGW <= minlen; pb += PB) {  // wave-uniform
-                int cq[PB];
+        // groups of PB passes whose columns all lie in every row of the run: in-place fused
+        // multiply-adds, no select, no merge of paths (the accumulators stay in place)
+        for (; (pb + PB) * NGW <= minlen; pb += PB) {  // wave-uniform
+            int cq[PB];
 #pragma unroll
-                for (int q = 0; q < PB; ++q)
-                    cq[q] = LDSV ? s_c[wave][((pb + q) * NGW + g) & 63] : __shfl(colj, ((pb + q) * NGW + g) & 63);
-                double2 xv[PB];
+            for (int q = 0; q < PB; ++q)
+                cq[q] = s_c[wave][((pb + q) * NGW + g) & 63];
+            double2 xv[PB];
 #pragma unroll
-                for (int q = 0; q < PB; ++q)
-                    xv[q] = *reinterpret_cast<const double2 *>(a.x + (size_t)cq[q] * a.ld + 2 * c);
+            for (int q = 0; q < PB; ++q)
+                xv[q] = *reinterpret_cast<const double2 *>(a.x + (size_t)cq[q] * a.ld + 2 * c);
 #pragma unroll
-                for (int q = 0; q < PB; ++q) {
-                    const int j = (pb + q) * NGW + g;
+            for (int q = 0; q < PB; ++q) {
+                const int j = (pb + q) * NGW + g;
 #pragma unroll
-                    for (int i = 0; i < KR; ++i) {
-                        const double v = LDSV ? s_v[wave][i][j & 63] : __shfl(vrow[i], j & 63);
-                        acc[i].x = __builtin_fma(v, xv[q].x, acc[i].x);
-                        acc[i].y = __builtin_fma(v, xv[q].y, acc[i].y);
-                    }
-                    // pass q + 1's value reads stay behind pass q's FMAs: without the fence the
-                    // compiler hoists them and the kernel no longer fits 64 VGPRs (8 waves)
-                    if (MSPMV_SPMM_BLK_QFENCE)
-                        asm volatile("" ::: "memory");
+                for (int i = 0; i < KR; ++i) {
+                    const double v = s_v[wave][i][j & 63];
+                    acc[i].x = __builtin_fma(v, xv[q].x, acc[i].x);
+                    acc[i].y = __builtin_fma(v, xv[q].y, acc[i].y);
                 }
+                // pass q + 1's value reads stay behind pass q's FMAs: without the fence the
+                // compiler hoists them and the kernel no longer fits 64 VGPRs (8 waves)
+                asm volatile("" ::: "memory");
             }
         }
         // the remaining passes one at a time, each product kept or skipped by a select (the
@@ -2765,31 +2331,17 @@ k_spmm_blk(TileArgs a)
         // never reaches that row)
         for (; pb * NGW < wc; ++pb) {  // wave-uniform
             const int j = pb * NGW + g;
-            const int cq = LDSV ? s_c[wave][j & 63] : __shfl(colj, j & 63);
+            const int cq = s_c[wave][j & 63];
             const double2 xv = *reinterpret_cast<const double2 *>(a.x + (size_t)cq * a.ld + 2 * c);
 #pragma unroll
             for (int i = 0; i < KR; ++i) {
-                const double v = LDSV ? s_v[wave][i][j & 63] : __shfl(vrow[i], j & 63);
+                const double v = s_v[wave][i][j & 63];
                 const bool on = i < h && j < blk_len(d, i);
                 acc[i].x += on ? v * xv.x : 0.0;
                 acc[i].y += on ? v * xv.y : 0.0;
             }
         }
-#if MSPMV_LAB_ABLATE == 10
-        if (lab_on) {
-            lab[2] = wall_clock64();
-            lab[5] = (unsigned long long)wc | ((unsigned long long)h << 8) | ((unsigned long long)nd << 16);
-        }
-#endif
         const double2 row = rows8_sum2<GL>(acc);
-#if MSPMV_LAB_ABLATE == 10
-        if (lab_on) {
-            lab[3] = wall_clock64();
-            unsigned hw;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-            lab[4] = hw;
-        }
-#endif
         if (store) {
             *reinterpret_cast<double2 *>(a.y + (size_t)(r0 + rofs + ri) * a.ld + 2 * c) = row;
             if (MODE == kModeDot) {
@@ -2949,8 +2501,8 @@ __global__ void k_fixup(const int *__restrict__ carry_tiles, const int *__restri
 static void fixup_launch(const TilePlan &plan, double *d_Y, int L, const CgControl *ctrl, int ld, hipStream_t s)
 {
     const long long waves = (long long)plan.num_carry_runs * L;
-    hipLaunchKernelGGL(k_fixup, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, plan.d_carry_tiles,
-                       plan.d_carry_rows, plan.d_carry_runs, plan.num_carry_runs, plan.d_carry_val, d_Y, L, ctrl, ld);
+    ggl(k_fixup, dim3((unsigned)((waves + 3) / 4)), dim3(256), s, plan.d_carry_tiles, plan.d_carry_rows,
+        plan.d_carry_runs, plan.num_carry_runs, (const double *)plan.d_carry_val, d_Y, L, ctrl, ld);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3035,36 +2587,19 @@ __device__ __forceinline__ long long sweep_index(long long k, long long nchunks,
     return (rev ? nchunks - 1 - k : k) * stride + i0;
 }
 
-// The pairs a thread of a streaming CG kernel visits, in order.  Grid-stride chunks (the whole grid
-// sweeps one chunk after another, rev: last chunk first) or, with MSPMV_VEC_SLICE, one contiguous
-// slice per workgroup walked 256 pairs at a time (rev: from the slice's end) -- the layout of the
-// measured read ceiling (tools/read_ceiling.hip).  Slices are a multiple of GL pairs long, so a
-// thread keeps its column pair (tid % GL) either way.
-#ifndef MSPMV_VEC_SLICE
-#define MSPMV_VEC_SLICE 0  // measured even: CG multi L = 8 0.920-0.921 vs 0.916-0.919 ms/iteration (r03aa)
-#endif
+// The pairs a thread of a streaming CG kernel visits, in order: grid-stride chunks (the whole grid
+// sweeps one chunk after another, rev: last chunk first).  (One contiguous slice per workgroup, the
+// read ceiling's layout, measured even: CG multi L = 8 0.920-0.921 vs 0.916-0.919 ms, r03aa.)
 template <int GL, typename F>
 __device__ __forceinline__ void for_pairs(long long npairs, int rev, F &&f)
 {
-    if (MSPMV_VEC_SLICE) {
-        long long per = (npairs + gridDim.x - 1) / gridDim.x;
-        per = (per + GL - 1) / GL * GL;
-        const long long lo = min(npairs, (long long)blockIdx.x * per), hi = min(npairs, lo + per);
-        const long long nch = (hi - lo + kBlock - 1) / kBlock;
-        for (long long k = 0; k < nch; ++k) {
-            const long long i = lo + (rev ? nch - 1 - k : k) * kBlock + threadIdx.x;
-            if (i < hi)
-                f(i);
-        }
-    } else {
-        const long long stride = (long long)gridDim.x * kBlock;
-        const long long i0 = (long long)blockIdx.x * kBlock + threadIdx.x;
-        const long long nch = (npairs + stride - 1) / stride;
-        for (long long k = 0; k < nch; ++k) {
-            const long long i = sweep_index(k, nch, stride, i0, rev);
-            if (i < npairs)
-                f(i);
-        }
+    const long long stride = (long long)gridDim.x * kBlock;
+    const long long i0 = (long long)blockIdx.x * kBlock + threadIdx.x;
+    const long long nch = (npairs + stride - 1) / stride;
+    for (long long k = 0; k < nch; ++k) {
+        const long long i = sweep_index(k, nch, stride, i0, rev);
+        if (i < npairs)
+            f(i);
     }
 }
 
@@ -3335,83 +2870,17 @@ __global__ __launch_bounds__(kBlock) void k_cg_xflush(CgVecArgs a, const double 
 }
 
 // ---- IC(0) preconditioner apply: sync-free sparse triangular solves ---------------------------
-// Spin on a ready flag written by another wave (agent-scope relaxed loads, s_sleep between
-// polls).  Bounded: after ~2^20 polls the caller reports a stall instead of hanging the GPU.
-__device__ __forceinline__ bool wait_flag(const int *f)
-{
-    for (int it = 0; it < (1 << 20); ++it) {
-        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0)
-            return true;
-        __builtin_amdgcn_s_sleep(2);
-    }
-    return false;
-}
-
-// x = T^-1 b for a triangular CSR T, one wave per row: ForwardSolveMultiple (FWD, T = L lower,
-// rows ascending) and BackwardSolveMultiple (T = L^T upper, rows descending),
-// incomplete_cholesky_decomp.hpp:231-348.  Lane (q, v) takes nonzeros q, q + 64/L, ... of the
-// row for right-hand side v; a dependency j waits on ready[j], then x[j] is read (sc1 loads); a
-// fixed xor butterfly folds the row's partial sums; x[i] is stored write-through (sc1), drained,
-// and ready[i] raised.  Waves are dispatched in dependency-level order and wait only on rows of
-// earlier levels, so every awaited row belongs to a wave already resident or finished: no
-// deadlock.  The partial
-// sums are folded in a tree, not in CSR order (the reference's sequential sum): results agree to
-// rounding.  BackwardSolveMultiple's zero-diagonal rule (x = 0) is kept; a forward row takes
-// the diagonal as stored.
-template <int L, bool FWD>
-__global__ __launch_bounds__(kBlock) void k_trsv(const int *__restrict__ ro, const int *__restrict__ ci,
-                                                 const double *__restrict__ va, int n,
-                                                 const int *__restrict__ order, const double *b, double *x,
-                                                 int *ready, CgControl *ctrl)
-{
-    constexpr int NZ = 64 / L;
-    const int w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    if (w >= n || ctrl->done)  // done is set only by earlier launches: uniform here
-        return;
-    const int i = order[w];  // rows in (level, row) order: awaited rows belong to earlier waves
-    const int lane = threadIdx.x & 63;
-    const int v = lane % L, q = lane / L;
-    const int k1 = ro[i + 1];
-    double sum = 0.0, diag = 0.0;
-    bool ok = true;
-    for (int k0 = ro[i]; k0 < k1; k0 += NZ) {
-        const int k = k0 + q;
-        if (k < k1) {
-            const int j = ci[k];
-            const double a = va[k];
-            if (j == i) {
-                diag = a;
-            } else {
-                ok = wait_flag(&ready[j]) && ok;
-                sum += a * load_sc1(&x[(size_t)j * L + v]);
-            }
-        }
-    }
-#pragma unroll
-    for (int off = L; off < 64; off <<= 1) {
-        sum += __shfl_xor(sum, off);
-        diag += __shfl_xor(diag, off);
-    }
-    if (q == 0) {
-        const double bi = b[(size_t)i * L + v];
-        const double xi = (!FWD && diag == 0.0) ? 0.0 : (bi - sum) / diag;
-        store_sc1(&x[(size_t)i * L + v], xi);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-        __hip_atomic_store(&ready[i], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (!ok) {  // a dependency never became ready: reported (MSPMV_ERR_STALL), never hung;
-            ctrl->breakdown = 2;  // later waves and launches see done and return at once
-            __hip_atomic_store(&ctrl->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-}
-
-// The same solve with data-tagged values instead of flags: the output starts filled with a NaN
-// pattern no arithmetic produces (kTrsvPending, written by one 32-bit fill), a row's x values are
-// stored by single 8-B write-through stores, and a consumer lane polls the very value it needs
-// until the pattern is gone -- one memory round trip per dependency hop instead of flag, drain
-// and payload.  Bounded like wait_flag (a stall is reported, never hung).
+// x = T^-1 b for a triangular CSR T, one wave per row: ForwardSolveMultiple (FWD, T = L lower, rows
+// ascending) and BackwardSolveMultiple (T = L^T upper, rows descending),
+// incomplete_cholesky_decomp.hpp:231-348.  Waves are dispatched in dependency-level order and wait
+// only on rows of earlier levels, so every awaited row belongs to a wave already resident or
+// finished: no deadlock.  Data-tagged values: the output starts filled with a NaN pattern no
+// arithmetic produces (kTrsvPending, written by one 32-bit fill), a row's x values are stored by
+// single 8-B write-through stores, and a consumer lane polls the very value it needs until the
+// pattern is gone -- one memory round trip per dependency hop (ready flags: poll, load, store, drain,
+// raise -- measured 9.8 vs 6.35 ms per iteration, round 1).  Bounded: after ~2^20 polls the solve
+// reports a stall instead of hanging the GPU.  The partial sums are folded in a tree, not in CSR
+// order (the reference's sequential sum): results agree to rounding.
 constexpr unsigned kTrsvPendingWord = 0x7ff4deadu;
 constexpr unsigned long long kTrsvPending = 0x7ff4dead7ff4deadull;
 
@@ -3653,122 +3122,52 @@ __global__ void k_flush_read(const double *p, long long n, double *sink)
 // host launchers
 // ------------------------------------------------------------------------------------------
 
-// SpMV tuning: items per thread (tile = 256 * ipt merge items) and nontemporal matrix loads.
-// Defaults are the measured best; MSPMV_SPMV_IPT / MSPMV_SPMV_NT override them for A/B runs.
-struct SpmvTuning {
-    int ipt = 8;
-    int nt = -1;      // nontemporal matrix loads: -1 auto (matrix > kNtBytes), 0 never, 1 always
-    int spmm_iptg = 0;  // merge items per lane group of the SpMM tiles (8, 16, 32; 0: per L)
-    int persist = 0;  // persistent software-pipelined kernel (VGPR-bound at 4 waves/SIMD: slower)
-    int bpc = 0;      // resident workgroups per CU for the persistent grid (0: occupancy query)
-    int rg_cost = 48; // k_tile_modes budget for row-group tiles (0: merge walk everywhere)
-    int spmm_rg_cost = -1;  // the same for the multi-RHS kernels (-1: scaled to the SpMM tile)
-    int cols16 = 1;   // single-RHS plans carry 16-bit column offsets where a tile's span allows
-    int tb = 256;     // threads per single-RHS SpMV tile: 256 (workgroup tiles) or 64 (one-wave tiles)
-    int tile_items = 0;  // single-RHS nominal merge items per tile (0: tb * ipt; smaller: fewer per thread)
-    int trsv_tagged = 1;  // IC(0) solves: data-tagged values (1) or ready flags (0)
-    int blocks = 1;   // single-RHS tiles staged by node blocks where rows share columns (k_build_blocks)
-    int blkreg = 1;   // plans of register node-block tiles only run the LDS-free k_spmv_blk
-    int runs = 0;     // ... or, for the plain SpMV, the persistent wave-pipelined k_spmv_runs
-    int spmm_blk = 1; // SpMM (L >= 2) on such a plan runs k_spmm_blk instead of its own L-wide tiles
-    int early_re = 1; // single-RHS tile kernel: row ends issued with the stream (TileArgs::early_re); with
-                      // the pair staging it measured 1-2 % faster (nlpkkt120 size, cant, pipelined CG: r03ah/r03ai)
-    int dict = 1;     // single-RHS SpMV through per-tile column dictionaries (k_build_dict) when
-                      // a tile's nonzeros repeat its distinct columns >= dict_ratio times (0: off)
+// Tuning.  The shipped values are the measured best; variants measured and not kept are listed in
+// DESIGN.md with their session tags.  Two switches stay, each with a GPU parity test of both
+// settings: MSPMV_SPMV_BLOCKS=0 (no node blocks in single-RHS plans; test_gpu_blocks.py) and
+// MSPMV_SPMM_BLK=0 (multi-RHS products on their own L-wide tiles instead of the node-block SpMM;
+// test_gpu_blocks.py, test_gpu_dist.py).  Read once per process.
+constexpr int kSpmvIpt = 8;     // merge items per thread of the single-RHS tiles (tile = 256 x 8)
+constexpr int kSpmvRgCost = 48; // k_tile_modes budget for single-RHS row-group tiles
+struct Switches {
+    bool blocks = true;
+    bool spmm_blk = true;
 };
-static const SpmvTuning &spmv_tuning()
+static const Switches &switches()
 {
-    static SpmvTuning t = [] {
-        SpmvTuning v;
-        if (const char *e = getenv("MSPMV_SPMV_IPT")) {
-            const int i = atoi(e);
-            if (i == 2 || i == 4 || i == 6 || i == 7 || i == 8 || i == 16)
-                v.ipt = i;
-        }
-        if (const char *e = getenv("MSPMV_SPMV_NT"))
-            v.nt = atoi(e) < 0 ? -1 : atoi(e) != 0;
-        if (const char *e = getenv("MSPMV_SPMM_IPTG")) {
-            const int i = atoi(e);
-            if (i == 8 || i == 16 || i == 32)
-                v.spmm_iptg = i;
-        }
-        if (const char *e = getenv("MSPMV_SPMV_PERSIST"))
-            v.persist = atoi(e) != 0;
-        if (const char *e = getenv("MSPMV_SPMV_BPC"))
-            v.bpc = atoi(e);
-        if (const char *e = getenv("MSPMV_SPMV_RG_COST"))
-            v.rg_cost = atoi(e);
-        if (const char *e = getenv("MSPMV_SPMM_RG_COST"))
-            v.spmm_rg_cost = atoi(e);
-        if (const char *e = getenv("MSPMV_SPMV_C16"))
-            v.cols16 = atoi(e) != 0;
+    static const Switches w = [] {
+        Switches v;
         if (const char *e = getenv("MSPMV_SPMV_BLOCKS"))
             v.blocks = atoi(e) != 0;
-        if (const char *e = getenv("MSPMV_SPMV_BLKREG"))
-            v.blkreg = atoi(e) != 0;
-        if (const char *e = getenv("MSPMV_SPMV_RUNS"))
-            v.runs = atoi(e) != 0;
         if (const char *e = getenv("MSPMV_SPMM_BLK"))
             v.spmm_blk = atoi(e) != 0;
-        if (const char *e = getenv("MSPMV_SPMV_EARLY_RE"))
-            v.early_re = atoi(e);
-        if (const char *e = getenv("MSPMV_SPMV_DICT"))
-            v.dict = atoi(e) > 0 ? atoi(e) : 0;
-        if (const char *e = getenv("MSPMV_TRSV_TAGGED"))
-            v.trsv_tagged = atoi(e) != 0;
-        if (const char *e = getenv("MSPMV_SPMV_TILE"))
-            v.tile_items = atoi(e);
-        if (const char *e = getenv("MSPMV_SPMV_TB"))
-            v.tb = atoi(e) == 64 ? 64 : 256;
         return v;
     }();
-    return t;
+    return w;
 }
 
 // Nontemporal policy for the matrix stream: a matrix larger than kNtBytes cannot stay in the
 // 256 MiB Infinity Cache across calls anyway, so its lines are not allowed to evict x / X.
 constexpr double kNtBytes = 128.0 * 1024 * 1024;
-bool stream_nt(const mspmv_handle_s *h)
-{
-    const int nt = spmv_tuning().nt;
-    if (nt >= 0)
-        return nt != 0;
-    return 12.0 * (double)h->nnz + 4.0 * (double)h->m > kNtBytes;
-}
+bool stream_nt(const mspmv_handle_s *h) { return 12.0 * (double)h->nnz + 4.0 * (double)h->m > kNtBytes; }
+
+// The node-block SpMV kernel's run height: the pair form holds KR = 6 rows of values per lane.
+int blk_kr(const TilePlan &p) { return p.blk_rows_max <= 6 ? 6 : 8; }
 
 std::string spmv_kernel_name(const mspmv_handle_s *h)
 {
-    const SpmvTuning &t = spmv_tuning();
+    const std::string nt = stream_nt(h) ? "true" : "false";
     const auto it = h->plans.find(plan_key(1));
-    if (h->spmv_onewave != 1 && it != h->plans.end() && it->second.d_blk &&
-        it->second.num_tiles_reg == it->second.num_tiles && t.blkreg && t.tb == kBlock && !t.persist)
-        return std::string(t.runs ? "k_spmv_runs<" : "k_spmv_blk<0,") + (stream_nt(h) ? "true" : "false") +
-               (t.runs ? ">" : MSPMV_BLK_PAIR && it->second.blk_rows_max <= 6 ? ",6>" : ",8>");
-    const bool one = !t.persist && (t.tb == 64 || h->spmv_onewave == 1);
-    return std::string(t.persist ? "k_spmv_persist<" : "k_spmv_tile<") + std::to_string(t.ipt) + ",0," +
-           (stream_nt(h) ? "true" : "false") + (one ? ",64>" : ">");
+    if (h->spmv_onewave != 1 && it != h->plans.end() && it->second.blk_spmv)
+        return "k_spmv_blk<0," + nt + "," + std::to_string(blk_kr(it->second)) + ">";
+    return "k_spmv_tile<" + std::to_string(kSpmvIpt) + ",0," + nt + (h->spmv_onewave == 1 ? ",64>" : ">");
 }
 
-int spmv_items_per_thread() { return spmv_tuning().ipt; }
-int spmv_tile_lanes() { return spmv_tuning().tb; }
-
-int spmv_onewave_mode()
-{
-    static const int m = [] {
-        const char *e = getenv("MSPMV_SPMV_ONEWAVE");
-        return e ? (atoi(e) < 0 ? -1 : atoi(e) != 0) : -1;
-    }();
-    return spmv_tuning().tb == 64 || spmv_tuning().persist ? 0 : m;
-}
-
+int spmv_items_per_thread() { return kSpmvIpt; }
 
 // SpMM tile depth: measured best 8 items per lane group for L <= 4 (fem-blocked pwtk shape,
 // L = 4: 55.6 vs 74.8 us at 16) and 16 for L >= 8 (nlpkkt120 shape, L = 8: 549 vs 741 us).
-int spmm_iptg_for(int L)
-{
-    const int i = spmv_tuning().spmm_iptg;
-    return i ? i : (L >= 8 ? 16 : 8);
-}
+int spmm_iptg_for(int L) { return L >= 8 ? 16 : 8; }
 
 // The kernel a plain SpMM of native width L (1, 2, 4, 8, 16) launches on `plan` (get_plan's
 // choice for L), spelled as rocprofv3 lists it: launch_spmm_L's dispatch, restated.
@@ -3777,11 +3176,10 @@ std::string spmm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan, int 
     if (L == 1)
         return spmv_kernel_name(h);
     const std::string nt = stream_nt(h) ? "true" : "false";
-    const SpmvTuning &t = spmv_tuning();
-    if (plan.d_blk && plan.num_tiles_reg == plan.num_tiles && t.blkreg && t.tb == kBlock && spmm_blk_enabled())
-        return "k_spmm_blk<" + std::to_string(L) + ",0," + nt + (plan.blk_rows_max <= 6 ? ",6>" : ",8>");
+    if (plan.d_blk && plan.num_tiles_reg == plan.num_tiles && spmm_blk_enabled())
+        return "k_spmm_blk<" + std::to_string(L) + ",0," + nt + "," + std::to_string(blk_kr(plan)) + ">";
     const int iptg = spmm_iptg_for(L);
-    const bool dict = L == 16 && iptg != 32 && plan.d_dict;
+    const bool dict = L == 16 && plan.d_dict;
     return "k_spmm_tile<" + std::to_string(L) + "," + std::to_string(iptg) + ",0," + nt + (dict ? ",true>" : ">");
 }
 
@@ -3800,50 +3198,33 @@ static int gfx950_blocks_per_cu(const void *fn)
     return std::max(0, std::min(by_waves, by_lds));
 }
 
-// Slots of the striped single-RHS tile kernels at IPT items per thread: the SpMV and the pipelined
-// CG (its form without node blocks; FEM plans run the node-block kernels, whose tile counts are
-// not near a generation boundary), from the kernels' own LDS / VGPR use (MSPMV_DEBUG_SLOTS prints
-// the runtime's occupancy query beside it; the query is the fallback without attributes).
-template <int I>
-static int tile_slots_per_cu()
-{
-    const void *ks = (const void *)k_spmv_tile<I, kModeSpmv, false>;
-    const void *kc = (const void *)k_spmv_tile<I, kModeCg, false, kBlock, false>;
-    int a = 0, b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_spmv_tile<I, kModeSpmv, false>, kBlock, 0) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_spmv_tile<I, kModeCg, false, kBlock, false>, kBlock, 0) !=
-            hipSuccess)
-        a = b = 0;
-    const int c = std::min(gfx950_blocks_per_cu(ks), gfx950_blocks_per_cu(kc));
-    if (getenv("MSPMV_DEBUG_SLOTS"))
-        fprintf(stderr, "mspmv: tile slots per CU (IPT %d): occupancy query %d/%d, from attributes %d\n", I, a, b, c);
-    return c > 0 ? c : std::min(a, b);
-}
-
+// Slots of the striped single-RHS tile kernels: the SpMV and the pipelined CG (its form without node
+// blocks; FEM plans run the node-block kernels, whose tile counts are not near a generation
+// boundary), from the kernels' own LDS / VGPR use (the runtime's occupancy query is the fallback
+// without attributes).
 int spmv_tile_blocks_per_cu()
 {
     static const int occ = [] {
-        const SpmvTuning &t = spmv_tuning();
-        if (const char *e = getenv("MSPMV_TILE_SLOTS_PER_CU"))  // lab knob: 0 disables the stretch
-            return std::max(0, atoi(e));
-        if (t.tb != kBlock || t.tile_items || t.persist)
+        const void *ks = (const void *)k_spmv_tile<kSpmvIpt, kModeSpmv, false>;
+        const void *kc = (const void *)k_spmv_tile<kSpmvIpt, kModeCg, false, kBlock, false>;
+        const int c = std::min(gfx950_blocks_per_cu(ks), gfx950_blocks_per_cu(kc));
+        if (c > 0)
+            return c;
+        int a = 0, b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_spmv_tile<kSpmvIpt, kModeSpmv, false>, kBlock, 0) !=
+                hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_spmv_tile<kSpmvIpt, kModeCg, false, kBlock, false>,
+                                                         kBlock, 0) != hipSuccess)
             return 0;
-        switch (t.ipt) {
-        case 4: return tile_slots_per_cu<4>();
-        case 8: return tile_slots_per_cu<8>();
-        default: return 0;
-        }
+        return std::min(a, b);
     }();
     return occ;
 }
 
 int tile_items_for(int L)
 {
-    if (L == 1) {
-        const int full = spmv_tuning().tb * spmv_tuning().ipt;
-        const int want = spmv_tuning().tile_items;  // 0: full tiles
-        return want > 0 ? std::max(64, std::min(want, full)) : full;
-    }
+    if (L == 1)
+        return kBlock * kSpmvIpt;
     return (kBlock / (L / 2)) * spmm_iptg_for(L);
 }
 
@@ -3865,10 +3246,8 @@ hipError_t launch_pack_cols16(const int *d_cols, const int2 *d_bounds, int num_t
     return hipGetLastError();
 }
 
-bool spmv_cols16_enabled() { return spmv_tuning().cols16 != 0; }
-bool spmv_dict_enabled() { return spmv_tuning().dict > 0; }
-bool spmv_blocks_enabled() { return spmv_tuning().blocks != 0; }
-bool spmm_blk_enabled() { return spmv_tuning().spmm_blk != 0 && spmv_tuning().blkreg != 0 && spmv_tuning().tb == kBlock; }
+bool spmv_blocks_enabled() { return switches().blocks; }
+bool spmm_blk_enabled() { return switches().spmm_blk; }
 
 hipError_t launch_build_blocks(const int *d_row_offsets, const int *d_cols, const int2 *d_bounds,
                                const unsigned char *d_split, const int *d_colbase, int num_tiles, uint4 *d_blk,
@@ -3882,60 +3261,12 @@ hipError_t launch_build_blocks(const int *d_row_offsets, const int *d_cols, cons
     return hipGetLastError();
 }
 
-// Plan time: do the run patterns of every node-block tile come in pairs of consecutive columns
-// (P[2j + 1] == P[2j] + 1)?  FEM nodes with an even number of unknowns do (pwtk: 6 per node).
-// One thread per tile (descriptors packed at `stride`); *ok is cleared by any pair that is not.
-__global__ void k_blk_pairs_check(const int *__restrict__ cols, const int2 *__restrict__ bounds,
-                                  const uint4 *__restrict__ blk, int stride, int num_tiles, int *ok)
-{
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= num_tiles)
-        return;
-    const int n0 = bounds[t].y;
-    const int nd = (int)((blk[(size_t)t * stride].y >> 8) & 255u);
-    bool good = true;
-    for (int di = 0; di < nd && good; ++di) {
-        const uint4 d = blk[(size_t)t * stride + di];
-        const int vofs = d.x & 0xffff, wc = d.x >> 24, h = d.y & 15, p = (d.y >> 4) & 7;
-        int start = 0, pstart = 0;
-        for (int i = 0; i < h; ++i) {
-            if (i == p)
-                pstart = start;
-            start += blk_len(d, i);
-        }
-        const int *c = cols + n0 + vofs + pstart;
-        for (int j = 0; 2 * j + 1 < wc && good; ++j)
-            good = c[2 * j + 1] == c[2 * j] + 1;
-    }
-    if (!good)
-        atomicAnd(ok, 0);
-}
-
-hipError_t launch_blk_pairs_check(const int *d_cols, const int2 *d_bounds, const uint4 *d_blk, int stride,
-                                  int num_tiles, int *d_ok, hipStream_t s)
-{
-    if (num_tiles <= 0)
-        return hipSuccess;
-    hipLaunchKernelGGL(k_blk_pairs_check, dim3((num_tiles + 255) / 256), dim3(256), 0, s, d_cols, d_bounds, d_blk,
-                       stride, num_tiles, d_ok);
-    return hipGetLastError();
-}
-
-bool spmm_dict_enabled()
-{
-    static const bool on = [] {
-        const char *e = getenv("MSPMV_SPMM_DICT");
-        return e ? atoi(e) != 0 : true;
-    }();
-    return on;
-}
-
 // multi: the L = 16 plan (dictionaries of at most spmm_dict_max(16) entries: what its kernel
 // parks in LDS; the kernel checks the limit again)
 hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_tiles, int max_items, int *d_dict,
                              int *d_ndict, unsigned short *d_idx16, hipStream_t s, bool multi)
 {
-    const int ratio = multi ? -1 : spmv_tuning().dict;
+    const int ratio = multi ? -1 : 1;
     const int dmax = multi ? spmm_dict_max(16) : 1 << 30;
     if (max_items <= 4096)
         hipLaunchKernelGGL(k_build_dict<4096>, dim3(num_tiles), dim3(kBlock), 0, s, d_cols, d_bounds, d_dict, d_ndict,
@@ -3962,20 +3293,11 @@ hipError_t launch_tile_modes(const int *d_row_offsets, const int2 *d_bounds, con
 {
     if (num_tiles == 0)
         return hipSuccess;
-    const SpmvTuning &tu = spmv_tuning();
     // SpMM budget: twice the walk's gather chunks (4 steps each) plus its search
-    const int cost = L == 1 ? tu.rg_cost : tu.spmm_rg_cost >= 0 ? tu.spmm_rg_cost : 2 * (4 * (spmm_iptg_for(L) / 4) + 2);
+    const int cost = L == 1 ? kSpmvRgCost : 2 * (4 * (spmm_iptg_for(L) / 4) + 2);
     const int lanes = L == 1 ? lanes_in : kBlock;  // threads sharing one tile
-    static const int force_lg = [] {
-        const char *e = getenv("MSPMV_SPMM_LG");
-        return e ? atoi(e) : -1;
-    }();
-    static const int force_lg1 = [] {  // the same lab knob for the single-RHS tiles
-        const char *e = getenv("MSPMV_SPMV_LG");
-        return e ? atoi(e) : -1;
-    }();
     hipLaunchKernelGGL(k_tile_modes, dim3((num_tiles + 255) / 256), dim3(256), 0, s, d_row_offsets, d_bounds, d_split,
-                       num_tiles, L == 1 ? 1 : L / 2, cost, lanes, d_modes, L == 1 ? force_lg1 : force_lg);
+                       num_tiles, L == 1 ? 1 : L / 2, cost, lanes, d_modes);
     return hipGetLastError();
 }
 
@@ -4000,70 +3322,19 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
         a.blk = plan.d_blk;
         a.blk_stride = plan.blk_stride;
         // L > 1 runs the node-block plan only while k_spmm_blk is enabled (get_plan's gate): L = 2
-        // shares the single-RHS tile size, so without this the knob-off plan would still be all-reg
-        a.all_reg = plan.d_blk && plan.num_tiles_reg == plan.num_tiles && spmv_tuning().blkreg &&
-                    spmv_tuning().tb == kBlock && (L == 1 || spmm_blk_enabled());
+        // shares the single-RHS tile size, so without this the switched-off plan would still be all-reg
+        a.all_reg = plan.d_blk && plan.num_tiles_reg == plan.num_tiles && (L == 1 || spmm_blk_enabled());
+        a.blk_spmv = L == 1 && plan.blk_spmv;
         a.blk_rows_max = plan.blk_rows_max;
     }
     a.dict = plan.d_dict;
     a.ndict = plan.d_ndict;
     a.idx16 = plan.d_idx16;
     a.ld = L;
-    a.early_re = L == 1 ? spmv_tuning().early_re : 0;
-    static const int tstreams = [] {  // lab knob: MSPMV_TILE_STREAMS=K (xcd_tile)
-        const char *e = getenv("MSPMV_TILE_STREAMS");
-        return e ? std::max(1, atoi(e)) : 1;
-    }();
-    a.tstreams = tstreams;
+    a.early_re = L == 1 ? 1 : 0;
     a.tb = L == 1 ? plan.lanes : kBlock;
-    a.blk_pairs = L == 1 && plan.blk_pairs && h->n >= 2;
     a.n = h->n;
     return a;
-}
-
-// Persistent grid for the single-RHS kernel: min(tiles, CUs x resident workgroups), each
-// workgroup taking an equal contiguous run of tiles.
-template <typename K>
-static void persist_grid(K kernel, int num_tiles, int num_cus, int bpc, int *grid, int *tpb)
-{
-    if (bpc <= 0) {
-        int occ = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, kBlock, 0) != hipSuccess || occ < 1)
-            occ = 1;
-        bpc = occ;
-    }
-    const long long slots = (long long)std::max(num_cus, 1) * bpc;
-    int t = (int)((num_tiles + slots - 1) / slots);
-    t = std::min(std::max(t, 1), kMaxTpb);  // the kernel stages <= kMaxTpb + 1 bounds in LDS
-    *tpb = t;
-    *grid = (num_tiles + t - 1) / t;
-}
-
-template <int I, int MODE, bool NTV>
-static void launch_spmv_persist(const TileArgs &a, hipStream_t s, int num_cus, int bpc)
-{
-    if constexpr (MODE != kModeCg) {
-        int g = 0, tpb = 0;
-        persist_grid(k_spmv_persist<I, MODE, NTV>, a.num_tiles, num_cus, bpc, &g, &tpb);
-        hipLaunchKernelGGL((k_spmv_persist<I, MODE, NTV>), dim3(g), dim3(kBlock), 0, s, a, tpb);
-    }
-}
-
-// k_spmv_runs grid: as many workgroups as are resident at once, fewer when that evens out the
-// tiles per workgroup, a multiple of 8 (each workgroup's tiles then stay on its XCD).
-template <bool NTV>
-static void launch_spmv_runs(const TileArgs &a, hipStream_t s, int num_cus)
-{
-    static int occ = 0;
-    if (occ < 1 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_spmv_runs<NTV>, kBlock, 0) != hipSuccess ||
-                    occ < 1))
-        occ = 1;
-    const long long slots = (long long)std::max(num_cus, 1) * occ;
-    const long long per = std::min<long long>((a.num_tiles + slots - 1) / slots, kRunsMaxTiles);
-    long long g = (a.num_tiles + per - 1) / per;
-    if (g > 8)
-        g = (g + 7) & ~7LL;  // up: a workgroup never gets more than kRunsMaxTiles tiles
-    hipLaunchKernelGGL((k_spmv_runs<NTV>), dim3((unsigned)g), dim3(kBlock), 0, s, a);
 }
 
 template <int LL, int I, int MODE>
@@ -4071,19 +3342,19 @@ static void launch_spmm_nt(const TileArgs &a, hipStream_t s, bool nt)
 {
     if constexpr (MODE != kModeCg) {
         const dim3 grid(a.num_tiles), block(kBlock);
-        if constexpr (LL == 16 && I != 32) {  // plans with column dictionaries (L = 16 only, below)
+        if constexpr (LL == 16) {  // plans with column dictionaries (L = 16 only)
             if (a.dict) {
                 if (nt)
-                    hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, true, true>), grid, block, 0, s, a);
+                    ggl(k_spmm_tile<LL, I, MODE, true, true>, grid, block, s, a);
                 else
-                    hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, false, true>), grid, block, 0, s, a);
+                    ggl(k_spmm_tile<LL, I, MODE, false, true>, grid, block, s, a);
                 return;
             }
         }
         if (nt)
-            hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, true>), grid, block, 0, s, a);
+            ggl(k_spmm_tile<LL, I, MODE, true>, grid, block, s, a);
         else
-            hipLaunchKernelGGL((k_spmm_tile<LL, I, MODE, false>), grid, block, 0, s, a);
+            ggl(k_spmm_tile<LL, I, MODE, false>, grid, block, s, a);
     }
 }
 
@@ -4092,99 +3363,61 @@ static void launch_spmm_L(const TileArgs &a, hipStream_t s, bool nt)
 {
     if constexpr (MODE != kModeCg) {
         if (a.all_reg) {  // a node-block plan (single-RHS tiles): every tile a register run tile
-#ifndef MSPMV_SPMM_BLK_KR6
-#define MSPMV_SPMM_BLK_KR6 1  // lab builds: 0 runs the 8-row kernel on every plan
-#endif
-            if (MSPMV_SPMM_BLK_KR6 && a.blk_rows_max <= 6) {
+            const dim3 grid(a.num_tiles), block(kBlock);
+            if (a.blk_rows_max <= 6) {
                 if (nt)
-                    hipLaunchKernelGGL((k_spmm_blk<LL, MODE, true, 6>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
+                    ggl(k_spmm_blk<LL, MODE, true, 6>, grid, block, s, a);
                 else
-                    hipLaunchKernelGGL((k_spmm_blk<LL, MODE, false, 6>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
+                    ggl(k_spmm_blk<LL, MODE, false, 6>, grid, block, s, a);
             } else if (nt) {
-                hipLaunchKernelGGL((k_spmm_blk<LL, MODE, true>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
+                ggl(k_spmm_blk<LL, MODE, true>, grid, block, s, a);
             } else {
-                hipLaunchKernelGGL((k_spmm_blk<LL, MODE, false>), dim3(a.num_tiles), dim3(kBlock), 0, s, a);
+                ggl(k_spmm_blk<LL, MODE, false>, grid, block, s, a);
             }
             return;
         }
     }
-    const int iptg = spmm_iptg_for(LL);
-    if (iptg == 32)
-        launch_spmm_nt<LL, 32, MODE>(a, s, nt);
-    else if (iptg == 16)
-        launch_spmm_nt<LL, 16, MODE>(a, s, nt);
-    else
-        launch_spmm_nt<LL, 8, MODE>(a, s, nt);
+    launch_spmm_nt<LL, (LL >= 8 ? 16 : 8), MODE>(a, s, nt);
 }
 
 // MODE 1 (pipelined single-RHS CG) exists for L == 1 in the one-tile kernel only.
 template <int MODE>
-static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, int num_cus, bool nt)
+static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, bool nt)
 {
     const dim3 grid(a.num_tiles), block(kBlock);
-    const SpmvTuning &tu = spmv_tuning();
     if (MODE == kModeCg && L != 1)
         return hipErrorInvalidValue;
     switch (L) {
-    case 1: {
-        // every tile a register node-block tile: the LDS-free kernel (SpMV and dot mode; the CG
-        // form's consumer-side partial sums take it to 86 VGPRs, 5 waves/SIMD, so the pipelined
-        // CG keeps k_spmv_tile, whose blk_rows path does the same per-tile work)
-        if (a.all_reg && !tu.persist && MODE == kModeSpmv && tu.runs) {
+    case 1:
+        if (MODE == kModeSpmv && a.blk_spmv) {
+            // a node-block plan (every tile, or most: the rest run the kernel's register fallback):
+            // the LDS-free kernel, column pairs, runs of <= 6 rows
             if (nt)
-                launch_spmv_runs<true>(a, s, num_cus);
+                ggl(k_spmv_blk<kModeSpmv, true, 6>, grid, block, s, a);
             else
-                launch_spmv_runs<false>(a, s, num_cus);
-            break;
-        }
-        if (MSPMV_BLK_PAIR && MODE == kModeSpmv && a.all_reg && !tu.persist && a.blk_rows_max <= 6) {
-            if (nt)  // runs of <= 6 rows (6-DOF FEM): the pair form's value arrays sized to them
-                hipLaunchKernelGGL((k_spmv_blk<kModeSpmv, true, 6>), grid, block, 0, s, a);
-            else
-                hipLaunchKernelGGL((k_spmv_blk<kModeSpmv, false, 6>), grid, block, 0, s, a);
-            break;
-        }
-        if (a.all_reg && !tu.persist && MODE != kModeCg) {
+                ggl(k_spmv_blk<kModeSpmv, false, 6>, grid, block, s, a);
+        } else if (MODE == kModeDot && a.all_reg) {
+            // every tile a register node-block tile, dot mode (the row-sharded CG): column owners
             if (nt)
-                hipLaunchKernelGGL((k_spmv_blk<MODE == kModeCg ? kModeSpmv : MODE, true>), grid, block, 0, s, a);
+                ggl(k_spmv_blk<kModeDot, true>, grid, block, s, a);
             else
-                hipLaunchKernelGGL((k_spmv_blk<MODE == kModeCg ? kModeSpmv : MODE, false>), grid, block, 0, s, a);
-            break;
+                ggl(k_spmv_blk<kModeDot, false>, grid, block, s, a);
+        } else if (MODE == kModeSpmv && a.tb == 64) {  // one-wave tiles (skewed rows, spmv_plan)
+            if (nt)
+                ggl(k_spmv_tile<kSpmvIpt, kModeSpmv, true, 64>, grid, dim3(64), s, a);
+            else
+                ggl(k_spmv_tile<kSpmvIpt, kModeSpmv, false, 64>, grid, dim3(64), s, a);
+        } else if (MODE == kModeCg && !a.blk) {  // the pipelined CG without node blocks: fewer VGPRs
+            if (nt)
+                ggl(k_spmv_tile<kSpmvIpt, MODE, true, kBlock, false>, grid, block, s, a);
+            else
+                ggl(k_spmv_tile<kSpmvIpt, MODE, false, kBlock, false>, grid, block, s, a);
+        } else if (nt) {
+            ggl(k_spmv_tile<kSpmvIpt, MODE, true>, grid, block, s, a);
+        } else {
+            ggl(k_spmv_tile<kSpmvIpt, MODE, false>, grid, block, s, a);
         }
-#define MSPMV_SPMV_CASE(I)                                                                          \
-    case I:                                                                                        \
-        if (tu.persist && MODE != kModeCg) {                                                       \
-            if (nt)                                                                                \
-                launch_spmv_persist<I, MODE, true>(a, s, num_cus, tu.bpc);                         \
-            else                                                                                   \
-                launch_spmv_persist<I, MODE, false>(a, s, num_cus, tu.bpc);                        \
-        } else if (MODE == kModeSpmv && a.tb == 64) {                                              \
-            if (nt)                                                                                \
-                hipLaunchKernelGGL((k_spmv_tile<I, kModeSpmv, true, 64>), grid, dim3(64), 0, s, a);   \
-            else                                                                                   \
-                hipLaunchKernelGGL((k_spmv_tile<I, kModeSpmv, false, 64>), grid, dim3(64), 0, s, a);  \
-        } else if (MODE == kModeCg && !a.blk) {                                                    \
-            if (nt)                                                                                \
-                hipLaunchKernelGGL((k_spmv_tile<I, MODE, true, kBlock, false>), grid, block, 0, s, a); \
-            else                                                                                   \
-                hipLaunchKernelGGL((k_spmv_tile<I, MODE, false, kBlock, false>), grid, block, 0, s, a); \
-        } else if (nt)                                                                             \
-            hipLaunchKernelGGL((k_spmv_tile<I, MODE, true>), grid, block, 0, s, a);                   \
-        else                                                                                       \
-            hipLaunchKernelGGL((k_spmv_tile<I, MODE, false>), grid, block, 0, s, a);                  \
         break;
-        switch (tu.ipt) {
-            MSPMV_SPMV_CASE(2)
-            MSPMV_SPMV_CASE(4)
-            MSPMV_SPMV_CASE(6)
-            MSPMV_SPMV_CASE(7)
-            MSPMV_SPMV_CASE(8)
-            MSPMV_SPMV_CASE(16)
-        default: return hipErrorInvalidValue;
-        }
-#undef MSPMV_SPMV_CASE
-        break;
-    }
     case 2: launch_spmm_L<2, MODE>(a, s, nt); break;
     case 4: launch_spmm_L<4, MODE>(a, s, nt); break;
     case 8: launch_spmm_L<8, MODE>(a, s, nt); break;
@@ -4202,7 +3435,7 @@ hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const 
     TileArgs a = make_args(h, plan, d_X, d_Y, L);
     if (ld > 0)
         a.ld = ld;
-    return launch_tile<kModeSpmv>(a, L, h->stream, h->num_cus, stream_nt(h));
+    return launch_tile<kModeSpmv>(a, L, h->stream, stream_nt(h));
 }
 
 hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L, int ld)
@@ -4454,14 +3687,9 @@ __global__ __launch_bounds__(kBlock) void k_cg1_xflush(Cg1Args a)
 
 int cg1_blocks(long long m)
 {
-    static const int cap = [] {  // lab knob: fewer update blocks (fewer r.r partials for every SpMV
-                                 // workgroup to load and sum, fewer p.Ap partial loads per block)
-        const char *e = getenv("MSPMV_CG1_BLOCKS");
-        const int v = e ? atoi(e) : 0;
-        return v > 0 && v <= kUpdateMaxBlocks ? v : kUpdateMaxBlocks;
-    }();
-    const long long b = (m + kBlock - 1) / kBlock;  // one element per thread up to the cap
-    return (int)std::max<long long>(1, std::min<long long>(b, cap));
+    // one element per thread up to kUpdateMaxBlocks (512 / 256 update blocks measured no faster, r02u)
+    const long long b = (m + kBlock - 1) / kBlock;
+    return (int)std::max<long long>(1, std::min<long long>(b, kUpdateMaxBlocks));
 }
 
 static Cg1Args cg1_args(mspmv_handle_s *h, double *d_x)
@@ -4563,7 +3791,7 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
         // streaming pass over p and Ap with the fold's breakdown checks (k_pcg_dot mode 2)
         TileArgs ta = make_args(h, plan, h->d_p0, h->d_ap, L);
         ta.ctrl = h->d_ctrl;
-        if ((e = launch_tile<kModeSpmv>(ta, L, h->stream, h->num_cus, stream_nt(h))) != hipSuccess)
+        if ((e = launch_tile<kModeSpmv>(ta, L, h->stream, stream_nt(h))) != hipSuccess)
             return e;
         if ((e = launch_fixup_ctrl(h, plan, h->d_ap, L)) != hipSuccess)
             return e;
@@ -4632,7 +3860,7 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *
     ta.tol = tol;
     ta.hist = h->d_hist;
     ta.hist_cap = h->hist_cap;
-    hipError_t e = launch_tile<kModeCg>(ta, 1, h->stream, h->num_cus, stream_nt(h));
+    hipError_t e = launch_tile<kModeCg>(ta, 1, h->stream, stream_nt(h));
     if (e != hipSuccess)
         return e;
     if ((e = launch_fixup_ctrl(h, plan, h->d_ap, 1)) != hipSuccess)
@@ -4701,7 +3929,7 @@ hipError_t launch_spmm_dot_tiles(mspmv_handle_s *h, const TilePlan &plan, const 
     ta.xr = d_X + row_off * L;  // the handle's rows start at row row_off of X
     ta.ctrl = ctrl;
     ta.partials = partials;
-    hipError_t e = launch_tile<kModeDot>(ta, L, s, h->num_cus, stream_nt(h));
+    hipError_t e = launch_tile<kModeDot>(ta, L, s, stream_nt(h));
     if (e != hipSuccess)
         return e;
     if (plan.num_carries) {
@@ -4749,14 +3977,12 @@ hipError_t launch_spmm_dot(mspmv_handle_s *h, const TilePlan &plan, const double
     return launch_fold_dot(plan.num_tiles, L, partials, gtickets, dot_out, scal, conv, ctrl, fold_mode, h->stream);
 }
 
+// Cold-cache flush between timed launches: a read sweep (caches left holding clean unrelated lines;
+// a write sweep left them dirty and the timed kernel paid the write-back: cant 35.1 vs 19.2 us, r02n).
 hipError_t launch_flush(void *p, size_t bytes, hipStream_t s, bool fresh)
 {
-    static const bool write_mode = [] {
-        const char *e = getenv("MSPMV_FLUSH");
-        return e && std::string(e) == "write";
-    }();
     const long long n = (long long)(bytes / sizeof(double));
-    if (fresh || write_mode)
+    if (fresh)
         hipLaunchKernelGGL(k_flush, dim3(2048), dim3(256), 0, s, (double *)p, n, 1.0);
     else
         hipLaunchKernelGGL(k_flush_read, dim3(2048), dim3(256), 0, s, (const double *)p, n, (double *)p);
@@ -4861,21 +4087,12 @@ template <int L>
 static void trsv_L(const mspmv_ic0_s *ic, bool fwd, const double *b, double *x, CgControl *ctrl, hipStream_t s)
 {
     const dim3 grid((ic->n + kBlock / 64 - 1) / (kBlock / 64)), block(kBlock);
-    if (spmv_tuning().trsv_tagged) {
-        if (fwd)
-            hipLaunchKernelGGL((k_trsv_tagged<L, true>), grid, block, 0, s, ic->d_lro, ic->d_lci, ic->d_lva, ic->n,
-                               ic->d_fwd_order, b, x, ctrl);
-        else
-            hipLaunchKernelGGL((k_trsv_tagged<L, false>), grid, block, 0, s, ic->d_uro, ic->d_uci, ic->d_uva, ic->n,
-                               ic->d_bwd_order, b, x, ctrl);
-        return;
-    }
     if (fwd)
-        hipLaunchKernelGGL((k_trsv<L, true>), grid, block, 0, s, ic->d_lro, ic->d_lci, ic->d_lva, ic->n,
-                           ic->d_fwd_order, b, x, ic->d_ready, ctrl);
+        hipLaunchKernelGGL((k_trsv_tagged<L, true>), grid, block, 0, s, ic->d_lro, ic->d_lci, ic->d_lva, ic->n,
+                           ic->d_fwd_order, b, x, ctrl);
     else
-        hipLaunchKernelGGL((k_trsv<L, false>), grid, block, 0, s, ic->d_uro, ic->d_uci, ic->d_uva, ic->n,
-                           ic->d_bwd_order, b, x, ic->d_ready, ctrl);
+        hipLaunchKernelGGL((k_trsv_tagged<L, false>), grid, block, 0, s, ic->d_uro, ic->d_uci, ic->d_uva, ic->n,
+                           ic->d_bwd_order, b, x, ctrl);
 }
 
 // Z = L^-T (L^-1 R): ForwardSolveMultiple into ic->d_y, then BackwardSolveMultiple
@@ -4884,14 +4101,12 @@ static hipError_t ic0_apply(mspmv_handle_s *h, mspmv_ic0_s *ic, int L, const dou
 {
     if (ic->n == 0)
         return hipSuccess;
-    const bool tagged = spmv_tuning().trsv_tagged != 0;
     for (int pass = 0; pass < 2; ++pass) {
         const bool fwd = pass == 0;
         const double *in = fwd ? r : ic->d_y;
         double *out = fwd ? ic->d_y : z;
-        hipError_t e = tagged ? hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(out), kTrsvPendingWord,
-                                                  2 * (size_t)ic->n * L, h->stream)
-                              : hipMemsetAsync(ic->d_ready, 0, sizeof(int) * (size_t)ic->n, h->stream);
+        hipError_t e = hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(out), kTrsvPendingWord,
+                                         2 * (size_t)ic->n * L, h->stream);
         if (e != hipSuccess)
             return e;
         switch (L) {
@@ -4963,16 +4178,3 @@ hipError_t launch_pcg_ic0_iteration(mspmv_handle_s *h, mspmv_ic0_s *ic, const Ti
 }
 
 }  // namespace mspmv
-
-#if MSPMV_LAB_ABLATE == 10
-extern "C" __attribute__((visibility("default"))) int mspmv_lab_blk_stamps(unsigned long long *host, int slots)
-{
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mspmv::g_lab_blk), sizeof(unsigned long long) * 8 * slots);
-}
-#endif
-#if MSPMV_LAB_ABLATE == 9
-extern "C" __attribute__((visibility("default"))) int mspmv_lab_stamps(unsigned long long *host, int tiles)
-{
-    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(mspmv::g_lab_stamps), sizeof(unsigned long long) * 6 * tiles);
-}
-#endif

@@ -15,8 +15,11 @@ and every compute call goes through the HIP library.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes
+import itertools
 import os
+import weakref
 from dataclasses import dataclass
 from typing import Optional
 
@@ -85,6 +88,7 @@ _SIGS = {
     "mspmv_dspmm_dev": (_I, [_P, _P, _P, _I]),
     "mspmv_dcg_single": (_I, [_P, _P, _P, _I, _D, _PI, _P, _I]),
     "mspmv_dcg_single_dev": (_I, [_P, _P, _P, _I, _D, _PI, _P, _I]),
+    "mspmv_cg_resident_stamps": (_I, [_P, _P, _P, _I, _D, _PI, _P, _I, _PI]),
     "mspmv_dcg_multi": (_I, [_P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
     "mspmv_dcg_multi_dev": (_I, [_P, _P, _P, _I, _I, _D, _I, _PI, _P, _I]),
     "mspmv_spai_values": (_I, [ctypes.POINTER(_CsrD), _P]),
@@ -158,6 +162,28 @@ def _load():
 
 
 lib = _load()
+
+# Live device objects, released in reverse creation order at interpreter exit (atexit runs before
+# the C runtime's exit handlers, so the HIP runtime -- and a profiler's hooks into it -- are still
+# up when the handles and buffers go).  A plain __del__ at shutdown may run after them or never.
+_LIVE = weakref.WeakValueDictionary()
+_SEQ = itertools.count()
+
+
+def _track(obj):
+    _LIVE[next(_SEQ)] = obj
+
+
+@atexit.register
+def _release_all():
+    for k in sorted(list(_LIVE.keys()), reverse=True):
+        obj = _LIVE.get(k)
+        if obj is None:
+            continue
+        try:
+            (obj.free if isinstance(obj, DeviceBuffer) else obj.close)()
+        except Exception:
+            pass
 
 
 def _check(status: int, where: str, allow=()):
@@ -308,6 +334,7 @@ class DeviceBuffer:
         _check(lib.mspmv_device_malloc(device, nbytes, ctypes.byref(p)), "device_malloc")
         self.ptr = p.value
         self.nbytes = nbytes
+        _track(self)
 
     @classmethod
     def from_array(cls, a: np.ndarray, device: int = 0) -> "DeviceBuffer":
@@ -354,6 +381,7 @@ class GpuCsr:
         self.h = h.value
         self.num_rows, self.num_cols, self.num_nonzeros = a.num_rows, a.num_cols, a.num_nonzeros
         self.device = device
+        _track(self)
 
     def close(self):
         if getattr(self, "h", None):
@@ -419,6 +447,17 @@ class GpuCsr:
     def cg_kernel_name(self) -> str:
         """The CG path the last solve on this matrix ran (mspmv_cg_kernel_name)."""
         return lib.mspmv_cg_kernel_name(self.h).decode()
+
+    def cg_resident_stamps(self, db: "DeviceBuffer", dx: "DeviceBuffer", max_iters: int, tolerance: float,
+                           stamp_iters: int):
+        """One register-resident single-RHS solve with wall_clock64() phase stamps
+        (mspmv_cg_resident_stamps): (iterations, stamps[stamp_iters][G][5] as uint64)."""
+        it, G = ctypes.c_int(), ctypes.c_int()
+        # one workgroup per CU: the buffer is sized for up to 1024 CUs (MI355X: 256)
+        st = np.zeros(stamp_iters * 1024 * 5, np.uint64)
+        _check(lib.mspmv_cg_resident_stamps(self.h, db.ptr, dx.ptr, max_iters, tolerance, ctypes.byref(it),
+                                            _ptr(st), stamp_iters, ctypes.byref(G)), "cg_resident_stamps")
+        return it.value, st[: stamp_iters * G.value * 5].reshape(stamp_iters, G.value, 5)
 
     def spmm_kernel_name(self, L: int) -> str:
         """The SpMM kernel instantiation launched for L right-hand sides (rocprofv3's spelling)."""
@@ -529,6 +568,7 @@ class GpuIc0:
         h = ctypes.c_void_p()
         _check(lib.mspmv_ic0_create(ctypes.byref(l._c()), device, ctypes.byref(h)), "ic0_create")
         self.h = h.value
+        _track(self)
 
     def close(self):
         if getattr(self, "h", None):
@@ -748,6 +788,7 @@ class Comm:
         h = ctypes.c_void_p()
         _check(lib.mspmv_comm_create(idb, nranks, rank, device, ctypes.byref(h)), "comm_create")
         self.h, self.nranks, self.rank, self.device = h.value, nranks, rank, device
+        _track(self)
 
     def close(self):
         if getattr(self, "h", None):
@@ -782,6 +823,7 @@ class DistCsr:
                                          ctypes.byref(h)), "dist_create")
         self.h = h.value
         self.n_own = loc.num_rows
+        _track(self)
 
     def info(self):
         a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()

@@ -1,5 +1,5 @@
 """GPU parity of the register-resident CGSolveSingle (csrc/mspmv_cg_resident.hip: the whole solve
-as one cooperative launch, matrix values in registers, columns in LDS, two in-launch hand-offs
+as one launch of one workgroup per CU, matrix values in registers, columns in LDS, two in-launch hand-offs
 per iteration) against the oracle's restatement of CGSolveSingle (single_strategy.hpp:102-170) and
 against the pipelined two-kernel path (MSPMV_CG_RESIDENT=0) on the same inputs.
 
@@ -103,3 +103,62 @@ def test_resident_max_iters_repeat_and_breakdown(orc):
     # b = 0: p.Ap = 0 -> alpha = 0/0 at the first iteration -> breakdown (status 4), x stays 0
     xb, itb, hb, stb, kb = solve(a, np.zeros(n), 10, 1e-8, True)
     assert kb.startswith("k_cg_resident") and stb == 4 and itb == 1 and not np.any(xb)
+
+
+def test_resident_follows_cu_limit(orc):
+    """The resident layout is one workgroup per CU of the whole device: after set_cu_limit(64) the
+    next single-RHS solve runs the pipelined CG (not a grid that cannot be co-resident), and after
+    the limit is lifted the resident path is rebuilt and runs again -- same results every time."""
+    a = CASES["fem2d"]()
+    b = orc.glibc_rand(42, a.num_rows)
+    with mspmv.GpuCsr(a) as g:
+        x0, it0, h0, st0 = g.cg_single(b, 3000, 1e-8, hist_cap=3000)
+        k0 = g.cg_kernel_name()
+        g.set_cu_limit(64)
+        x1, it1, h1, st1 = g.cg_single(b, 3000, 1e-8, hist_cap=3000)
+        k1 = g.cg_kernel_name()
+        g.set_cu_limit(0)
+        x2, it2, h2, st2 = g.cg_single(b, 3000, 1e-8, hist_cap=3000)
+        k2 = g.cg_kernel_name()
+    assert k0.startswith("k_cg_resident") and k2.startswith("k_cg_resident"), (k0, k2)
+    assert k1.startswith("pipelined"), k1
+    assert st0 == st1 == st2 == 0
+    np.testing.assert_array_equal(x0, x2)
+    assert abs(it1 - it0) <= 1
+    k = min(len(h0), len(h1))
+    np.testing.assert_allclose(h1[:k], h0[:k], rtol=0, atol=1e-10)
+
+
+def test_resident_nan_rhs_reports_breakdown(orc):
+    """b holding the all-ones NaN pattern (the hand-off slots' 'empty' marker) must end in a breakdown
+    (or a NaN result) promptly, never in a stalled hand-off (MSPMV_ERR_STALL, status 8)."""
+    a = CASES["fem2d"]()
+    b = orc.glibc_rand(42, a.num_rows)
+    b[17] = np.frombuffer(np.uint64(0xFFFFFFFFFFFFFFFF).tobytes(), np.float64)[0]
+    x, it, h, st, kname = solve(a, b, 50, 1e-8, True)
+    assert kname.startswith("k_cg_resident"), kname
+    assert st in (0, 4), st
+
+
+def test_resident_phase_stamps(orc):
+    """mspmv_cg_resident_stamps: the same iterations and x as the plain solve, and stamps that are
+    monotone within every workgroup's iteration (start <= Ap done <= p.Ap total <= r done <= r.r
+    total) and across iterations."""
+    a = CASES["fem2d"]()
+    b = orc.glibc_rand(42, a.num_rows)
+    with mspmv.GpuCsr(a) as g:
+        db = mspmv.DeviceBuffer.from_array(b)
+        dx = mspmv.DeviceBuffer(8 * a.num_rows)
+        it, _, st = g.cg_dev(db, dx, 1, 3000, 1e-8)
+        x_plain = dx.download(a.num_rows)
+        its, stamps = g.cg_resident_stamps(db, dx, 3000, 1e-8, 64)
+        x_st = dx.download(a.num_rows)
+        db.free()
+        dx.free()
+    assert st == 0 and its == it
+    np.testing.assert_array_equal(x_st, x_plain)
+    k = min(its, 64)
+    s = stamps[:k].astype(np.int64)
+    assert s.shape[1] >= 8 and np.all(s > 0)
+    assert np.all(np.diff(s, axis=2) >= 0)
+    assert np.all(s[1:, :, 0] >= s[:-1, :, 4])

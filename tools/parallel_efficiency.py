@@ -154,7 +154,13 @@ def sweep_cus(args):
                f"--num_vectors={args.num_vectors}", f"--timing_iters={args.timing_iters}",
                f"--max_iters={args.max_iters}", f"--tolerance={args.tolerance}", f"--device={args.device}",
                f"--mtx_dir={args.mtx_dir}"] + (["--synthetic"] if args.synthetic else [])
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=args.child_timeout)
+        # one algorithm at every point: the register-resident single-RHS CG needs the whole device
+        # (one workgroup per CU), so a CU-limited child would fall back to the pipelined CG and the
+        # full-device point alone would compare a different algorithm -- L = 1 sweeps run pipelined
+        env = dict(os.environ)
+        if args.num_vectors == 1:
+            env["MSPMV_CG_RESIDENT"] = "0"
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=args.child_timeout, env=env)
         if r.returncode != 0:
             raise SystemExit(f"CUs={u}: child failed ({r.returncode}): {r.stderr[-1500:]}")
         for ln in r.stdout.splitlines():
