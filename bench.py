@@ -190,7 +190,7 @@ def cpu_baseline(a, x, seconds):
 
 
 FLUSH_BYTES = 512 << 20   # >= 512 MB MALL flush between cold calls (a read sweep: clean lines,
-                          # so the timed launch does not pay the flush's own write-back; MSPMV_FLUSH=write)
+                          # so the timed launch does not pay the flush's own write-back)
 CANT = dict(m=62451, nnz=4007383, band=2000, seed=1)
 RMA10 = dict(m=46835, nnz=2374001, band=3000, seed=2)
 
@@ -284,6 +284,42 @@ def run_spmv_shapes(dev, cpu_seconds, do_cpu):
             best = max(v["gflops"] for v in r["cpu_baselines"].values())
             r["gpu_cold_vs_best_cpu"] = round(r["gflops_cold"] / best, 1)
         out[name] = r
+    return out
+
+
+def run_pwtk_perturbed(dev, batch=4, steps=50):
+    """The headline's FEM shape made imperfect (the node-block plan must not be all-or-
+    nothing): pwtk's m and nnz, ~2 % of the nodes with 5 or 7 unknowns instead of 6 and ~1 % of the
+    rows with one column outside their node's pattern (mspmv_synth_fem_perturbed).  Timed as the
+    headline is: a batch of `batch` such matrices (> the Infinity Cache) back to back, per-launch
+    kernel time from the kernels' own events."""
+    mats, gs, dxs, dys = [], [], [], []
+    for i in range(batch):
+        a = mspmv.CsrMatrix.synth_fem_perturbed(PWTK["m"], PWTK["nnz"], PWTK["block"], PWTK["half_band_nodes"],
+                                                0.02, 0.01, seed=11 + i)
+        mats.append(a)
+        gs.append(mspmv.GpuCsr(a, device=dev))
+        dxs.append(mspmv.DeviceBuffer.from_array(np.random.default_rng(12 + i).uniform(0, 1, a.num_cols), dev))
+        dys.append(mspmv.DeviceBuffer(8 * a.num_rows, dev))
+    mspmv.time_spmm_batch(gs, dxs, dys, 1, 5)
+    step_ms, kern_ms, kps = mspmv.time_spmm_batch(gs, dxs, dys, 1, steps)
+    a0 = mats[0]
+    nb = sum(spmv_bytes(a.num_rows, a.num_cols, a.num_nonzeros) for a in mats) / batch
+    plan = gs[0].tile_plan(1)
+    nt = plan["num_tiles"]
+    reg = int(np.sum(plan["modes"] == 255))
+    out = {"workload": "pwtk-shaped FEM, imperfect: 2 % of nodes 5 or 7 unknowns, 1 % of rows one off-pattern "
+                       f"column; batch of {batch}, back to back",
+           "m": a0.num_rows, "nnz": a0.num_nonzeros, "kernel": gs[0].kernel_name(),
+           "tiles": nt, "block_tiles": gs[0].plan_block_tiles(1), "register_tiles_reported": reg,
+           "bytes_per_launch": round(nb), "kernel_ms": round(kern_ms, 5), "step_ms": round(step_ms, 5),
+           "kernels_per_step": kps, "GBps": round(nb / kern_ms / 1e6, 1),
+           "gflops": round(2.0 * a0.num_nonzeros / kern_ms / 1e6, 1),
+           "frac": round(nb / kern_ms / 1e6 / HBM_PEAK_GBS, 4)}
+    for g in gs:
+        g.close()
+    for b in dxs + dys:
+        b.free()
     return out
 
 
@@ -589,7 +625,7 @@ def main():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the hot-matrix and scatter-band side measurements (profiling runs: the "
                          "headline kernel's rocprofv3 average then covers exactly the timed launches)")
-    ap.add_argument("--only", choices=["spmm16", "spmv_shapes", "cg_single", "cg_multi"],
+    ap.add_argument("--only", choices=["spmm16", "spmv_shapes", "cg_single", "cg_multi", "pwtk_perturbed"],
                     help="run one side measurement alone and print its JSON (profiling: rocprofv3 then sees only "
                          "that leg's launches; tools/profile_legs.sh)")
     args = ap.parse_args()
@@ -604,6 +640,8 @@ def main():
             r = run_spmv_shapes(dev, min(args.cpu_seconds, 3.0), do_cpu)
         elif args.only == "cg_single":
             r = run_cg_single(dev, min(args.cpu_seconds, 10.0), do_cpu)
+        elif args.only == "pwtk_perturbed":
+            r = run_pwtk_perturbed(dev)
         else:
             r, large = run_cg_multi(d, dev)
             if large:
@@ -708,6 +746,7 @@ def main():
                                              "note": "pwtk size, 53 columns per row scattered over +-10,000"}
 
         if d.rank == 0 and not args.no_extras:
+            result["spmv_pwtk_perturbed"] = run_pwtk_perturbed(dev)
             result["spmm16"] = run_spmm16(dev, min(args.cpu_seconds, 5.0), d.world == 1 and not args.no_cpu)
             result["spmv_shapes"] = run_spmv_shapes(dev, min(args.cpu_seconds, 3.0), d.world == 1 and not args.no_cpu)
 

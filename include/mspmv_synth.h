@@ -41,6 +41,18 @@ MSPMV_API mspmv_status mspmv_synth_fem_blocked_rows(int m, long long nnz, int bl
                                                     unsigned long long seed, int row_lo, int row_hi,
                                                     int *row_offsets, int *cols, double *vals);
 
+/* An imperfect node-blocked FEM pattern (real FEM matrices are not all regular): nodes of `block`
+ * unknowns, a fraction odd_node_frac of them with block - 1 or block + 1 instead (half each); node
+ * I's pattern is every unknown of its neighbour nodes (chosen as mspmv_synth_fem_blocked chooses
+ * them, in node-index space), row i takes the first min(floor((i+1)nnz/m) - floor(i nnz/m),
+ * |pattern|) of them, and a fraction extra_row_frac of rows gets one more column of the node band
+ * that the pattern lacks, in order.  Columns unique and sorted per row; values U(0.5, 1.5).
+ * Call with cols/vals NULL to size (row_offsets and *nnz_out). */
+MSPMV_API mspmv_status mspmv_synth_fem_perturbed(int m, long long nnz, int block, int half_band_nodes,
+                                                 double odd_node_frac, double extra_row_frac,
+                                                 unsigned long long seed, int *row_offsets, int *cols,
+                                                 double *vals, long long *nnz_out);
+
 /* Power-law row lengths with the same contract as mspmv_synth_banded: row lengths drawn
  * from a Zipf-like law (a handful of rows hold a large share of nnz), columns spread over
  * the whole matrix.  Exercises merge-path load balance and long-row carries. */

@@ -154,6 +154,135 @@ mspmv_status mspmv_synth_fem_blocked_rows(int m, long long nnz, int block, int h
     return fem_blocked_rows(m, nnz, block, half_band_nodes, seed, row_lo, row_hi, row_offsets, cols, vals);
 }
 
+// Imperfect node-blocked FEM pattern (include/mspmv_synth.h): nodes of `block` unknowns, a fraction
+// of them with block - 1 or block + 1; row targets as mspmv_synth_fem_blocked's; a fraction of rows
+// with one column outside its node's pattern.  Pass 1 sizes (row_offsets), pass 2 fills.
+mspmv_status mspmv_synth_fem_perturbed(int m, long long nnz, int block, int half_band_nodes, double odd_node_frac,
+                                       double extra_row_frac, unsigned long long seed, int *row_offsets, int *cols,
+                                       double *vals, long long *nnz_out)
+{
+    if (m <= 0 || block < 2 || nnz < 0 || nnz > 0x7fffffffLL || !row_offsets || half_band_nodes < 0 ||
+        odd_node_frac < 0.0 || odd_node_frac > 1.0 || extra_row_frac < 0.0 || extra_row_frac > 1.0)
+        return MSPMV_ERR_INVALID;
+    // nodes: sizes block, or block -+ 1 with probability odd_node_frac / 2 each
+    std::vector<int> nstart;
+    nstart.reserve((size_t)m / (block - 1) + 2);
+    for (int r = 0, I = 0; r < m; ++I) {
+        nstart.push_back(r);
+        const double u = u01(seed ^ 0x0dd5eedull, (uint64_t)I);
+        const int dof = u < 0.5 * odd_node_frac ? block - 1 : u < odd_node_frac ? block + 1 : block;
+        r = std::min(m, r + dof);
+    }
+    const int nodes = (int)nstart.size();
+    nstart.push_back(m);
+    std::vector<int> node_of((size_t)m);
+#pragma omp parallel for schedule(static)
+    for (int I = 0; I < nodes; ++I)
+        for (int r = nstart[(size_t)I]; r < nstart[(size_t)I + 1]; ++r)
+            node_of[(size_t)r] = I;
+    const long long maxlen = (nnz + m - 1) / m;
+    const int maxblk = std::min<int>((int)((maxlen + block - 1) / block), 1024);
+    if (2LL * half_band_nodes + 1 < maxblk || maxblk > nodes)
+        return MSPMV_ERR_INVALID;
+    // the node's pattern: all unknowns of maxblk neighbour nodes (one per slice of the node band,
+    // own node forced), ascending
+    auto pattern = [&](int I, std::vector<int> &pat) {
+        int nb[1024];
+        const int lo = std::max(0, I - half_band_nodes), hi = std::min(nodes - 1, I + half_band_nodes);
+        const int take = std::min(maxblk, hi - lo + 1);
+        bucket_cols(lo, hi, take, seed, (uint64_t)I, nb);
+        bool has_self = false;
+        for (int k = 0; k < take; ++k)
+            has_self |= nb[k] == I;
+        if (!has_self) {
+            int k = 0;
+            while (k + 1 < take && nb[k + 1] <= I)
+                ++k;
+            if (nb[k] > I)
+                k = 0;
+            nb[k] = I;
+            std::sort(nb, nb + take);
+            for (int q = 1; q < take; ++q)
+                if (nb[q] <= nb[q - 1])
+                    nb[q] = nb[q - 1] + 1;
+        }
+        pat.clear();
+        for (int q = 0; q < take; ++q)
+            for (int c = nstart[(size_t)nb[q]]; c < nstart[(size_t)nb[q] + 1]; ++c)
+                pat.push_back(c);
+    };
+    // row i: the first min(target, |pattern|) pattern columns, plus (perturbed rows) one column of the
+    // node band that the pattern lacks, inserted in order
+    auto extra_col = [&](int i, const std::vector<int> &pat, int ell) {
+        if (u01(seed ^ 0xe7a2ull, (uint64_t)i) >= extra_row_frac)
+            return -1;
+        const int I = node_of[(size_t)i];
+        const int lo = nstart[(size_t)std::max(0, I - half_band_nodes)];
+        const int hi = nstart[(size_t)std::min(nodes - 1, I + half_band_nodes) + 1] - 1;
+        for (int tries = 0; tries < 16; ++tries) {
+            const int c = lo + (int)(u01(seed ^ 0xc01ull, (uint64_t)i * 16 + tries) * (double)(hi - lo + 1));
+            if (c < lo || c > hi)
+                continue;
+            if (!std::binary_search(pat.begin(), pat.begin() + ell, c))
+                return c;
+        }
+        return -1;
+    };
+    auto target = [&](long long i) { return (int)((i + 1) * nnz / m - i * nnz / m); };
+    std::vector<int> len((size_t)m);
+#pragma omp parallel
+    {
+        std::vector<int> pat;
+#pragma omp for schedule(dynamic, 64)
+        for (int I = 0; I < nodes; ++I) {
+            pattern(I, pat);
+            for (int i = nstart[(size_t)I]; i < nstart[(size_t)I + 1]; ++i) {
+                const int ell = std::min(target(i), (int)pat.size());
+                len[(size_t)i] = ell + (extra_col(i, pat, ell) >= 0 ? 1 : 0);
+            }
+        }
+    }
+    long long acc = 0;
+    row_offsets[0] = 0;
+    for (int i = 0; i < m; ++i) {
+        acc += len[(size_t)i];
+        if (acc > 0x7fffffffLL)
+            return MSPMV_ERR_INVALID;
+        row_offsets[i + 1] = (int)acc;
+    }
+    if (nnz_out)
+        *nnz_out = acc;
+    if (!cols || !vals)  // sizing call
+        return MSPMV_OK;
+#pragma omp parallel
+    {
+        std::vector<int> pat;
+#pragma omp for schedule(dynamic, 64)
+        for (int I = 0; I < nodes; ++I) {
+            pattern(I, pat);
+            for (int i = nstart[(size_t)I]; i < nstart[(size_t)I + 1]; ++i) {
+                const int s = row_offsets[i];
+                const int ell = std::min(target(i), (int)pat.size());
+                const int x = extra_col(i, pat, ell);
+                int k = 0;
+                bool placed = x < 0;
+                for (int q = 0; q < ell; ++q) {
+                    if (!placed && x < pat[(size_t)q]) {
+                        cols[s + k++] = x;
+                        placed = true;
+                    }
+                    cols[s + k++] = pat[(size_t)q];
+                }
+                if (!placed)
+                    cols[s + k++] = x;
+                for (int q = 0; q < k; ++q)
+                    vals[s + q] = 0.5 + u01(seed ^ 0x5bd1e995ull, (uint64_t)(s + q));
+            }
+        }
+    }
+    return MSPMV_OK;
+}
+
 mspmv_status mspmv_synth_powerlaw(int m, int n, long long nnz, double exponent, unsigned long long seed,
                                   int *row_offsets, int *cols, double *vals)
 {

@@ -142,6 +142,8 @@ _SIGS = {
     "mspmv_dist_cg_dev": (_I, [_P, _P, _P, _I, _I, _D, _PI, _P, _I]),
     "mspmv_synth_fem_blocked": (_I, [_I, ctypes.c_longlong, _I, _I, ctypes.c_ulonglong, _P, _P, _P]),
     "mspmv_synth_fem_blocked_rows": (_I, [_I, ctypes.c_longlong, _I, _I, ctypes.c_ulonglong, _I, _I, _P, _P, _P]),
+    "mspmv_synth_fem_perturbed": (_I, [_I, ctypes.c_longlong, _I, _I, _D, _D, ctypes.c_ulonglong, _P, _P, _P,
+                                       ctypes.POINTER(ctypes.c_longlong)]),
     "mspmv_synth_powerlaw": (_I, [_I, _I, ctypes.c_longlong, _D, ctypes.c_ulonglong, _P, _P, _P]),
     "mspmv_synth_stencil": (_I, [_I, _I, _I, _I, _I, ctypes.c_ulonglong, _D, _P, _P, _P,
                                  ctypes.POINTER(ctypes.c_longlong)]),
@@ -298,6 +300,21 @@ class CsrMatrix:
         _check(lib.mspmv_synth_fem_blocked_rows(m, nnz, block, half_band_nodes, seed, row_lo, row_hi, _ptr(ro),
                                                 _ptr(ci), _ptr(va)), "synth_fem_blocked_rows")
         return cls(row_hi - row_lo, m, k, ro, ci[:k], va[:k])
+
+    @classmethod
+    def synth_fem_perturbed(cls, m: int, nnz: int, block: int, half_band_nodes: int, odd_node_frac: float = 0.02,
+                            extra_row_frac: float = 0.01, seed: int = 1) -> "CsrMatrix":
+        """Imperfect FEM pattern: ~odd_node_frac of the nodes with block -+ 1 unknowns, ~extra_row_frac
+        of the rows with one column outside their node's pattern (mspmv_synth_fem_perturbed)."""
+        ro = np.empty(m + 1, np.int32)
+        nz = ctypes.c_longlong(0)
+        _check(lib.mspmv_synth_fem_perturbed(m, nnz, block, half_band_nodes, odd_node_frac, extra_row_frac, seed,
+                                             _ptr(ro), None, None, ctypes.byref(nz)), "synth_fem_perturbed(size)")
+        ci = np.empty(max(nz.value, 1), np.int32)
+        va = np.empty(max(nz.value, 1), np.float64)
+        _check(lib.mspmv_synth_fem_perturbed(m, nnz, block, half_band_nodes, odd_node_frac, extra_row_frac, seed,
+                                             _ptr(ro), _ptr(ci), _ptr(va), ctypes.byref(nz)), "synth_fem_perturbed")
+        return cls(m, m, int(nz.value), ro, ci[: nz.value], va[: nz.value])
 
     @classmethod
     def synth_powerlaw(cls, m: int, n: int, nnz: int, exponent: float = 1.2, seed: int = 3) -> "CsrMatrix":

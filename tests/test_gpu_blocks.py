@@ -10,8 +10,11 @@ blocks switched off (MSPMV_SPMV_BLOCKS=0, in a child process since the tuning is
 process).  Covered: equal-length node rows,
 prefix runs (rows of one node 52 and 53 long, as the pwtk-shaped generator makes them), rows
 wider than 64 columns (pattern chunks), runs longer than 8 rows (split), empty rows inside runs,
-a Kronecker FEM matrix solved by the pipelined single-RHS CG (blocks in the fused CG SpMV), and
-the full pwtk shape."""
+a Kronecker FEM matrix solved by the pipelined single-RHS CG (blocks in the fused CG SpMV), the
+full pwtk shape, and imperfect FEM plans: nodes of 5 / 7 unknowns, rows with an off-pattern column,
+long rows split between tiles and stencil rows mixed in -- a plan whose tiles are mostly register run
+tiles runs the column-pair kernel whole (k_spmv_blk), its register fallback taking the other tiles
+(every tile reported 255: all rows within the reordering bound)."""
 import os
 import subprocess
 import sys
@@ -172,10 +175,12 @@ def test_blocks_not_taken_where_they_lose():
             assert g.plan_block_tiles(1) == 0
 
 
-def test_blocks_in_pipelined_cg(orc):
+@pytest.mark.parametrize("dof", [6, 7])
+def test_blocks_in_pipelined_cg(orc, dof):
     """The fused CG SpMV (MODE 1: p = r + beta p_old gathered as {r, p} pairs) stages node blocks
-    too; the solve must match the oracle's CGSolveSingle as every single-RHS CG does."""
-    a = kron_fem9(60, 50, 6)
+    too; the solve must match the oracle's CGSolveSingle as every single-RHS CG does.  dof 7: runs
+    of 6 + 1 rows, column pairs broken at every node boundary."""
+    a = kron_fem9(60, 50, dof)
     b = orc.glibc_rand(42, a.num_rows)
     xo, it_o, ho = orc.cg_single(a, b, 5000, 1e-10, hist_cap=5000)
     with mspmv.GpuCsr(a) as g:
@@ -277,3 +282,99 @@ def test_blocks_spai_pcg(orc):
     assert st == 0 and it_g == it_o
     np.testing.assert_allclose(hg, ho[: len(hg)], rtol=0, atol=1e-10)
     assert np.linalg.norm(Xg - Xo) <= 1e-8 * np.linalg.norm(Xo)
+
+
+# ---- imperfect FEM: mixed plans (k_spmv_blk's register fallback, per-chunk pair flags) ----------
+def fem_with_long_rows(a, rows, length, seed=5):
+    """`a` with the given rows replaced by `length` random sorted columns: rows longer than the snap
+    distance (tile / 8) are split between tiles, so the plan carries (k_fixup) and those tiles are
+    not node blocks."""
+    rng = np.random.default_rng(seed)
+    ro, ci, va = a.row_offsets, a.column_indices, a.values
+    new_ro, new_ci, new_va = [0], [], []
+    rows = set(rows)
+    for i in range(a.num_rows):
+        if i in rows:
+            c = np.sort(rng.choice(a.num_cols, length, replace=False)).astype(np.int32)
+            v = rng.uniform(0.5, 1.5, length)
+        else:
+            c, v = ci[ro[i]:ro[i + 1]], va[ro[i]:ro[i + 1]]
+        new_ci.append(c)
+        new_va.append(v)
+        new_ro.append(new_ro[-1] + len(c))
+    return mspmv.CsrMatrix.from_arrays(a.num_cols, np.array(new_ro, np.int32), np.concatenate(new_ci),
+                                       np.concatenate(new_va))
+
+
+def stack_rows(a, b):
+    """Rows of a, then rows of b (same column count)."""
+    ro = np.concatenate([a.row_offsets, a.row_offsets[-1] + b.row_offsets[1:]]).astype(np.int32)
+    return mspmv.CsrMatrix.from_arrays(a.num_cols, ro, np.concatenate([a.column_indices, b.column_indices]),
+                                       np.concatenate([a.values, b.values]))
+
+
+def mixed_cases():
+    base = lambda: mspmv.CsrMatrix.synth_fem_blocked(21792, 1152443, 6, 170, seed=3)  # noqa: E731
+    return {
+        "perturbed_small": lambda: mspmv.CsrMatrix.synth_fem_perturbed(21792, 1152443, 6, 170, 0.02, 0.01, seed=4),
+        "perturbed_heavy": lambda: mspmv.CsrMatrix.synth_fem_perturbed(21792, 1152443, 6, 170, 0.2, 0.1, seed=5),
+        "long_rows": lambda: fem_with_long_rows(base(), [100, 5000, 5001, 17000], 1500),
+        # a stencil block beside the FEM rows: its tiles have no runs (the register fallback, G = 2)
+        "fem_plus_stencil": lambda: stack_rows(base(), _stencil_rows(21792, 3000)),
+    }
+
+
+def _stencil_rows(ncols, m):
+    """m rows of 7 nonzeros in a narrow band, num_cols = ncols."""
+    rng = np.random.default_rng(9)
+    ro = np.arange(0, 7 * m + 1, 7, dtype=np.int32)
+    base = rng.integers(0, ncols - 40, m)
+    ci = (base[:, None] + np.arange(0, 35, 5)[None, :]).astype(np.int32).reshape(-1)
+    va = rng.uniform(0.5, 1.5, 7 * m)
+    return mspmv.CsrMatrix.from_arrays(ncols, ro, ci, va)
+
+
+@pytest.mark.parametrize("name", list(mixed_cases()))
+def test_blocks_mixed_plan(orc, name):
+    a = mixed_cases()[name]()
+    x = np.random.default_rng(17).uniform(-1, 1, a.num_cols)
+    with mspmv.GpuCsr(a) as g:
+        plan = g.tile_plan(1)
+        nb = g.plan_block_tiles(1)
+        y = g.spmv(x)
+        y2 = g.spmv(x)
+        kname = g.kernel_name()
+        check_parity(a, y, orc.spmv_gold(a, x), x, plan, 1)
+    assert y.tobytes() == y2.tobytes()
+    assert kname.startswith("k_spmv_blk<0,"), kname
+    assert np.all(plan["modes"] == 255)
+    assert 0 < nb <= plan["num_tiles"]
+    if name == "long_rows":
+        assert plan["num_carries"] > 0
+
+
+def test_blocks_perturbed_full_size(orc):
+    """The bench's imperfect pwtk leg (m = 217,918; 2 % odd nodes, 1 % off-pattern rows) at full size."""
+    a = mspmv.CsrMatrix.synth_fem_perturbed(217918, 11524432, 6, 1700, 0.02, 0.01, seed=11)
+    x = np.random.default_rng(12).uniform(-1, 1, a.num_cols)
+    with mspmv.GpuCsr(a) as g:
+        plan = g.tile_plan(1)
+        y = g.spmv(x)
+        kname = g.kernel_name()
+        check_parity(a, y, orc.spmv_gold(a, x), x, plan, 1)
+        nb = g.plan_block_tiles(1)
+    assert kname.startswith("k_spmv_blk<0,"), kname
+    assert nb >= 0.9 * plan["num_tiles"], (nb, plan["num_tiles"])
+
+
+@pytest.mark.parametrize("name", ["perturbed_small", "long_rows"])
+@pytest.mark.parametrize("L", [1, 8])
+def test_blocks_mixed_plan_spmm(orc, name, L):
+    """Mixed plans under the SpMM (k_spmm_blk when every tile is a register run tile, else the L-wide
+    merge tiles) against the oracle's row-split SpMM."""
+    from gpu_common import check_parity_chunked
+    a = mixed_cases()[name]()
+    X = np.random.default_rng(L).uniform(-1, 1, (a.num_cols, L))
+    with mspmv.GpuCsr(a) as g:
+        Y = g.spmm(X)
+        check_parity_chunked(a, g, Y, orc.csr_spmm_t(a, X), X, L)
