@@ -141,8 +141,7 @@ static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out, boo
         // multiplies L columns on that plan with k_spmm_blk -- one panel-row gather per (run,
         // column) -- instead of its own L-wide merge tiles
         auto one = h->plans.find(plan_key(1));
-        if (one != h->plans.end() && one->second.d_blk && one->second.num_tiles_reg == one->second.num_tiles &&
-            one->second.num_tiles_shift == 0) {
+        if (one != h->plans.end() && one->second.d_blk && one->second.num_tiles_reg == one->second.num_tiles) {
             ST_TRY(ensure_modes(h, one->second, L));
             *out = &one->second;
             return MSPMV_OK;
@@ -309,20 +308,17 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
             return fail(MSPMV_ERR_HIP);
         }
         p.h_blk_reg.assign((size_t)T, 0);
-        int maxnd = 0, maxh = 0, maxwc = 0;
+        int maxnd = 0, maxh = 0;
         std::vector<unsigned char> reg((size_t)T, 0);
         for (int t = 0; t < T; ++t) {
             const uint4 *d = &hd[(size_t)t * kBlkPerTile];
-            const int nd = (int)((d[0].y >> 8) & 127u);
+            const int nd = (int)((d[0].y >> 8) & 255u);
             if (nd == 0)
                 continue;
             ++p.num_tiles_blk;
-            p.num_tiles_shift += (d[0].y & 0x8000u) ? 1 : 0;
             maxnd = std::max(maxnd, nd);
-            for (int i = 0; i < nd; ++i) {
+            for (int i = 0; i < nd; ++i)
                 maxh = std::max(maxh, (int)(d[i].y & 15u));
-                maxwc = std::max(maxwc, (int)(d[i].x >> 24));
-            }
             bool one = true;  // the kernels' own test: every chunk starts at pattern column 0
             for (int i = 0; i < nd; ++i)
                 one = one && ((d[i].x >> 16) & 255u) == 0;
@@ -333,12 +329,9 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         // other tiles) when most tiles are register run tiles; otherwise k_spmv_tile, whose register
         // path takes the run tiles of one round (<= kBlkTileChunks chunks)
         p.blk_spmv = p.num_tiles_reg > 0 && 2LL * p.num_tiles_reg >= T;
-        p.blk_rl = maxwc <= 32 ? 16 : 32;  // four runs per wave when every chunk fits 16 lanes x 2 columns
         for (int t = 0; t < T; ++t) {
-            const uint4 d0 = hd[(size_t)t * kBlkPerTile];
-            const int nd = (int)((d0.y >> 8) & 127u);
-            p.h_blk_reg[(size_t)t] =
-                p.blk_spmv || (reg[(size_t)t] && nd <= kBlkTileChunks && !(d0.y & 0x8000u));
+            const int nd = (int)((hd[(size_t)t * kBlkPerTile].y >> 8) & 255u);
+            p.h_blk_reg[(size_t)t] = p.blk_spmv || (reg[(size_t)t] && nd <= kBlkTileChunks);
         }
         dev_free(p.d_blk);
         p.d_blk = nullptr;
@@ -347,7 +340,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
             p.blk_stride = maxnd <= 16 ? 16 : maxnd <= 32 ? 32 : 64;
             std::vector<uint4> packed((size_t)T * p.blk_stride, make_uint4(0u, 0u, 0u, 0u));
             for (int t = 0; t < T; ++t)
-                for (int i = 0, nd = (int)((hd[(size_t)t * kBlkPerTile].y >> 8) & 127u); i < nd; ++i)
+                for (int i = 0, nd = (int)((hd[(size_t)t * kBlkPerTile].y >> 8) & 255u); i < nd; ++i)
                     packed[(size_t)t * p.blk_stride + i] = hd[(size_t)t * kBlkPerTile + i];
             if ((st = dev_alloc(&p.d_blk, packed.size())) != MSPMV_OK)
                 return fail(st);
@@ -1876,7 +1869,7 @@ mspmv_status mspmv_tile_modes(mspmv_handle h, int L, unsigned char *modes)
         HIP_TRY(hipMemcpy(modes, plan->d_modes[l_index(L)], plan->num_tiles, hipMemcpyDeviceToHost));
     // node-block tiles reduced in registers (lane tree, not the plan's mode): L = 1 on any plan
     // with node blocks, L > 1 when get_plan chose the node-block plan (k_spmm_blk)
-    if (plan->d_blk && (L == 1 || (plan->num_tiles_reg == plan->num_tiles && plan->num_tiles_shift == 0)))
+    if (plan->d_blk && (L == 1 || plan->num_tiles_reg == plan->num_tiles))
         for (int t = 0; t < plan->num_tiles; ++t)
             if (plan->h_blk_reg[(size_t)t])
                 modes[t] = 255;

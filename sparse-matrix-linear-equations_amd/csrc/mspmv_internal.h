@@ -70,9 +70,6 @@ struct TilePlan {
     int blk_rows_max = 8;               // the tallest run (rows of one node) over the descriptors
     bool blk_spmv = false;              // the plain SpMV runs k_spmv_blk (most tiles register run tiles;
                                         // the rest take its register fallback)
-    int blk_rl = 32;                    // k_spmv_blk lanes per run: 16 when every chunk is <= 32 columns wide
-    int num_tiles_shift = 0;            // tiles holding shifted runs (column-pair kernel only: the other
-                                        // node-block paths stage them striped; no k_spmm_blk on the plan)
     std::vector<unsigned char> h_blk_reg;  // [num_tiles] 1: the plain SpMV reduces the tile in registers
                                            // (a reordered sum: mspmv_tile_modes reports 255)
 };
@@ -208,7 +205,7 @@ bool spmm_blk_enabled();
 constexpr int kBlkPerTile = 64;  // == kBlkMax in the kernels: descriptor capacity of a tile
 // Chunks per tile k_build_blocks may describe for the plain SpMV's column-pair kernel (two rounds of
 // its eight half-wave run slots), and the one-round limit of k_spmv_tile's node-block paths.
-constexpr int kBlkPlanChunks = 32;
+constexpr int kBlkPlanChunks = 16;
 constexpr int kBlkTileChunks = 8;
 hipError_t launch_build_blocks(const int *d_row_offsets, const int *d_cols, const int2 *d_bounds,
                                const unsigned char *d_split, const int *d_colbase, int num_tiles, uint4 *d_blk,

@@ -507,15 +507,9 @@ __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ c
 // plan's stride being the smallest of 16, 32, 64 that holds every tile's set):
 //   x: vofs (nonzero offset of the run's first row in the tile, bits 0-15) | j0 (first pattern
 //      column of this chunk, 16-23) | wc (chunk width <= 64, 24-31)
-//   y: h (rows, 1..8, bits 0-3) | p (row holding P, 4-6) | pairs (bit 7: the chunk's pattern columns
-//      come in consecutive pairs, P[j0 + 2i + 1] == P[j0 + 2i] + 1, at least one pair) | nd (descriptor
-//      count, in entry 0 only, 8-15; 0 = the tile stages the plain way) | rofs (the run's first row in
-//      the tile, 16-31)
-//   z, w: the h row lengths, 8 bits each (rows of a run are <= 255 long); w bit 31 (row 7's length,
-//      never a row: runs hold <= kBlkRunRows = 6): a SHIFTED run -- row g + i's columns are row g's
-//      plus i (equal lengths, P = row g: the x-lines of a 3-D stencil), for k_spmv_blk's
-//      column-pair form only; entry 0's y bit 15 marks a tile holding such runs (nd <= 64 fits
-//      bits 8-14; the other node-block paths stage such tiles the striped way)
+//   y: h (rows, 1..8, bits 0-3) | p (row holding P, 4-6) | nd (descriptor count, in entry 0 only,
+//      8-15; 0 = the tile stages the plain way) | rofs (the run's first row in the tile, 16-31)
+//   z, w: the h row lengths, 8 bits each (rows of a run are <= 255 long)
 constexpr int kBlkMax = 64;  // descriptors a tile may have (the plan stores them at a stride of 16, 32 or 64)
 constexpr int kBlkRows = 8;
 // Rows per run: at most 6, the column-pair SpMV kernel's value registers (k_spmv_blk<.., 6>); a node
@@ -531,7 +525,9 @@ __device__ __forceinline__ int blk_len(const uint4 &d, int i)
 }
 
 // One thread per tile.  A tile qualifies when it holds whole rows only (no split boundary), is on
-// the 16-bit column stream, fits in kBlkMax chunks, and its runs pay (below).
+// the 16-bit column stream, fits in kBlkMax chunks, and its runs pay (below).  (Runs tolerating one
+// row with one extra pattern column -- imperfect FEM rows -- measured 24.1 vs 24.4 us on the pwtk
+// shape with 1 % such rows, and cost the regular shape: not kept, r04e.)
 __global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *__restrict__ cols,
                                const int2 *__restrict__ bounds, const unsigned char *__restrict__ split,
                                const int *__restrict__ colbase, int num_tiles, uint4 *__restrict__ blk,
@@ -548,58 +544,40 @@ __global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *_
     if (split[t] || split[t + 1] || colbase[t] < 0 || n1 <= n0 || row_offsets[r0] != n0 || row_offsets[r1] != n1)
         return;
     int nd = 0, sum_w = 0, nruns = 0;
-    bool tile_shift = false;
     int r = r0;
     while (r < r1) {
         const int g = r, gs = row_offsets[g];
         int p = g, plen = row_offsets[g + 1] - gs;
         unsigned lens[2] = {0u, 0u};
         int h = 0;
-        int shift = -1;  // -1 undecided (one row), 0 node rows, 1 shifted rows
         for (; r < r1 && h < kBlkRunRows; ++r, ++h) {
             const int s = row_offsets[r], len = row_offsets[r + 1] - s;
             if (len > 255)
                 return;
-            if (h > 0) {
-                bool same = false, shifted = false;
-                if (shift <= 0) {  // a prefix of P, or P a prefix of it
-                    const int ps = row_offsets[p], m = min(len, plen);
-                    same = true;
-                    for (int q = 0; q < m && same; ++q)
-                        same = cols[s + q] == cols[ps + q];
-                }
-                if (!same && shift != 0 && len == plen) {  // row g's columns + (r - g), all of them
-                    shifted = true;
-                    for (int q = 0; q < len && shifted; ++q)
-                        shifted = cols[s + q] == cols[gs + q] + h;
-                }
-                if (!same && !shifted)
+            if (h > 0) {  // a prefix of P, or P a prefix of it
+                const int ps = row_offsets[p], m = min(len, plen);
+                bool same = true;
+                for (int q = 0; q < m && same; ++q)
+                    same = cols[s + q] == cols[ps + q];
+                if (!same)
                     break;
-                shift = same ? 0 : 1;
-                if (same && len > plen) {
+                if (len > plen) {
                     p = r;
                     plen = len;
                 }
             }
             lens[h >> 2] |= (unsigned)len << (8 * (h & 3));
         }
-        const bool sh = shift == 1;
-        tile_shift |= sh;
         sum_w += plen;
         ++nruns;
         const int vofs = gs - n0;
-        const int ps = row_offsets[p];
         for (int j0 = 0; j0 < plen || (j0 == 0 && plen == 0); j0 += 64) {
             if (nd == kBlkMax || j0 > 255)
                 return;
             const int wc = min(64, plen - j0);
-            bool pairs = wc >= 2;  // one 16-B x load per column pair (k_spmv_blk's pair form)
-            for (int q = j0; q + 1 < j0 + wc && pairs; q += 2)
-                pairs = cols[ps + q + 1] == cols[ps + q] + 1;
             const uint4 dd = make_uint4((unsigned)vofs | ((unsigned)j0 << 16) | ((unsigned)wc << 24),
-                                        (unsigned)h | ((unsigned)(p - g) << 4) | (pairs ? 0x80u : 0u) |
-                                            ((unsigned)(g - r0) << 16),
-                                        lens[0], lens[1] | (sh ? 0x80000000u : 0u));
+                                        (unsigned)h | ((unsigned)(p - g) << 4) | ((unsigned)(g - r0) << 16),
+                                        lens[0], lens[1]);
             if (nd == 0)
                 d0 = dd;
             else
@@ -615,12 +593,12 @@ __global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *_
     // the 4 waves take the tile in ONE round of two chunks each (nd <= 8): a second round waits
     // for the first's sums.  2-D Kronecker FEM matrices with 3, 4 and 6 unknowns per node (15-30
     // columns, ~11-20 runs per tile) ran 3.1x, 2.0x and 1.2x slower on node blocks than striped;
-    // the pwtk shape (53 columns, ~7 runs per tile) 1.14x faster.  Tiles with shifted runs (the
-    // 27-point stencil's x-lines) run only in the column-pair kernel, whose 16-lane form (16 run
-    // slots per round) takes patterns of >= 16 columns.
-    if (5 * sum_w > 3 * (n1 - n0) || sum_w < (tile_shift ? 16 : 32) * nruns || nd > max_chunks)
+    // the pwtk shape (53 columns, ~7 runs per tile) 1.14x faster.  (Shifted runs -- rows whose columns
+    // are the previous row's plus one, the 27-point stencil's x-lines -- in a 16-lane column-pair form
+    // measured slower than the striped staging on the nlpkkt120 size: 266-268 vs 220-224 us, r04d.)
+    if (5 * sum_w > 3 * (n1 - n0) || sum_w < 32 * nruns || nd > max_chunks)
         return;
-    d0.y |= (unsigned)nd << 8 | (tile_shift ? 0x8000u : 0u);
+    d0.y |= (unsigned)nd << 8;
     out[0] = d0;
 }
 
@@ -724,8 +702,6 @@ struct TileArgs {
     int blk_rows_max;  // node-block plans: the tallest run (TilePlan::blk_rows_max; k_spmm_blk's KR)
     int tb;            // threads sharing one tile (the plan's lanes: 256, or 64 for one-wave SpMV plans)
     int blk_spmv;      // the plain SpMV runs k_spmv_blk on this plan (TilePlan::blk_spmv; mixed plans too)
-    int blk_rl;        // its lanes per run (TilePlan::blk_rl)
-    int blk_shift;     // the plan holds shifted runs (TilePlan::num_tiles_shift > 0)
     int n;             // columns (x holds n entries)
 };
 
@@ -1079,64 +1055,24 @@ __device__ __forceinline__ double rows8_sum32(const double (&p)[kBlkRows])
     return v;
 }
 
-// rows8_sum32 over 16-lane groups: row i's total lands in lanes 2i, 2i + 1 of the group
-// (i = (lane & 15) >> 1); shuffles with xor <= 8 stay inside the group, so four groups fold four
-// runs with the same 10 shuffles.
-__device__ __forceinline__ double rows8_sum16(const double (&p)[kBlkRows])
-{
-    const int lane = threadIdx.x & 63;
-    const bool b3 = lane & 8, b2 = lane & 4, b1 = lane & 2;
-    double q4[4], q2[2];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        q4[k] = (b3 ? p[k + 4] : p[k]) + __shfl_xor(b3 ? p[k] : p[k + 4], 8);
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-        q2[k] = (b2 ? q4[k + 2] : q4[k]) + __shfl_xor(b2 ? q4[k] : q4[k + 2], 4);
-    double v = (b1 ? q2[1] : q2[0]) + __shfl_xor(b1 ? q2[0] : q2[1], 2);
-    v += __shfl_xor(v, 1);
-    return v;
-}
-
-// x[c + i] for i < KR (a shifted run's column c): 16-B loads at c, c + 2, ... (8-B aligned at worst),
-// each starting at n - 2 at most and picking its half -- row i of the run needs x[c + i] <= x[n - 1]
-// only for i < h, and the entries past it are never used (their products are selected away).
-template <int KR>
-__device__ __forceinline__ void shifted_x(const double *x, int n, int c, double (&out)[KR + 2])
-{
-#pragma unroll
-    for (int k = 0; k < (KR + 2) / 2; ++k) {
-        const int q = min(c + 2 * k, n - 2);
-        const double2 xx = *reinterpret_cast<const double2 *>(x + q);
-        out[2 * k] = q == c + 2 * k ? xx.x : xx.y;
-        out[2 * k + 1] = xx.y;
-    }
-}
-
-// Plain SpMV form of blk_rows with column PAIRS: each group of RL lanes (32: half a wave, 64-column
-// runs; 16: a quarter, runs of <= 32 columns such as the 27-point stencil's, four runs per wave)
-// owns one run per round and its lane l owns pattern columns 2l and 2l + 1, so a row of the run
-// arrives in ONE 16-B load per lane (half the value-load instructions of column-owner lanes; the
-// loads may be 8-B aligned only -- gfx9's unaligned access mode), and one reduce-scatter folds the
-// wave's runs (rows8_sum32 / rows8_sum16).  A lane's two products are added before the group tree:
-// a fixed order, so rows stay reproducible and within the reordering bound (mode 255).  Column-owner
-// lanes instead: pwtk shape 24.98 vs 22.6-23.1 us (r03t).
-// Per chunk (descriptor bit 7): pattern columns in consecutive pairs take ONE 16-B x load per lane.
-// SHIFT (plans with shifted runs, k_build_blocks): row i of a shifted run reads x[P[j] + i], so a
-// lane loads x[c .. c + KR - 1] contiguously (KR / 2 + 1 16-B loads, or KR + 2 values of one sweep
-// when its two columns are adjacent) instead of one gather per nonzero.
-template <bool NT, int KR, int RL, bool SHIFT>
+// Plain SpMV form of blk_rows with column PAIRS: each half-wave owns one run per round and its lane
+// l owns pattern columns 2l and 2l + 1, so a row of the run arrives in ONE 16-B load per lane (half
+// the value-load instructions of column-owner lanes; the loads may be 8-B aligned only -- gfx9's
+// unaligned access mode), and one rows8_sum32 folds both halves' runs (half the shuffles).  A
+// lane's two products are added before the half-wave tree: a fixed order, so rows stay
+// reproducible and within the reordering bound (mode 255).  Column-owner lanes instead: pwtk shape
+// 24.98 vs 22.6-23.1 us (r03t).  Per chunk (descriptor bit 7): pattern columns in consecutive pairs
+// take ONE 16-B x load per lane.
+template <bool NT, int KR>
 __device__ __forceinline__ void blk_rows_pair(const TileArgs &a, const uint4 &bd, int nd, int r0, int n0,
                                               int colbase)
 {
-    static_assert(RL == 32 || RL == 16, "run lanes");
     constexpr int NW = kBlock / 64;
-    constexpr int RPW = 64 / RL;  // runs per wave per round
     const int lane = threadIdx.x & 63;
-    const int grp = lane / RL, hl = lane % RL;
+    const int half = lane >> 5, hl = lane & 31;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    for (int round = 0; round * RPW * NW < nd; ++round) {
-        const int di = wave + NW * (RPW * round + grp);
+    for (int round = 0; round * 2 * NW < nd; ++round) {
+        const int di = wave + NW * (2 * round + half);
         const bool valid = di < nd;
         const int src = min(di, nd - 1);  // descriptor lane (every wave holds all of them in bd)
         const uint4 d = make_uint4((unsigned)__shfl((int)bd.x, src), (unsigned)__shfl((int)bd.y, src),
@@ -1157,59 +1093,30 @@ __device__ __forceinline__ void blk_rows_pair(const TileArgs &a, const uint4 &bd
                 v[i] = ld_stream<NT>(reinterpret_cast<const double2 *>(a.vals + n0 + vofs + start + 2 * hl));
             start += i < h ? len : 0;
         }
-        const bool pairs = (d.y >> 7) & 1u;  // uniform per lane group (its run)
-        int c0 = 0, c1 = 0;  // column 0 of x: always valid to gather
+        // the lane's two pattern columns: ONE 4-B load of both 16-bit offsets (2-B aligned at worst; the
+        // second belongs to the next position, in bounds by the stream's padding, and is replaced when
+        // the lane has one column), then ONE 16-B x load (8-B aligned at worst) for an adjacent pair --
+        // FEM nodes list their unknowns consecutively, so nearly every lane's pair is -- and a second
+        // load only in lanes whose pair is not (an exec-masked load, skipped when no lane needs it).
+        // The load starts at n - 2 at most and picks its half (the last column sits at n - 1 at most).
+        unsigned cc = 0u;
         if (valid && 2 * hl < wc)
-            c0 = colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + 2 * hl);
-        if (!pairs && valid && 2 * hl + 1 < wc)
-            c1 = colbase + (int)ld_stream<NT>(a.cols16 + n0 + vofs + pstart + 2 * hl + 1);
-        double xa[KR], xb[KR];
-        if (SHIFT && (d.w >> 31)) {  // a shifted run (uniform per lane group)
-            double w0[KR + 2];
-            shifted_x<KR>(a.x, a.n, c0, w0);
-            if (pairs) {  // columns c0, c0 + 1: one sweep of KR + 1 values serves both
-#pragma unroll
-                for (int i = 0; i < KR; ++i) {
-                    xa[i] = w0[i];
-                    xb[i] = w0[i + 1];
-                }
-            } else {
-                double w1[KR + 2];
-                shifted_x<KR>(a.x, a.n, c1, w1);
-#pragma unroll
-                for (int i = 0; i < KR; ++i) {
-                    xa[i] = w0[i];
-                    xb[i] = w1[i];
-                }
-            }
-        } else {
-            double x0, x1;
-            if (pairs) {
-                // the plan checked P[2j + 1] == P[2j] + 1 for this chunk (k_build_blocks, so n >= 2): one
-                // column offset and ONE 16-B gather (8-B aligned at worst) per lane; the last column sits
-                // at n - 1 at most, so the load starts at n - 2 at most and picks its half
-                const int base = min(c0, a.n - 2);
-                const double2 xx = *reinterpret_cast<const double2 *>(a.x + base);
-                x0 = base == c0 ? xx.x : xx.y;
-                x1 = xx.y;  // used only where 2 hl + 1 < wc, i.e. column c0 + 1 <= n - 1 and base == c0
-            } else {
-                x0 = a.x[c0];
-                x1 = a.x[c1];
-            }
-#pragma unroll
-            for (int i = 0; i < KR; ++i) {
-                xa[i] = x0;
-                xb[i] = x1;
-            }
-        }
+            cc = ld_stream<NT>(reinterpret_cast<const unsigned *>(a.cols16 + n0 + vofs + pstart + 2 * hl));
+        const int c0 = colbase + (int)(cc & 0xffffu);
+        const int c1 = (valid && 2 * hl + 1 < wc) ? colbase + (int)(cc >> 16) : c0 + 1;
+        const int base = min(c0, a.n - 2);
+        const double2 xx = *reinterpret_cast<const double2 *>(a.x + base);
+        const double x0 = base == c0 ? xx.x : xx.y;
+        double x1 = xx.y;  // c1 == c0 + 1 <= n - 1: base == c0
+        if (c1 != c0 + 1)
+            x1 = a.x[c1];
         double pr[kBlkRows];
 #pragma unroll
         for (int i = 0; i < kBlkRows; ++i)
-            pr[i] = i < KR ? (in0[i] ? v[i].x * xa[i] : 0.0) + (in1[i] ? v[i].y * xb[i] : 0.0) : 0.0;
-        const double sum = RL == 32 ? rows8_sum32(pr) : rows8_sum16(pr);
-        constexpr int RS = RL / 8;  // lanes per row slot
-        const int myrow = hl / RS;
-        if (valid && hl % RS == 0 && myrow < h)
+            pr[i] = i < KR ? (in0[i] ? v[i].x * x0 : 0.0) + (in1[i] ? v[i].y * x1 : 0.0) : 0.0;
+        const double sum = rows8_sum32(pr);
+        const int myrow = hl >> 2;
+        if (valid && (hl & 3) == 0 && myrow < h)
             a.y[r0 + rofs + myrow] = sum;
     }
 }
@@ -1699,10 +1606,8 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
     uint4 bd = make_uint4(0u, 0u, 0u, 0u);
     if (BLK && a.blk && (tid & 63) < a.blk_stride)
         bd = a.blk[(size_t)t * a.blk_stride + (tid & 63)];
-    const unsigned bd0y = (BLK && a.blk) ? (unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) : 0u;
-    int nblk = (int)((bd0y >> 8) & 127u);
-    // more than one round of runs, or shifted runs: striped staging here (k_spmv_blk takes them)
-    if (nblk > kBlkTileChunks || (bd0y & 0x8000u))
+    int nblk = (BLK && a.blk) ? (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u) : 0;
+    if (nblk > kBlkTileChunks)  // more than one round of runs: striped staging here (k_spmv_blk takes them)
         nblk = 0;
     bool staged = false;
     // every run one chunk wide (block-uniform: each wave holds all descriptors): no LDS at all
@@ -1799,8 +1704,8 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
 // Register fallback of the plain node-block SpMV for the tiles of a mixed plan that are not register
 // run tiles (rows outside any run pattern, patterns wider than 64 columns, split boundaries): groups
 // of G lanes take the tile's row segments round-robin (its whole rows, then the trailing partial row
-// of a split boundary), lane j of a group sums products j, j + G, ... of its segment in order with
-// four loads in flight, a fixed xor butterfly folds the group and its lane 0 stores the row (the
+// of a split boundary), lane j of a group sums products j, j + G, ... of its segment in order, a
+// fixed xor butterfly folds the group and its lane 0 stores the row (the
 // trailing partial row: the tile's carry, which k_fixup adds).  No LDS, so the kernel keeps its
 // register-only occupancy.  G is the smallest power of two with 4 G >= the tile's mean segment
 // length.  Reproducible, and within the 2 (len+1) eps (|A||x|)_i reordering bound of the CSR-order
@@ -1826,23 +1731,7 @@ __device__ __forceinline__ void tile_rows_reg(const TileArgs &a, int t, int r0, 
         const int s0 = r == 0 ? 0 : a.row_offsets[r0 + r] - n0;
         const int e = r < nrows ? a.row_offsets[r0 + r + 1] - n0 : nnzt;
         double v = 0.0;
-        int k = s0 + lane;
-        for (; k + 3 * G < e; k += 4 * G) {
-            int c[4];
-            double w[4], xv[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                c[u] = col(k + u * G);
-                w[u] = ld_stream<NT>(a.vals + n0 + k + u * G);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                xv[u] = a.x[c[u]];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                v += w[u] * xv[u];
-        }
-        for (; k < e; k += G)
+        for (int k = s0 + lane; k < e; k += G)
             v += ld_stream<NT>(a.vals + n0 + k) * a.x[col(k)];
         for (int off = G >> 1; off > 0; off >>= 1)
             v += __shfl_xor(v, off);
@@ -1868,14 +1757,12 @@ struct BlkSmem {
     int last;
 };
 
-// 8 workgroups (32 waves) per CU: <= 64 VGPRs, and SGPRs capped at 80 -- 256-thread workgroups are
-// admitted 8 per CU only up to .sgpr_count 80 (7 at 82-96, MI355X_MICROARCH.md "Residency"); the
-// register fallback's loop would otherwise take 84 SGPRs and 65 VGPRs.  The shifted-run form holds
-// the runs' x sweeps: 6 waves per SIMD (80 VGPRs; unconstrained it took 84, 5 waves).
-constexpr int spmv_blk_waves(int MODE, bool SHIFT) { return MODE != 0 ? 1 : SHIFT ? 6 : 8; }
-template <int MODE, bool NT, int KR = kBlkRows, int RL = 32, bool SHIFT = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80)))
-__attribute__((amdgpu_waves_per_eu(spmv_blk_waves(MODE, SHIFT)))) void k_spmv_blk(TileArgs a)
+// FB (plain SpMV): the plan has tiles that are not register run tiles, so the register fallback is
+// compiled in; without it the kernel takes 62 SGPRs, with it 84 -- and 256-thread workgroups are
+// admitted 8 per CU only up to .sgpr_count 80 (7 at 82-96, MI355X_MICROARCH.md "Residency"), so plans
+// of run tiles only keep the lean form.
+template <int MODE, bool NT, int KR = kBlkRows, bool FB = false>
+__global__ __launch_bounds__(kBlock) void k_spmv_blk(TileArgs a)
 {
     constexpr bool CG = MODE == kModeCg;
     __shared__ BlkSmem sm;
@@ -1886,7 +1773,7 @@ __attribute__((amdgpu_waves_per_eu(spmv_blk_waves(MODE, SHIFT)))) void k_spmv_bl
     const int colbase = a.colbase[t];
     const uint4 bd =
         (tid & 63) < a.blk_stride ? a.blk[(size_t)t * a.blk_stride + (tid & 63)] : make_uint4(0u, 0u, 0u, 0u);
-    const int nblk = (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 127u);
+    const int nblk = (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u);
     double beta = 0.0, dot = 0.0;
     bool go = true;
     PartRegs<CG ? kUpdateMaxBlocks / kBlock : 1> pin;
@@ -1897,11 +1784,14 @@ __attribute__((amdgpu_waves_per_eu(spmv_blk_waves(MODE, SHIFT)))) void k_spmv_bl
             return;
         // a register run tile: every chunk starts at pattern column 0 (wave-uniform: each wave holds
         // all descriptors)
-        const bool reg = nblk > 0 && __ballot((tid & 63) < nblk && ((bd.x >> 16) & 255u) != 0) == 0;
-        if (reg)
-            blk_rows_pair<NT, KR, RL, SHIFT>(a, bd, nblk, b0.x, b0.y, colbase);
-        else
-            tile_rows_reg<NT>(a, t, b0.x, b0.y, a.cols16 ? colbase : -1);
+        if constexpr (FB) {
+            const bool reg = nblk > 0 && __ballot((tid & 63) < nblk && ((bd.x >> 16) & 255u) != 0) == 0;
+            if (!reg) {
+                tile_rows_reg<NT>(a, t, b0.x, b0.y, a.cols16 ? colbase : -1);
+                return;
+            }
+        }
+        blk_rows_pair<NT, KR>(a, bd, nblk, b0.x, b0.y, colbase);
         return;
     }
     blk_rows<MODE, NT, kBlock>(a, bd, nblk, b0.x, b0.y, colbase, beta, dot, [&]() {
@@ -2343,7 +2233,7 @@ k_spmm_blk(TileArgs a)
     const int r0 = b0.x, n0 = b0.y;
     const int colbase = a.colbase[t];
     const uint4 bd = lane < a.blk_stride ? a.blk[(size_t)t * a.blk_stride + lane] : make_uint4(0u, 0u, 0u, 0u);
-    const int nd = (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 127u);
+    const int nd = (int)(((unsigned)__builtin_amdgcn_readfirstlane((int)bd.y) >> 8) & 255u);
     const int wave = __builtin_amdgcn_readfirstlane((int)(tid >> 6));
     double2 dot = make_double2(0.0, 0.0);
     // lane j: P[j] and the run's values in column j of chunk di, one coalesced load per row
@@ -3255,8 +3145,7 @@ std::string spmv_kernel_name(const mspmv_handle_s *h)
     const std::string nt = stream_nt(h) ? "true" : "false";
     const auto it = h->plans.find(plan_key(1));
     if (h->spmv_onewave != 1 && it != h->plans.end() && it->second.blk_spmv)
-        return "k_spmv_blk<0," + nt + ",6," + std::to_string(it->second.blk_rl) + "," +
-               (it->second.num_tiles_shift ? "true>" : "false>");
+        return "k_spmv_blk<0," + nt + (it->second.num_tiles_reg == it->second.num_tiles ? ",6>" : ",6,true>");
     return "k_spmv_tile<" + std::to_string(kSpmvIpt) + ",0," + nt + (h->spmv_onewave == 1 ? ",64>" : ">");
 }
 
@@ -3273,7 +3162,7 @@ std::string spmm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan, int 
     if (L == 1)
         return spmv_kernel_name(h);
     const std::string nt = stream_nt(h) ? "true" : "false";
-    if (plan.d_blk && plan.num_tiles_reg == plan.num_tiles && plan.num_tiles_shift == 0 && spmm_blk_enabled())
+    if (plan.d_blk && plan.num_tiles_reg == plan.num_tiles && spmm_blk_enabled())
         return "k_spmm_blk<" + std::to_string(L) + ",0," + nt + "," + std::to_string(blk_kr(plan)) + ">";
     const int iptg = spmm_iptg_for(L);
     const bool dict = L == 16 && plan.d_dict;
@@ -3420,11 +3309,8 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
         a.blk_stride = plan.blk_stride;
         // L > 1 runs the node-block plan only while k_spmm_blk is enabled (get_plan's gate): L = 2
         // shares the single-RHS tile size, so without this the switched-off plan would still be all-reg
-        a.all_reg = plan.d_blk && plan.num_tiles_reg == plan.num_tiles && plan.num_tiles_shift == 0 &&
-                    (L == 1 || spmm_blk_enabled());
+        a.all_reg = plan.d_blk && plan.num_tiles_reg == plan.num_tiles && (L == 1 || spmm_blk_enabled());
         a.blk_spmv = L == 1 && plan.blk_spmv;
-        a.blk_rl = plan.blk_rl;
-        a.blk_shift = plan.num_tiles_shift > 0;
         a.blk_rows_max = plan.blk_rows_max;
     }
     a.dict = plan.d_dict;
@@ -3480,21 +3366,6 @@ static void launch_spmm_L(const TileArgs &a, hipStream_t s, bool nt)
     launch_spmm_nt<LL, (LL >= 8 ? 16 : 8), MODE>(a, s, nt);
 }
 
-template <bool NT>
-static void launch_blk_pairs(const TileArgs &a, dim3 grid, dim3 block, hipStream_t s)
-{
-    if (a.blk_rl == 16) {
-        if (a.blk_shift)
-            ggl(k_spmv_blk<kModeSpmv, NT, 6, 16, true>, grid, block, s, a);
-        else
-            ggl(k_spmv_blk<kModeSpmv, NT, 6, 16, false>, grid, block, s, a);
-    } else if (a.blk_shift) {
-        ggl(k_spmv_blk<kModeSpmv, NT, 6, 32, true>, grid, block, s, a);
-    } else {
-        ggl(k_spmv_blk<kModeSpmv, NT, 6, 32, false>, grid, block, s, a);
-    }
-}
-
 // MODE 1 (pipelined single-RHS CG) exists for L == 1 in the one-tile kernel only.
 template <int MODE>
 static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, bool nt)
@@ -3507,10 +3378,12 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, bool nt)
         if (MODE == kModeSpmv && a.blk_spmv) {
             // a node-block plan (every tile, or most: the rest run the kernel's register fallback):
             // the LDS-free kernel, column pairs, runs of <= 6 rows
-            if (nt)
-                launch_blk_pairs<true>(a, grid, block, s);
+            if (a.all_reg)  // every tile a register run tile: no register fallback compiled in
+                nt ? ggl(k_spmv_blk<kModeSpmv, true, 6>, grid, block, s, a)
+                   : ggl(k_spmv_blk<kModeSpmv, false, 6>, grid, block, s, a);
             else
-                launch_blk_pairs<false>(a, grid, block, s);
+                nt ? ggl(k_spmv_blk<kModeSpmv, true, 6, true>, grid, block, s, a)
+                   : ggl(k_spmv_blk<kModeSpmv, false, 6, true>, grid, block, s, a);
         } else if (MODE == kModeDot && a.all_reg) {
             // every tile a register node-block tile, dot mode (the row-sharded CG): column owners
             if (nt)

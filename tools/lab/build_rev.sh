@@ -10,6 +10,7 @@ TMP=$(mktemp -d)
 trap 'rm -rf "$TMP"' EXIT
 git archive "$REV" sparse-matrix-linear-equations_amd/csrc include | tar -x -C "$TMP"
 mkdir -p "$TMP/sparse-matrix-linear-equations_amd/mspmv"
-make -s -C "$TMP/sparse-matrix-linear-equations_amd/csrc" -j8
+C=$TMP/sparse-matrix-linear-equations_amd/csrc
+make -s -C "$C" -j8 "$C/../mspmv/libmspmv.so"
 cp "$TMP/sparse-matrix-linear-equations_amd/mspmv/libmspmv.so" "tools/lab/libmspmv_$NAME.so"
 echo "tools/lab/libmspmv_$NAME.so <- $REV"
