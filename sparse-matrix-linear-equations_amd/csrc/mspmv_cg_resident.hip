@@ -121,10 +121,15 @@ __device__ __forceinline__ double res_block_sum(double v, double *s_red)
 // workgroup meets, one lane stores the partial (sc1) -- the flag of the hand-off.
 // A NaN partial is published as the canonical quiet NaN: a payload equal to kSlotEmpty (b memset
 // to 0xFF) would otherwise read as "not published yet" and the solve would stall instead of
-// reporting the breakdown.
+// reporting the breakdown.  DRAIN: every storing wave's payload stores complete before the flag --
+// needed only where the flag hands payload over (r.r: the {r, p} pairs the next iteration gathers);
+// the p.Ap hand-off carries none (the p stores it follows are drained by the r.r publish, which every
+// reader waits for before its next gathers), so its partial goes out without waiting for them.
+template <bool DRAIN>
 __device__ __forceinline__ void res_publish(double part, double *slot, double *s_red)
 {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its payload is out
+    if (DRAIN)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its payload is out
     double t = res_block_sum(part, s_red);             // (contains the workgroup barrier)
     if (threadIdx.x == 0) {
         if (t != t)
@@ -248,7 +253,7 @@ __global__ __launch_bounds__(kRB) void k_cg_resident(ResArgs a)
         }
     }
     __syncthreads();  // s_col complete
-    res_publish(bb, a.slots + w, s_red);
+    res_publish<true>(bb, a.slots + w, s_red);
     int iters = a.max_iters, brk = 0;
     if (!res_wait_sum<NSL>(a.slots, G, a.abort_word, &s_tot, &s_ok)) {
         iters = 0;
@@ -295,7 +300,7 @@ __global__ __launch_bounds__(kRB) void k_cg_resident(ResArgs a)
             if (a.stamps)
                 __syncthreads();  // stamped solves: the phase ends when every wave's rows are done
             res_stamp(a, k, w, 1);
-            res_publish(dot, slot_a + w, s_red);
+            res_publish<false>(dot, slot_a + w, s_red);
             if (!res_wait_sum<NSL>(slot_a, G, a.abort_word, &s_tot, &s_ok)) {
                 iters = k;
                 brk = 2;
@@ -323,7 +328,7 @@ __global__ __launch_bounds__(kRB) void k_cg_resident(ResArgs a)
             if (a.stamps)
                 __syncthreads();
             res_stamp(a, k, w, 3);
-            res_publish(rr, slot_b + w, s_red);
+            res_publish<true>(rr, slot_b + w, s_red);
             if (!res_wait_sum<NSL>(slot_b, G, a.abort_word, &s_tot, &s_ok)) {
                 iters = k;
                 brk = 2;
