@@ -70,7 +70,8 @@ def pmc_traffic(kernel, bytes_launch):
             continue
         for name, v in d.get("kernels", {}).items():
             short = name.replace("void mspmv::", "").split("(")[0].replace(" ", "")
-            if short.replace(",256>", ">") == kernel:  # the default threads-per-tile argument
+            norm = lambda k: k.replace(",256>", ">").replace(",6,false>", ",6>")  # noqa: E731  default arguments
+            if norm(short) == norm(kernel):
                 return v["traffic_bytes"], os.path.basename(path)
     return None, None
 PWTK = dict(m=217918, nnz=11524432, block=6, half_band_nodes=1700)

@@ -3145,7 +3145,7 @@ std::string spmv_kernel_name(const mspmv_handle_s *h)
     const std::string nt = stream_nt(h) ? "true" : "false";
     const auto it = h->plans.find(plan_key(1));
     if (h->spmv_onewave != 1 && it != h->plans.end() && it->second.blk_spmv)
-        return "k_spmv_blk<0," + nt + (it->second.num_tiles_reg == it->second.num_tiles ? ",6>" : ",6,true>");
+        return "k_spmv_blk<0," + nt + (it->second.num_tiles_reg == it->second.num_tiles ? ",6,false>" : ",6,true>");
     return "k_spmv_tile<" + std::to_string(kSpmvIpt) + ",0," + nt + (h->spmv_onewave == 1 ? ",64>" : ">");
 }
 

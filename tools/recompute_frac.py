@@ -98,7 +98,8 @@ def main(src, dst):
         write_csv(rows, out("headline_kernel_grid_stats.csv"))
         prof_bench = last_json(os.path.join(src, "prof_bench.json"))
         rf = prof_bench["roofline"]
-        kr = max((r for r in rows if r["kernel"].replace(",256>", ">") == rf["kernel"]), key=lambda r: r["grid"])
+        norm = lambda k: k.replace(",256>", ">").replace(",6,false>", ",6>")  # noqa: E731  default template arguments
+        kr = max((r for r in rows if norm(r["kernel"]) == norm(rf["kernel"])), key=lambda r: r["grid"])
         lines.append(f"| headline {rf['kernel']} | frac {bench['roofline']['frac'] if bench else '-'} "
                      f"(kernel_ms {bench['roofline']['kernel_ms'] if bench else '-'}) | frac "
                      f"{frac(rf['bytes_per_launch'], kr['avg_us']):.4f} (avg {kr['avg_us']} us, median "
@@ -106,7 +107,10 @@ def main(src, dst):
         if os.path.isdir(os.path.join(src, "pmc_fetch")):
             pmc_traffic.main(["", src, out("pmc_traffic.json")])
 
-    for leg in ("spmm16", "spmv_shapes", "cg_single", "cg_multi"):
+    if tr and os.path.exists(os.path.join(src, "prof", "bench_kernel_stats.csv")):  # rocprofv3's own --stats
+        open(out("headline_kernel_stats.csv"), "w").write(open(os.path.join(src, "prof", "bench_kernel_stats.csv")).read())
+
+    for leg in ("spmm16", "spmv_shapes", "cg_single", "cg_multi", "pwtk_perturbed"):
         ld = os.path.join(src, leg)
         if not os.path.isdir(ld):
             continue
@@ -117,7 +121,16 @@ def main(src, dst):
         write_csv(rows, out(f"{leg}_kernel_grid_stats.csv"))
         if os.path.isdir(os.path.join(ld, "pmc_fetch")) and os.path.isdir(os.path.join(ld, "pmc_write")):
             pmc_traffic.main(["", "--leg", ld, out(f"{leg}_pmc_traffic.json")])
-        if leg in ("spmm16", "spmv_shapes"):
+        st = os.path.join(ld, "prof", "leg_kernel_stats.csv")
+        if os.path.exists(st):
+            open(out(f"{leg}_kernel_stats.csv"), "w").write(open(st).read())
+        if leg == "pwtk_perturbed":
+            norm = lambda k: k.replace(",6,false>", ",6>")  # noqa: E731
+            kr = max((r for r in rows if norm(r["kernel"]) == norm(lj["kernel"])), key=lambda r: r["calls"])
+            lines.append(f"| {leg} {lj['kernel']} | frac {lj['frac']} (kernel_ms {lj['kernel_ms']}) | frac "
+                         f"{frac(lj['bytes_per_launch'], kr['avg_us']):.4f} (avg {kr['avg_us']} us, median "
+                         f"{kr['median_us']} us) | {kr['kernel']} grid {kr['grid']} x{kr['calls']} |")
+        elif leg in ("spmm16", "spmv_shapes"):
             L = 16 if leg == "spmm16" else 1
             shapes = [k for k in (("cant", "pwtk") if leg == "spmm16" else ("cant", "rma10", "powerlaw")) if k in lj]
             cold = sorted((r for r in rows if r["after_flush"] and r["kernel"].startswith(("k_spmm", "k_spmv"))),
