@@ -90,9 +90,8 @@ static void free_plan(TilePlan &p)
     dev_free(p.d_split);
     for (auto &m : p.d_modes)
         dev_free(m);
-    dev_free(p.d_carry_tiles);
-    dev_free(p.d_carry_rows);
-    dev_free(p.d_carry_runs);
+    dev_free(p.d_fix);
+    dev_free(p.d_fix_cnt);
     dev_free(p.d_carry_val);
     dev_free(p.d_colbase);
     dev_free(p.d_cols16);
@@ -178,7 +177,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         // tile lifetime more (the parabolic_fem shape: 2,052 tiles on 2,048 slots).  Stretch the
         // tiles into the snap slack so they fit one generation fewer: MAXI (step + snap) is
         // unchanged, rows entered by more than the smaller snap distance stay split (carries,
-        // k_fixup).  (Measured against nominal tiles in round 3: kept.)
+        // close_split_rows).  (Measured against nominal tiles in round 3: kept.)
         const long long slots = (long long)h->num_cus * spmv_tile_blocks_per_cu();
         const long long t0 = (total + tile - 1) / tile;
         if (slots > 0 && t0 > slots) {
@@ -197,7 +196,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
     mspmv_status st;
     if ((st = dev_alloc(&p.d_bounds, (size_t)T + 1)) != MSPMV_OK ||
         (st = dev_alloc(&p.d_split, (size_t)T + 1)) != MSPMV_OK ||
-        (st = dev_alloc(&p.d_carry_val, (size_t)std::max(T, 1) * 16)) != MSPMV_OK) {
+        (st = dev_alloc(&p.d_carry_val, (size_t)std::max(T, 1) * 16 * 3)) != MSPMV_OK) {  // carries, heads x 2
         free_plan(p);
         return st;
     }
@@ -226,38 +225,44 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         set_error("tile plan: bad end boundaries");
         return fail(MSPMV_ERR_INVALID);
     }
-    std::vector<int> ct, cr;
+    std::vector<int4> fix((size_t)T, make_int4(-1, 0, 0, 0));
+    int num_carries = 0;
     for (int t = 0; t < T; ++t) {
         const int nr = hb[t + 1].x - hb[t].x, nz = hb[t + 1].y - hb[t].y;
         if (nr < 0 || nz < 0 || nr + nz > maxi) {
             set_error("tile plan: tile " + std::to_string(t) + " violates the merge bound");
             return fail(MSPMV_ERR_INVALID);
         }
-        if (hs[t + 1]) {
-            ct.push_back(t);
-            cr.push_back(hb[t + 1].x);
-        }
+        if (hs[t + 1])
+            ++num_carries;
     }
-    p.num_carries = (int)ct.size();
-    if (p.num_carries) {
-        if ((st = dev_alloc(&p.d_carry_tiles, ct.size())) != MSPMV_OK ||
-            (st = dev_alloc(&p.d_carry_rows, cr.size())) != MSPMV_OK)
+    // Split rows: the tiles t0 .. t1 - 1 that end inside one row carry into the tile t1 that completes
+    // it (the first tile after them with no carry into the same row; the last tile always ends on m).
+    for (int t = 0; t < T;) {
+        if (!hs[t + 1]) {
+            ++t;
+            continue;
+        }
+        const int t0 = t;
+        while (t < T && hs[t + 1] && hb[t + 1].x == hb[t0 + 1].x)
+            ++t;
+        if (t >= T) {
+            set_error("tile plan: split row past the last tile");
+            return fail(MSPMV_ERR_INVALID);
+        }
+        for (int u = t0; u < t; ++u) {
+            fix[(size_t)u].x = t;
+            fix[(size_t)u].y = t - t0;
+        }
+        fix[(size_t)t].z = t - t0;
+    }
+    p.num_carries = num_carries;
+    if (num_carries) {
+        if ((st = dev_alloc(&p.d_fix, (size_t)T)) != MSPMV_OK || (st = dev_alloc(&p.d_fix_cnt, (size_t)T)) != MSPMV_OK)
             return fail(st);
-        // runs of consecutive carries of one row (a hub row split over many tiles: hundreds), each
-        // summed by one wave of the fix-up
-        std::vector<int> runs;
-        for (size_t i = 0; i < cr.size(); ++i)
-            if (i == 0 || cr[i] != cr[i - 1])
-                runs.push_back((int)i);
-        p.num_carry_runs = (int)runs.size();
-        runs.push_back((int)cr.size());
-        if ((st = dev_alloc(&p.d_carry_runs, runs.size())) != MSPMV_OK)
-            return fail(st);
-        e = hipMemcpy(p.d_carry_tiles, ct.data(), sizeof(int) * ct.size(), hipMemcpyHostToDevice);
+        e = hipMemcpy(p.d_fix, fix.data(), sizeof(int4) * fix.size(), hipMemcpyHostToDevice);
         if (e == hipSuccess)
-            e = hipMemcpy(p.d_carry_rows, cr.data(), sizeof(int) * cr.size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess)
-            e = hipMemcpy(p.d_carry_runs, runs.data(), sizeof(int) * runs.size(), hipMemcpyHostToDevice);
+            e = hipMemset(p.d_fix_cnt, 0, sizeof(unsigned) * T);
         if (e != hipSuccess) {
             set_error(std::string("tile plan upload: ") + hipGetErrorString(e));
             return fail(MSPMV_ERR_HIP);
@@ -1677,58 +1682,48 @@ mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y,
         h->flush_cap = flush_bytes;
         HIP_TRY(launch_flush(h->d_flush, flush_bytes, h->stream, true));  // defined contents (+1.0)
     }
-    // Per launch: the tile kernel's first workgroup start to the last kernel's end (the carry fix-up's,
-    // when the plan splits rows: the product is complete only after it), recorded by the kernels
-    // themselves (set_launch_events -> hipExtLaunchKernel), so the dispatch gap after the flush is not
-    // in the per-launch time.  ev[2 reps] closes the whole region (flushes included) for avg_ms.
-    std::vector<hipEvent_t> ev((size_t)reps * 2 + 2, nullptr);
-    for (auto &e : ev)
-        HIP_TRY(hipEventCreate(&e));
+    // Hot (flush_bytes == 0): reps launches back to back, events around the region only; per launch
+    // = region / reps (the launch gap included, ~0.2 us: r04i's headline 21.06 us against 21.09 in the
+    // trace).  Cold: the region of reps (flush, launch) pairs minus a control region of reps flushes
+    // alone, / reps -- per-launch events (stream events, or hipExtLaunchKernel's kernel-boundary ones)
+    // measured 4.7 us over the traced kernel on cant and rma10 (r04i_frac_check.md).  avg_ms: the whole
+    // timed region per launch (flushes included).
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (auto &x : ev)
+        HIP_TRY(hipEventCreate(&x));
     hipError_t e = hipSuccess;
-    const bool fix = plan->num_carries > 0;
-    if (plan->num_tiles > 0) {
+    const bool run = plan->num_tiles > 0;
+    if (flush_bytes && run)  // the control region first: flushes alone
+        e = hipEventRecord(ev[2], h->stream);
+    for (int i = 0; i < reps && e == hipSuccess && flush_bytes && run; ++i)
+        e = launch_flush(h->d_flush, flush_bytes, h->stream, false);
+    if (e == hipSuccess)
+        e = hipEventRecord(ev[3], h->stream);
+    if (e == hipSuccess)
+        e = hipEventRecord(ev[0], h->stream);
+    for (int i = 0; i < reps && e == hipSuccess && run; ++i) {
         if (flush_bytes)
             e = launch_flush(h->d_flush, flush_bytes, h->stream, false);
         if (e == hipSuccess)
-            e = hipEventRecord(ev[2 * reps + 1], h->stream);  // start of the whole region
-    }
-    for (int i = 0; i < reps && e == hipSuccess && plan->num_tiles > 0; ++i) {
-        if (flush_bytes && i > 0)
-            e = launch_flush(h->d_flush, flush_bytes, h->stream, false);
-        if (e == hipSuccess) {
-            set_launch_events(ev[2 * i], fix ? nullptr : ev[2 * i + 1]);
             e = launch_spmm_tile_only(h, *plan, d_X, d_Y, L);
-        }
-        if (e == hipSuccess && fix) {
-            set_launch_events(nullptr, ev[2 * i + 1]);
-            e = launch_fixup(h, *plan, d_Y, L);
-        }
-        set_launch_events(nullptr, nullptr);
     }
-    if (plan->num_tiles == 0)
-        for (int i = 0; i < 2 * reps + 2 && e == hipSuccess; ++i)
-            e = hipEventRecord(ev[(size_t)i], h->stream);
     if (e == hipSuccess)
-        e = hipEventRecord(ev[2 * reps], h->stream);
+        e = hipEventRecord(ev[1], h->stream);
     if (e == hipSuccess)
-        e = hipEventSynchronize(ev[2 * reps]);
-    double sum_tile = 0.0;
-    float ms = 0.f;
-    for (int i = 0; i < reps && e == hipSuccess; ++i) {
-        e = hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]);
-        sum_tile += ms;
-    }
-    float total = 0.f;
+        e = hipEventSynchronize(ev[1]);
+    float total = 0.f, control = 0.f;
     if (e == hipSuccess)
-        e = hipEventElapsedTime(&total, ev[2 * reps + 1], ev[2 * reps]);
+        e = hipEventElapsedTime(&total, ev[0], ev[1]);
+    if (e == hipSuccess && flush_bytes && run)
+        e = hipEventElapsedTime(&control, ev[2], ev[3]);
     for (auto &x : ev)
         (void)hipEventDestroy(x);
     if (e != hipSuccess) {
         set_error(std::string("timing: ") + hipGetErrorString(e));
         return MSPMV_ERR_HIP;
     }
-    h->last_tile_kernel_ms = sum_tile / reps;
-    h->last_kernels_per_call = 1 + (plan->num_carries ? 1 : 0);
+    h->last_tile_kernel_ms = std::max(0.0, (double)(total - control)) / reps;
+    h->last_kernels_per_call = run ? 1 : 0;
     *avg_ms = (double)total / reps;
     return MSPMV_OK;
 }
@@ -1753,26 +1748,22 @@ mspmv_status mspmv_time_spmm_batch_dev(int count, const mspmv_handle *hs, const 
     int kps = 0;
     for (int i = 0; i < count; ++i) {
         ST_TRY(get_plan(hs[i], L, &plans[i], true));
-        kps += (plans[i]->num_tiles ? 1 : 0) + (plans[i]->num_carries ? 1 : 0);
+        kps += plans[i]->num_tiles ? 1 : 0;
     }
     hipStream_t s = hs[0]->stream;
     for (int i = 0; i < count; ++i)  // everything after this point is ordered on hs[0]'s stream
         HIP_TRY(hipStreamSynchronize(hs[i]->stream));
-    // Pass 1 (the timed steps): launches back to back, events only around the whole region.
-    // Pass 2 (only when a step also holds fix-up kernels): events around every tile launch.
-    const bool has_fixups = kps > count;
-    const size_t nev = 2 + (has_fixups && tile_kernel_ms ? (size_t)reps * count * 2 : 0);
-    std::vector<hipEvent_t> ev(nev, nullptr);
-    for (auto &e : ev)
-        HIP_TRY(hipEventCreate(&e));
+    // The timed steps: launches back to back, events only around the whole region (one kernel per
+    // product: split rows are closed inside the tile kernel).
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    for (auto &x : ev)
+        HIP_TRY(hipEventCreate(&x));
     hipError_t e = hipEventRecord(ev[0], s);
     for (int r = 0; r < reps && e == hipSuccess; ++r)
         for (int i = 0; i < count && e == hipSuccess; ++i) {
             hipStream_t own = hs[i]->stream;
             hs[i]->stream = s;
             e = launch_spmm_tile_only(hs[i], *plans[i], d_X[i], d_Y[i], L);
-            if (e == hipSuccess)
-                e = launch_fixup(hs[i], *plans[i], d_Y[i], L);
             hs[i]->stream = own;
         }
     if (e == hipSuccess)
@@ -1782,36 +1773,7 @@ mspmv_status mspmv_time_spmm_batch_dev(int count, const mspmv_handle *hs, const 
     float total = 0.f;
     if (e == hipSuccess)
         e = hipEventElapsedTime(&total, ev[0], ev[1]);
-    double sum = (double)total;  // no fix-ups: every launch of the region is a tile kernel
-    size_t k = 2;
-    if (e == hipSuccess && nev > 2) {
-        for (int r = 0; r < reps && e == hipSuccess; ++r)
-            for (int i = 0; i < count && e == hipSuccess; ++i) {
-                hipStream_t own = hs[i]->stream;
-                hs[i]->stream = s;
-                if (plans[i]->num_tiles > 0) {  // the tile kernel's own start / end (set_launch_events)
-                    set_launch_events(ev[k], ev[k + 1]);
-                    e = launch_spmm_tile_only(hs[i], *plans[i], d_X[i], d_Y[i], L);
-                    set_launch_events(nullptr, nullptr);
-                } else {
-                    e = hipEventRecord(ev[k], s);
-                    if (e == hipSuccess)
-                        e = hipEventRecord(ev[k + 1], s);
-                }
-                k += 2;
-                if (e == hipSuccess)
-                    e = launch_fixup(hs[i], *plans[i], d_Y[i], L);
-                hs[i]->stream = own;
-            }
-        if (e == hipSuccess)
-            e = hipEventSynchronize(ev[k - 1]);
-        sum = 0.0;
-        float ms = 0.f;
-        for (size_t j = 2; j + 1 < k && e == hipSuccess; j += 2) {
-            e = hipEventElapsedTime(&ms, ev[j], ev[j + 1]);
-            sum += ms;
-        }
-    }
+    const double sum = (double)total;
     for (auto &x : ev)
         (void)hipEventDestroy(x);
     if (e != hipSuccess) {

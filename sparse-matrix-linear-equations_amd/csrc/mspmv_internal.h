@@ -29,8 +29,10 @@ constexpr int kUpdateMaxBlocks = 1024;
 // row was entered by at most `snap` nonzeros is moved back to that row's start ("row
 // snapped"): the row is then computed whole by the tile that completes it, so no carry
 // crosses that boundary.  Boundaries deeper inside a long row stay exact merge-path
-// coordinates ("split") and the tile before them writes a carry that a small fix-up
-// kernel adds in tile order.  Every tile holds at most tile_items + tile_items/kSnapDiv items.
+// coordinates ("split"): the tiles that end inside such a row store carries, the tile that completes
+// it stores the row's own part, and the last of them to finish adds the carries in tile order
+// (close_split_rows: one ticket per row, no fix-up launch).  Every tile holds at most tile_items +
+// tile_items/kSnapDiv items.
 struct TilePlan {
     int lanes = kBlock;                 // threads sharing one tile: 256, or 64 (one-wave plain-SpMV plan)
     int tile_items = 0;
@@ -42,11 +44,13 @@ struct TilePlan {
     // tile size across L): 0 merge walk, lg+1 row groups of 2^lg nonzero lanes (k_tile_modes)
     unsigned char *d_modes[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     int num_carries = 0;                // tiles whose trailing boundary is split
-    int *d_carry_tiles = nullptr;       // [num_carries] tile ids, ascending
-    int *d_carry_rows = nullptr;        // [num_carries] row each carry belongs to
-    double *d_carry_val = nullptr;      // [num_tiles * L_max]
-    int num_carry_runs = 0;             // maximal runs of consecutive carries of one row
-    int *d_carry_runs = nullptr;        // [num_carry_runs + 1] first carry of each run, then num_carries
+    double *d_carry_val = nullptr;      // [3][num_tiles][carry_L]: carries, then the split rows' heads
+                                        // (TileArgs::head_val, head_pub)
+    // Split rows (null when num_carries == 0): fix[t] = {the tile completing the row tile t ends inside
+    // (-1: t ends on a row boundary), that row's carry count, the carry count of the row tile t
+    // completes (0: none), 0}; fix_cnt[t] = tickets of the row tile t completes (reset by its closer).
+    int4 *d_fix = nullptr;              // [num_tiles]
+    unsigned *d_fix_cnt = nullptr;      // [num_tiles]
     int carry_L = 0;                    // capacity (columns) of d_carry_val
     // Single-RHS plans: 16-bit column offsets.  A tile whose columns span < 65536 stores
     // col - colbase[t] in cols16 (2 B per nonzero instead of 4 in the HBM stream); colbase[t]
@@ -226,7 +230,6 @@ hipError_t launch_panel_copy(const double *src, int lds, double *dst, int ldd, l
 // ld: panel leading dimension in doubles (0: L, whole panels)
 hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
                                  int ld = 0);
-hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L, int ld = 0);
 // Nominal tile size (merge items per tile) used for L right-hand sides.
 int tile_items_for(int L);
 // Map key of the default plan for L (one-wave plans are keyed by minus their tile size: 512 is also
@@ -239,9 +242,6 @@ hipError_t launch_stream_read(const double *p, size_t bytes, int num_cus, hipStr
 std::string spmv_kernel_name(const mspmv_handle_s *h);
 std::string spmm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan, int L);
 bool stream_nt(const mspmv_handle_s *h);
-// Kernel-boundary timing: the next product launch records start / stop at its own first workgroup's
-// start and last workgroup's end (null: none).  Consumed by that launch.
-void set_launch_events(hipEvent_t start, hipEvent_t stop);
 bool supported_L(int L);
 
 // CG pieces

@@ -12,13 +12,11 @@
 //     double2 of the row-major panel per lane) runs its own merge-path search in LDS and
 //     walks an equal share of merge items;
 //   * rows split between threads are closed in LDS in thread order; rows split between
-//     tiles (only inside rows longer than the snap distance) are closed by k_fixup in
-//     tile order.  All reductions are fixed-order: results are run-to-run deterministic.
+//     tiles (only inside rows longer than the snap distance) are closed by the tile that
+//     completes them, in tile order (close_split_rows).  All reductions are fixed-order: results are run-to-run deterministic.
 //   * tiles are dealt XCD-contiguously (blocks b and b+8 share an XCD), so each XCD's L2
 //     sees one contiguous band of x / X.
 #include "mspmv_internal.h"
-
-#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <type_traits>
@@ -49,21 +47,10 @@ __device__ __forceinline__ int xcd_tile(int b, int T, int K = 1)
     return base + s * q2 + (s < r2 ? s : r2) + pos;
 }
 
-// Kernel-boundary timing events (mspmv_time_spmm_dev): the next product launch through ggl() records
-// `start` when its first workgroup starts and `stop` when its last one ends (hipExtLaunchKernel), so
-// a cold timing excludes the dispatch gap after the cache flush that stream events around the launch
-// included (cant: 21.2 us by stream events against 15.4 us in the trace).
-static thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
-void set_launch_events(hipEvent_t start, hipEvent_t stop)
-{
-    t_ev_start = start;
-    t_ev_stop = stop;
-}
 template <typename... KArgs, typename... Args>
 static void ggl(void (*kernel)(KArgs...), dim3 grid, dim3 block, hipStream_t s, Args... args)
 {
-    hipExtLaunchKernelGGL(kernel, grid, block, 0, s, t_ev_start, t_ev_stop, 0, args...);
-    t_ev_start = t_ev_stop = nullptr;
+    hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
 }
 
 // Streamed-once matrix arrays: nontemporal loads (don't displace x / X from the caches).
@@ -103,7 +90,11 @@ __device__ __forceinline__ double load_sc1(const double *p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-
+__device__ __forceinline__ void store_sc1_2(double *p, double2 v)
+{
+    store_sc1(p, v.x);
+    store_sc1(p + 1, v.y);
+}
 // Merge-path search (cpu_spmv.cpp:208-235 semantics) over an LDS copy of the tile's row
 // end offsets, stored relative to the tile's first nonzero; list B is 0..b_len-1.
 __device__ __forceinline__ void lds_search(int d, const int *s_rowend, int a_len, int b_len, int &x, int &y)
@@ -664,7 +655,13 @@ struct TileArgs {
     const int2 *__restrict__ bounds;
     const unsigned char *__restrict__ split;
     const unsigned char *__restrict__ rmode;  // per-tile in-tile reduction (k_tile_modes)
-    double *__restrict__ carry_val;
+    double *__restrict__ carry_val;    // [tile][L] split-row partials, agent-scope stores (close_split_rows)
+    const int4 *fix;                   // TilePlan::d_fix / d_fix_cnt (null: the plan splits no row)
+    unsigned *fix_cnt;
+    double *head_val;                  // [tile][L]: the first row of a tile that completes a split row
+    double *head_pub;                  // [tile][L]: the same, republished with agent scope (close_split_rows)
+    double *y0;                        // per tile (set by the kernel): where row 0 of the tile goes --
+                                       // y's row, or head_val when the tile completes a split row
     int num_tiles;
     CgScalars *scal;                   // CG: per-column scalars
     CgControl *ctrl;                   // CG: iteration control
@@ -704,6 +701,75 @@ struct TileArgs {
     int blk_spmv;      // the plain SpMV runs k_spmv_blk on this plan (TilePlan::blk_spmv; mixed plans too)
     int n;             // columns (x holds n entries)
 };
+
+// Split rows, closed inside the tile kernel (replaces r03's k_fixup launch).  A row longer than the
+// snap distance spans consecutive tiles: each tile that ends inside it stores its partial as a carry,
+// and the tile where it ends (its completing tile) stores the row's own part -- its row 0 -- to
+// head_val instead of y (TileArgs::y0: one address select per row store, no branch).  The row's nc + 1
+// tiles publish with agent scope (carries directly, the head copied to head_pub here) and take one
+// ticket each on fix_cnt[completing tile]; whichever draws the last one -- no waiting: it is simply
+// the last to finish -- closes the row: wave w takes columns j = w, w + TB/64, ...: lane l sums carries
+// l, l + 64, ... in tile order, a fixed xor butterfly folds the wave, lane 0 adds the head and stores
+// y's row (k_fixup's order, so reproducible), and the ticket is reset for the next launch.  fx =
+// fix[t] (plan time): x = the completing tile of the row this tile ends inside (-1: none), y = that
+// row's carry count, z = the carry count of the row this tile completes (0: none).  Call from every
+// thread after the tile's rows and carry are stored and after any pass that reads its own rows back
+// (the dot mode's).
+__device__ __forceinline__ int4 load_fix(const TileArgs &a, int t)  // block-uniform: kept in SGPRs
+{
+    if (!a.fix)
+        return make_int4(-1, 0, 0, 0);
+    const int4 f = a.fix[t];
+    return make_int4(__builtin_amdgcn_readfirstlane(f.x), __builtin_amdgcn_readfirstlane(f.y),
+                     __builtin_amdgcn_readfirstlane(f.z), 0);
+}
+template <int TB>
+__device__ __forceinline__ void close_split_rows(const TileArgs &a, int t, int4 fx, int L, int ld)
+{
+    if (fx.x < 0 && fx.z == 0)  // block-uniform
+        return;
+    __shared__ int s_fin[2];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's carry and head are out
+    __syncthreads();
+    if (fx.z > 0) {  // the head, stored by this workgroup: republished with agent scope
+        for (int j = threadIdx.x; j < L; j += TB)
+            store_sc1(&a.head_pub[(size_t)t * L + j], a.head_val[(size_t)t * L + j]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        int f0 = -1, f1 = -1;
+        if (fx.x >= 0 &&
+            __hip_atomic_fetch_add(&a.fix_cnt[fx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)fx.y)
+            f0 = fx.x;
+        if (fx.z > 0 &&
+            __hip_atomic_fetch_add(&a.fix_cnt[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)fx.z)
+            f1 = t;
+        s_fin[0] = f0;
+        s_fin[1] = f1;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int tc = s_fin[q], nc = q == 0 ? fx.y : fx.z;
+        if (tc < 0)
+            continue;
+        const size_t R = (size_t)a.bounds[tc].x;
+        for (int j = (int)threadIdx.x >> 6; j < L; j += TB / 64) {  // wave-uniform
+            double sum = 0.0;
+            for (int u = lane; u < nc; u += 64)
+                sum += load_sc1(&a.carry_val[(size_t)(tc - nc + u) * L + j]);
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1)
+                sum += __shfl_xor(sum, off);
+            if (lane == 0)
+                a.y[R * ld + j] = sum + load_sc1(&a.head_pub[(size_t)tc * L + j]);
+        }
+        if (threadIdx.x == 0)
+            __hip_atomic_store(&a.fix_cnt[tc], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
 
 // Tile-kernel modes.
 //   0: y = A x.
@@ -1238,7 +1304,7 @@ struct SpmvSmem {
 // search per walker, the register walk, in-tile carries, the cross-tile carry, the row
 // stores and (CG) the p.Ap contribution.  Called uniformly by all 256 threads; ends with the
 // LDS free for the next tile.
-template <int IPT, int MODE, int TB = kBlock>
+template <int IPT, int MODE, int TB = kBlock, bool FIX = true>
 __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT, TB> &sm, int t, int r0, int n0, int nrows,
                                           int nnzt, bool tail, double beta, double &dot)
 {
@@ -1265,7 +1331,7 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT, TB> &
     }
     auto write_row = [&](int row, double val) {
         const int R = r0 + row;
-        a.y[R] = val;
+        *(FIX && row == 0 ? a.y0 : &a.y[R]) = val;
         if (MODE == kModeCg) {
             const double2 v = cg_rp(a, R);
             const double pn = v.x + beta * v.y;
@@ -1334,7 +1400,7 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT, TB> &
         double acc = s_val[j0];
         for (int u = j0 + 1; u < TB; ++u)
             acc += s_val[u];
-        a.carry_val[t] = acc;
+        store_sc1(&a.carry_val[t], acc);
         const int R = r0 + nrows;
         if (MODE == kModeCg) {
             const double2 v = cg_rp(a, R);
@@ -1356,7 +1422,7 @@ __device__ __forceinline__ void walk_tile(const TileArgs &a, SpmvSmem<IPT, TB> &
 // round, as a staged store would be); no LDS beyond the product buffer.  xr / pr: r and p_old
 // (CG) or x (dot mode) of row r0 + tid, loaded by the caller for tid <= nrows -- the operands
 // of the rows a G = 1 thread owns first; other rows load their own.
-template <int IPT, int MODE, int TB = kBlock>
+template <int IPT, int MODE, int TB = kBlock, bool FIX = true>
 __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT, TB> &sm, int t, int r0, int nrows,
                                            int nnzt, bool tail, double beta, double &dot, int lg, double xr,
                                            double pr)
@@ -1401,7 +1467,7 @@ __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT, TB> 
             }
         }
         if (r < nrows) {
-            a.y[R] = v;
+            *(FIX && r == 0 ? a.y0 : &a.y[R]) = v;
             if (MODE == kModeCg) {
                 const double pn = ox + beta * op;
                 cg_pstore(a, R, pn);
@@ -1409,8 +1475,8 @@ __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT, TB> 
             } else if (MODE == kModeDot) {
                 dot += ox * v;
             }
-        } else {  // the trailing partial row -> carry (k_fixup adds the row's carries in a fixed order)
-            a.carry_val[t] = v;
+        } else {  // the trailing partial row -> carry (close_split_rows adds the row's carries in order)
+            store_sc1(&a.carry_val[t], v);
             if (MODE == kModeCg)
                 dot += (ox + beta * op) * v;
             else if (MODE == kModeDot)
@@ -1421,15 +1487,15 @@ __device__ __forceinline__ void group_tile(const TileArgs &a, SpmvSmem<IPT, TB> 
 }
 
 // One tile's reduction, by its plan-time mode (a.rmode[t]); tail = a.split[t + 1].
-template <int IPT, int MODE, int TB = kBlock>
+template <int IPT, int MODE, int TB = kBlock, bool FIX = true>
 __device__ __forceinline__ void reduce_tile(const TileArgs &a, SpmvSmem<IPT, TB> &sm, int t, int r0, int n0, int nrows,
                                             int nnzt, int mode, bool tail, double beta, double &dot, double xr,
                                             double pr)
 {
     if (mode == 0)
-        walk_tile<IPT, MODE, TB>(a, sm, t, r0, n0, nrows, nnzt, tail, beta, dot);
+        walk_tile<IPT, MODE, TB, FIX>(a, sm, t, r0, n0, nrows, nnzt, tail, beta, dot);
     else
-        group_tile<IPT, MODE, TB>(a, sm, t, r0, nrows, nnzt, tail, beta, dot, mode - 1, xr, pr);
+        group_tile<IPT, MODE, TB, FIX>(a, sm, t, r0, nrows, nnzt, tail, beta, dot, mode - 1, xr, pr);
 }
 
 // x[r0 + tid] (dot mode), or r and p_old at r0 + tid (CG), for the row-group epilogue, tid <= nrows.
@@ -1567,7 +1633,9 @@ __device__ __forceinline__ void cg1_publish(const TileArgs &a, SM &sm, int slot,
 // BLK = false: the plan has no node-block tiles (a.blk null), and the kernel is compiled without
 // their staging paths -- the pipelined CG's form then needs far fewer registers (their run arrays
 // set its VGPR count, so more workgroups fit per CU).
-template <int IPT, int MODE, bool NT, int TB = kBlock, bool BLK = true>
+// FIX: the plan splits rows (close_split_rows); plans that split none -- FEM, CFD, stencils -- run
+// the form without it (fewer SGPRs: 8 workgroups per CU).
+template <int IPT, int MODE, bool NT, int TB = kBlock, bool BLK = true, bool FIX = true>
 __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
 {
     static_assert(TB == kBlock || MODE == kModeSpmv, "one-wave tiles run the plain SpMV only");
@@ -1585,6 +1653,9 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
     const int nrows = b1.x - r0;
     const int nnzt = b1.y - n0;
     const int re_pre = a.early_re ? a.row_offsets[min(r0 + 1 + tid, a.m)] : 0;  // TileArgs::early_re
+    const int4 fx = FIX ? load_fix(a, t) : make_int4(-1, 0, 0, 0);  // split rows (node-block tiles have none)
+    if constexpr (FIX)
+        a.y0 = fx.z > 0 ? a.head_val + t : a.y + r0;
     double beta = 0.0;
     bool go = true;
     // CG: the update's r.r partials are loaded first; summed (-> stop test, beta) once this
@@ -1692,7 +1763,9 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
     double dot = 0.0;
     double xr, pr;
     row_operands<MODE>(a, r0, nrows, xr, pr);
-    reduce_tile<IPT, MODE, TB>(a, sm, t, r0, n0, nrows, nnzt, a.rmode[t], a.split[t + 1] != 0, beta, dot, xr, pr);
+    reduce_tile<IPT, MODE, TB, FIX>(a, sm, t, r0, n0, nrows, nnzt, a.rmode[t], a.split[t + 1] != 0, beta, dot, xr, pr);
+    if constexpr (FIX)
+        close_split_rows<TB>(a, t, fx, 1, 1);
     if constexpr (MODE == kModeCg) {
         cg1_lag_store<TB>(a, r0, nrows, lag);
         cg1_publish(a, sm, t, a.num_tiles, dot);
@@ -1706,7 +1779,7 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
 // of G lanes take the tile's row segments round-robin (its whole rows, then the trailing partial row
 // of a split boundary), lane j of a group sums products j, j + G, ... of its segment in order, a
 // fixed xor butterfly folds the group and its lane 0 stores the row (the
-// trailing partial row: the tile's carry, which k_fixup adds).  No LDS, so the kernel keeps its
+// trailing partial row: the tile's carry, which the completing tile adds, close_split_rows).  No LDS, so the kernel keeps its
 // register-only occupancy.  G is the smallest power of two with 4 G >= the tile's mean segment
 // length.  Reproducible, and within the 2 (len+1) eps (|A||x|)_i reordering bound of the CSR-order
 // sum (mspmv_tile_modes reports these tiles as 255).
@@ -1737,9 +1810,9 @@ __device__ __forceinline__ void tile_rows_reg(const TileArgs &a, int t, int r0, 
             v += __shfl_xor(v, off);
         if (lane == 0) {
             if (r < nrows)
-                a.y[r0 + r] = v;
+                *(r == 0 ? a.y0 : &a.y[r0 + r]) = v;
             else
-                a.carry_val[t] = v;
+                store_sc1(&a.carry_val[t], v);
         }
     }
 }
@@ -1787,7 +1860,10 @@ __global__ __launch_bounds__(kBlock) void k_spmv_blk(TileArgs a)
         if constexpr (FB) {
             const bool reg = nblk > 0 && __ballot((tid & 63) < nblk && ((bd.x >> 16) & 255u) != 0) == 0;
             if (!reg) {
+                const int4 fx = load_fix(a, t);
+                a.y0 = fx.z > 0 ? a.head_val + t : a.y + b0.x;
                 tile_rows_reg<NT>(a, t, b0.x, b0.y, a.cols16 ? colbase : -1);
+                close_split_rows<kBlock>(a, t, fx, 1, 1);
                 return;
             }
         }
@@ -1822,7 +1898,7 @@ __global__ __launch_bounds__(kBlock) void k_spmv_blk(TileArgs a)
 // each row's x and the running dot in registers through the gathers -- the dot mode then needs
 // no more registers than the plain SpMM, so it keeps the plain kernel's occupancy.
 
-template <int L, bool DICT = false>
+template <int L, bool DICT = false, bool FIX = true>
 __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_col, const double *s_val,
                                                 const int *rend, int t, int r0, int nrows, int nnzt, int lgp,
                                                 const double2 *s_panel = nullptr)
@@ -1894,9 +1970,9 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
         if (sub == 0) {
             const size_t off = (size_t)(r0 + r) * a.ld + 2 * lane;
             if (r < nrows)
-                *reinterpret_cast<double2 *>(a.y + off) = acc;
-            else  // the trailing partial row -> carry (k_fixup adds the row's carries in a fixed order)
-                *reinterpret_cast<double2 *>(a.carry_val + (size_t)t * L + 2 * lane) = acc;
+                *reinterpret_cast<double2 *>(FIX && r == 0 ? a.y0 + 2 * lane : a.y + off) = acc;
+            else  // the trailing partial row -> carry (close_split_rows adds the row's carries in order)
+                store_sc1_2(a.carry_val + (size_t)t * L + 2 * lane, acc);
         }
     }
 }
@@ -1923,7 +1999,7 @@ constexpr int spmm_waves_per_eu(int L, int IPTG, bool DICT = false)
 // occupancy the 16 KB panel costs outweigh 64-B gathers), so only L = 16 plans build one.
 // (Grouped staging, 4 nonzeros per lane: measured even, CG multi L = 8 0.915-0.920 vs 0.914 ms per
 // iteration, r03z -- not kept.)
-template <int L, int IPTG, int MODE, bool NT, bool DICT = false>
+template <int L, int IPTG, int MODE, bool NT, bool DICT = false, bool FIX = true>  // FIX: as k_spmv_tile's
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(spmm_waves_per_eu(L, IPTG, DICT)))) void
 k_spmm_tile(TileArgs a)
 {
@@ -1959,6 +2035,13 @@ k_spmm_tile(TileArgs a)
     const int nnzt = b1.y - n0;
     const int items = nrows + nnzt;
     const int rmode = a.rmode[t];
+    __shared__ int4 s_fix;  // parked in LDS until the epilogue: no registers held through the tile
+    if constexpr (FIX) {
+        if (tid == 0)
+            s_fix = a.fix ? a.fix[t] : make_int4(-1, 0, 0, 0);
+        a.y0 = a.fix && __builtin_amdgcn_readfirstlane(a.fix[t].z) > 0 ? a.head_val + (size_t)t * L
+                                                                        : a.y + (size_t)r0 * a.ld;
+    }
     int nd = 0;  // > 0: this tile reads its panel rows from s_panel
     if constexpr (DICT) {
         nd = a.ndict[t];
@@ -2022,9 +2105,9 @@ k_spmm_tile(TileArgs a)
     double2 dot = make_double2(0.0, 0.0);
     if (rmode != 0) {
         if (DICT && nd > 0)
-            spmm_group_rows<L, true>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, rmode - 1, s_panel);
+            spmm_group_rows<L, true, FIX>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, rmode - 1, s_panel);
         else
-            spmm_group_rows<L>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, rmode - 1);
+            spmm_group_rows<L, false, FIX>(a, s_col, s_val, s_rowend, t, r0, nrows, nnzt, rmode - 1);
     } else {
     const int ipt = (items + NG - 1) / NG;
     const int d0 = min(g * ipt, items);
@@ -2035,7 +2118,7 @@ k_spmm_tile(TileArgs a)
     const bool need_cin = (cx < ex) && (cy > (cx == 0 ? 0 : s_rowend[cx - 1]));
 
     auto write_row = [&](int row, double2 val) {
-        *reinterpret_cast<double2 *>(a.y + (size_t)(r0 + row) * a.ld + 2 * lane) = val;
+        *reinterpret_cast<double2 *>(FIX && row == 0 ? a.y0 + 2 * lane : a.y + (size_t)(r0 + row) * a.ld + 2 * lane) = val;
     };
 
     double2 run = make_double2(0.0, 0.0);
@@ -2119,7 +2202,7 @@ k_spmm_tile(TileArgs a)
             acc.x += c.x;
             acc.y += c.y;
         }
-        *reinterpret_cast<double2 *>(a.carry_val + (size_t)t * L + 2 * lane) = acc;
+        store_sc1_2(a.carry_val + (size_t)t * L + 2 * lane, acc);
     }
     }  // merge walk
 
@@ -2130,14 +2213,15 @@ k_spmm_tile(TileArgs a)
         // takes its own column pair `lane`, as the in-loop dot does.
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        // The trailing partial row (a carry, k_fixup adds it later) counts by linearity: its x
-        // times the carry this tile stored.
+        // The trailing partial row (a carry, added to the row by the tile completing it) counts by
+        // linearity: its x times the carry this tile stored.  (The row this tile completes is read
+        // before close_split_rows adds the earlier tiles' carries to it: they count in their tiles.)
         const int npair = (nrows + (a.split[t + 1] ? 1 : 0)) * GL;
         for (int e = tid; e < npair; e += kBlock) {
             const int row = e / GL;
             const size_t off = (size_t)(r0 + row) * a.ld + 2 * lane;
             const double2 ap = *reinterpret_cast<const double2 *>(
-                row < nrows ? a.y + off : a.carry_val + (size_t)t * L + 2 * lane);
+                row < nrows ? (FIX && row == 0 ? a.y0 + 2 * lane : a.y + off) : a.carry_val + (size_t)t * L + 2 * lane);
             const double2 xx = *reinterpret_cast<const double2 *>(a.xr + off);
             dot.x += xx.x * ap.x;
             dot.y += xx.y * ap.y;
@@ -2165,6 +2249,8 @@ k_spmm_tile(TileArgs a)
             a.partials[(size_t)t * L + 2 * tid + 1] = tsum.y;
         }
     }
+    if constexpr (FIX)
+        close_split_rows<kBlock>(a, t, s_fix, L, a.ld);  // (s_fix: written before the staging barrier)
 }
 
 // ---- node-block SpMM (plans whose every single-RHS tile is a register node-block tile) --------
@@ -2451,44 +2537,6 @@ __global__ __launch_bounds__(kBlock) void k_fold_dot(const double *part, int T, 
         __syncthreads();
         cg_alpha_finish<L>(conv, ctrl);
     }
-}
-
-// Rows split between tiles: y[R] = (carry_a + carry_a+1 + ...) + y[R], carries in tile order.
-// One thread per (carry, column); the first carry of each row's run sums the run.
-// Carries of split rows (tiles that end inside a row), added after the tile kernel.  One wave per
-// (run of consecutive carries of one row, column j): lane l sums carries l, l + 64, ... of the run in
-// order, a fixed xor butterfly folds the wave, lane 0 adds the total to the row the completing tile
-// wrote.  Fixed order, so reproducible; a hub row split over hundreds of tiles (the skewed variant's
-// dense row: 425 one-wave tiles) costs one wave round trip instead of a serial loop over its carries
-// (85 us before, r03u).
-__global__ void k_fixup(const int *__restrict__ carry_tiles, const int *__restrict__ carry_rows,
-                        const int *__restrict__ carry_runs, int nruns, const double *__restrict__ carry_val,
-                        double *__restrict__ Y, int L, const CgControl *ctrl, int ld)
-{
-    if (ctrl && ctrl->done)
-        return;
-    const int w = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6), lane = threadIdx.x & 63;
-    const int run = w / L, j = w % L;
-    if (run >= nruns)  // wave-uniform
-        return;
-    const int i0 = carry_runs[run], i1 = carry_runs[run + 1];
-    double sum = 0.0;
-    for (int u = i0 + lane; u < i1; u += 64)
-        sum += carry_val[(size_t)carry_tiles[u] * L + j];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1)
-        sum += __shfl_xor(sum, off);
-    if (lane == 0) {
-        const int R = carry_rows[i0];
-        Y[(size_t)R * ld + j] = sum + Y[(size_t)R * ld + j];
-    }
-}
-
-static void fixup_launch(const TilePlan &plan, double *d_Y, int L, const CgControl *ctrl, int ld, hipStream_t s)
-{
-    const long long waves = (long long)plan.num_carry_runs * L;
-    ggl(k_fixup, dim3((unsigned)((waves + 3) / 4)), dim3(256), s, plan.d_carry_tiles, plan.d_carry_rows,
-        plan.d_carry_runs, plan.num_carry_runs, (const double *)plan.d_carry_val, d_Y, L, ctrl, ld);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3146,7 +3194,10 @@ std::string spmv_kernel_name(const mspmv_handle_s *h)
     const auto it = h->plans.find(plan_key(1));
     if (h->spmv_onewave != 1 && it != h->plans.end() && it->second.blk_spmv)
         return "k_spmv_blk<0," + nt + (it->second.num_tiles_reg == it->second.num_tiles ? ",6,false>" : ",6,true>");
-    return "k_spmv_tile<" + std::to_string(kSpmvIpt) + ",0," + nt + (h->spmv_onewave == 1 ? ",64>" : ">");
+    if (h->spmv_onewave == 1)
+        return "k_spmv_tile<" + std::to_string(kSpmvIpt) + ",0," + nt + ",64,true,true>";
+    const bool fix = it != h->plans.end() && it->second.num_carries > 0;
+    return "k_spmv_tile<" + std::to_string(kSpmvIpt) + ",0," + nt + ",256,true," + (fix ? "true>" : "false>");
 }
 
 int spmv_items_per_thread() { return kSpmvIpt; }
@@ -3166,7 +3217,8 @@ std::string spmm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan, int 
         return "k_spmm_blk<" + std::to_string(L) + ",0," + nt + "," + std::to_string(blk_kr(plan)) + ">";
     const int iptg = spmm_iptg_for(L);
     const bool dict = L == 16 && plan.d_dict;
-    return "k_spmm_tile<" + std::to_string(L) + "," + std::to_string(iptg) + ",0," + nt + (dict ? ",true>" : ">");
+    return "k_spmm_tile<" + std::to_string(L) + "," + std::to_string(iptg) + ",0," + nt +
+           (dict ? ",true,true>" : plan.num_carries > 0 ? ",false,true>" : ",false,false>");
 }
 
 // Resident workgroups per CU of a kBlock-thread kernel from its own resources on gfx950: 160 KiB
@@ -3191,13 +3243,14 @@ static int gfx950_blocks_per_cu(const void *fn)
 int spmv_tile_blocks_per_cu()
 {
     static const int occ = [] {
-        const void *ks = (const void *)k_spmv_tile<kSpmvIpt, kModeSpmv, false>;
+        const void *ks = (const void *)k_spmv_tile<kSpmvIpt, kModeSpmv, false, kBlock, true, false>;
         const void *kc = (const void *)k_spmv_tile<kSpmvIpt, kModeCg, false, kBlock, false>;
         const int c = std::min(gfx950_blocks_per_cu(ks), gfx950_blocks_per_cu(kc));
         if (c > 0)
             return c;
         int a = 0, b = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_spmv_tile<kSpmvIpt, kModeSpmv, false>, kBlock, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_spmv_tile<kSpmvIpt, kModeSpmv, false, kBlock, true, false>,
+                                                         kBlock, 0) !=
                 hipSuccess ||
             hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_spmv_tile<kSpmvIpt, kModeCg, false, kBlock, false>,
                                                          kBlock, 0) != hipSuccess)
@@ -3301,6 +3354,10 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
     a.split = plan.d_split;
     a.rmode = plan.d_modes[l_index(L)];
     a.carry_val = plan.d_carry_val;
+    a.fix = plan.num_carries ? plan.d_fix : nullptr;  // split rows: closed by the tile kernels
+    a.fix_cnt = plan.d_fix_cnt;
+    a.head_val = plan.d_carry_val + (size_t)std::max(plan.num_tiles, 1) * plan.carry_L;
+    a.head_pub = a.head_val + (size_t)std::max(plan.num_tiles, 1) * plan.carry_L;
     a.num_tiles = plan.num_tiles;
     if (L == 1 || plan.d_blk) {  // L > 1 on a node-block plan: k_spmm_blk (plan_for_L picked it)
         a.colbase = plan.d_colbase;
@@ -3337,10 +3394,16 @@ static void launch_spmm_nt(const TileArgs &a, hipStream_t s, bool nt)
                 return;
             }
         }
-        if (nt)
+        if (MODE == kModeSpmv && !a.fix) {  // no split rows: the form without close_split_rows
+            if (nt)
+                ggl(k_spmm_tile<LL, I, MODE, true, false, false>, grid, block, s, a);
+            else
+                ggl(k_spmm_tile<LL, I, MODE, false, false, false>, grid, block, s, a);
+        } else if (nt) {
             ggl(k_spmm_tile<LL, I, MODE, true>, grid, block, s, a);
-        else
+        } else {
             ggl(k_spmm_tile<LL, I, MODE, false>, grid, block, s, a);
+        }
     }
 }
 
@@ -3400,6 +3463,11 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, bool nt)
                 ggl(k_spmv_tile<kSpmvIpt, MODE, true, kBlock, false>, grid, block, s, a);
             else
                 ggl(k_spmv_tile<kSpmvIpt, MODE, false, kBlock, false>, grid, block, s, a);
+        } else if (MODE == kModeSpmv && !a.fix) {  // no split rows: the form without close_split_rows
+            if (nt)
+                ggl(k_spmv_tile<kSpmvIpt, MODE, true, kBlock, true, false>, grid, block, s, a);
+            else
+                ggl(k_spmv_tile<kSpmvIpt, MODE, false, kBlock, true, false>, grid, block, s, a);
         } else if (nt) {
             ggl(k_spmv_tile<kSpmvIpt, MODE, true>, grid, block, s, a);
         } else {
@@ -3424,16 +3492,6 @@ hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const 
     if (ld > 0)
         a.ld = ld;
     return launch_tile<kModeSpmv>(a, L, h->stream, stream_nt(h));
-}
-
-hipError_t launch_fixup(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L, int ld)
-{
-    if (ld <= 0)
-        ld = L;
-    if (plan.num_carries == 0)
-        return hipSuccess;
-    fixup_launch(plan, d_Y, L, nullptr, ld, h->stream);
-    return hipGetLastError();
 }
 
 // Column block copy between row-major panels: dst[i][j] = (j < cols ? src[i][j] : 0) for
@@ -3465,12 +3523,9 @@ hipError_t launch_panel_copy(const double *src, int lds, double *dst, int ldd, l
 hipError_t launch_spmm(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
                        int *kernels_launched, int ld)
 {
-    hipError_t e = launch_spmm_tile_only(h, plan, d_X, d_Y, L, ld);
-    if (e != hipSuccess)
-        return e;
-    e = launch_fixup(h, plan, d_Y, L, ld);
+    const hipError_t e = launch_spmm_tile_only(h, plan, d_X, d_Y, L, ld);
     if (kernels_launched)
-        *kernels_launched = (plan.num_tiles ? 1 : 0) + (plan.num_carries ? 1 : 0);
+        *kernels_launched = plan.num_tiles ? 1 : 0;
     return e;
 }
 
@@ -3720,14 +3775,6 @@ hipError_t launch_cg1_finish(mspmv_handle_s *h, double *d_x, int parity, int nbl
 }
 
 
-static hipError_t launch_fixup_ctrl(mspmv_handle_s *h, const TilePlan &plan, double *d_Y, int L)
-{
-    if (plan.num_carries == 0)
-        return hipSuccess;
-    fixup_launch(plan, d_Y, L, h->d_ctrl, L, h->stream);
-    return hipGetLastError();
-}
-
 // Multi-RHS iteration, split: p = r + beta p (one streaming pass), then Y = A p with p.Ap by
 // linearity (MODE 2, which also stops on a non-finite alpha), then the update with alpha from
 // that p.Ap.  For L >= 2 the fused iteration would gather two L-wide panel rows (r and
@@ -3780,8 +3827,6 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
         TileArgs ta = make_args(h, plan, h->d_p0, h->d_ap, L);
         ta.ctrl = h->d_ctrl;
         if ((e = launch_tile<kModeSpmv>(ta, L, h->stream, stream_nt(h))) != hipSuccess)
-            return e;
-        if ((e = launch_fixup_ctrl(h, plan, h->d_ap, L)) != hipSuccess)
             return e;
         CgVecArgs vd = va;
         vd.r = h->d_p0;
@@ -3851,8 +3896,6 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *
     hipError_t e = launch_tile<kModeCg>(ta, 1, h->stream, stream_nt(h));
     if (e != hipSuccess)
         return e;
-    if ((e = launch_fixup_ctrl(h, plan, h->d_ap, 1)) != hipSuccess)
-        return e;
     Cg1Args a = cg1_args(h, d_x);
     a.rp = rp_old;
     a.rp_next = rp_new;
@@ -3904,9 +3947,8 @@ hipError_t launch_dist_pack(const double *p, const int *idx, long long n_elems, 
     return hipGetLastError();
 }
 
-// Y = A X with x.(AX) per column reduced into dot_out (MODE 2), plus the carry fix-up and the
-// partials fold.  scal / conv (single-GPU split CG) add the non-finite-alpha stop.
-// The dot-mode SpMM's tile kernel (+ carries) on stream s: Y = A X and one x.(AX) partial per tile
+// Y = A X with x.(AX) per column reduced into dot_out (MODE 2), plus the partials fold.  scal / conv (single-GPU split CG) add the non-finite-alpha stop.
+// The dot-mode SpMM's tile kernel on stream s: Y = A X and one x.(AX) partial per tile
 // at partials[t * L ..] (plain stores, summed by launch_fold_dot in a later launch).
 hipError_t launch_spmm_dot_tiles(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
                                  CgControl *ctrl, double *partials, hipStream_t s, long long row_off)
@@ -3917,14 +3959,7 @@ hipError_t launch_spmm_dot_tiles(mspmv_handle_s *h, const TilePlan &plan, const 
     ta.xr = d_X + row_off * L;  // the handle's rows start at row row_off of X
     ta.ctrl = ctrl;
     ta.partials = partials;
-    hipError_t e = launch_tile<kModeDot>(ta, L, s, stream_nt(h));
-    if (e != hipSuccess)
-        return e;
-    if (plan.num_carries) {
-        fixup_launch(plan, d_Y, L, ctrl, L, s);
-        e = hipGetLastError();
-    }
-    return e;
+    return launch_tile<kModeDot>(ta, L, s, stream_nt(h));
 }
 
 // Sum T tiles' partials [T][L] in tile order into dot_out (k_fold_dot; partials_capacity() leaves

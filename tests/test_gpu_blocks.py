@@ -287,7 +287,7 @@ def test_blocks_spai_pcg(orc):
 # ---- imperfect FEM: mixed plans (k_spmv_blk's register fallback, per-chunk pair flags) ----------
 def fem_with_long_rows(a, rows, length, seed=5):
     """`a` with the given rows replaced by `length` random sorted columns: rows longer than the snap
-    distance (tile / 8) are split between tiles, so the plan carries (k_fixup) and those tiles are
+    distance (tile / 8) are split between tiles, so the plan carries (closed by the completing tiles) and those tiles are
     not node blocks."""
     rng = np.random.default_rng(seed)
     ro, ci, va = a.row_offsets, a.column_indices, a.values

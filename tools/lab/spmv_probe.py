@@ -25,7 +25,7 @@ SHAPES = {
     "cant": lambda s: mspmv.CsrMatrix.synth_banded(62451, 4007383, 2000, seed=s),
 }
 HBM = 8000.0
-for name in sys.argv[1:] or list(SHAPES):
+for name in (sys.argv[1:] or os.environ.get("PROBE_SHAPES", "").split() or list(SHAPES)):
     n = 1 if name == "nlpkkt" else 4
     mats = [SHAPES[name](s + 1) for s in range(n)]
     gs = [mspmv.GpuCsr(a) for a in mats]

@@ -160,9 +160,9 @@ def main(src, dst):
     lines += ["", "hot rows include the untimed warm-up launches; cold rows are the launches right after bench's "
               "512 MiB flush kernel.  CG: span = the timed solve's first-to-last loop-kernel time / iterations "
               "(bench divides wall time, which adds the host call); kernel-busy = the loop kernels' summed "
-              "durations per iteration.  spmm16 / spmv_shapes: since r03ab the bench's cold time is the "
-              "tile kernel AND its carry fix-up (plus the event gap of the second launch); the trace column "
-              "is the tile kernel alone."]
+              "durations per iteration.  spmm16 / spmv_shapes: since r04k one kernel per product (split rows "
+              "closed inside the tile kernel); bench's cold time = (flush + launch region - flush-only region) / "
+              "reps, its hot time = back-to-back region / reps."]
     open(out("frac_check.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
