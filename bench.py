@@ -205,7 +205,7 @@ def gpu_spmv_hot_cold(a, dev, seed=2):
         dx, dy = mspmv.DeviceBuffer.from_array(x, dev), mspmv.DeviceBuffer(8 * a.num_rows, dev)
         g.time_spmm(dx, dy, 1, 5)
         _, hot, _ = g.time_spmm(dx, dy, 1, 200)
-        _, cold, _ = g.time_spmm(dx, dy, 1, 50, FLUSH_BYTES)
+        _, cold, _ = g.time_spmm(dx, dy, 1, 160, FLUSH_BYTES)  # 8 blocks beside flush-only controls
         kname = g.kernel_name()
     nb = spmv_bytes(a.num_rows, a.num_cols, a.num_nonzeros)
     return x, {"m": a.num_rows, "nnz": a.num_nonzeros, "kernel": kname, "bytes_per_launch": nb,
@@ -341,7 +341,7 @@ def run_spmm16(dev, cpu_seconds, do_cpu):
             dY = mspmv.DeviceBuffer(8 * a.num_rows * L, dev)
             g.time_spmm(dX, dY, L, 5)
             _, kern_ms, _ = g.time_spmm(dX, dY, L, 100)
-            _, cold_ms, _ = g.time_spmm(dX, dY, L, 30, FLUSH_BYTES)
+            _, cold_ms, _ = g.time_spmm(dX, dY, L, 80, FLUSH_BYTES)  # 8 blocks beside flush-only controls
         nb = 12 * a.num_nonzeros + 4 * (a.num_rows + 1) + 8 * L * (a.num_cols + a.num_rows)
         out[name] = {"m": a.num_rows, "nnz": a.num_nonzeros, "bytes_per_launch": nb,
                      "hot_kernel_ms": round(kern_ms, 5), "hot_GBps": round(nb / kern_ms / 1e6, 1),

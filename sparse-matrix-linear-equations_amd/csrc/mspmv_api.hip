@@ -1684,47 +1684,65 @@ mspmv_status mspmv_time_spmm_dev(mspmv_handle h, const double *d_X, double *d_Y,
     }
     // Hot (flush_bytes == 0): reps launches back to back, events around the region only; per launch
     // = region / reps (the launch gap included, ~0.2 us: r04i's headline 21.06 us against 21.09 in the
-    // trace).  Cold: the region of reps (flush, launch) pairs minus a control region of reps flushes
-    // alone, / reps -- per-launch events (stream events, or hipExtLaunchKernel's kernel-boundary ones)
-    // measured 4.7 us over the traced kernel on cant and rma10 (r04i_frac_check.md).  avg_ms: the whole
-    // timed region per launch (flushes included).
-    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // trace).  Cold: blocks of n (flush, launch) pairs, each beside a control block of n flushes alone;
+    // per launch = the median over blocks of (pairs - control) / n.  Per-launch events (stream events,
+    // or hipExtLaunchKernel's kernel-boundary ones) measured 4.7 us over the traced kernel on cant and
+    // rma10 (r04i_frac_check.md); one control region for all reps left rma10 at 7.4 us against 9.5 in
+    // the trace (r04m).  avg_ms: the timed regions per launch (flushes included).
+    const bool run = plan->num_tiles > 0;
+    const int nblk = flush_bytes && run ? std::min(reps, 8) : 1;
+    std::vector<hipEvent_t> ev((size_t)nblk * 4, nullptr);
     for (auto &x : ev)
         HIP_TRY(hipEventCreate(&x));
     hipError_t e = hipSuccess;
-    const bool run = plan->num_tiles > 0;
-    if (flush_bytes && run)  // the control region first: flushes alone
-        e = hipEventRecord(ev[2], h->stream);
-    for (int i = 0; i < reps && e == hipSuccess && flush_bytes && run; ++i)
-        e = launch_flush(h->d_flush, flush_bytes, h->stream, false);
-    if (e == hipSuccess)
-        e = hipEventRecord(ev[3], h->stream);
-    if (e == hipSuccess)
-        e = hipEventRecord(ev[0], h->stream);
-    for (int i = 0; i < reps && e == hipSuccess && run; ++i) {
-        if (flush_bytes)
-            e = launch_flush(h->d_flush, flush_bytes, h->stream, false);
+    std::vector<int> nper((size_t)nblk);
+    for (int b = 0, done = 0; b < nblk && e == hipSuccess; ++b) {
+        const int n = (reps - done) / (nblk - b);
+        nper[(size_t)b] = n;
+        done += n;
+        hipEvent_t *q = &ev[(size_t)b * 4];
+        if (flush_bytes && run) {  // the control: n flushes alone
+            e = hipEventRecord(q[2], h->stream);
+            for (int i = 0; i < n && e == hipSuccess; ++i)
+                e = launch_flush(h->d_flush, flush_bytes, h->stream, false);
+            if (e == hipSuccess)
+                e = hipEventRecord(q[3], h->stream);
+        }
         if (e == hipSuccess)
-            e = launch_spmm_tile_only(h, *plan, d_X, d_Y, L);
+            e = hipEventRecord(q[0], h->stream);
+        for (int i = 0; i < n && e == hipSuccess && run; ++i) {
+            if (flush_bytes)
+                e = launch_flush(h->d_flush, flush_bytes, h->stream, false);
+            if (e == hipSuccess)
+                e = launch_spmm_tile_only(h, *plan, d_X, d_Y, L);
+        }
+        if (e == hipSuccess)
+            e = hipEventRecord(q[1], h->stream);
     }
     if (e == hipSuccess)
-        e = hipEventRecord(ev[1], h->stream);
-    if (e == hipSuccess)
-        e = hipEventSynchronize(ev[1]);
-    float total = 0.f, control = 0.f;
-    if (e == hipSuccess)
-        e = hipEventElapsedTime(&total, ev[0], ev[1]);
-    if (e == hipSuccess && flush_bytes && run)
-        e = hipEventElapsedTime(&control, ev[2], ev[3]);
+        e = hipEventSynchronize(ev[(size_t)nblk * 4 - 3]);
+    double total = 0.0;
+    std::vector<double> per;
+    for (int b = 0; b < nblk && e == hipSuccess; ++b) {
+        float t = 0.f, c = 0.f;
+        e = hipEventElapsedTime(&t, ev[(size_t)b * 4], ev[(size_t)b * 4 + 1]);
+        if (e == hipSuccess && flush_bytes && run)
+            e = hipEventElapsedTime(&c, ev[(size_t)b * 4 + 2], ev[(size_t)b * 4 + 3]);
+        total += t;
+        per.push_back(nper[(size_t)b] > 0 ? (double)(t - c) / nper[(size_t)b] : 0.0);
+    }
     for (auto &x : ev)
         (void)hipEventDestroy(x);
     if (e != hipSuccess) {
         set_error(std::string("timing: ") + hipGetErrorString(e));
         return MSPMV_ERR_HIP;
     }
-    h->last_tile_kernel_ms = std::max(0.0, (double)(total - control)) / reps;
+    std::sort(per.begin(), per.end());
+    const double med = per.empty() ? 0.0 : per.size() % 2 ? per[per.size() / 2]
+                                                         : 0.5 * (per[per.size() / 2 - 1] + per[per.size() / 2]);
+    h->last_tile_kernel_ms = std::max(0.0, med);
     h->last_kernels_per_call = run ? 1 : 0;
-    *avg_ms = (double)total / reps;
+    *avg_ms = total / reps;
     return MSPMV_OK;
 }
 
