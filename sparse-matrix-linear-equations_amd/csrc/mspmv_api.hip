@@ -99,6 +99,8 @@ static void free_plan(TilePlan &p)
     dev_free(p.d_ndict);
     dev_free(p.d_idx16);
     dev_free(p.d_blk);
+    free_slab(p.slab);
+    p.slab = nullptr;
 }
 
 // Build (once) the tile plan for L right-hand sides, validating on the host every bound the
@@ -161,6 +163,52 @@ static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out, boo
     *out = &it->second;
     return MSPMV_OK;
 }
+
+namespace mspmv {
+// Split rows of a plan (boundaries hb, split flags hs; p.num_tiles set): the tiles t0 .. t1 - 1 that
+// end inside one row carry into the tile t1 that completes it (the first tile after them with no
+// carry into the same row; the last tile always ends on m) -- TilePlan::d_fix / d_fix_cnt, closed by
+// close_split_rows.  No arrays when nothing is split.
+mspmv_status plan_split_rows(TilePlan &p, const std::vector<int2> &hb, const std::vector<unsigned char> &hs)
+{
+    const int T = p.num_tiles;
+    std::vector<int4> fix((size_t)T, make_int4(-1, 0, 0, 0));
+    int carries = 0;
+    for (int t = 0; t < T;) {
+        if (!hs[(size_t)t + 1]) {
+            ++t;
+            continue;
+        }
+        const int t0 = t;
+        while (t < T && hs[(size_t)t + 1] && hb[(size_t)t + 1].x == hb[(size_t)t0 + 1].x)
+            ++t;
+        if (t >= T) {
+            set_error("tile plan: split row past the last tile");
+            return MSPMV_ERR_INVALID;
+        }
+        for (int u = t0; u < t; ++u) {
+            fix[(size_t)u].x = t;
+            fix[(size_t)u].y = t - t0;
+        }
+        fix[(size_t)t].z = t - t0;
+        carries += t - t0;
+    }
+    p.num_carries = carries;
+    if (carries == 0)
+        return MSPMV_OK;
+    mspmv_status st;
+    if ((st = dev_alloc(&p.d_fix, (size_t)T)) != MSPMV_OK || (st = dev_alloc(&p.d_fix_cnt, (size_t)T)) != MSPMV_OK)
+        return st;
+    hipError_t e = hipMemcpy(p.d_fix, fix.data(), sizeof(int4) * fix.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMemset(p.d_fix_cnt, 0, sizeof(unsigned) * T);
+    if (e != hipSuccess) {
+        set_error(std::string("tile plan upload: ") + hipGetErrorString(e));
+        return MSPMV_ERR_HIP;
+    }
+    return MSPMV_OK;
+}
+}  // namespace mspmv
 
 static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes)
 {
@@ -225,49 +273,15 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         set_error("tile plan: bad end boundaries");
         return fail(MSPMV_ERR_INVALID);
     }
-    std::vector<int4> fix((size_t)T, make_int4(-1, 0, 0, 0));
-    int num_carries = 0;
     for (int t = 0; t < T; ++t) {
         const int nr = hb[t + 1].x - hb[t].x, nz = hb[t + 1].y - hb[t].y;
         if (nr < 0 || nz < 0 || nr + nz > maxi) {
             set_error("tile plan: tile " + std::to_string(t) + " violates the merge bound");
             return fail(MSPMV_ERR_INVALID);
         }
-        if (hs[t + 1])
-            ++num_carries;
     }
-    // Split rows: the tiles t0 .. t1 - 1 that end inside one row carry into the tile t1 that completes
-    // it (the first tile after them with no carry into the same row; the last tile always ends on m).
-    for (int t = 0; t < T;) {
-        if (!hs[t + 1]) {
-            ++t;
-            continue;
-        }
-        const int t0 = t;
-        while (t < T && hs[t + 1] && hb[t + 1].x == hb[t0 + 1].x)
-            ++t;
-        if (t >= T) {
-            set_error("tile plan: split row past the last tile");
-            return fail(MSPMV_ERR_INVALID);
-        }
-        for (int u = t0; u < t; ++u) {
-            fix[(size_t)u].x = t;
-            fix[(size_t)u].y = t - t0;
-        }
-        fix[(size_t)t].z = t - t0;
-    }
-    p.num_carries = num_carries;
-    if (num_carries) {
-        if ((st = dev_alloc(&p.d_fix, (size_t)T)) != MSPMV_OK || (st = dev_alloc(&p.d_fix_cnt, (size_t)T)) != MSPMV_OK)
-            return fail(st);
-        e = hipMemcpy(p.d_fix, fix.data(), sizeof(int4) * fix.size(), hipMemcpyHostToDevice);
-        if (e == hipSuccess)
-            e = hipMemset(p.d_fix_cnt, 0, sizeof(unsigned) * T);
-        if (e != hipSuccess) {
-            set_error(std::string("tile plan upload: ") + hipGetErrorString(e));
-            return fail(MSPMV_ERR_HIP);
-        }
-    }
+    if ((st = plan_split_rows(p, hb, hs)) != MSPMV_OK)
+        return fail(st);
     // the single-RHS kernels' 16-bit column stream; keyed on the tile size, not L, because the
     // L = 2 SpMM shares the single-RHS plan.  (The SpMM itself keeps int32 columns: it is gather
     // bound, and the 16-bit stream measured 0% at L = 4/8 and 7% slower at L = 16.)
@@ -399,10 +413,58 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
 // barriers only), so a tile's hub-row closing and its walkers' latencies stall one wave, not four.
 // Measured on the skewed pwtk-sized variant 100.1 -> 78.3 us; on row-group plans (banded, FEM,
 // stencils) one-wave tiles lost 1-15 % (r03r), so those keep the workgroup plan.
+// Column-slab plan (mspmv_slab.hip) for the plain SpMV: MSPMV_SPMV_SLAB=1 takes it for every matrix
+// it can hold, =0 never; by default a matrix takes it when its workgroup plan gathers through column
+// dictionaries on most tiles (x gathers line-bound: scattered columns) and the slab plan stages at
+// most kSlabAutoBytes of x per nonzero (the columns of a block lie in a few slabs: a band, not the
+// whole width).
+constexpr double kSlabAutoBytes = 4.0;
+constexpr bool kSlabAuto = false;  // the default choice is off until measured on the GPU
+static int slab_switch()  // read at each handle's decision (tests set it per matrix)
+{
+    const char *e = getenv("MSPMV_SPMV_SLAB");
+    return e && *e ? (atoi(e) != 0 ? 1 : 0) : -1;
+}
+
+static mspmv_status spmv_slab_decide(mspmv_handle_s *h, const TilePlan *wg)
+{
+    const int sw = slab_switch();
+    bool cand = sw == 1;
+    if (sw < 0 && kSlabAuto)
+        cand = wg->lanes == kBlock && wg->num_tiles >= 64 && !wg->blk_spmv && 2 * wg->num_tiles_dict >= wg->num_tiles;
+    h->spmv_slab = 0;
+    if (!cand)
+        return MSPMV_OK;
+    TilePlan p;
+    const mspmv_status st = build_slab_plan(h, p);
+    if (st == MSPMV_ERR_UNSUPPORTED) {
+        free_plan(p);
+        set_error("");
+        return MSPMV_OK;
+    }
+    if (st != MSPMV_OK) {
+        free_plan(p);
+        return st;
+    }
+    if (sw < 0 && p.slab->x_bytes_per_nnz > kSlabAutoBytes) {
+        free_plan(p);
+        return MSPMV_OK;
+    }
+    h->plans.emplace(kSlabPlanKey, p);
+    h->spmv_slab = 1;
+    return MSPMV_OK;
+}
+
 static mspmv_status spmv_plan(mspmv_handle_s *h, const TilePlan **out)
 {
     const TilePlan *wg = nullptr;
     ST_TRY(get_plan(h, 1, &wg));
+    if (h->spmv_slab < 0)
+        ST_TRY(spmv_slab_decide(h, wg));
+    if (h->spmv_slab == 1) {
+        *out = &h->plans.find(kSlabPlanKey)->second;
+        return MSPMV_OK;
+    }
     if (h->spmv_onewave < 0) {
         bool want = false;
         if (wg->lanes == kBlock && wg->num_tiles >= 64 && !wg->d_blk) {
@@ -799,6 +861,7 @@ mspmv_status mspmv_set_cu_limit(mspmv_handle h, int num_cus)
             free_plan(kv.second);
         h->plans.clear();
         h->spmv_onewave = -1;
+        h->spmv_slab = -1;
         h->num_cus = n;
         const TilePlan *plan = nullptr;
         ST_TRY(get_plan(h, 1, &plan));

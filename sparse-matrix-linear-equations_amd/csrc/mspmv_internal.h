@@ -23,6 +23,25 @@ constexpr int kTicketStride = 64;  // tickets 256 B apart: one per memory line
 constexpr int kConsumeTile = 4096;
 constexpr int kUpdateMaxBlocks = 1024;
 
+// Column-slab form of the plain single-RHS SpMV (mspmv_slab.hip): the plan's tiles are large blocks
+// (two per CU), each block's nonzeros reordered by column slab (kSlabCols columns of x, staged in LDS
+// once per block and slab) and cut into chunks of <= kSlabChunk nonzeros of one slab; a chunk's
+// entries are its runs of one row.
+constexpr int kSlabThreads = 512;
+constexpr int kSlabCols = 4096;     // columns per slab: 32 KB of x in LDS
+constexpr int kSlabRows = 2047;     // rows ending in one block (+ a trailing partial row)
+constexpr int kSlabChunk = 2048;    // nonzeros per chunk (4 per thread)
+constexpr int kSlabEntries = 1024;  // row runs per chunk
+struct SlabData {
+    int num_chunks = 0, num_entries = 0;
+    int4 *d_blk = nullptr;              // [blocks] {first row, rows ending in the block, chunk0, chunk1}
+    int4 *d_chunk = nullptr;            // [chunks + 1] {stream start, length | lanes_log2 << 16, slab, entry0}
+    uint2 *d_ent = nullptr;             // [entries] {offset in chunk | length << 16, row in block}
+    double *d_val = nullptr;            // [nnz + pad] values, slab-major within each block
+    unsigned short *d_col = nullptr;    // [nnz + pad] column - slab * kSlabCols
+    double x_bytes_per_nnz = 0.0;       // x staged per nonzero (plan statistic, spmv_plan's choice)
+};
+
 // A merge-path tile plan for one nominal tile size (merge items per tile).
 //
 // Tile t covers the merge-path diagonals between boundary t and t+1.  A boundary whose
@@ -76,6 +95,7 @@ struct TilePlan {
                                         // the rest take its register fallback)
     std::vector<unsigned char> h_blk_reg;  // [num_tiles] 1: the plain SpMV reduces the tile in registers
                                            // (a reordered sum: mspmv_tile_modes reports 255)
+    SlabData *slab = nullptr;           // column-slab plan (tiles = blocks; mspmv_slab.hip), else null
 };
 
 // Device-resident CG scalars (one set per right-hand side column).
@@ -166,6 +186,9 @@ struct mspmv_handle_s {
     // plain single-RHS SpMV on one-wave tiles (a plan of its own, TilePlan::lanes = 64): -1 not
     // decided yet, 0 no, 1 yes (mspmv_api.hip spmv_plan: skewed rows, most tiles merge walks)
     int spmv_onewave = -1;
+    // plain single-RHS SpMV on the column-slab plan (mspmv_slab.hip, plan key kSlabPlanKey): -1 not
+    // decided yet, 0 no, 1 yes (spmv_plan; MSPMV_SPMV_SLAB)
+    int spmv_slab = -1;
 };
 
 // IC(0) factor on the device (mspmv_ic0_create): L and its transpose for the two sync-free
@@ -187,6 +210,16 @@ struct mspmv_ic0_s {
 };
 
 namespace mspmv {
+
+// ---- column-slab SpMV (mspmv_slab.hip) ---------------------------------------------
+constexpr int kSlabPlanKey = -1;
+// Builds the column-slab plan into *p (blocks, split rows, reordered stream); MSPMV_ERR_UNSUPPORTED
+// when the matrix does not fit the form (rows per block); p is freed by the caller on any error.
+mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p);
+void free_slab(SlabData *s);
+hipError_t launch_slab(mspmv_handle_s *h, const TilePlan &plan, const double *d_x, double *d_y);
+std::string slab_kernel_name(const mspmv_handle_s *h);
+mspmv_status plan_split_rows(TilePlan &p, const std::vector<int2> &hb, const std::vector<unsigned char> &hs);
 
 // ---- launchers (mspmv_kernels.hip) --------------------------------------------------
 void set_error(const std::string &msg);

@@ -17,6 +17,7 @@
 //   * tiles are dealt XCD-contiguously (blocks b and b+8 share an XCD), so each XCD's L2
 //     sees one contiguous band of x / X.
 #include "mspmv_internal.h"
+#include "mspmv_device.h"
 
 #include <algorithm>
 #include <type_traits>
@@ -29,23 +30,6 @@ namespace mspmv {
 // ------------------------------------------------------------------------------------------
 // helpers
 // ------------------------------------------------------------------------------------------
-__device__ __forceinline__ int xcd_tile(int b, int T, int K = 1)
-{
-    // Blocks are dealt round-robin over the 8 XCDs; give XCD k (= b % 8, a label only) the
-    // contiguous tile range [k*q + min(k,r), +q + (k<r)).  Bijective for any T.
-    // K > 1: that range is cut into K contiguous sub-ranges walked side by side (the XCD's i-th
-    // block takes sub-range i % K, position i / K), so the resident workgroups stream from K
-    // places per XCD instead of one window.  Bijective for any T, K >= 1.
-    const int q = T >> 3, r = T & 7;
-    const int k = b & 7, i = b >> 3;
-    const int base = k * q + (k < r ? k : r);
-    if (K <= 1)
-        return base + i;
-    const int cnt = q + (k < r ? 1 : 0);
-    const int q2 = cnt / K, r2 = cnt - q2 * K;
-    const int s = i % K, pos = i / K;
-    return base + s * q2 + (s < r2 ? s : r2) + pos;
-}
 
 template <typename... KArgs, typename... Args>
 static void ggl(void (*kernel)(KArgs...), dim3 grid, dim3 block, hipStream_t s, Args... args)
@@ -82,19 +66,6 @@ __device__ __forceinline__ double2 ld_stream(const double2 *p)
     return *p;
 }
 
-__device__ __forceinline__ void store_sc1(double *p, double v)
-{
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double load_sc1(const double *p)
-{
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void store_sc1_2(double *p, double2 v)
-{
-    store_sc1(p, v.x);
-    store_sc1(p + 1, v.y);
-}
 // Merge-path search (cpu_spmv.cpp:208-235 semantics) over an LDS copy of the tile's row
 // end offsets, stored relative to the tile's first nonzero; list B is 0..b_len-1.
 __device__ __forceinline__ void lds_search(int d, const int *s_rowend, int a_len, int b_len, int &x, int &y)
@@ -701,75 +672,6 @@ struct TileArgs {
     int blk_spmv;      // the plain SpMV runs k_spmv_blk on this plan (TilePlan::blk_spmv; mixed plans too)
     int n;             // columns (x holds n entries)
 };
-
-// Split rows, closed inside the tile kernel (replaces r03's k_fixup launch).  A row longer than the
-// snap distance spans consecutive tiles: each tile that ends inside it stores its partial as a carry,
-// and the tile where it ends (its completing tile) stores the row's own part -- its row 0 -- to
-// head_val instead of y (TileArgs::y0: one address select per row store, no branch).  The row's nc + 1
-// tiles publish with agent scope (carries directly, the head copied to head_pub here) and take one
-// ticket each on fix_cnt[completing tile]; whichever draws the last one -- no waiting: it is simply
-// the last to finish -- closes the row: wave w takes columns j = w, w + TB/64, ...: lane l sums carries
-// l, l + 64, ... in tile order, a fixed xor butterfly folds the wave, lane 0 adds the head and stores
-// y's row (k_fixup's order, so reproducible), and the ticket is reset for the next launch.  fx =
-// fix[t] (plan time): x = the completing tile of the row this tile ends inside (-1: none), y = that
-// row's carry count, z = the carry count of the row this tile completes (0: none).  Call from every
-// thread after the tile's rows and carry are stored and after any pass that reads its own rows back
-// (the dot mode's).
-__device__ __forceinline__ int4 load_fix(const TileArgs &a, int t)  // block-uniform: kept in SGPRs
-{
-    if (!a.fix)
-        return make_int4(-1, 0, 0, 0);
-    const int4 f = a.fix[t];
-    return make_int4(__builtin_amdgcn_readfirstlane(f.x), __builtin_amdgcn_readfirstlane(f.y),
-                     __builtin_amdgcn_readfirstlane(f.z), 0);
-}
-template <int TB>
-__device__ __forceinline__ void close_split_rows(const TileArgs &a, int t, int4 fx, int L, int ld)
-{
-    if (fx.x < 0 && fx.z == 0)  // block-uniform
-        return;
-    __shared__ int s_fin[2];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this tile's carry and head are out
-    __syncthreads();
-    if (fx.z > 0) {  // the head, stored by this workgroup: republished with agent scope
-        for (int j = threadIdx.x; j < L; j += TB)
-            store_sc1(&a.head_pub[(size_t)t * L + j], a.head_val[(size_t)t * L + j]);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        int f0 = -1, f1 = -1;
-        if (fx.x >= 0 &&
-            __hip_atomic_fetch_add(&a.fix_cnt[fx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)fx.y)
-            f0 = fx.x;
-        if (fx.z > 0 &&
-            __hip_atomic_fetch_add(&a.fix_cnt[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)fx.z)
-            f1 = t;
-        s_fin[0] = f0;
-        s_fin[1] = f1;
-    }
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int tc = s_fin[q], nc = q == 0 ? fx.y : fx.z;
-        if (tc < 0)
-            continue;
-        const size_t R = (size_t)a.bounds[tc].x;
-        for (int j = (int)threadIdx.x >> 6; j < L; j += TB / 64) {  // wave-uniform
-            double sum = 0.0;
-            for (int u = lane; u < nc; u += 64)
-                sum += load_sc1(&a.carry_val[(size_t)(tc - nc + u) * L + j]);
-#pragma unroll
-            for (int off = 32; off > 0; off >>= 1)
-                sum += __shfl_xor(sum, off);
-            if (lane == 0)
-                a.y[R * ld + j] = sum + load_sc1(&a.head_pub[(size_t)tc * L + j]);
-        }
-        if (threadIdx.x == 0)
-            __hip_atomic_store(&a.fix_cnt[tc], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
 
 // Tile-kernel modes.
 //   0: y = A x.
@@ -1970,7 +1872,10 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
         if (sub == 0) {
             const size_t off = (size_t)(r0 + r) * a.ld + 2 * lane;
             if (r < nrows)
-                *reinterpret_cast<double2 *>(FIX && r == 0 ? a.y0 + 2 * lane : a.y + off) = acc;
+                // nontemporal: Y does not displace the panel X from the caches (nlpkkt120 size, L = 8:
+                // 476 -> 450 us per SpMM, r04n)
+                __builtin_nontemporal_store(v2d_t{acc.x, acc.y},
+                                            reinterpret_cast<v2d_t *>(FIX && r == 0 ? a.y0 + 2 * lane : a.y + off));
             else  // the trailing partial row -> carry (close_split_rows adds the row's carries in order)
                 store_sc1_2(a.carry_val + (size_t)t * L + 2 * lane, acc);
         }
@@ -2118,7 +2023,9 @@ k_spmm_tile(TileArgs a)
     const bool need_cin = (cx < ex) && (cy > (cx == 0 ? 0 : s_rowend[cx - 1]));
 
     auto write_row = [&](int row, double2 val) {
-        *reinterpret_cast<double2 *>(FIX && row == 0 ? a.y0 + 2 * lane : a.y + (size_t)(r0 + row) * a.ld + 2 * lane) = val;
+        __builtin_nontemporal_store(v2d_t{val.x, val.y},  // nontemporal, as spmm_group_rows' row stores
+                                    reinterpret_cast<v2d_t *>(FIX && row == 0 ? a.y0 + 2 * lane
+                                                                              : a.y + (size_t)(r0 + row) * a.ld + 2 * lane));
     };
 
     double2 run = make_double2(0.0, 0.0);
@@ -3190,6 +3097,8 @@ int blk_kr(const TilePlan &p) { return p.blk_rows_max <= 6 ? 6 : 8; }
 
 std::string spmv_kernel_name(const mspmv_handle_s *h)
 {
+    if (h->spmv_slab == 1)
+        return slab_kernel_name(h);
     const std::string nt = stream_nt(h) ? "true" : "false";
     const auto it = h->plans.find(plan_key(1));
     if (h->spmv_onewave != 1 && it != h->plans.end() && it->second.blk_spmv)
@@ -3488,6 +3397,8 @@ hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const 
 {
     if (plan.num_tiles == 0)
         return hipSuccess;
+    if (plan.slab)  // the column-slab plan (single RHS, plain SpMV only: spmv_plan)
+        return L == 1 ? launch_slab(h, plan, d_X, d_Y) : hipErrorInvalidValue;
     TileArgs a = make_args(h, plan, d_X, d_Y, L);
     if (ld > 0)
         a.ld = ld;
