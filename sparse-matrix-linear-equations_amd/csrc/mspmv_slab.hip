@@ -3,14 +3,14 @@
 // wide band), which the tile kernels serve one L2 line per nonzero.  Here the work is cut into a few
 // large blocks (two resident per CU, merge-path balanced like the tiles: cpu_spmv.cpp:208-235), and
 // each block's nonzeros are reordered at plan time by column slab -- kSlabCols columns of x, 32 KB --
-// so the block stages each slab of x it touches into LDS once, with coalesced 16-B loads, and gathers
+// so the block stages each slab of x it touches into LDS once, with coalesced loads, and gathers
 // from LDS.  A scattered band of +-10,000 columns then reads ~3 slabs of x per block instead of one L2
 // line per nonzero.
 //
 // Per block: rows ending in the block accumulate in LDS (yacc); the reordered stream is cut into
 // chunks of <= kSlabChunk nonzeros of one slab, each chunk's runs of one row listed as entries
-// {offset, length, row}.  Per chunk: the products val * x[col] go to LDS (the chunk's stream and
-// entries were loaded into registers during the previous chunk), then groups of 2^lg lanes take the
+// {offset, length, row}.  Per chunk: the products val * x[col] go to LDS (the chunk's stream, its
+// entries and, at a slab change, its slab of x were loaded into registers during the previous chunk), then groups of 2^lg lanes take the
 // entries round-robin, lane j summing products j, j + 2^lg, ... of its run in order, a fixed xor
 // butterfly folds the group and its lane 0 adds the run to yacc[row] -- a row has one run per chunk,
 // and chunks run in order, so every sum is fixed-order (reproducible) and within the 2 (len+1) eps
@@ -93,26 +93,31 @@ __global__ __launch_bounds__(kSlabThreads) void k_spmv_slab(SlabArgs a)
             e[j] = k < ne ? a.ent[e0 + k] : make_uint2(0u, 0u);
         }
     };
-    if (bd.z < bd.w)
+    constexpr int XPT = kSlabCols / TB;  // x values per thread and slab
+    double xq[XPT];
+    auto fetch_x = [&](int slab) {  // a slab of x, into registers (coalesced: lane-consecutive columns)
+        const int c0 = slab * kSlabCols;
+#pragma unroll
+        for (int j = 0; j < XPT; ++j) {
+            const int col = c0 + tid + j * TB;
+            xq[j] = col < a.n ? a.x[col] : 0.0;
+        }
+    };
+    if (bd.z < bd.w) {
         fetch(bd.z);
+        fetch_x(a.chunk[bd.z].z);
+    }
     int cur = -1;
     for (int ci = bd.z; ci < bd.w; ++ci) {
         const int4 cd = a.chunk[ci];
         const int len = cd.y & 0xffff, lg = cd.y >> 16;
         const int ne = a.chunk[ci + 1].w - cd.w;
-        if (cd.z != cur) {  // block-uniform: stage the chunk's slab of x
+        if (cd.z != cur) {  // block-uniform: the chunk's slab, fetched during the previous chunk
             cur = cd.z;
             __syncthreads();  // the previous chunk's readers of xs are done
-            const int c0 = cur * kSlabCols;
-            double q[kSlabCols / TB];
 #pragma unroll
-            for (int j = 0; j < kSlabCols / TB; ++j) {
-                const int col = c0 + tid + j * TB;
-                q[j] = col < a.n ? a.x[col] : 0.0;
-            }
-#pragma unroll
-            for (int j = 0; j < kSlabCols / TB; ++j)
-                xs[tid + j * TB] = q[j];
+            for (int j = 0; j < XPT; ++j)
+                xs[tid + j * TB] = xq[j];
             __syncthreads();
         }
 #pragma unroll
@@ -127,8 +132,12 @@ __global__ __launch_bounds__(kSlabThreads) void k_spmv_slab(SlabArgs a)
             if (k < ne)
                 sent[k] = e[j];
         }
-        if (ci + 1 < bd.w)
-            fetch(ci + 1);  // in flight while this chunk's runs are summed
+        if (ci + 1 < bd.w) {  // in flight while this chunk's runs are summed
+            fetch(ci + 1);
+            const int ns = a.chunk[ci + 1].z;
+            if (ns != cur)
+                fetch_x(ns);
+        }
         __syncthreads();
         const int G = 1 << lg, lane = tid & (G - 1);
         for (int q = tid >> lg; q < ne; q += TB >> lg) {  // uniform within a group

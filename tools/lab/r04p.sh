@@ -14,4 +14,4 @@ for rep in 1 2; do
     echo "slab=$sw $rep"; cat $OUT/spmv_slab${sw}_$rep.json
   done
 done
-bash tools/lab/ab_libs.sh $OUT/spmm 1 tools/lab/spmm_probe.py tree libmspmv_g64.so libmspmv_g0.so || exit 1
+bash tools/lab/ab_libs.sh $OUT/spmm 1 tools/lab/spmm_probe.py tree libmspmv_g64.so libmspmv_g0.so libmspmv_lg1.so libmspmv_lg2.so || exit 1
