@@ -417,9 +417,10 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
 // it can hold, =0 never; by default a matrix takes it when its workgroup plan gathers through column
 // dictionaries on most tiles (x gathers line-bound: scattered columns) and the slab plan stages at
 // most kSlabAutoBytes of x per nonzero (the columns of a block lie in a few slabs: a band, not the
-// whole width).
-constexpr double kSlabAutoBytes = 4.0;
-constexpr bool kSlabAuto = false;  // the default choice is off until measured on the GPU
+// whole width).  Scattered band at pwtk size: 58.9 -> 43.9 us per launch (r04t); cant (not
+// line-bound) 13.8 us on tiles against 16.2 on slabs, so it keeps its tiles.
+constexpr double kSlabAutoBytes = 16.0;
+constexpr bool kSlabAuto = true;
 static int slab_switch()  // read at each handle's decision (tests set it per matrix)
 {
     const char *e = getenv("MSPMV_SPMV_SLAB");

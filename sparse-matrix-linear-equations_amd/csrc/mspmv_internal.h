@@ -32,6 +32,8 @@ constexpr int kSlabCols = 4096;     // columns per slab: 32 KB of x in LDS
 constexpr int kSlabRows = 2047;     // rows ending in one block (+ a trailing partial row)
 constexpr int kSlabChunk = 2048;    // nonzeros per chunk (4 per thread)
 constexpr int kSlabEntries = 1024;  // row runs per chunk
+constexpr int kSlabBlocksPerCu = 2; // resident blocks per CU (LDS: 76 KB per block)
+constexpr int kSlabMaxChunks = 255; // chunks per block (their descriptors sit in LDS)
 struct SlabData {
     int num_chunks = 0, num_entries = 0;
     int4 *d_blk = nullptr;              // [blocks] {first row, rows ending in the block, chunk0, chunk1}

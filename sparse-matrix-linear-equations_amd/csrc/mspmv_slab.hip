@@ -9,8 +9,8 @@
 //
 // Per block: rows ending in the block accumulate in LDS (yacc); the reordered stream is cut into
 // chunks of <= kSlabChunk nonzeros of one slab, each chunk's runs of one row listed as entries
-// {offset, length, row}.  Per chunk: the products val * x[col] go to LDS (the chunk's stream, its
-// entries and, at a slab change, its slab of x were loaded into registers during the previous chunk), then groups of 2^lg lanes take the
+// {offset, length, row}.  Per chunk: the products val * x[col] go to LDS (the chunk's stream and
+// entries were loaded into registers two chunks earlier, its slab of x during the previous chunk), then groups of 2^lg lanes take the
 // entries round-robin, lane j summing products j, j + 2^lg, ... of its run in order, a fixed xor
 // butterfly folds the group and its lane 0 adds the run to yacc[row] -- a row has one run per chunk,
 // and chunks run in order, so every sum is fixed-order (reproducible) and within the 2 (len+1) eps
@@ -65,32 +65,45 @@ __global__ __launch_bounds__(kSlabThreads) void k_spmv_slab(SlabArgs a)
     __shared__ double yacc[kSlabRows + 1];
     __shared__ double prod[kSlabChunk];
     __shared__ uint2 sent[kSlabEntries];
+    __shared__ int4 schunk[kSlabMaxChunks + 1];
     const int tid = threadIdx.x;
     const int b = xcd_tile(blockIdx.x, a.num_tiles);
     const int4 bd = a.blk[b];  // {first row, rows ending here, chunk0, chunk1}
+    // the block's chunk descriptors (and the next one's entry start) in LDS: a scalar load per chunk
+    // would put its round trip at the head of every chunk
+    for (int i = tid; i <= bd.w - bd.z; i += TB)
+        schunk[i] = a.chunk[bd.z + i];
+    __syncthreads();
+    auto chunk = [&](int ci) {  // block-uniform
+        const int4 c = schunk[ci - bd.z];
+        return make_int4(__builtin_amdgcn_readfirstlane(c.x), __builtin_amdgcn_readfirstlane(c.y),
+                         __builtin_amdgcn_readfirstlane(c.z), __builtin_amdgcn_readfirstlane(c.w));
+    };
     const int4 fx = load_fix(a, b);
     const int nrows = bd.y;
     const bool tail = a.split[b + 1] != 0;
     for (int i = tid; i < nrows + (tail ? 1 : 0); i += TB)
         yacc[i] = 0.0;
 
-    double v[IPT];
-    unsigned short c[IPT];
-    uint2 e[EPT];
-    auto fetch = [&](int ci) {  // chunk ci's stream and entries, into registers
-        const int4 cd = a.chunk[ci];
+    struct Regs {  // one chunk's stream and entries, in registers
+        double v[IPT];
+        unsigned short c[IPT];
+        uint2 e[EPT];
+    };
+    auto fetch = [&](int ci, Regs &r) {
+        const int4 cd = chunk(ci);
         const int len = cd.y & 0xffff;
-        const int e0 = cd.w, ne = a.chunk[ci + 1].w - e0;
+        const int e0 = cd.w, ne = chunk(ci + 1).w - e0;
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
             const int k = min(tid + j * TB, len - 1);  // clamped: every load is issued
-            v[j] = slab_stream<NT>(a.val + cd.x + k);
-            c[j] = slab_stream<NT>(a.col + cd.x + k);
+            r.v[j] = slab_stream<NT>(a.val + cd.x + k);
+            r.c[j] = slab_stream<NT>(a.col + cd.x + k);
         }
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
             const int k = tid + j * TB;
-            e[j] = k < ne ? a.ent[e0 + k] : make_uint2(0u, 0u);
+            r.e[j] = k < ne ? a.ent[e0 + k] : make_uint2(0u, 0u);
         }
     };
     constexpr int XPT = kSlabCols / TB;  // x values per thread and slab
@@ -103,16 +116,16 @@ __global__ __launch_bounds__(kSlabThreads) void k_spmv_slab(SlabArgs a)
             xq[j] = col < a.n ? a.x[col] : 0.0;
         }
     };
-    if (bd.z < bd.w) {
-        fetch(bd.z);
-        fetch_x(a.chunk[bd.z].z);
-    }
     int cur = -1;
-    for (int ci = bd.z; ci < bd.w; ++ci) {
-        const int4 cd = a.chunk[ci];
+    // One chunk: its slab (fetched during the previous chunk) into LDS when it changes, the products
+    // and entries from registers into LDS, the registers refilled two chunks ahead (chunk ci + 2:
+    // the stream's latency hides behind two chunks' sums, not one), the next slab fetched when the
+    // next chunk changes it, then the runs summed into yacc.
+    auto process = [&](int ci, Regs &r) {
+        const int4 cd = chunk(ci);
         const int len = cd.y & 0xffff, lg = cd.y >> 16;
-        const int ne = a.chunk[ci + 1].w - cd.w;
-        if (cd.z != cur) {  // block-uniform: the chunk's slab, fetched during the previous chunk
+        const int ne = chunk(ci + 1).w - cd.w;
+        if (cd.z != cur) {  // block-uniform
             cur = cd.z;
             __syncthreads();  // the previous chunk's readers of xs are done
 #pragma unroll
@@ -124,17 +137,18 @@ __global__ __launch_bounds__(kSlabThreads) void k_spmv_slab(SlabArgs a)
         for (int j = 0; j < IPT; ++j) {
             const int k = tid + j * TB;
             if (k < len)
-                prod[k] = v[j] * xs[c[j]];
+                prod[k] = r.v[j] * xs[r.c[j]];
         }
 #pragma unroll
         for (int j = 0; j < EPT; ++j) {
             const int k = tid + j * TB;
             if (k < ne)
-                sent[k] = e[j];
+                sent[k] = r.e[j];
         }
-        if (ci + 1 < bd.w) {  // in flight while this chunk's runs are summed
-            fetch(ci + 1);
-            const int ns = a.chunk[ci + 1].z;
+        if (ci + 2 < bd.w)
+            fetch(ci + 2, r);
+        if (ci + 1 < bd.w) {
+            const int ns = chunk(ci + 1).z;
             if (ns != cur)
                 fetch_x(ns);
         }
@@ -152,6 +166,18 @@ __global__ __launch_bounds__(kSlabThreads) void k_spmv_slab(SlabArgs a)
                 yacc[en.y] += s;
         }
         __syncthreads();
+    };
+    Regs ra, rb;
+    if (bd.z < bd.w) {
+        fetch(bd.z, ra);
+        fetch_x(chunk(bd.z).z);
+        if (bd.z + 1 < bd.w)
+            fetch(bd.z + 1, rb);
+    }
+    for (int ci = bd.z; ci < bd.w; ci += 2) {
+        process(ci, ra);
+        if (ci + 1 < bd.w)
+            process(ci + 1, rb);
     }
     // rows ending in the block; its first row goes to the head slot when it completes a split row
     for (int i = tid; i < nrows; i += TB)
@@ -270,8 +296,8 @@ static void slab_block(const std::vector<int> &ro, const std::vector<int> &ci, c
         for (int k = k0; k < k1; ++k) {
             const int s = ci[(size_t)k] / kSlabCols;
             const int q = put[(size_t)(s - smin)]++;
-            oval[q] = va[(size_t)k];
-            ocol[q] = (unsigned short)(ci[(size_t)k] - s * kSlabCols);
+            oval[(size_t)n0 + q] = va[(size_t)k];
+            ocol[(size_t)n0 + q] = (unsigned short)(ci[(size_t)k] - s * kSlabCols);
             row[(size_t)q] = r - r0;
         }
     }
@@ -310,7 +336,7 @@ mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p)
     std::vector<unsigned char> hs;
     int T = 0;
     long long step = 0;
-    for (int G = 2 * h->num_cus;; G *= 2) {  // two resident blocks per CU; more when rows are short
+    for (int G = kSlabBlocksPerCu * h->num_cus;; G *= 2) {  // one resident generation; more when rows are short
         if (G > 64 * h->num_cus)
             return MSPMV_ERR_UNSUPPORTED;
         step = (total + G - 1) / G;
@@ -399,6 +425,10 @@ mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p)
         }
         ents.insert(ents.end(), o.ents.begin(), o.ents.end());
         blk[(size_t)t] = make_int4(hb[(size_t)t].x, hb[(size_t)t + 1].x - hb[(size_t)t].x, c0, (int)chunks.size());
+        if ((int)o.chunks.size() > kSlabMaxChunks) {  // more slabs than one block's LDS table holds
+            delete s;
+            return MSPMV_ERR_UNSUPPORTED;
+        }
         staged += (long long)o.slabs * kSlabCols * 8;
     }
     chunks.push_back(make_int4(0, 0, 0, (int)ents.size()));  // sentinel: the last chunk's entry end
