@@ -318,10 +318,19 @@ static void slab_block(const std::vector<int> &ro, const std::vector<int> &ci, c
                 q = k;
             }
             const int len = q - start;
+            // lanes per run: the fewest latency steps -- rounds of runs over the workgroup x (the run's
+            // products per lane + its butterfly + ~8 steps of LDS round trips); the older rule, the
+            // smallest G with 4 G >= the mean run, took two rounds where one does (44 -> 40 us, r04w)
             const int mean = (len + ne - 1) / ne;
-            int lg = 0;
-            while (lg < 6 && (4 << lg) < mean)
-                ++lg;
+            int lg = 0, best = 1 << 30;
+            for (int l = 0; l <= 6; ++l) {
+                const int rounds = (ne + (kSlabThreads >> l) - 1) / (kSlabThreads >> l);
+                const int cost = rounds * ((mean + (1 << l) - 1) / (1 << l) + 2 * l + 8);
+                if (cost < best) {
+                    best = cost;
+                    lg = l;
+                }
+            }
             out.chunks.push_back(make_int4(n0 + start, len | (lg << 16), smin + s, e0));
         }
     }
