@@ -417,9 +417,12 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
 // it can hold, =0 never; by default a matrix takes it when its workgroup plan gathers through column
 // dictionaries on most tiles (x gathers line-bound: scattered columns) and the slab plan stages at
 // most kSlabAutoBytes of x per nonzero (the columns of a block lie in a few slabs: a band, not the
-// whole width).  Scattered band at pwtk size: 58.9 -> 43.9 us per launch (r04t); cant (not
-// line-bound) 13.8 us on tiles against 16.2 on slabs, so it keeps its tiles.
+// whole width).  Scattered band at pwtk size: 58.9 -> 40 us per launch (r04w).
 constexpr double kSlabAutoBytes = 16.0;
+// ... and its blocks hold >= kSlabAutoNnzPerBlock nonzeros: a block's fixed costs (its descriptors,
+// yacc, the first slab, the write-out) then spread over >= 6 chunks.  cant (7,800 per block) took the
+// slab plan without it and lost: 0.396 against 0.43 on tiles (r04x).
+constexpr double kSlabAutoNnzPerBlock = 12288.0;
 constexpr bool kSlabAuto = true;
 static int slab_switch()  // read at each handle's decision (tests set it per matrix)
 {
@@ -447,7 +450,7 @@ static mspmv_status spmv_slab_decide(mspmv_handle_s *h, const TilePlan *wg)
         free_plan(p);
         return st;
     }
-    if (sw < 0 && p.slab->x_bytes_per_nnz > kSlabAutoBytes) {
+    if (sw < 0 && (p.slab->x_bytes_per_nnz > kSlabAutoBytes || (double)h->nnz < kSlabAutoNnzPerBlock * p.num_tiles)) {
         free_plan(p);
         return MSPMV_OK;
     }

@@ -6,7 +6,7 @@ scattered, skewed, split, empty and rectangular rows; checked against the oracle
 (cpu_spmv.cpp:241-265) within the reordering bound (the slab order is a reordered CSR sum:
 mspmv_tile_modes reports every block as 255), bit-identical on repeats and under a CU limit's
 rebuilt plan against the oracle again.  The default choice (scattered band: slab; FEM, stencil,
-power-law: tiles) is checked on its own.
+cant: tiles) is checked on its own.
 """
 import numpy as np
 import pytest
@@ -101,6 +101,7 @@ def test_slab_default_choice(monkeypatch):
         "scatter": (lambda: scatter_band(217918, 53, 10000, 77), True),
         "fem": (lambda: mspmv.CsrMatrix.synth_fem_blocked(21792, 1152443, 6, 170, seed=3), False),
         "stencil": (lambda: mspmv.CsrMatrix.synth_stencil(1, 40 * 30 * 30, 40, 30, 30, seed=1, diag_shift=1e-2), False),
+        "cant": (lambda: scatter_band(62451, 64, 2000, 1), False),  # small blocks: tiles win (r04x)
     }
     for name, (make, slab) in want.items():
         with mspmv.GpuCsr(make()) as g:
