@@ -371,7 +371,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
     }
     // multi-RHS: only the L = 16 plan (k_spmm_tile's DICT path runs at L = 16 only)
     const bool multi = !single;
-    const bool want = multi ? L == 16 && tile != tile_items_for(8) : true;
+    const bool want = multi ? spmm_dict_max(L) > 0 && (L == 8 || tile != tile_items_for(8)) : true;
     if (T > 0 && h->nnz > 0 && want) {
         if ((st = dev_alloc(&p.d_dict, (size_t)h->nnz + kNnzPad)) != MSPMV_OK ||
             (st = dev_alloc(&p.d_ndict, (size_t)T)) != MSPMV_OK ||
@@ -381,7 +381,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         if (e == hipSuccess)
             e = hipMemsetAsync(p.d_idx16, 0, sizeof(unsigned short) * ((size_t)h->nnz + kNnzPad), h->stream);
         if (e == hipSuccess)
-            e = launch_build_dict(h->d_cols, p.d_bounds, T, maxi, p.d_dict, p.d_ndict, p.d_idx16, h->stream, multi);
+            e = launch_build_dict(h->d_cols, p.d_bounds, T, maxi, p.d_dict, p.d_ndict, p.d_idx16, h->stream, multi, L);
         std::vector<int> hnd((size_t)T);
         if (e == hipSuccess)
             e = hipMemcpyAsync(hnd.data(), p.d_ndict, sizeof(int) * T, hipMemcpyDeviceToHost, h->stream);

@@ -250,12 +250,14 @@ hipError_t launch_build_blocks(const int *d_row_offsets, const int *d_cols, cons
                                const unsigned char *d_split, const int *d_colbase, int num_tiles, uint4 *d_blk,
                                hipStream_t s, int max_chunks = 8);
 hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_tiles, int max_items, int *d_dict,
-                             int *d_ndict, unsigned short *d_idx16, hipStream_t s, bool multi);
+                             int *d_ndict, unsigned short *d_idx16, hipStream_t s, bool multi, int L = 1);
 // Multi-RHS column dictionaries: the distinct panel rows a tile parks in LDS, 8 KB per workgroup
 // (L = 16: 64 rows), which keeps 7 workgroups per CU; 16 KB (5 per CU) measured 105 vs 102 us and
 // 24 KB 119 us on the pwtk shape.
-constexpr int kSpmmDictBytes = 8192;
-constexpr int spmm_dict_max(int L) { return kSpmmDictBytes / (8 * L); }
+constexpr int kSpmmDictBytes = 8192;   // L = 16: 64 distinct panel rows per tile
+constexpr int kSpmmDict8Bytes = 0;     // L = 8 (0: no dictionaries at L = 8)
+constexpr int spmm_dict_bytes(int L) { return L == 16 ? kSpmmDictBytes : L == 8 ? kSpmmDict8Bytes : 0; }
+constexpr int spmm_dict_max(int L) { return spmm_dict_bytes(L) / (8 * L); }
 // y = A x (L == 1) or Y = A X (row-major panels), tile kernel + optional carry fix-up.
 hipError_t launch_spmm(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
                        int *kernels_launched, int ld = 0);

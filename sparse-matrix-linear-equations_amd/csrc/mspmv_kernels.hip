@@ -1890,7 +1890,7 @@ __device__ __forceinline__ void spmm_group_rows(const TileArgs &a, const int *s_
 constexpr int spmm_waves_per_eu(int L, int IPTG, bool DICT = false)
 {
     const int items = (kBlock / (L / 2)) * IPTG;
-    const int lds = 16 * (items + items / kSnapDiv) + 6144 + (DICT ? kSpmmDictBytes : 0);  // + s_crow, s_cval, s_red2
+    const int lds = 16 * (items + items / kSnapDiv) + 6144 + (DICT ? spmm_dict_bytes(L) : 0);  // + s_crow, s_cval, s_red2
     const int w = 163840 / lds;
     return w < 1 ? 1 : w > 7 ? 7 : w;
 }
@@ -3125,7 +3125,7 @@ std::string spmm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan, int 
     if (plan.d_blk && plan.num_tiles_reg == plan.num_tiles && spmm_blk_enabled())
         return "k_spmm_blk<" + std::to_string(L) + ",0," + nt + "," + std::to_string(blk_kr(plan)) + ">";
     const int iptg = spmm_iptg_for(L);
-    const bool dict = L == 16 && plan.d_dict;
+    const bool dict = spmm_dict_max(L) > 0 && plan.d_dict;
     return "k_spmm_tile<" + std::to_string(L) + "," + std::to_string(iptg) + ",0," + nt +
            (dict ? ",true,true>" : plan.num_carries > 0 ? ",false,true>" : ",false,false>");
 }
@@ -3209,13 +3209,13 @@ hipError_t launch_build_blocks(const int *d_row_offsets, const int *d_cols, cons
     return hipGetLastError();
 }
 
-// multi: the L = 16 plan (dictionaries of at most spmm_dict_max(16) entries: what its kernel
-// parks in LDS; the kernel checks the limit again)
+// multi: an L-wide plan (dictionaries of at most spmm_dict_max(L) entries: what its kernel parks in
+// LDS; the kernel checks the limit again)
 hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_tiles, int max_items, int *d_dict,
-                             int *d_ndict, unsigned short *d_idx16, hipStream_t s, bool multi)
+                             int *d_ndict, unsigned short *d_idx16, hipStream_t s, bool multi, int L)
 {
     const int ratio = multi ? -1 : 1;
-    const int dmax = multi ? spmm_dict_max(16) : 1 << 30;
+    const int dmax = multi ? spmm_dict_max(L) : 1 << 30;
     if (max_items <= 4096)
         hipLaunchKernelGGL(k_build_dict<4096>, dim3(num_tiles), dim3(kBlock), 0, s, d_cols, d_bounds, d_dict, d_ndict,
                            d_idx16, ratio, dmax);
@@ -3294,7 +3294,7 @@ static void launch_spmm_nt(const TileArgs &a, hipStream_t s, bool nt)
 {
     if constexpr (MODE != kModeCg) {
         const dim3 grid(a.num_tiles), block(kBlock);
-        if constexpr (LL == 16) {  // plans with column dictionaries (L = 16 only)
+        if constexpr (spmm_dict_max(LL) > 0) {  // plans with column dictionaries (L = 16; L = 8 when enabled)
             if (a.dict) {
                 if (nt)
                     ggl(k_spmm_tile<LL, I, MODE, true, true>, grid, block, s, a);
