@@ -254,7 +254,7 @@ hipError_t launch_build_dict(const int *d_cols, const int2 *d_bounds, int num_ti
 // Multi-RHS column dictionaries: the distinct panel rows a tile parks in LDS, 8 KB per workgroup
 // (L = 16: 64 rows), which keeps 7 workgroups per CU; 16 KB (5 per CU) measured 105 vs 102 us and
 // 24 KB 119 us on the pwtk shape.
-constexpr int kSpmmDictBytes = 8192;   // L = 16: 64 distinct panel rows per tile
+constexpr int kSpmmDictBytes = 16384;  // L = 16: 128 distinct panel rows per 1,024-item tile
 constexpr int kSpmmDict8Bytes = 0;     // L = 8 (0: no dictionaries at L = 8)
 constexpr int spmm_dict_bytes(int L) { return L == 16 ? kSpmmDictBytes : L == 8 ? kSpmmDict8Bytes : 0; }
 constexpr int spmm_dict_max(int L) { return spmm_dict_bytes(L) / (8 * L); }
