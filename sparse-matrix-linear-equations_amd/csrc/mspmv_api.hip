@@ -371,7 +371,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
     }
     // multi-RHS: only the L = 16 plan (k_spmm_tile's DICT path runs at L = 16 only)
     const bool multi = !single;
-    const bool want = multi ? spmm_dict_max(L) > 0 && (L == 8 || tile != tile_items_for(8)) : true;
+    const bool want = multi ? spmm_dict_max(L) > 0 : true;
     if (T > 0 && h->nnz > 0 && want) {
         if ((st = dev_alloc(&p.d_dict, (size_t)h->nnz + kNnzPad)) != MSPMV_OK ||
             (st = dev_alloc(&p.d_ndict, (size_t)T)) != MSPMV_OK ||
@@ -402,7 +402,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
             p.d_idx16 = nullptr;
         }
     }
-    auto res = h->plans.emplace(p.lanes == 64 ? -tile : tile, p);  // one-wave: negative keys
+    auto res = h->plans.emplace(p.lanes == 64 ? -tile : plan_key(L), p);  // one-wave: negative keys
     *out = &res.first->second;
     return MSPMV_OK;
 }
