@@ -342,8 +342,9 @@ def run_spmm16(dev, cpu_seconds, do_cpu):
             g.time_spmm(dX, dY, L, 5)
             _, kern_ms, _ = g.time_spmm(dX, dY, L, 100)
             _, cold_ms, _ = g.time_spmm(dX, dY, L, 80, FLUSH_BYTES)  # 8 blocks beside flush-only controls
+            kname = g.spmm_kernel_name(L)
         nb = 12 * a.num_nonzeros + 4 * (a.num_rows + 1) + 8 * L * (a.num_cols + a.num_rows)
-        out[name] = {"m": a.num_rows, "nnz": a.num_nonzeros, "bytes_per_launch": nb,
+        out[name] = {"m": a.num_rows, "nnz": a.num_nonzeros, "kernel": kname, "bytes_per_launch": nb,
                      "hot_kernel_ms": round(kern_ms, 5), "hot_GBps": round(nb / kern_ms / 1e6, 1),
                      "hot_frac": round(nb / kern_ms / 1e6 / HBM_PEAK_GBS, 4),
                      "cold_kernel_ms": round(cold_ms, 5), "gflops_cold": round(2.0 * L * a.num_nonzeros / cold_ms / 1e6, 1),
