@@ -1158,7 +1158,7 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
         HIP_TRY(hipStreamSynchronize(hm->stream));  // hm's SpMMs are enqueued on h's stream
     }
     const bool pipelined = !hm && !ic && !cg_split_iteration(L);  // single RHS: consumer-side reductions
-    const int nblk = pipelined ? cg1_blocks(h->m) : cg_update_blocks((long long)h->m * L);
+    const int nblk = pipelined ? cg1_blocks(h->m) : cg_update_blocks((long long)h->m * L, h->num_cus);
     const int cap = hist ? std::max(hist_cap, 0) : 0;
     ST_TRY(ensure_cg_workspace(h, L, nblk, std::max(plan->num_tiles, mplan ? mplan->num_tiles : 0), cap));
     const int use_cap = hist ? cap : 0;

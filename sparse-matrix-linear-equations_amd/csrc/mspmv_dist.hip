@@ -740,7 +740,7 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
     const TilePlan *plan = nullptr;
     D_ST(get_local_plan(d, L, &plan));
     const long long elems = (long long)d->n_own * L;
-    const int nblk = cg_update_blocks(std::max(elems, 2LL));
+    const int nblk = cg_update_blocks(std::max(elems, 2LL), d->local->num_cus);
     const int cap = max_err_hist ? std::max(hist_cap, 0) : 0;
     // overlapped iteration (the local rows split head | interior | tail, as mspmv_dist_spmm_dev):
     // each part's dot-mode tiles write their p.Ap partials at the part's offset, one fold sums

@@ -287,7 +287,7 @@ bool supported_L(int L);
 hipError_t launch_cg_init(mspmv_handle_s *h, const double *d_b, double *d_x, int L, double tol, int nblk);
 hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *d_x, int L, int parity, int nblk,
                                double tol);
-int cg_update_blocks(long long elems);
+int cg_update_blocks(long long elems, int num_cus);
 // Iterations per CG batch / graph replay for an m-row, nnz-nonzero matrix and L columns (mspmv_api.hip).
 int cg_batch_iters(long long m, long long nnz, int L);
 // Pipelined single-RHS CG (L == 1 unless MSPMV_CG_SPLIT=1): init (x = 0, r = p0 = b, b.b

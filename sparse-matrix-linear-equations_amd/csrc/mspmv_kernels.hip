@@ -3442,14 +3442,19 @@ hipError_t launch_spmm(mspmv_handle_s *h, const TilePlan &plan, const double *d_
     return e;
 }
 
-int cg_update_blocks(long long elems)
+// Workgroups of the CG's streaming passes: ~12 pairs per thread, at most three per CU -- fewer,
+// longer-lived workgroups stream faster here: configs[4] (nlpkkt120 size, L = 8) 0.915 -> 0.886 ms
+// per iteration against the old 2,048 (~4 pairs per thread); 4 and 2 per CU 0.895 / 0.893 (r04ae,
+// r04af).
+int cg_update_blocks(long long elems, int num_cus)
 {
     const long long pairs = (elems + 1) / 2;
-    long long b = (pairs + kBlock * 4 - 1) / (kBlock * 4);  // ~4 pairs per thread
+    long long b = (pairs + kBlock * 12 - 1) / (kBlock * 12);
+    const long long cap = 3LL * std::max(num_cus, 1);
     if (b < 1)
         b = 1;
-    if (b > 2048)
-        b = 2048;
+    if (b > cap)
+        b = cap;
     return (int)b;
 }
 
