@@ -272,7 +272,7 @@ int tile_items_for(int L);
 // Map key of the default plan for L (one-wave plans are keyed by minus their tile size: 512 is also
 // the L = 16 tile size)
 // Plans are shared by tile size (the L = 2 SpMM runs on the single-RHS plan), except that the L = 16
-// plan, whose 1,024-item tiles equal L = 8's, keeps its own (its column dictionaries).
+// plan, whose 1,024-item tiles equal L = 4's, keeps its own (its column dictionaries).
 inline int plan_key(int L) { return L == 16 ? tile_items_for(16) + 1 : tile_items_for(L); }
 // Resident single-RHS tile workgroups per CU at the default tile shape (0: non-default tuning).
 int spmv_tile_blocks_per_cu();

@@ -3112,10 +3112,11 @@ std::string spmv_kernel_name(const mspmv_handle_s *h)
 int spmv_items_per_thread() { return kSpmvIpt; }
 
 // SpMM tile depth: measured best 8 items per lane group for L <= 4 (fem-blocked pwtk shape,
-// L = 4: 55.6 vs 74.8 us at 16), 16 for L = 8 (nlpkkt120 shape, L = 8: 549 vs 741 us; 8: 705 vs 451
-// us, r04z) and 32 for L = 16 (cant shape: 39.2 -> 28.0 us -- half the tile start-ups at 6
+// L = 4: 55.6 vs 74.8 us at 16), 24 for L = 8 (nlpkkt120 shape, L = 8: 1,536-item tiles of ~55 stencil
+// rows -- one round of the 64 row groups -- 439 us vs 467 at 16, 455 at 28, 550 at 32, r04ai; pwtk
+// shape flat) and 32 for L = 16 (cant shape: 39.2 -> 28.0 us -- half the tile start-ups at 6
 // workgroups per CU instead of 7, r04aa).
-int spmm_iptg_for(int L) { return L >= 16 ? 32 : L >= 8 ? 16 : 8; }
+int spmm_iptg_for(int L) { return L >= 16 ? 32 : L >= 8 ? 24 : 8; }
 
 // The kernel a plain SpMM of native width L (1, 2, 4, 8, 16) launches on `plan` (get_plan's
 // choice for L), spelled as rocprofv3 lists it: launch_spmm_L's dispatch, restated.
@@ -3337,7 +3338,7 @@ static void launch_spmm_L(const TileArgs &a, hipStream_t s, bool nt)
             return;
         }
     }
-    launch_spmm_nt<LL, (LL >= 16 ? 32 : LL >= 8 ? 16 : 8), MODE>(a, s, nt);
+    launch_spmm_nt<LL, (LL >= 16 ? 32 : LL >= 8 ? 24 : 8), MODE>(a, s, nt);
 }
 
 // MODE 1 (pipelined single-RHS CG) exists for L == 1 in the one-tile kernel only.
