@@ -47,6 +47,7 @@ __device__ __forceinline__ T ld_stream(const T *p)
 }
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef double v2d_t __attribute__((ext_vector_type(2)));
+typedef int v2i_t __attribute__((ext_vector_type(2)));
 template <bool NT>
 __device__ __forceinline__ int4 ld_stream(const int4 *p)
 {
@@ -1963,7 +1964,40 @@ k_spmm_tile(TileArgs a)
     // Every round's loads are issued before any is stored to LDS (indices clamped into the
     // tile), the first round of row ends with them: one memory round trip per tile, not STG.
     const int re0 = a.row_offsets[min(r0 + 1 + min(tid, max(nrows - 1, 0)), a.m)];  // clamped: always issued
-    if (nnzt > 0) {  // block-uniform
+    if (!DICT && nnzt > 0) {  // block-uniform: aligned pairs (one 8-B column load and one 16-B value load
+                              // per two nonzeros: half the stream instructions; pairs straddling the
+                              // tile's ends load a neighbour's element and skip its store)
+        constexpr int STG2 = (MAXI / 2 + 1 + kBlock - 1) / kBlock;
+        const int q0 = n0 >> 1, qlast = (n0 + nnzt - 1) >> 1;
+        int2 cp[STG2];
+        double2 vp[STG2];
+#pragma unroll
+        for (int j = 0; j < STG2; ++j) {
+            const int q = min(q0 + tid + j * kBlock, qlast);
+            const v2i_t c = NT ? __builtin_nontemporal_load(reinterpret_cast<const v2i_t *>(a.cols) + q)
+                               : reinterpret_cast<const v2i_t *>(a.cols)[q];
+            cp[j] = make_int2(c.x, c.y);
+        }
+#pragma unroll
+        for (int j = 0; j < STG2; ++j)
+            vp[j] = ld_stream<NT>(reinterpret_cast<const double2 *>(a.vals) + min(q0 + tid + j * kBlock, qlast));
+#pragma unroll
+        for (int j = 0; j < STG2; ++j) {
+            const int q = q0 + tid + j * kBlock;
+            const int k = 2 * q - n0;
+            if (q <= qlast) {
+                if (k >= 0) {
+                    s_col[k] = cp[j].x;
+                    s_val[k] = vp[j].x;
+                }
+                if (k + 1 < nnzt) {
+                    s_col[k + 1] = cp[j].y;
+                    s_val[k + 1] = vp[j].y;
+                }
+            }
+        }
+    }
+    if (DICT && nnzt > 0) {  // block-uniform
         int cst[STG];
         double vst[STG];
         if (DICT && nd > 0) {
