@@ -394,14 +394,22 @@ def resident_phases(g, db, dx, thr, stamp_iters=256):
     last1 = t[:, :, 1].max(axis=1, keepdims=True)
     last3 = t[:, :, 3].max(axis=1, keepdims=True)
     med = lambda a: round(float(np.median(a)) * us, 3)
-    out = {"stamped_iterations": int(k - 1), "workgroups": int(t.shape[1]),
-           "spmv_us": med(t[:, :, 1] - t[:, :, 0]),
-           "skew1_us": med(last1[:, 0:1] - t[:, :, 1]),
-           "handoff1_us": med(t[:, :, 2] - last1),
-           "update_us": med(t[:, :, 3] - t[:, :, 2]),
-           "skew2_us": med(last3[:, 0:1] - t[:, :, 3]),
-           "handoff2_us": med(t[:, :, 4] - last3),
-           "spmv_max_us": round(float(np.median((t[:, :, 1] - t[:, :, 0]).max(axis=1))) * us, 3)}
+    if "single_reduction" in g.cg_kernel_name():
+        # one hand-off per iteration: stamps 1 = 2 = 3 after the SpMV (A w) and the vector updates
+        out = {"form": "single_reduction", "stamped_iterations": int(k - 1), "workgroups": int(t.shape[1]),
+               "spmv_update_us": med(t[:, :, 1] - t[:, :, 0]),
+               "skew_us": med(last3[:, 0:1] - t[:, :, 3]),
+               "handoff_us": med(t[:, :, 4] - last3),
+               "spmv_update_max_us": round(float(np.median((t[:, :, 1] - t[:, :, 0]).max(axis=1))) * us, 3)}
+    else:
+        out = {"form": "classic", "stamped_iterations": int(k - 1), "workgroups": int(t.shape[1]),
+               "spmv_us": med(t[:, :, 1] - t[:, :, 0]),
+               "skew1_us": med(last1[:, 0:1] - t[:, :, 1]),
+               "handoff1_us": med(t[:, :, 2] - last1),
+               "update_us": med(t[:, :, 3] - t[:, :, 2]),
+               "skew2_us": med(last3[:, 0:1] - t[:, :, 3]),
+               "handoff2_us": med(t[:, :, 4] - last3),
+               "spmv_max_us": round(float(np.median((t[:, :, 1] - t[:, :, 0]).max(axis=1))) * us, 3)}
     out["iteration_us"] = med(t[1:, :, 0] - t[:-1, :, 0])
     out["note"] = ("medians over workgroups x iterations of wall_clock64 phase stamps; handoff = last "
                    "publisher -> total received; skew = own publish -> last publisher")

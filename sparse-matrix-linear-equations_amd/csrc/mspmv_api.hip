@@ -130,6 +130,7 @@ static mspmv_status ensure_modes(mspmv_handle_s *h, TilePlan &p, int L)
 }
 
 static mspmv_status spmv_plan(mspmv_handle_s *h, const TilePlan **out);
+static mspmv_status spmm_slab_decide(mspmv_handle_s *h, int L);
 
 // plain: the caller runs the plain product (y = A x / Y = A X), whose single-RHS form may take a
 // one-wave plan of its own (spmv_plan); CG, dot-mode and sharded callers use the workgroup plan.
@@ -137,6 +138,21 @@ static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out, boo
 {
     if (plain && L == 1)
         return spmv_plan(h, out);
+    if (plain && (L == 8 || L == 16)) {
+        // the plain L-wide product on a column-slab plan when one was chosen (spmm_slab_decide, after the
+        // node-block check: FEM matrices keep k_spmm_blk)
+        const TilePlan *tp = nullptr;
+        ST_TRY(get_plan(h, L, &tp, false));
+        if (tp->d_blk && tp->num_tiles_reg == tp->num_tiles && spmm_blk_enabled()) {
+            *out = tp;
+            return MSPMV_OK;
+        }
+        if (h->spmm_slab[l_index(L)] < 0)
+            ST_TRY(spmm_slab_decide(h, L));
+        auto it = h->spmm_slab[l_index(L)] == 1 ? h->plans.find(slab_mm_key(L)) : h->plans.end();
+        *out = it != h->plans.end() ? &it->second : tp;
+        return MSPMV_OK;
+    }
     if (L > 1 && spmm_blk_enabled()) {
         // a matrix of node blocks only (every single-RHS tile a register run tile: FEM node rows)
         // multiplies L columns on that plan with k_spmm_blk -- one panel-row gather per (run,
@@ -440,22 +456,70 @@ static mspmv_status spmv_slab_decide(mspmv_handle_s *h, const TilePlan *wg)
     if (!cand)
         return MSPMV_OK;
     TilePlan p;
-    const mspmv_status st = build_slab_plan(h, p);
-    if (st == MSPMV_ERR_UNSUPPORTED) {
+    // automatic: the blocks-per-nonzero test runs inside the builder before anything past the bounds is
+    // copied or allocated, and any failure (an allocation near capacity included) means "no slab plan":
+    // the workgroup plan is ready, so the product must not fail for an optional plan
+    const mspmv_status st = build_slab_plan(h, p, sw < 0 ? kSlabAutoNnzPerBlock : 0.0);
+    if (st != MSPMV_OK && (sw < 0 || st == MSPMV_ERR_UNSUPPORTED)) {
         free_plan(p);
         set_error("");
+        (void)hipGetLastError();
         return MSPMV_OK;
     }
     if (st != MSPMV_OK) {
         free_plan(p);
         return st;
     }
-    if (sw < 0 && (p.slab->x_bytes_per_nnz > kSlabAutoBytes || (double)h->nnz < kSlabAutoNnzPerBlock * p.num_tiles)) {
+    if (sw < 0 && p.slab->x_bytes_per_nnz > kSlabAutoBytes) {
         free_plan(p);
         return MSPMV_OK;
     }
     h->plans.emplace(kSlabPlanKey, p);
     h->spmv_slab = 1;
+    return MSPMV_OK;
+}
+
+// Column-slab plan for the plain SpMM of width L = 8 or 16 (mspmv_slab.hip k_spmm_slab): MSPMV_SPMM_SLAB=1
+// takes it for every matrix it can hold, =0 never; by default a matrix whose L-wide product runs the
+// merge tiles (not the node-block SpMM) takes it when the plan stages at most kSlabMmAutoFrac of the
+// panel bytes the tiles gather (L x 8 B per nonzero): a band or a stencil, whose blocks reuse each staged
+// panel row several times, not scattered columns.
+constexpr double kSlabMmAutoFrac = 0.5;
+constexpr long long kSlabMmAutoMinNnz = 1 << 20;
+// Off by default until it beats the L-wide tiles on the BASELINE shapes: cant-shaped L = 16 48 vs 27 us,
+// nlpkkt120-size L = 8 715 vs 460 us (r05f).
+constexpr bool kSlabMmAuto = false;
+static int slab_mm_switch()
+{
+    const char *e = getenv("MSPMV_SPMM_SLAB");
+    return e && *e ? (atoi(e) != 0 ? 1 : 0) : -1;
+}
+
+static mspmv_status spmm_slab_decide(mspmv_handle_s *h, int L)
+{
+    int &dec = h->spmm_slab[l_index(L)];
+    const int sw = slab_mm_switch();
+    dec = 0;
+    if (!(sw == 1 || (sw < 0 && kSlabMmAuto && h->nnz >= kSlabMmAutoMinNnz)))
+        return MSPMV_OK;
+    TilePlan p;
+    const mspmv_status st = build_slab_mm_plan(h, L, p);
+    if (st != MSPMV_OK && (sw < 0 || st == MSPMV_ERR_UNSUPPORTED)) {  // optional: never fail the product
+        free_plan(p);
+        set_error("");
+        (void)hipGetLastError();
+        return MSPMV_OK;
+    }
+    if (st != MSPMV_OK) {
+        free_plan(p);
+        return st;
+    }
+    if (sw < 0 && p.slab->x_bytes_per_nnz > kSlabMmAutoFrac * 8.0 * L) {
+        free_plan(p);
+        return MSPMV_OK;
+    }
+    h->plans.emplace(slab_mm_key(L), p);
+    dec = 1;
     return MSPMV_OK;
 }
 
@@ -866,6 +930,8 @@ mspmv_status mspmv_set_cu_limit(mspmv_handle h, int num_cus)
         h->plans.clear();
         h->spmv_onewave = -1;
         h->spmv_slab = -1;
+        for (int &v : h->spmm_slab)
+            v = -1;
         h->num_cus = n;
         const TilePlan *plan = nullptr;
         ST_TRY(get_plan(h, 1, &plan));
@@ -1151,13 +1217,21 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
         *iters = 0;
     if (h->m == 0)
         return MSPMV_OK;
-    const TilePlan *plan = nullptr, *mplan = nullptr;
+    const TilePlan *plan = nullptr, *mplan = nullptr, *splan = nullptr;
     ST_TRY(get_plan(h, L, &plan));
+    if (!hm && !ic && cg_split_iteration(L) && (L == 8 || L == 16)) {
+        // the split iteration's plain SpMM runs on the handle's column-slab plan when the plain product
+        // takes one: decided here, before any graph capture (it may copy the matrix to the host)
+        ST_TRY(get_plan(h, L, &splan, true));
+        if (!splan->slab)
+            splan = nullptr;
+    }
     if (hm) {
         ST_TRY(get_plan(hm, L, &mplan));
         HIP_TRY(hipStreamSynchronize(hm->stream));  // hm's SpMMs are enqueued on h's stream
     }
     const bool pipelined = !hm && !ic && !cg_split_iteration(L);  // single RHS: consumer-side reductions
+    bool stalled = false;
     const int nblk = pipelined ? cg1_blocks(h->m) : cg_update_blocks((long long)h->m * L, h->num_cus);
     const int cap = hist ? std::max(hist_cap, 0) : 0;
     ST_TRY(ensure_cg_workspace(h, L, nblk, std::max(plan->num_tiles, mplan ? mplan->num_tiles : 0), cap));
@@ -1166,16 +1240,31 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
         // the whole solve as one register-resident launch, where the matrix fits (mspmv_cg_resident.hip)
         ResidentCg *rc = nullptr;
         ST_TRY(resident_for(h, &rc));
-        if (rc)
-            return cg_solve_resident(h, rc, d_b, d_x, max_iters, tol, iters, hist, use_cap);
+        if (rc) {
+            const mspmv_status rs = cg_solve_resident(h, rc, d_b, d_x, max_iters, tol, iters, hist, use_cap);
+            if (rs != MSPMV_ERR_STALL)
+                return rs;
+            // A hand-off never completed: the one-workgroup-per-CU grid was not co-resident (work on
+            // another stream or process held CUs).  The solve is run again on the pipelined kernels,
+            // whose init resets x, r and p; nothing of the stalled launch is kept.
+            set_error("");
+            stalled = true;
+        }
     }
-    h->last_cg_kernel = pipelined ? "pipelined (k_spmv_tile MODE 1 + k_cg1_update)"
+    h->last_cg_kernel = pipelined ? (stalled ? "pipelined (k_spmv_tile MODE 1 + k_cg1_update) after a resident-CG stall"
+                                             : "pipelined (k_spmv_tile MODE 1 + k_cg1_update)")
                         : hm      ? "SPAI-PCG (split)"
                         : ic      ? "IC0-PCG (split)"
                                   : "split (p update, SpMM, p.Ap, update)";
     const int saved_cap = h->hist_cap;
     h->hist_cap = use_cap;  // kernels record only what the caller asked for
     HIP_TRY(hipMemsetAsync(h->d_ctrl, 0, sizeof(CgControl), h->stream));
+    // Split-row tickets reset themselves when every tile sharing a row reaches close_split_rows; a CG
+    // SpMM returns at its stop test before that (all tiles alike, but an aborted launch might not), so
+    // every solve starts from zeroed tickets
+    for (const TilePlan *tp : {plan, splan, mplan})
+        if (tp && tp->d_fix_cnt)
+            HIP_TRY(hipMemsetAsync(tp->d_fix_cnt, 0, sizeof(unsigned) * (size_t)tp->num_tiles, h->stream));
     if (hm)
         HIP_TRY(launch_pcg_init(h, hm, *mplan, d_b, d_x, L, tol, nblk));
     else if (ic)
@@ -1203,7 +1292,7 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
         std::memcpy(&tk, &tol, sizeof tk);
         const std::vector<const void *> key = {
             d_x, h->d_r, h->d_p0, h->d_p1, h->d_ap, h->d_partials, h->d_partials_b, h->d_gtickets, h->d_scal,
-            h->d_conv, h->d_red, h->d_ctrl, h->d_hist, h->stream, plan, tk,
+            h->d_conv, h->d_red, h->d_ctrl, h->d_hist, h->stream, plan, splan, tk,
             reinterpret_cast<const void *>((intptr_t)L), reinterpret_cast<const void *>((intptr_t)nblk),
             reinterpret_cast<const void *>((intptr_t)use_cap), hm, mplan,
             hm ? (const void *)hm->d_vals : nullptr, ic, ic ? (const void *)ic->d_y : nullptr,

@@ -76,8 +76,10 @@ struct ResArgs {
     // phase boundaries of iterations k < stamp_iters, [k][w][kResStamps]; null in every other solve
     unsigned long long *stamps;
     int stamp_iters;
+    int force_stall;  // test switch (MSPMV_CG_RESIDENT_STALL): the first hand-off reports a stall
 };
-constexpr int kResStamps = 5;  // iteration start | Ap done | p.Ap summed | r done | r.r summed
+constexpr int kResStamps = 5;
+constexpr bool kResPipelinedDefault = true;  // configs[3]: 14.3 -> 9.45 us per iteration (r05i)  // iteration start | Ap done | p.Ap summed | r done | r.r summed
 
 __device__ __forceinline__ void st_sc1(double *p, double v)
 {
@@ -145,40 +147,46 @@ __device__ __forceinline__ void res_stamp(const ResArgs &a, int k, int w, int ph
         a.stamps[((size_t)k * a.G + w) * kResStamps + phase] = wall_clock64();
 }
 
-// Wave 0 polls the G slots of one phase until none holds the empty pattern (s_sleep between
-// rounds, bounded), lane l sums slots l, l + 64, ... in order, a fixed butterfly folds the lanes;
-// the total lands in *s_tot for the whole workgroup.  false: the solve stalled (timeout / abort).
-template <int NSL>
+// Wave 0 polls the G slots of one phase (NV arrays of them, slot + q G) until none holds the empty
+// pattern (s_sleep between rounds, bounded), lane l sums slots l, l + 64, ... of each array in order, a
+// fixed butterfly folds the lanes; the totals land in s_tot[q] for the whole workgroup.  false: the
+// solve stalled (timeout / abort).
+template <int NSL, int NV = 1>
 __device__ __forceinline__ bool res_wait_sum(const double *slot, int G, unsigned *abort_word, double *s_tot,
                                              int *s_ok)
 {
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
-        double v[NSL];
+        double v[NV][NSL];
         unsigned have = 0;
         bool ok = true;
 #pragma unroll
-        for (int j = 0; j < NSL; ++j)
-            v[j] = 0.0;
+        for (int q = 0; q < NV; ++q)
+#pragma unroll
+            for (int j = 0; j < NSL; ++j)
+                v[q][j] = 0.0;
         for (unsigned spin = 0;; ++spin) {
             bool miss = false;
 #pragma unroll
-            for (int j = 0; j < NSL; ++j) {
-                const int i = lane + 64 * j;
-                if (!((have >> j) & 1u)) {
-                    if (i < G) {
-                        const double q = ld_sc1(slot + i);
-                        if ((unsigned long long)__double_as_longlong(q) != kSlotEmpty) {
-                            v[j] = q;
-                            have |= 1u << j;
+            for (int q = 0; q < NV; ++q)
+#pragma unroll
+                for (int j = 0; j < NSL; ++j) {
+                    const int i = lane + 64 * j;
+                    const unsigned bit = 1u << (q * NSL + j);
+                    if (!(have & bit)) {
+                        if (i < G) {
+                            const double x = ld_sc1(slot + (size_t)q * G + i);
+                            if ((unsigned long long)__double_as_longlong(x) != kSlotEmpty) {
+                                v[q][j] = x;
+                                have |= bit;
+                            } else {
+                                miss = true;
+                            }
                         } else {
-                            miss = true;
+                            have |= bit;
                         }
-                    } else {
-                        have |= 1u << j;
                     }
                 }
-            }
             if (!__any(miss))
                 break;
             if ((spin & 63) == 63 &&
@@ -194,29 +202,231 @@ __device__ __forceinline__ bool res_wait_sum(const double *slot, int G, unsigned
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        double s = v[0];
 #pragma unroll
-        for (int j = 1; j < NSL; ++j)
-            s += v[j];
+        for (int q = 0; q < NV; ++q) {
+            double t = v[q][0];
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1)
-            s += __shfl_xor(s, off);
-        if (lane == 0) {
-            *s_tot = s;
-            *s_ok = ok ? 1 : 0;
+            for (int j = 1; j < NSL; ++j)
+                t += v[q][j];
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1)
+                t += __shfl_xor(t, off);
+            if (lane == 0)
+                s_tot[q] = t;
         }
+        if (lane == 0)
+            *s_ok = ok ? 1 : 0;
     }
     __syncthreads();
     return *s_ok != 0;
 }
 
+// Two partials of one workgroup published together (the pipelined form's r.r and w.r): fixed-order
+// block sums (wave butterflies, waves in order), every storing wave's payload drained first, then the
+// two flags.  NaN partials as res_publish.
+__device__ __forceinline__ void res_publish2(double g, double d, double *slot_g, double *slot_d, double2 *s_red2)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its payload (w) is out
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        g += __shfl_xor(g, off);
+        d += __shfl_xor(d, off);
+    }
+    if ((threadIdx.x & 63) == 0)
+        s_red2[threadIdx.x >> 6] = make_double2(g, d);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double2 t = s_red2[0];
+#pragma unroll
+        for (int w = 1; w < kRB / 64; ++w) {
+            t.x += s_red2[w].x;
+            t.y += s_red2[w].y;
+        }
+        if (t.x != t.x)
+            t.x = __longlong_as_double(0x7ff8000000000000ll);
+        if (t.y != t.y)
+            t.y = __longlong_as_double(0x7ff8000000000000ll);
+        st_sc1(slot_g, t.x);
+        st_sc1(slot_d, t.y);
+    }
+}
+
+// The pipelined (single-reduction) form: Ghysels & Vanroose's pipelined CG without preconditioner,
+// i.e. the Chronopoulos-Gear recurrence with the SpMV moved next to the reduction.  Per iteration ONE
+// hand-off carries both dot products, gamma = r.r and delta = w.r (w = A r), and the payload the next
+// SpMV gathers (w, published before the partials): the classic form needs two (p.Ap, then r.r with
+// the {r, p} payload), and each costs 3-4 us on 256 workgroups (r04 stamps), about half an iteration.
+//   i = 0: alpha = gamma / delta;  i > 0: beta = gamma_i / gamma_{i-1},
+//          alpha = gamma_i / (delta_i - beta gamma_i / alpha_{i-1})
+//   n = A w;  z = n + beta z;  s = w + beta s;  p = r + beta p;
+//   x += alpha p;  r += (-alpha) s;  w += (-alpha) z;  then gamma, delta of the new r, w
+// Exactly CGSolveSingle's iterates in exact arithmetic (alpha = r.r / p.Ap, beta, x, r), with the same
+// stop test (||r_i|| / ||b|| < tol -> i iterations, hist[i-1]), breakdown rule (a non-finite alpha stops
+// before x changes) and b_norm; the rounding differs (r and Ap come from recurrences), so it is held to
+// the oracle's CGSolveSingle by the same parity bars as the classic form (tests/test_gpu_cg_resident.py).
+// LDS vectors of the pipelined form next to the columns: x and p always, z too where it fits.
+template <int RPT, int NZR>
+constexpr int res_nxp()
+{
+    const int free = 163840 - RPT * NZR * kRB * 4 - 1024;
+    return free >= 3 * RPT * kRB * 8 ? 3 : 2;
+}
+
 template <int RPT, int NZR, int NSL>
+__device__ __forceinline__ void res_pipelined(const ResArgs &a, const double (&v)[RPT][NZR], const int (&len)[RPT],
+                                              const int (&s_col)[RPT][NZR][kRB],
+                                              double (&s_xp)[res_nxp<RPT, NZR>()][RPT][kRB], double *s_red,
+                                              double *s_tot, int *s_ok, int r0, int wgi)
+{
+    constexpr bool ZL = res_nxp<RPT, NZR>() >= 3;  // z in LDS
+    const int t = threadIdx.x;
+    const int G = a.G;
+    const unsigned wbytes = a.pair_bytes / 2;  // w buffers: one double per row
+    const __amdgpu_buffer_rsrc_t rb_b = __builtin_amdgcn_make_buffer_rsrc((void *)a.b, (short)0, (int)wbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw0 = __builtin_amdgcn_make_buffer_rsrc(a.pair0, (short)0, (int)wbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw1 = __builtin_amdgcn_make_buffer_rsrc(a.pair1, (short)0, (int)wbytes, 0x00020000);
+    double2 *s_red2 = reinterpret_cast<double2 *>(s_red);  // 16 waves x 16 B: s_red's 128 B + the next 128 B
+    // A src for this thread's rows (CSR-order sequential sums; padded slots gather row 0 and their
+    // products are dropped by a select: acc starts at +0.0, so the sum is SpmvGold's)
+    auto spmv = [&](const __amdgpu_buffer_rsrc_t src, int s) __attribute__((always_inline)) {
+        double g[NZR];
+#pragma unroll
+        for (int kk = 0; kk < NZR; ++kk)
+            g[kk] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(src, s_col[s][kk][t] * 8, 0, 16));
+        double acc = 0.0;
+#pragma unroll
+        for (int kk = 0; kk < NZR; ++kk) {
+            const double prod = v[s][kk] * g[kk];
+            acc += kk < len[s] ? prod : 0.0;
+        }
+        return acc;
+    };
+    // r, w, s, z in registers; x and p (touched once per iteration each) in this thread's LDS slots, so
+    // the form needs no more registers than the classic one
+    double r[RPT], sv[RPT], z[RPT], w[RPT];
+    double gam = 0.0, del = 0.0;
+#pragma unroll
+    for (int s = 0; s < RPT; ++s) {
+        sv[s] = z[s] = w[s] = r[s] = 0.0;
+#pragma unroll
+        for (int q = 0; q < res_nxp<RPT, NZR>(); ++q)
+            s_xp[q][s][t] = 0.0;
+        if (len[s] >= 0) {
+            const size_t R = (size_t)r0 + t + (size_t)s * kRB;
+            r[s] = a.b[R];  // x = 0, r = b (single_strategy.hpp:117-124)
+            w[s] = spmv(rb_b, s);  // w_0 = A b: b is complete from the start, no hand-off needed
+            st_sc1(a.pair0 + R, w[s]);
+            gam += r[s] * r[s];
+            del += w[s] * r[s];
+        }
+    }
+    __syncthreads();  // s_col complete (the loop above read it: every wave's columns are in)
+    int iters = a.max_iters, brk = 0;
+    res_publish2(gam, del, a.slots + (size_t)1 * G + wgi, a.slots + (size_t)2 * G + wgi, s_red2);
+    if (!res_wait_sum<NSL, 2>(a.slots + (size_t)1 * G, G, a.abort_word, s_tot, s_ok) || a.force_stall) {
+        iters = 0;
+        brk = 2;
+    } else {
+        gam = s_tot[0];
+        del = s_tot[1];
+        const double bn = sqrt(gam);
+        const double b_norm = bn == 0.0 ? 1.0 : bn;  // single_strategy.hpp:127-129
+        double gam_prev = 0.0, alpha_prev = 0.0;
+        for (int i = 0;; ++i) {
+            // (gam, del) of r_i, w_i; w_i complete in buffer i & 1
+            res_stamp(a, i, wgi, 0);
+            if (i > 0) {
+                const double rel = sqrt(gam) / b_norm;
+                if (wgi == 0 && t == 0 && a.hist && i - 1 < a.hist_cap)
+                    a.hist[i - 1] = rel;
+                if (rel < a.tol) {
+                    iters = i;
+                    break;
+                }
+            }
+            if (i == a.max_iters) {
+                iters = i;
+                break;
+            }
+            const double beta = i == 0 ? 0.0 : gam / gam_prev;
+            const double alpha = i == 0 ? gam / del : gam / (del - beta * gam / alpha_prev);
+            if (!(alpha == alpha && fabs(alpha) < HUGE_VAL)) {  // breakdown: stop before x and r change
+                iters = i + 1;
+                brk = 1;
+                break;
+            }
+            const double nal = -alpha;
+            const __amdgpu_buffer_rsrc_t cur = (i & 1) ? rw1 : rw0;
+            double *nxt = (i & 1) ? a.pair0 : a.pair1;
+            double g2 = 0.0, d2 = 0.0;
+#pragma unroll
+            for (int s = 0; s < RPT; ++s) {
+                const double n = spmv(cur, s);  // n = A w_i
+                if (len[s] >= 0) {
+                    const size_t R = (size_t)r0 + t + (size_t)s * kRB;
+                    double zs;
+                    if constexpr (ZL) {
+                        zs = n + beta * s_xp[ZL ? 2 : 0][s][t];
+                        s_xp[ZL ? 2 : 0][s][t] = zs;
+                    } else {
+                        zs = z[s] = n + beta * z[s];
+                    }
+                    sv[s] = w[s] + beta * sv[s];
+                    const double ps = r[s] + beta * s_xp[1][s][t];  // UpdatePSingle
+                    s_xp[1][s][t] = ps;
+                    s_xp[0][s][t] = s_xp[0][s][t] + alpha * ps;  // AxpySingle
+                    r[s] = r[s] + nal * sv[s];   // AxpySingle(-alpha), s = A p by recurrence
+                    w[s] = w[s] + nal * zs;
+                    st_sc1(nxt + R, w[s]);
+                    g2 += r[s] * r[s];
+                    d2 += w[s] * r[s];
+                }
+            }
+            if (a.stamps)
+                __syncthreads();
+            res_stamp(a, i, wgi, 1);
+            res_stamp(a, i, wgi, 2);
+            res_stamp(a, i, wgi, 3);
+            double *sg = a.slots + (size_t)(1 + 2 * ((i + 1) % kResRing)) * G;
+            res_publish2(g2, d2, sg + wgi, sg + G + wgi, s_red2);
+            if (!res_wait_sum<NSL, 2>(sg, G, a.abort_word, s_tot, s_ok)) {
+                iters = i;
+                brk = 2;
+                break;
+            }
+            res_stamp(a, i, wgi, 4);
+            gam_prev = gam;
+            alpha_prev = alpha;
+            gam = s_tot[0];
+            del = s_tot[1];
+            if (t == 0) {  // this workgroup's slots of ring position i + 1 + kResRing/2: empty again
+                double *ra = a.slots + (size_t)(1 + 2 * ((i + 1 + kResRing / 2) % kResRing)) * G + wgi;
+                __hip_atomic_store((unsigned long long *)ra, kSlotEmpty, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store((unsigned long long *)(ra + G), kSlotEmpty, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < RPT; ++s)
+        if (len[s] >= 0)
+            a.x[(size_t)r0 + t + (size_t)s * kRB] = s_xp[0][s][t];
+    if (wgi == 0 && t == 0) {
+        a.ctrl->iter = iters;
+        a.ctrl->iters_out = iters;
+        a.ctrl->done = 1;
+        a.ctrl->breakdown = brk;
+    }
+}
+
+template <int RPT, int NZR, int NSL, bool PIPE>
 __global__ __launch_bounds__(kRB) void k_cg_resident(ResArgs a)
 {
     __shared__ int s_col[RPT][NZR][kRB];
-    __shared__ double s_red[kRB / 64];
-    __shared__ double s_tot;
+    __shared__ double s_red[2 * (kRB / 64)];  // (the pipelined form's two-value block sums use all of it)
+    __shared__ double s_tot[2];
     __shared__ int s_ok;
+    __shared__ double s_xp[PIPE ? res_nxp<RPT, NZR>() : 1][PIPE ? RPT : 1][kRB];  // the pipelined form's x, p (z)
     const int t = threadIdx.x;
     const int w = blockIdx.x;
     const int G = a.G;
@@ -237,6 +447,10 @@ __global__ __launch_bounds__(kRB) void k_cg_resident(ResArgs a)
             s_col[s][k][t] = a.cols[e];
         }
     }
+    if constexpr (PIPE) {
+        res_pipelined<RPT, NZR, NSL>(a, v, len, s_col, s_xp, s_red, s_tot, &s_ok, r0, w);
+        return;
+    }
     // x = 0, r = p = b (single_strategy.hpp:117-124); {r_0, p_-1} = {b, b} with beta = 0 gives p_0 = b
     double x[RPT], r[RPT], p[RPT];
     double bb = 0.0;
@@ -255,11 +469,11 @@ __global__ __launch_bounds__(kRB) void k_cg_resident(ResArgs a)
     __syncthreads();  // s_col complete
     res_publish<true>(bb, a.slots + w, s_red);
     int iters = a.max_iters, brk = 0;
-    if (!res_wait_sum<NSL>(a.slots, G, a.abort_word, &s_tot, &s_ok)) {
+    if (!res_wait_sum<NSL>(a.slots, G, a.abort_word, s_tot, &s_ok) || a.force_stall) {
         iters = 0;
         brk = 2;
     } else {
-        double rs = s_tot;
+        double rs = s_tot[0];
         const double bn = sqrt(rs);
         const double b_norm = bn == 0.0 ? 1.0 : bn;  // single_strategy.hpp:127-129
         double beta = 0.0;
@@ -301,13 +515,13 @@ __global__ __launch_bounds__(kRB) void k_cg_resident(ResArgs a)
                 __syncthreads();  // stamped solves: the phase ends when every wave's rows are done
             res_stamp(a, k, w, 1);
             res_publish<false>(dot, slot_a + w, s_red);
-            if (!res_wait_sum<NSL>(slot_a, G, a.abort_word, &s_tot, &s_ok)) {
+            if (!res_wait_sum<NSL>(slot_a, G, a.abort_word, s_tot, &s_ok)) {
                 iters = k;
                 brk = 2;
                 break;
             }
             res_stamp(a, k, w, 2);
-            const double alpha = rs / s_tot;
+            const double alpha = rs / s_tot[0];
             if (!(alpha == alpha && fabs(alpha) < HUGE_VAL)) {  // breakdown: stop before x and r change
                 iters = k + 1;
                 brk = 1;
@@ -329,13 +543,13 @@ __global__ __launch_bounds__(kRB) void k_cg_resident(ResArgs a)
                 __syncthreads();
             res_stamp(a, k, w, 3);
             res_publish<true>(rr, slot_b + w, s_red);
-            if (!res_wait_sum<NSL>(slot_b, G, a.abort_word, &s_tot, &s_ok)) {
+            if (!res_wait_sum<NSL>(slot_b, G, a.abort_word, s_tot, &s_ok)) {
                 iters = k;
                 brk = 2;
                 break;
             }
             res_stamp(a, k, w, 4);
-            const double rs_new = s_tot;
+            const double rs_new = s_tot[0];
             const double rel = sqrt(rs_new) / b_norm;
             if (w == 0 && t == 0 && a.hist && k < a.hist_cap)
                 a.hist[k] = rel;
@@ -397,32 +611,39 @@ struct ResShape {
 constexpr ResShape kResShapes[] = {{1, 4}, {2, 4}, {1, 8}, {3, 4}, {2, 7}, {3, 7}, {2, 8}, {1, 16}, {3, 8}};
 
 template <int RPT, int NZR>
-hipError_t res_launch_t(const ResArgs &a, hipStream_t s, bool check_only, int *occ)
+hipError_t res_launch_t(const ResArgs &a, hipStream_t s, bool check_only, int *occ, bool pipe)
 {
     const int nsl = (a.G + 63) / 64;
     void *args[] = {(void *)&a};
-    auto go = [&](const void *kern) -> hipError_t {
-        if (check_only)
-            return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, kern, kRB, 0);
+    auto go = [&](const void *kc, const void *kp) -> hipError_t {
+        if (check_only) {  // both forms must fit one workgroup per CU
+            int o1 = 0, o2 = 0;
+            hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, kc, kRB, 0);
+            if (e == hipSuccess)
+                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, kp, kRB, 0);
+            *occ = std::min(o1, o2);
+            return e;
+        }
         // A plain launch: the grid is one workgroup per CU and the occupancy check above admitted
         // one, so every workgroup is resident -- the residency a cooperative launch would check,
         // without its per-launch host cost and its separate queue (whose teardown at process exit
         // crashed under rocprofv3: r03u).  Every spin in the kernel is bounded, so a grid that is
-        // not co-resident after all ends in MSPMV_ERR_STALL, never a hang.
-        return hipLaunchKernel(kern, dim3(a.G), dim3(kRB), args, 0, s);
+        // not co-resident after all ends in MSPMV_ERR_STALL (the caller then runs the pipelined
+        // kernels), never a hang.
+        return hipLaunchKernel(pipe ? kp : kc, dim3(a.G), dim3(kRB), args, 0, s);
     };
     if (nsl <= 4)
-        return go((const void *)k_cg_resident<RPT, NZR, 4>);
+        return go((const void *)k_cg_resident<RPT, NZR, 4, false>, (const void *)k_cg_resident<RPT, NZR, 4, true>);
     if (nsl <= 8)
-        return go((const void *)k_cg_resident<RPT, NZR, 8>);
+        return go((const void *)k_cg_resident<RPT, NZR, 8, false>, (const void *)k_cg_resident<RPT, NZR, 8, true>);
     return hipErrorInvalidValue;
 }
 
-hipError_t res_dispatch(int rpt, int nzr, const ResArgs &a, hipStream_t s, bool check_only, int *occ)
+hipError_t res_dispatch(int rpt, int nzr, const ResArgs &a, hipStream_t s, bool check_only, int *occ, bool pipe)
 {
 #define RES_CASE(R, Z)                                                                                       \
     if (rpt == R && nzr == Z)                                                                                \
-        return res_launch_t<R, Z>(a, s, check_only, occ);
+        return res_launch_t<R, Z>(a, s, check_only, occ, pipe);
     RES_CASE(1, 4)
     RES_CASE(2, 4)
     RES_CASE(1, 8)
@@ -458,6 +679,18 @@ hipError_t res_fill(int rpt, int nzr, const int *ro, const int *ci, const double
 }
 
 }  // namespace
+
+// The resident kernel's iteration: classic CGSolveSingle (two hand-offs) or the single-reduction
+// form (one; res_pipelined).  MSPMV_CG_RESIDENT_FORM=single_reduction | classic, read per solve.
+bool cg_resident_pipelined()
+{
+    const char *e = getenv("MSPMV_CG_RESIDENT_FORM");
+    if (e && std::strcmp(e, "single_reduction") == 0)
+        return true;
+    if (e && std::strcmp(e, "classic") == 0)
+        return false;
+    return kResPipelinedDefault;
+}
 
 bool cg_resident_enabled()
 {
@@ -527,7 +760,7 @@ static bool resident_build(mspmv_handle_s *h, ResidentCg *r)
     ResArgs probe{};
     probe.G = G;
     int occ = 0;
-    if (res_dispatch(rpt, nzr, probe, h->stream, true, &occ) != hipSuccess || occ < 1)
+    if (res_dispatch(rpt, nzr, probe, h->stream, true, &occ, false) != hipSuccess || occ < 1)
         return false;
     const size_t ell = (size_t)G * rpt * nzr * kRB;
     r->slot_bytes = sizeof(double) * (size_t)(1 + 2 * kResRing) * G;
@@ -546,9 +779,6 @@ static bool resident_build(mspmv_handle_s *h, ResidentCg *r)
     r->G = G;
     r->rpt = rpt;
     r->nzr = nzr;
-    char buf[64];
-    snprintf(buf, sizeof buf, "k_cg_resident<%d,%d> x %d", rpt, nzr, G);
-    r->name = buf;
     return true;
 }
 
@@ -603,7 +833,15 @@ hipError_t launch_cg_resident(mspmv_handle_s *h, ResidentCg *r, const double *d_
     a.G = r->G;
     a.stamps = d_stamps;
     a.stamp_iters = d_stamps ? stamp_iters : 0;
-    return res_dispatch(r->rpt, r->nzr, a, h->stream, false, nullptr);
+    // MSPMV_CG_RESIDENT_STALL=1 (test switch, read per solve): the first hand-off reports a stall, so
+    // tests/test_gpu_cg_resident.py can check the caller's fallback to the two-kernel CG
+    const char *fs = getenv("MSPMV_CG_RESIDENT_STALL");
+    a.force_stall = fs && atoi(fs) != 0 && !d_stamps;
+    const bool pipe = cg_resident_pipelined();
+    char buf[80];
+    snprintf(buf, sizeof buf, "k_cg_resident<%d,%d,%s> x %d", r->rpt, r->nzr, pipe ? "single_reduction" : "classic", r->G);
+    r->name = buf;
+    return res_dispatch(r->rpt, r->nzr, a, h->stream, false, nullptr, pipe);
 }
 
 }  // namespace mspmv

@@ -6,22 +6,16 @@
 
 namespace mspmv {
 
-__device__ __forceinline__ int xcd_tile(int b, int T, int K = 1)
+typedef double v2d_t __attribute__((ext_vector_type(2)));  // 16-B nontemporal loads / stores
+
+__device__ __forceinline__ int xcd_tile(int b, int T)
 {
     // Blocks are dealt round-robin over the 8 XCDs; give XCD k (= b % 8, a label only) the
-    // contiguous tile range [k*q + min(k,r), +q + (k<r)).  Bijective for any T.
-    // K > 1: that range is cut into K contiguous sub-ranges walked side by side (the XCD's i-th
-    // block takes sub-range i % K, position i / K), so the resident workgroups stream from K
-    // places per XCD instead of one window.  Bijective for any T, K >= 1.
+    // contiguous tile range [k*q + min(k,r), +q + (k<r)).  Bijective for any T (host check:
+    // tests/test_abi.py mirrors this map).
     const int q = T >> 3, r = T & 7;
     const int k = b & 7, i = b >> 3;
-    const int base = k * q + (k < r ? k : r);
-    if (K <= 1)
-        return base + i;
-    const int cnt = q + (k < r ? 1 : 0);
-    const int q2 = cnt / K, r2 = cnt - q2 * K;
-    const int s = i % K, pos = i / K;
-    return base + s * q2 + (s < r2 ? s : r2) + pos;
+    return k * q + (k < r ? k : r) + i;
 }
 
 __device__ __forceinline__ void store_sc1(double *p, double v)

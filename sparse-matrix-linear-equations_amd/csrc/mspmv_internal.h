@@ -35,14 +35,32 @@ constexpr int kSlabEntries = 1024;  // row runs per chunk
 constexpr int kSlabBlocksPerCu = 2; // resident blocks per CU (LDS: 76 KB per block)
 constexpr int kSlabMaxChunks = 255; // chunks per block (their descriptors sit in LDS)
 struct SlabData {
+    int L = 1;                          // 1: the SpMV's plan (k_spmv_slab); 8 / 16: an SpMM plan (k_spmm_slab)
+    int cfg = 0;                        // SpMM: the kernel configuration the plan was cut for (slab_mm_cfg)
     int num_chunks = 0, num_entries = 0;
     int4 *d_blk = nullptr;              // [blocks] {first row, rows ending in the block, chunk0, chunk1}
-    int4 *d_chunk = nullptr;            // [chunks + 1] {stream start, length | lanes_log2 << 16, slab, entry0}
+    int4 *d_chunk = nullptr;            // [chunks + 1] SpMV: {stream start, length | lanes_log2 << 16, slab, entry0};
+                                        // SpMM: {stream start, length | lanes_log2 << 13 | columns << 16,
+                                        // first column of the chunk's segment, entry0}
     uint2 *d_ent = nullptr;             // [entries] {offset in chunk | length << 16, row in block}
     double *d_val = nullptr;            // [nnz + pad] values, slab-major within each block
-    unsigned short *d_col = nullptr;    // [nnz + pad] column - slab * kSlabCols
-    double x_bytes_per_nnz = 0.0;       // x staged per nonzero (plan statistic, spmv_plan's choice)
+    unsigned short *d_col = nullptr;    // [nnz + pad] column - slab * kSlabCols (SpMM: - segment's first column)
+    double x_bytes_per_nnz = 0.0;       // x (SpMM: panel rows, all L columns) staged per nonzero (plan statistic)
 };
+
+// Column-slab SpMM (Y = A X, L = 8 or 16; mspmv_slab.hip): blocks of rows (merge-path balanced), each
+// block's nonzeros reordered by column segment (a greedy cut of the block's sorted columns into ranges
+// of <= cols panel rows, gaps between them skipped), the segment's panel rows staged in LDS once, and
+// the block's rows accumulated in LDS.  One configuration per launch shape.
+struct SlabMmCfg {
+    int L;        // right-hand sides
+    int threads;  // per block
+    int rows;     // rows ending in one block (+ a trailing partial row)
+    int cols;     // panel rows per segment (LDS: cols x L x 8 B)
+    int chunk;    // nonzeros per chunk
+    int entries;  // row runs per chunk
+};
+constexpr int kSlabMmMaxChunks = 127;  // chunks per block (their descriptors sit in LDS)
 
 // A merge-path tile plan for one nominal tile size (merge items per tile).
 //
@@ -191,6 +209,9 @@ struct mspmv_handle_s {
     // plain single-RHS SpMV on the column-slab plan (mspmv_slab.hip, plan key kSlabPlanKey): -1 not
     // decided yet, 0 no, 1 yes (spmv_plan; MSPMV_SPMV_SLAB)
     int spmv_slab = -1;
+    // plain SpMM of width L (index l_index(L)) on a column-slab plan (key slab_mm_key(L)): -1 not
+    // decided yet, 0 no, 1 yes (mspmv_api.hip spmm_slab_decide; MSPMV_SPMM_SLAB)
+    int spmm_slab[5] = {-1, -1, -1, -1, -1};
 };
 
 // IC(0) factor on the device (mspmv_ic0_create): L and its transpose for the two sync-free
@@ -216,11 +237,20 @@ namespace mspmv {
 // ---- column-slab SpMV (mspmv_slab.hip) ---------------------------------------------
 constexpr int kSlabPlanKey = -1;
 // Builds the column-slab plan into *p (blocks, split rows, reordered stream); MSPMV_ERR_UNSUPPORTED
-// when the matrix does not fit the form (rows per block); p is freed by the caller on any error.
-mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p);
+// when the matrix does not fit the form (rows per block) or its blocks would hold fewer than
+// min_nnz_per_block nonzeros on average; p is freed by the caller on any error.
+mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p, double min_nnz_per_block = 0.0);
 void free_slab(SlabData *s);
 hipError_t launch_slab(mspmv_handle_s *h, const TilePlan &plan, const double *d_x, double *d_y);
 std::string slab_kernel_name(const mspmv_handle_s *h);
+// Column-slab SpMM plans (L = 8, 16), keyed apart from every tile plan.
+inline int slab_mm_key(int L) { return -(1 << 20) - L; }
+const SlabMmCfg &slab_mm_cfg(int L, int which = -1);  // which < 0: the shipped configuration for L
+mspmv_status build_slab_mm_plan(mspmv_handle_s *h, int L, TilePlan &p);
+// ctrl (CG): the launch returns at once when ctrl->done is set; ld: panel stride (0: L)
+hipError_t launch_slab_mm(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L, int ld,
+                          const CgControl *ctrl);
+std::string slab_mm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan);
 mspmv_status plan_split_rows(TilePlan &p, const std::vector<int2> &hb, const std::vector<unsigned char> &hs);
 
 // ---- launchers (mspmv_kernels.hip) --------------------------------------------------
@@ -300,6 +330,7 @@ hipError_t launch_cg1_finish(mspmv_handle_s *h, double *d_x, int parity, int nbl
 // Register-resident single-RHS CG (one launch for the whole solve; MSPMV_CG_RESIDENT=0
 // turns it off): the layout is built on first use; r->ok false when the matrix does not fit.
 bool cg_resident_enabled();
+bool cg_resident_pipelined();  // the resident kernel's iteration form (MSPMV_CG_RESIDENT_FORM)
 mspmv_status resident_prepare(mspmv_handle_s *h, ResidentCg **out);
 void resident_free(ResidentCg *r);
 // d_stamps (diagnostic solves, mspmv_cg_resident_stamps): [stamp_iters][G][5] wall_clock64() phase

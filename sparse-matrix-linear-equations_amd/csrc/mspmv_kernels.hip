@@ -46,7 +46,6 @@ __device__ __forceinline__ T ld_stream(const T *p)
     return *p;
 }
 typedef int v4i_t __attribute__((ext_vector_type(4)));
-typedef double v2d_t __attribute__((ext_vector_type(2)));
 typedef int v2i_t __attribute__((ext_vector_type(2)));
 template <bool NT>
 __device__ __forceinline__ int4 ld_stream(const int4 *p)
@@ -3174,6 +3173,8 @@ std::string spmm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan, int 
 {
     if (L == 1)
         return spmv_kernel_name(h);
+    if (plan.slab)
+        return slab_mm_kernel_name(h, plan);
     const std::string nt = stream_nt(h) ? "true" : "false";
     if (plan.d_blk && plan.num_tiles_reg == plan.num_tiles && spmm_blk_enabled())
         return "k_spmm_blk<" + std::to_string(L) + ",0," + nt + "," + std::to_string(blk_kr(plan)) + ">";
@@ -3450,8 +3451,11 @@ hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const 
 {
     if (plan.num_tiles == 0)
         return hipSuccess;
-    if (plan.slab)  // the column-slab plan (single RHS, plain SpMV only: spmv_plan)
-        return L == 1 ? launch_slab(h, plan, d_X, d_Y) : hipErrorInvalidValue;
+    if (plan.slab) {  // a column-slab plan: the plain SpMV's (spmv_plan) or an L-wide SpMM's (get_plan)
+        if (plan.slab->L != L)
+            return hipErrorInvalidValue;
+        return L == 1 ? launch_slab(h, plan, d_X, d_Y) : launch_slab_mm(h, plan, d_X, d_Y, L, ld, nullptr);
+    }
     TileArgs a = make_args(h, plan, d_X, d_Y, L);
     if (ld > 0)
         a.ld = ld;
@@ -3793,10 +3797,18 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
         // the plain SpMM (its tile kernel holds fewer registers than the dot mode's, so more
         // workgroups per CU, and never spills), stopped by the control word, then p.Ap in one
         // streaming pass over p and Ap with the fold's breakdown checks (k_pcg_dot mode 2)
-        TileArgs ta = make_args(h, plan, h->d_p0, h->d_ap, L);
-        ta.ctrl = h->d_ctrl;
-        if ((e = launch_tile<kModeSpmv>(ta, L, h->stream, stream_nt(h))) != hipSuccess)
-            return e;
+        // (on the column-slab plan when the handle's plain L-wide product took one: spmm_slab_decide)
+        const auto sp = (L == 8 || L == 16) && h->spmm_slab[l_index(L)] == 1 ? h->plans.find(slab_mm_key(L))
+                                                                              : h->plans.end();
+        if (sp != h->plans.end()) {
+            if ((e = launch_slab_mm(h, sp->second, h->d_p0, h->d_ap, L, L, h->d_ctrl)) != hipSuccess)
+                return e;
+        } else {
+            TileArgs ta = make_args(h, plan, h->d_p0, h->d_ap, L);
+            ta.ctrl = h->d_ctrl;
+            if ((e = launch_tile<kModeSpmv>(ta, L, h->stream, stream_nt(h))) != hipSuccess)
+                return e;
+        }
         CgVecArgs vd = va;
         vd.r = h->d_p0;
         vd.p = h->d_ap;

@@ -21,6 +21,7 @@
 #include "mspmv_device.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -336,22 +337,21 @@ static void slab_block(const std::vector<int> &ro, const std::vector<int> &ci, c
     }
 }
 
-mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p)
+// Merge-path blocks of (rows + nonzeros) for a slab plan: at least g0 of them (one resident generation
+// of the slab kernel), more -- x 9/8 at a time, up to max_g -- while a block would end more than rows_cap
+// rows (its row sums sit in LDS).  Fills p.d_bounds / p.d_split, their host copies and the step.
+static mspmv_status slab_bounds(mspmv_handle_s *h, long long g0, long long max_g, int rows_cap, TilePlan &p,
+                                std::vector<int2> &hb, std::vector<unsigned char> &hs, long long &step)
 {
-    if (h->m <= 0 || h->nnz <= 0)
-        return MSPMV_ERR_UNSUPPORTED;
     const long long total = (long long)h->m + h->nnz;
-    std::vector<int2> hb;
-    std::vector<unsigned char> hs;
-    int T = 0;
-    long long step = 0;
-    for (int G = kSlabBlocksPerCu * h->num_cus;; G *= 2) {  // one resident generation; more when rows are short
-        if (G > 64 * h->num_cus)
+    long long G = std::max(g0, ((long long)h->m + rows_cap - 1) / rows_cap);
+    for (;; G = G + std::max(1LL, G / 8)) {
+        if (G > max_g)
             return MSPMV_ERR_UNSUPPORTED;
         step = (total + G - 1) / G;
         if (step > (1LL << 30))
             return MSPMV_ERR_UNSUPPORTED;
-        T = (int)((total + step - 1) / step);
+        const int T = (int)((total + step - 1) / step);
         if (p.d_bounds)
             (void)hipFree(p.d_bounds);
         if (p.d_split)
@@ -393,17 +393,19 @@ mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p)
             set_error("column-slab plan: non-monotone boundaries");
             return MSPMV_ERR_INVALID;
         }
-        if (rows_max <= kSlabRows)
-            break;
+        p.num_tiles = T;
+        if (rows_max <= rows_cap)
+            return MSPMV_OK;
     }
-    p.lanes = kSlabThreads;
-    p.tile_items = (int)step;
-    p.snap = (int)(step / kSnapDiv);
-    p.num_tiles = T;
+}
 
-    // the matrix on the host, reordered block by block
-    std::vector<int> ro((size_t)h->m + 1), ci((size_t)h->nnz);
-    std::vector<double> va((size_t)h->nnz);
+// The matrix back on the host (the plan builders reorder it block by block).
+static mspmv_status slab_host_matrix(mspmv_handle_s *h, std::vector<int> &ro, std::vector<int> &ci,
+                                     std::vector<double> &va)
+{
+    ro.resize((size_t)h->m + 1);
+    ci.resize((size_t)h->nnz);
+    va.resize((size_t)h->nnz);
     hipError_t e = hipMemcpy(ro.data(), h->d_row_offsets, sizeof(int) * ro.size(), hipMemcpyDeviceToHost);
     if (e == hipSuccess)
         e = hipMemcpy(ci.data(), h->d_cols, sizeof(int) * ci.size(), hipMemcpyDeviceToHost);
@@ -413,6 +415,33 @@ mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p)
         set_error(std::string("column-slab plan: ") + hipGetErrorString(e));
         return MSPMV_ERR_HIP;
     }
+    return MSPMV_OK;
+}
+
+mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p, double min_nnz_per_block)
+{
+    if (h->m <= 0 || h->nnz <= 0)
+        return MSPMV_ERR_UNSUPPORTED;
+    std::vector<int2> hb;
+    std::vector<unsigned char> hs;
+    long long step = 0;
+    mspmv_status st0 = slab_bounds(h, (long long)kSlabBlocksPerCu * h->num_cus, 64LL * h->num_cus, kSlabRows, p, hb,
+                                   hs, step);
+    if (st0 != MSPMV_OK)
+        return st0;
+    const int T = p.num_tiles;
+    if ((double)h->nnz < min_nnz_per_block * T)  // before the matrix is copied or anything allocated
+        return MSPMV_ERR_UNSUPPORTED;
+    p.lanes = kSlabThreads;
+    p.tile_items = (int)step;
+    p.snap = (int)(step / kSnapDiv);
+    p.num_tiles = T;
+
+    // the matrix on the host, reordered block by block
+    std::vector<int> ro, ci;
+    std::vector<double> va;
+    if ((st0 = slab_host_matrix(h, ro, ci, va)) != MSPMV_OK)
+        return st0;
     std::vector<double> oval((size_t)h->nnz);
     std::vector<unsigned short> ocol((size_t)h->nnz);
     std::vector<SlabBlockOut> outs((size_t)T);
@@ -459,6 +488,529 @@ mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p)
     }
     if (hipMemset(p.d_modes[0], 255, (size_t)T) != hipSuccess) {
         set_error("column-slab plan: memset failed");
+        return MSPMV_ERR_HIP;
+    }
+    return plan_split_rows(p, hb, hs);
+}
+
+
+// ---- column-slab SpMM (Y = A X, L = 8 or 16) ------------------------------------------------------
+// The L-wide tile kernels gather one L x 8-B panel row per nonzero from L2 (k_spmm_tile): on matrices
+// that are not node-blocked that is 64-128 B of L2 -> CU traffic per 12 B of matrix, and a CU takes in
+// ~70 GB/s of such gathers, so the gathers, not HBM, set the time (configs[2] cant-shaped L = 16: 513 MB
+// of panel lines for 64 MB of HBM bytes; configs[4]'s 27-point L = 8 SpMM: 6 GB per product).  Here a
+// block of rows stages each panel row it touches into LDS once, with coalesced loads, and the runs of
+// one row read it there: the reference's OmpMergeCsrmm (work_2025/spmm/merge_based.hpp:46-153) computes
+// the same y_i = sum_k a_ik X[c_k][:], its merge-path row/nonzero balance (the partition, :62-75)
+// re-derived at block granularity.
+//
+// Plan (build_slab_mm_plan): merge-path blocks of <= cfg.rows rows; a block's distinct columns, sorted,
+// are cut greedily into segments of <= cfg.cols consecutive column ids (a segment starts at its first
+// touched column, so the gaps between a stencil's planes or a band's ends cost nothing); the block's
+// nonzeros are reordered by segment, CSR order within it (rows ascending), and cut into chunks of
+// <= cfg.chunk nonzeros and <= cfg.entries runs of one row.  Per chunk: its stream and runs go to LDS
+// (loaded two chunks earlier), its segment's panel rows too when the segment changes (loaded during the
+// previous chunk); groups of L/2 column-pair lanes x 2^lg nonzero lanes take the runs round-robin, lane
+// (c, j) sums products j, j + 2^lg, ... of its run for columns 2c, 2c + 1 in order, a fixed xor
+// butterfly folds the group and lane (c, 0) adds the run to the row's sums in LDS.  A row has one run
+// per chunk and chunks run in order, so every sum is fixed-order (reproducible) and within the 2 (len+1)
+// eps (|A||X|)_i reordering bound of the CSR-order sum (mspmv_tile_modes reports the blocks as 255).
+// Rows split between blocks are closed as the tile kernels close them (close_split_rows).
+struct SlabMmArgs {
+    const int4 *blk;
+    const int4 *chunk;
+    const uint2 *ent;
+    const double *val;
+    const unsigned short *col;
+    const double *x;  // panel X, row stride ld
+    double *y;        // panel Y, row stride ld
+    int ld;
+    int num_tiles;
+    const CgControl *ctrl;
+    // split rows (close_split_rows reads these names)
+    const int2 *bounds;
+    const unsigned char *split;
+    const int4 *fix;
+    unsigned *fix_cnt;
+    double *carry_val;
+    double *head_val;
+    double *head_pub;
+};
+
+// Configurations (one kernel instance each): LDS = 2 x cols x L x 8 (two segment buffers) + (rows + 1) x
+// L x 8 (row sums) + 10 x chunk (stream) + 8 x entries + the chunk table.
+constexpr SlabMmCfg kSlabMmCfgs[] = {
+    {8, 512, 384, 256, 1024, 256},     // 0: L = 8, 71 KB, two blocks per CU
+    {8, 1024, 768, 512, 2048, 512},    // 1: L = 8, 139 KB, one block per CU
+    {16, 1024, 256, 320, 2048, 512},   // 2: L = 16, 139 KB, one block per CU
+    {16, 512, 192, 128, 1024, 256},    // 3: L = 16, 71 KB, two blocks per CU
+};
+constexpr int kSlabMmNumCfgs = (int)(sizeof(kSlabMmCfgs) / sizeof(kSlabMmCfgs[0]));
+constexpr int kSlabMmSets = 4;  // stream chunks in flight per block (register sets)
+
+static int slab_mm_lab_cfg()  // lab: MSPMV_SPMM_SLAB_CFG picks a configuration by index (A/B runs)
+{
+    static const int v = [] {
+        const char *e = getenv("MSPMV_SPMM_SLAB_CFG");
+        return e && *e ? atoi(e) : -1;
+    }();
+    return v;
+}
+
+const SlabMmCfg &slab_mm_cfg(int L, int which)
+{
+    if (which < 0)
+        which = slab_mm_lab_cfg();
+    if (which >= 0 && which < kSlabMmNumCfgs && kSlabMmCfgs[which].L == L)
+        return kSlabMmCfgs[which];
+    return L == 8 ? kSlabMmCfgs[0] : kSlabMmCfgs[2];
+}
+
+static int slab_mm_cfg_index(const SlabMmCfg &c) { return (int)(&c - kSlabMmCfgs); }
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// One 16-B-per-lane LDS-DMA load (global_load_lds_dwordx4): lane l's 16 bytes from its own gsrc land at
+// LDS byte address lds_base + 16 l.  Inline asm, so the compiler neither tracks it (with the builtin it
+// treats the DMA as a pending LDS write and waits vmcnt(0) before the kernel's LDS reads, in both wave
+// roles) nor keeps M0 (saved and restored here; the callers retire the DMA with their own vmcnt wait).
+__device__ __forceinline__ void glds16(const void *gsrc, unsigned lds_base)
+{
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(gsrc), "s"(lds_base)
+                 : "memory");
+}
+
+// Two wave roles per block, so that each load kind waits on its own counter (vmcnt is per wave and
+// in order: a block whose waves issued both kinds had to drain every older stream load to use a fresh
+// panel load, which capped the stream at ~2 chunks in flight and ~2 TB/s, r05c-r05e):
+//  * stream waves (the first half) hold the chunk stream kSlabMmSets chunks ahead in registers and
+//    write each chunk's values, columns and runs into LDS; compiler-counted waits, __syncthreads;
+//  * panel waves (the second half) stage each segment's panel rows by LDS-DMA (global_load_lds_dwordx4,
+//    no registers) into one of two LDS buffers, one segment ahead: a segment's DMA is retired by the
+//    panel waves' own vmcnt(0) before the barrier that opens the segment to readers, and the next one
+//    is issued into the buffer whose readers passed the previous barrier; raw s_barrier with
+//    lgkmcnt(0) only (a __syncthreads would drain the DMA in flight).
+// Every wave then sums runs.  Both roles run the same chunk loop, so they meet at every barrier.
+template <int CFG, bool NT>
+__global__ __launch_bounds__(kSlabMmCfgs[CFG].threads) void k_spmm_slab(SlabMmArgs a)
+{
+    constexpr SlabMmCfg C = kSlabMmCfgs[CFG];
+    constexpr int L = C.L, TB = C.threads, GL = L / 2;
+    constexpr int LGL = GL == 4 ? 2 : 3;                  // log2 GL
+    constexpr int TS = TB / 2;                            // stream threads
+    constexpr int XW = (TB - TS) / 64;                    // panel waves
+    constexpr int IPT = (C.chunk + TS - 1) / TS;          // stream items per stream thread and chunk
+    constexpr int EPT = (C.entries + TS - 1) / TS;        // entries per stream thread and chunk
+    constexpr int NS = kSlabMmSets;
+    static_assert(GL == 4 || GL == 8, "L = 8 or 16");
+    static_assert((C.cols * GL) % 64 == 0, "whole 1-KB DMA pieces per segment buffer");
+    __shared__ double2 xs[2][C.cols * GL];
+    __shared__ double2 yacc[(C.rows + 1) * GL];
+    __shared__ double s_val[C.chunk];
+    __shared__ unsigned short s_col[C.chunk];
+    __shared__ uint2 sent[C.entries];
+    __shared__ int4 schunk[kSlabMmMaxChunks + 1];
+    const int tid = threadIdx.x;
+    // CG: the stop flag is loaded first and tested once the block's table is in
+    const int stopped = a.ctrl ? a.ctrl->done : 0;
+    const int b = xcd_tile(blockIdx.x, a.num_tiles);
+    const int4 bd = a.blk[b];  // {first row, rows ending here, chunk0, chunk1}
+    for (int i = tid; i <= bd.w - bd.z; i += TB)
+        schunk[i] = a.chunk[bd.z + i];
+    const int4 fx = load_fix(a, b);
+    const int nrows = bd.y;
+    const bool tail = a.split[b + 1] != 0;
+    for (int i = tid; i < (nrows + (tail ? 1 : 0)) * GL; i += TB)
+        yacc[i] = make_double2(0.0, 0.0);
+    __syncthreads();
+    if (stopped)  // block-uniform (every block of the launch reads the same word)
+        return;
+    auto chunk = [&](int ci) __attribute__((always_inline)) {  // block-uniform
+        const int4 c = schunk[ci - bd.z];
+        return make_int4(__builtin_amdgcn_readfirstlane(c.x), __builtin_amdgcn_readfirstlane(c.y),
+                         __builtin_amdgcn_readfirstlane(c.z), __builtin_amdgcn_readfirstlane(c.w));
+    };
+    const int last = bd.w - 1;
+    // The runs of chunk ci over the segment in xb: groups of GL column-pair lanes x 2^lg nonzero lanes
+    // take the runs round-robin, lane (c, j) sums products j, j + 2^lg, ... in order, a fixed xor
+    // butterfly folds the group, lane (c, 0) adds the run to its row in yacc.
+    auto runs = [&](int ci, const double2 *xb) __attribute__((always_inline)) {
+        const int4 cd = chunk(ci);
+        const int lg = (cd.y >> 13) & 7;
+        const int ne = chunk(ci + 1).w - cd.w;
+        const int lgg = LGL + lg, Gp = 1 << lg;
+        const int c = tid & (GL - 1), j = (tid >> LGL) & (Gp - 1);
+        for (int q = tid >> lgg; q < ne; q += TB >> lgg) {  // uniform within a group
+            const uint2 en = sent[q];
+            const int off = (int)(en.x & 0xffffu), e = off + (int)(en.x >> 16);
+            double2 acc = make_double2(0.0, 0.0);
+            int k = off + j;
+            for (; k + 3 * Gp < e; k += 4 * Gp) {  // 4 panel reads in flight per lane, summed in order
+                double v[4];
+                double2 xv[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    v[u] = s_val[k + u * Gp];
+                    xv[u] = xb[(int)s_col[k + u * Gp] * GL + c];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    acc.x += v[u] * xv[u].x;
+                    acc.y += v[u] * xv[u].y;
+                }
+            }
+            if (k < e) {  // the rest (< 4 per lane) as one batch: clamped reads, skipped products
+                double v[3];
+                double2 xv[3];
+#pragma unroll
+                for (int u = 0; u < 3; ++u) {
+                    const int kk = min(k + u * Gp, e - 1);
+                    v[u] = s_val[kk];
+                    xv[u] = xb[(int)s_col[kk] * GL + c];
+                }
+#pragma unroll
+                for (int u = 0; u < 3; ++u) {
+                    const bool on = k + u * Gp < e;      // acc starts at +0.0 and never becomes -0.0:
+                    acc.x += on ? v[u] * xv[u].x : 0.0;  // adding +0.0 is the identity
+                    acc.y += on ? v[u] * xv[u].y : 0.0;
+                }
+            }
+            for (int o = Gp >> 1; o > 0; o >>= 1) {
+                acc.x += __shfl_xor(acc.x, o * GL);
+                acc.y += __shfl_xor(acc.y, o * GL);
+            }
+            if (j == 0) {
+                double2 &yr = yacc[(int)en.y * GL + c];
+                yr.x += acc.x;
+                yr.y += acc.y;
+            }
+        }
+    };
+    if (bd.z < bd.w && tid < TS) {  // ---- stream waves (wave-uniform branch)
+        struct Regs {
+            double v[IPT];
+            unsigned short c[IPT];
+            uint2 e[EPT];
+        };
+        auto fetch = [&](int ci, Regs &r) __attribute__((always_inline)) {
+            ci = min(ci, last);  // past the block's end: a repeat of its last chunk, never used (every
+                                 // chunk issues the same loads, so the compiler's waits stay counted)
+            const int4 cd = chunk(ci);
+            const int len = cd.y & 0x1fff;
+            const int e0 = cd.w, ne = chunk(ci + 1).w - e0;
+#pragma unroll
+            for (int j = 0; j < IPT; ++j) {
+                const int k = min(tid + j * TS, len - 1);  // clamped: every load is issued
+                r.v[j] = slab_stream<NT>(a.val + cd.x + k);
+                r.c[j] = slab_stream<NT>(a.col + cd.x + k);
+            }
+#pragma unroll
+            for (int j = 0; j < EPT; ++j)
+                r.e[j] = a.ent[e0 + min(tid + j * TS, ne - 1)];
+        };
+        Regs rs[NS];
+#pragma unroll
+        for (int u = 0; u < NS; ++u)
+            fetch(bd.z + u, rs[u]);
+        int cur = -1, seg = -1;
+        for (int ci = bd.z; ci < bd.w; ci += NS) {
+#pragma unroll
+            for (int u = 0; u < NS; ++u) {
+                const int c = ci + u;
+                const bool valid = c <= last;
+                const int4 cd = chunk(min(c, last));
+                if (valid) {
+                    if (cd.z != cur) {
+                        cur = cd.z;
+                        ++seg;
+                    }
+                    const int len = cd.y & 0x1fff, ne = chunk(c + 1).w - cd.w;
+#pragma unroll
+                    for (int j = 0; j < IPT; ++j) {
+                        const int k = tid + j * TS;
+                        if (k < len) {
+                            s_val[k] = rs[u].v[j];
+                            s_col[k] = rs[u].c[j];
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < EPT; ++j) {
+                        const int k = tid + j * TS;
+                        if (k < ne)
+                            sent[k] = rs[u].e[j];
+                    }
+                }
+                fetch(c + NS, rs[u]);
+                __syncthreads();
+                if (valid)
+                    runs(c, xs[seg & 1]);
+                __syncthreads();
+            }
+        }
+    } else if (bd.z < bd.w) {  // ---- panel waves
+        const int xw = (tid - TS) >> 6, lane = tid & 63;
+        auto stage = [&](int c0, int ncols, int buf) __attribute__((always_inline)) {
+            const int n2 = ncols * GL;  // double2s of the segment
+            for (int p = xw; p * 64 < n2; p += XW) {  // wave-uniform; the DMA writes lane-linear 1-KB pieces
+                const int e = min(p * 64 + lane, n2 - 1);
+                const unsigned dst = (unsigned)(uintptr_t)(lds_void_t *)&xs[buf][p * 64];
+                glds16(a.x + (size_t)(c0 + (e >> LGL)) * a.ld + 2 * (e & (GL - 1)), __builtin_amdgcn_readfirstlane(dst));
+            }
+        };
+        stage(chunk(bd.z).z, chunk(bd.z).y >> 16, 0);
+        int cur = -1, seg = -1;
+        for (int ci = bd.z; ci < bd.w; ci += NS) {
+#pragma unroll
+            for (int u = 0; u < NS; ++u) {
+                const int c = ci + u;
+                const bool valid = c <= last;
+                const int4 cd = chunk(min(c, last));
+                if (valid && cd.z != cur) {  // chunk c opens the next segment
+                    cur = cd.z;
+                    ++seg;
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // its DMA has landed
+                    int n = c + 1;  // the following segment, into the other buffer (its readers are done)
+                    while (n <= last && chunk(n).z == cur)
+                        ++n;
+                    if (n <= last)
+                        stage(chunk(n).z, chunk(n).y >> 16, (seg + 1) & 1);
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+                if (valid)
+                    runs(c, xs[seg & 1]);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_s_barrier();
+            }
+        }
+    }
+    // rows ending in the block (row 0 to the head slot when it completes a split row), nontemporal so
+    // Y does not displace the panel X from the caches; the trailing partial row -> its carry
+    const int r0 = bd.x;
+    for (int e = tid; e < nrows * GL; e += TB) {
+        const int row = e >> LGL, cp = e & (GL - 1);
+        const double2 v = yacc[e];
+        double *dst = row == 0 && fx.z > 0 ? a.head_val + (size_t)b * L + 2 * cp : a.y + (size_t)(r0 + row) * a.ld + 2 * cp;
+        __builtin_nontemporal_store(v2d_t{v.x, v.y}, reinterpret_cast<v2d_t *>(dst));
+    }
+    if (tail)
+        for (int cp = tid; cp < GL; cp += TB)
+            store_sc1_2(a.carry_val + (size_t)b * L + 2 * cp, yacc[nrows * GL + cp]);
+    close_split_rows<TB>(a, b, fx, L, a.ld);
+}
+
+template <int CFG>
+static void launch_slab_mm_cfg(const SlabMmArgs &a, bool nt, hipStream_t s)
+{
+    const dim3 grid(a.num_tiles), block(kSlabMmCfgs[CFG].threads);
+    if (nt)
+        hipLaunchKernelGGL((k_spmm_slab<CFG, true>), grid, block, 0, s, a);
+    else
+        hipLaunchKernelGGL((k_spmm_slab<CFG, false>), grid, block, 0, s, a);
+}
+
+hipError_t launch_slab_mm(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L, int ld,
+                          const CgControl *ctrl)
+{
+    const SlabData &s = *plan.slab;
+    if (s.L != L || L != kSlabMmCfgs[s.cfg].L)
+        return hipErrorInvalidValue;
+    SlabMmArgs a{};
+    a.blk = s.d_blk;
+    a.chunk = s.d_chunk;
+    a.ent = s.d_ent;
+    a.val = s.d_val;
+    a.col = s.d_col;
+    a.x = d_X;
+    a.y = d_Y;
+    a.ld = ld > 0 ? ld : L;
+    a.num_tiles = plan.num_tiles;
+    a.ctrl = ctrl;
+    a.bounds = plan.d_bounds;
+    a.split = plan.d_split;
+    a.fix = plan.num_carries ? plan.d_fix : nullptr;
+    a.fix_cnt = plan.d_fix_cnt;
+    a.carry_val = plan.d_carry_val;
+    a.head_val = plan.d_carry_val + (size_t)std::max(plan.num_tiles, 1) * plan.carry_L;
+    a.head_pub = a.head_val + (size_t)std::max(plan.num_tiles, 1) * plan.carry_L;
+    if (plan.num_tiles == 0)
+        return hipSuccess;
+    const bool nt = stream_nt(h);
+    switch (s.cfg) {
+    case 0: launch_slab_mm_cfg<0>(a, nt, h->stream); break;
+    case 1: launch_slab_mm_cfg<1>(a, nt, h->stream); break;
+    case 2: launch_slab_mm_cfg<2>(a, nt, h->stream); break;
+    case 3: launch_slab_mm_cfg<3>(a, nt, h->stream); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+std::string slab_mm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan)
+{
+    return "k_spmm_slab<" + std::to_string(plan.slab ? plan.slab->cfg : 0) + "," + (stream_nt(h) ? "true" : "false") +
+           ">";
+}
+
+// Per block: its nonzeros [n0, n1) reordered by column segment (CSR order within it), cut into chunks
+// of one segment, <= cfg.chunk nonzeros and <= cfg.entries runs of one row.  chunk.x is relative to n0.
+struct SlabMmBlockOut {
+    std::vector<int4> chunks;  // entry0 relative to the block
+    std::vector<uint2> ents;
+    long long staged_cols = 0;
+    bool ok = true;
+};
+
+static void slab_mm_block(const SlabMmCfg &cfg, const std::vector<int> &ro, const std::vector<int> &ci,
+                          const std::vector<double> &va, int r0, int n0, int r1, int n1, double *oval,
+                          unsigned short *ocol, SlabMmBlockOut &out)
+{
+    const int cnt = n1 - n0;
+    if (cnt <= 0)
+        return;
+    std::vector<int> u(ci.begin() + n0, ci.begin() + n1);  // distinct columns, ascending
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    std::vector<int> seg_lo, seg_n;  // greedy segments: [lo, lo + n), n <= cfg.cols
+    for (size_t i = 0; i < u.size();) {
+        const int lo = u[i];
+        size_t k = i;
+        while (k < u.size() && u[k] < lo + cfg.cols)
+            ++k;
+        seg_lo.push_back(lo);
+        seg_n.push_back(u[k - 1] - lo + 1);
+        out.staged_cols += u[k - 1] - lo + 1;
+        i = k;
+    }
+    const int ns = (int)seg_lo.size();
+    auto seg_of = [&](int c) { return (int)(std::upper_bound(seg_lo.begin(), seg_lo.end(), c) - seg_lo.begin()) - 1; };
+    std::vector<int> off((size_t)ns + 1, 0);
+    for (int k = n0; k < n1; ++k)
+        ++off[(size_t)seg_of(ci[(size_t)k]) + 1];
+    for (int s = 0; s < ns; ++s)
+        off[(size_t)s + 1] += off[(size_t)s];
+    std::vector<int> row((size_t)cnt);
+    std::vector<int> put(off.begin(), off.end() - 1);
+    const int rlast = n1 > ro[(size_t)r1] ? r1 : r1 - 1;  // the trailing partial row, when there is one
+    for (int r = r0; r <= rlast; ++r) {
+        const int k0 = std::max(ro[(size_t)r], n0), k1 = std::min(ro[(size_t)r + 1], n1);
+        for (int k = k0; k < k1; ++k) {
+            const int s = seg_of(ci[(size_t)k]);
+            const int q = put[(size_t)s]++;
+            oval[(size_t)n0 + q] = va[(size_t)k];
+            ocol[(size_t)n0 + q] = (unsigned short)(ci[(size_t)k] - seg_lo[(size_t)s]);
+            row[(size_t)q] = r - r0;
+        }
+    }
+    constexpr int kGL[2] = {4, 8};
+    const int GL = kGL[cfg.L == 16 ? 1 : 0];
+    int lg_max = 0;
+    while ((GL << (lg_max + 1)) <= 64)  // a run's lanes stay inside one wave (xor butterfly)
+        ++lg_max;
+    for (int s = 0; s < ns; ++s) {
+        int q = off[(size_t)s];
+        const int qe = off[(size_t)s + 1];
+        while (q < qe) {  // chunks of this segment
+            const int start = q, e0 = (int)out.ents.size();
+            int ne = 0;
+            while (q < qe && q - start < cfg.chunk && ne < cfg.entries) {
+                int k = q;
+                while (k < qe && k - start < cfg.chunk && row[(size_t)k] == row[(size_t)q])
+                    ++k;
+                out.ents.push_back(make_uint2((unsigned)(q - start) | ((unsigned)(k - q) << 16), (unsigned)row[(size_t)q]));
+                ++ne;
+                q = k;
+            }
+            const int len = q - start;
+            // nonzero lanes per run: the fewest latency steps -- rounds of runs over the block's groups
+            // x (the run's products per lane + its butterfly + ~8 steps of LDS round trips)
+            const int mean = (len + ne - 1) / ne;
+            int lg = 0, best = 1 << 30;
+            for (int l = 0; l <= lg_max; ++l) {
+                const int groups = cfg.threads / (GL << l);
+                const int rounds = (ne + groups - 1) / groups;
+                const int cost = rounds * ((mean + (1 << l) - 1) / (1 << l) + 2 * l + 8);
+                if (cost < best) {
+                    best = cost;
+                    lg = l;
+                }
+            }
+            out.chunks.push_back(make_int4(start, len | (lg << 13) | (seg_n[(size_t)s] << 16), seg_lo[(size_t)s], e0));
+        }
+    }
+    out.ok = (int)out.chunks.size() <= kSlabMmMaxChunks;
+}
+
+mspmv_status build_slab_mm_plan(mspmv_handle_s *h, int L, TilePlan &p)
+{
+    const SlabMmCfg &cfg = slab_mm_cfg(L);
+    if (h->m <= 0 || h->nnz <= 0 || (L != 8 && L != 16) || cfg.chunk > 0x1fff || cfg.cols > 0xffff)
+        return MSPMV_ERR_UNSUPPORTED;
+    const int per_cu = 163840 / (2 * cfg.cols * L * 8 + (cfg.rows + 1) * L * 8 + 10 * cfg.chunk + 8 * cfg.entries + 2048);
+    std::vector<int2> hb;
+    std::vector<unsigned char> hs;
+    long long step = 0;
+    mspmv_status st = slab_bounds(h, (long long)std::max(per_cu, 1) * h->num_cus,
+                                  (long long)h->m + h->nnz, cfg.rows, p, hb, hs, step);
+    if (st != MSPMV_OK)
+        return st;
+    const int T = p.num_tiles;
+    p.lanes = cfg.threads;
+    p.tile_items = (int)step;
+    p.snap = (int)(step / kSnapDiv);
+    std::vector<int> ro, ci;
+    std::vector<double> va;
+    if ((st = slab_host_matrix(h, ro, ci, va)) != MSPMV_OK)
+        return st;
+    std::vector<double> oval((size_t)h->nnz);
+    std::vector<unsigned short> ocol((size_t)h->nnz);
+    std::vector<SlabMmBlockOut> outs((size_t)T);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int t = 0; t < T; ++t) {
+        const int2 b0 = hb[(size_t)t], b1 = hb[(size_t)t + 1];
+        slab_mm_block(cfg, ro, ci, va, b0.x, b0.y, b1.x, b1.y, oval.data(), ocol.data(), outs[(size_t)t]);
+    }
+    std::vector<int4> blk((size_t)T), chunks;
+    std::vector<uint2> ents;
+    long long staged = 0;
+    for (int t = 0; t < T; ++t) {
+        const SlabMmBlockOut &o = outs[(size_t)t];
+        if (!o.ok)  // more segments x chunks than one block's LDS table holds
+            return MSPMV_ERR_UNSUPPORTED;
+        const int c0 = (int)chunks.size(), ebase = (int)ents.size();
+        for (int4 c : o.chunks) {
+            c.x += hb[(size_t)t].y;
+            c.w += ebase;
+            chunks.push_back(c);
+        }
+        ents.insert(ents.end(), o.ents.begin(), o.ents.end());
+        blk[(size_t)t] = make_int4(hb[(size_t)t].x, hb[(size_t)t + 1].x - hb[(size_t)t].x, c0, (int)chunks.size());
+        staged += o.staged_cols;
+    }
+    chunks.push_back(make_int4(0, 0, 0, (int)ents.size()));  // sentinel: the last chunk's entry end
+    SlabData *s = new SlabData();
+    s->L = L;
+    s->cfg = slab_mm_cfg_index(cfg);
+    s->num_chunks = (int)chunks.size() - 1;
+    s->num_entries = (int)ents.size();
+    s->x_bytes_per_nnz = (double)staged * 8.0 * L / (double)h->nnz;
+    p.slab = s;
+    if ((st = slab_upload(&s->d_blk, blk)) != MSPMV_OK || (st = slab_upload(&s->d_chunk, chunks)) != MSPMV_OK ||
+        (st = slab_upload(&s->d_ent, ents)) != MSPMV_OK || (st = slab_upload(&s->d_val, oval, kNnzPad)) != MSPMV_OK ||
+        (st = slab_upload(&s->d_col, ocol, kNnzPad)) != MSPMV_OK)
+        return st;
+    // split rows, their carries and heads (three [T][16] slots, as the tile plans), block modes 255
+    p.carry_L = 16;
+    if (hipMalloc((void **)&p.d_carry_val, sizeof(double) * (size_t)T * 16 * 3) != hipSuccess ||
+        hipMalloc((void **)&p.d_modes[l_index(L)], (size_t)T) != hipSuccess) {
+        set_error("column-slab SpMM plan: hipMalloc failed");
+        return MSPMV_ERR_HIP;
+    }
+    if (hipMemset(p.d_modes[l_index(L)], 255, (size_t)T) != hipSuccess) {
+        set_error("column-slab SpMM plan: memset failed");
         return MSPMV_ERR_HIP;
     }
     return plan_split_rows(p, hb, hs);

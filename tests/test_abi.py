@@ -78,3 +78,17 @@ def test_synth_powerlaw_exact(mspmv):
     for i in np.flatnonzero(lens)[:50]:
         c = a.column_indices[a.row_offsets[i]:a.row_offsets[i + 1]]
         assert np.all(np.diff(c) > 0) and c.max() < 4000
+
+
+def xcd_tile(b, T):
+    """Host mirror of mspmv_device.h xcd_tile: block b -> tile (XCD k = b % 8 walks a contiguous range)."""
+    q, r = T >> 3, T & 7
+    k, i = b & 7, b >> 3
+    return k * q + (k if k < r else r) + i
+
+
+@pytest.mark.parametrize("T", [1, 2, 7, 8, 9, 15, 16, 17, 255, 256, 257, 1023, 9221, 12123])
+def test_xcd_tile_bijective(T):
+    """Every tile kernel maps blockIdx through xcd_tile: it must be a permutation of 0..T-1."""
+    got = sorted(xcd_tile(b, T) for b in range(T))
+    assert got == list(range(T))
