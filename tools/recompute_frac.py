@@ -71,10 +71,12 @@ def cg_loop_times(trace, iterations):
         calls[k] = calls.get(k, 0) + 1
     loop = {k for k, c in calls.items() if c >= iterations}
     if not loop:  # the register-resident CG: the whole solve is ONE cooperative launch (the last one is timed)
+        # launches: the warm solve, the timed one, then (bench's resident_phases) a stamped one
         res = [r for r in recs if short_name(r["Kernel_Name"]).startswith("k_cg_resident")]
         if res:
-            dur = (int(res[-1]["End_Timestamp"]) - int(res[-1]["Start_Timestamp"])) / 1000.0
-            return dur / iterations, dur / iterations, [short_name(res[-1]["Kernel_Name"])]
+            r = res[1] if len(res) >= 2 else res[-1]
+            dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1000.0
+            return dur / iterations, dur / iterations, [short_name(r["Kernel_Name"])]
     lrecs = [r for r in recs if short_name(r["Kernel_Name"]) in loop]
     busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in lrecs) / 1000.0
     half = lrecs[len(lrecs) // 2:]
@@ -115,6 +117,7 @@ def main(src, dst):
         if not os.path.isdir(ld):
             continue
         lj = last_json(os.path.join(ld, "leg.json"))
+        lj0 = lj  # the leg's own (profiled) run, before the unprofiled bench numbers are merged in
         json.dump(lj, open(out(f"{leg}.json"), "w"), indent=1)
         # the bench column: the unprofiled bench run's numbers where it holds the leg (the leg's own
         # run is under rocprofv3, whose per-dispatch bookkeeping widens back-to-back launch gaps);
@@ -161,10 +164,23 @@ def main(src, dst):
             it = lj["iterations"]
             busy, span, loop = cg_loop_times(tr, it)
             nb = cg_iter_bytes(m, nnz, L)
-            lines.append(f"| {leg} | roofline_frac {lj['roofline_frac']} ({lj.get('us_per_iter') or lj.get('ms_per_iter')} "
+            fk = "roofline_frac" if "roofline_frac" in lj else "speed_equiv_frac"
+            lines.append(f"| {leg} | {fk} {lj[fk]} ({lj.get('us_per_iter') or lj.get('ms_per_iter')} "
                          f"{'us' if 'us_per_iter' in lj else 'ms'}/iter, wall) | span frac {frac(nb, span):.4f} "
                          f"({span:.2f} us/iter); kernel-busy frac {frac(nb, busy):.4f} ({busy:.2f} us/iter) | "
                          f"{', '.join(loop)} |")
+            if leg == "cg_multi" and bench and isinstance(bench.get("spmv_nlpkkt120_size"), dict):
+                # SURVEY 8(d)'s named 70 % case: the nlpkkt120-size single-RHS SpMV timed in the same leg
+                # (back-to-back launches) against its rows in this trace
+                sl = bench["spmv_nlpkkt120_size"]
+                sp = [r for r in rows if r["kernel"].startswith("k_spmv") and r["calls"] >= 40]
+                if sp:
+                    r = max(sp, key=lambda q: q["grid"])
+                    own = lj0.get("spmv_nlpkkt120_size") if isinstance(lj0, dict) else None
+                    own_s = f"; this profiled run's own events: kernel_ms {own['kernel_ms']}" if own else ""
+                    lines.append(f"| spmv_nlpkkt120_size | frac {sl['frac']} (kernel_ms {sl['kernel_ms']}{own_s}) | frac "
+                                 f"{frac(sl['bytes_per_launch'], r['avg_us']):.4f} (avg {r['avg_us']} us, median "
+                                 f"{r['median_us']} us) | {r['kernel']} grid {r['grid']} x{r['calls']} |")
     lines += ["", "hot rows include the untimed warm-up launches; cold rows are the launches right after bench's "
               "512 MiB flush kernel.  CG: span = the timed solve's first-to-last loop-kernel time / iterations "
               "(bench divides wall time, which adds the host call); kernel-busy = the loop kernels' summed "
