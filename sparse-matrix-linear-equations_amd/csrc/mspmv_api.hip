@@ -106,7 +106,8 @@ static void free_plan(TilePlan &p)
 // Build (once) the tile plan for L right-hand sides, validating on the host every bound the
 // kernels rely on (monotone boundaries, <= 1.25 * tile_items merge items per tile) before any
 // tile kernel can run on it.
-static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes = 0);
+static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes = 0,
+                               const std::vector<int2> *fixed = nullptr);
 
 // The in-tile reduction modes of a plan for L right-hand sides, built on first use.
 static mspmv_status ensure_modes(mspmv_handle_s *h, TilePlan &p, int L)
@@ -131,6 +132,7 @@ static mspmv_status ensure_modes(mspmv_handle_s *h, TilePlan &p, int L)
 
 static mspmv_status spmv_plan(mspmv_handle_s *h, const TilePlan **out);
 static mspmv_status spmm_slab_decide(mspmv_handle_s *h, int L);
+static mspmv_status spmv_runs_decide(mspmv_handle_s *h, const TilePlan *wg);
 
 // plain: the caller runs the plain product (y = A x / Y = A X), whose single-RHS form may take a
 // one-wave plan of its own (spmv_plan); CG, dot-mode and sharded callers use the workgroup plan.
@@ -138,6 +140,27 @@ static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out, boo
 {
     if (plain && L == 1)
         return spmv_plan(h, out);
+    if (L > 1 && spmm_blk_enabled()) {
+        // a matrix of node blocks only (every single-RHS tile a register run tile: FEM node rows)
+        // multiplies L columns on that plan with k_spmm_blk -- one panel-row gather per (run,
+        // column) -- instead of its own L-wide merge tiles
+        auto one = h->plans.find(plan_key(1));
+        if (one != h->plans.end() && one->second.d_blk && one->second.num_tiles_reg == one->second.num_tiles) {
+            if (plain) {  // the plain product on the run-balanced plan, as the plain SpMV (spmv_runs_decide)
+                if (h->spmv_runs < 0)
+                    ST_TRY(spmv_runs_decide(h, &one->second));
+                auto rp = h->spmv_runs == 1 ? h->plans.find(kRunPlanKey) : h->plans.end();
+                if (rp != h->plans.end()) {
+                    ST_TRY(ensure_modes(h, rp->second, L));
+                    *out = &rp->second;
+                    return MSPMV_OK;
+                }
+            }
+            ST_TRY(ensure_modes(h, one->second, L));
+            *out = &one->second;
+            return MSPMV_OK;
+        }
+    }
     if (plain && (L == 8 || L == 16)) {
         // the plain L-wide product on a column-slab plan when one was chosen (spmm_slab_decide, after the
         // node-block check: FEM matrices keep k_spmm_blk)
@@ -152,17 +175,6 @@ static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out, boo
         auto it = h->spmm_slab[l_index(L)] == 1 ? h->plans.find(slab_mm_key(L)) : h->plans.end();
         *out = it != h->plans.end() ? &it->second : tp;
         return MSPMV_OK;
-    }
-    if (L > 1 && spmm_blk_enabled()) {
-        // a matrix of node blocks only (every single-RHS tile a register run tile: FEM node rows)
-        // multiplies L columns on that plan with k_spmm_blk -- one panel-row gather per (run,
-        // column) -- instead of its own L-wide merge tiles
-        auto one = h->plans.find(plan_key(1));
-        if (one != h->plans.end() && one->second.d_blk && one->second.num_tiles_reg == one->second.num_tiles) {
-            ST_TRY(ensure_modes(h, one->second, L));
-            *out = &one->second;
-            return MSPMV_OK;
-        }
     }
     const int key = plan_key(L);
     auto it = h->plans.find(key);
@@ -226,10 +238,13 @@ mspmv_status plan_split_rows(TilePlan &p, const std::vector<int2> &hb, const std
 }
 }  // namespace mspmv
 
-static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes)
+static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes,
+                               const std::vector<int2> *fixed)
 {
     // lanes: 64 builds the one-wave single-RHS plan (tile = 64 x items per thread, keyed by minus
-    // that size); 0 the default plan for L
+    // that size); 0 the default plan for L.  fixed: the run-balanced single-RHS plan's boundaries
+    // (whole rows, no split; spmv_run_plan), keyed kRunPlanKey -- run by the node-block SpMV only,
+    // whose tiles have no LDS item bound
     const bool onewave = L == 1 && lanes == 64;
     const int tile = onewave ? 64 * spmv_items_per_thread() : tile_items_for(L);
     TilePlan p;
@@ -253,9 +268,16 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
             }
         }
     }
+    if (fixed) {
+        int most = 0;
+        for (size_t t = 0; t + 1 < fixed->size(); ++t)
+            most = std::max(most, ((*fixed)[t + 1].x - (*fixed)[t].x) + ((*fixed)[t + 1].y - (*fixed)[t].y));
+        step = most;
+        snap = 0;
+    }
     p.tile_items = step;
     p.snap = snap;
-    p.num_tiles = (int)((total + step - 1) / step);
+    p.num_tiles = fixed ? (int)fixed->size() - 1 : (int)((total + step - 1) / step);
     const int T = p.num_tiles;
     mspmv_status st;
     if ((st = dev_alloc(&p.d_bounds, (size_t)T + 1)) != MSPMV_OK ||
@@ -269,9 +291,16 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         free_plan(p);
         return s;
     };
-    hipError_t e = launch_merge_coords(h->d_row_offsets, h->m, h->nnz, step, T, p.d_bounds, h->stream);
-    if (e == hipSuccess)
-        e = launch_snap(h->d_row_offsets, h->m, p.d_bounds, p.d_split, T, p.snap, h->stream);
+    hipError_t e = hipSuccess;
+    if (fixed) {
+        e = hipMemcpyAsync(p.d_bounds, fixed->data(), sizeof(int2) * (T + 1), hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess)
+            e = hipMemsetAsync(p.d_split, 0, (size_t)T + 1, h->stream);
+    } else {
+        e = launch_merge_coords(h->d_row_offsets, h->m, h->nnz, step, T, p.d_bounds, h->stream);
+        if (e == hipSuccess)
+            e = launch_snap(h->d_row_offsets, h->m, p.d_bounds, p.d_split, T, p.snap, h->stream);
+    }
     std::vector<int2> hb((size_t)T + 1);
     std::vector<unsigned char> hs((size_t)T + 1);
     if (e == hipSuccess)
@@ -284,7 +313,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         set_error(std::string("tile plan: ") + hipGetErrorString(e));
         return fail(MSPMV_ERR_HIP);
     }
-    const int maxi = tile + tile / kSnapDiv;
+    const int maxi = fixed ? step : tile + tile / kSnapDiv;
     if (hb[0].x != 0 || hb[0].y != 0 || hb[T].x != h->m || hb[T].y != h->nnz) {
         set_error("tile plan: bad end boundaries");
         return fail(MSPMV_ERR_INVALID);
@@ -367,6 +396,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         for (int t = 0; t < T; ++t) {
             const int nd = (int)((hd[(size_t)t * kBlkPerTile].y >> 8) & 255u);
             p.h_blk_reg[(size_t)t] = p.blk_spmv || (reg[(size_t)t] && nd <= kBlkTileChunks);
+            p.blk_two_rounds += nd > kBlkTileChunks;
         }
         dev_free(p.d_blk);
         p.d_blk = nullptr;
@@ -385,9 +415,10 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
             }
         }
     }
-    // multi-RHS: only the L = 16 plan (k_spmm_tile's DICT path runs at L = 16 only)
+    // multi-RHS: only the L = 16 plan (k_spmm_tile's DICT path runs at L = 16 only); not the run-
+    // balanced plan (its kernel gathers x directly)
     const bool multi = !single;
-    const bool want = multi ? spmm_dict_max(L) > 0 : true;
+    const bool want = fixed ? false : multi ? spmm_dict_max(L) > 0 : true;
     if (T > 0 && h->nnz > 0 && want) {
         if ((st = dev_alloc(&p.d_dict, (size_t)h->nnz + kNnzPad)) != MSPMV_OK ||
             (st = dev_alloc(&p.d_ndict, (size_t)T)) != MSPMV_OK ||
@@ -418,7 +449,7 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
             p.d_idx16 = nullptr;
         }
     }
-    auto res = h->plans.emplace(p.lanes == 64 ? -tile : plan_key(L), p);  // one-wave: negative keys
+    auto res = h->plans.emplace(fixed ? kRunPlanKey : p.lanes == 64 ? -tile : plan_key(L), p);  // one-wave: negative keys
     *out = &res.first->second;
     return MSPMV_OK;
 }
@@ -523,6 +554,101 @@ static mspmv_status spmm_slab_decide(mspmv_handle_s *h, int L)
     return MSPMV_OK;
 }
 
+// Run-balanced plan for the node-block SpMV / SpMM (round 5).  The merge-path tiles of a node-block plan hold
+// ~2,048 items: 6-7 runs on the pwtk shape, one round of k_spmv_blk's eight half-wave run slots.  On
+// imperfect FEM (odd-size nodes, off-pattern rows: more, shorter runs) a quarter of the tiles need 9-14
+// slots, i.e. a second round after the first has returned (24.2 vs 21.1 us per launch, r04).  This plan
+// cuts the tiles at run starts instead, each holding whole runs of <= kBlkTileChunks chunks (the
+// runs k_build_blocks forms, restated here on the host: <= kBlkRunRows rows whose column lists are
+// prefixes of the run's longest, <= 64 pattern columns per chunk), so every tile is one round.  Only
+// the plain SpMV on an all-register node-block plan runs it (k_spmv_blk has no LDS item bound); CG,
+// dot-mode callers keep the merge-path plan; the plain L-wide node-block SpMM (k_spmm_blk: the same
+// per-round run slots) takes it too.  MSPMV_SPMV_RUNS=0/1 forces it off / on.
+static int runs_switch()
+{
+    const char *e = getenv("MSPMV_SPMV_RUNS");
+    return e && *e ? (atoi(e) != 0 ? 1 : 0) : -1;
+}
+
+static mspmv_status spmv_runs_decide(mspmv_handle_s *h, const TilePlan *wg)
+{
+    h->spmv_runs = 0;
+    const int sw = runs_switch();
+    if (sw == 0 || !wg->blk_spmv || wg->num_tiles_reg != wg->num_tiles || h->m <= 0)
+        return MSPMV_OK;
+    std::vector<int> ro((size_t)h->m + 1), ci((size_t)h->nnz);
+    if (hipMemcpy(ro.data(), h->d_row_offsets, sizeof(int) * ro.size(), hipMemcpyDeviceToHost) != hipSuccess ||
+        (h->nnz && hipMemcpy(ci.data(), h->d_cols, sizeof(int) * ci.size(), hipMemcpyDeviceToHost) != hipSuccess)) {
+        (void)hipGetLastError();
+        set_error("");
+        return MSPMV_OK;  // optional plan: the merge-path plan stays
+    }
+    // tiles of whole runs: <= kBlkTileChunks chunks and about the merge-path plan's items, and always
+    // at least one run
+    // (caps measured, r05l: 112 / 125 / 150 / 200 % of the merge-path tile's items within 1 % on pwtk,
+    // 7 chunks per tile slower on the imperfect shape)
+    const long long items_cap = (long long)wg->tile_items + wg->tile_items / 4;
+    std::vector<int2> hb;
+    hb.push_back(make_int2(0, 0));
+    int chunks = 0;
+    long long items = 0;
+    for (int r = 0; r < h->m;) {
+        const int g = r;
+        int p = g, plen = ro[(size_t)g + 1] - ro[(size_t)g], hgt = 0;
+        for (; r < h->m && hgt < kBlkRunRows; ++r, ++hgt) {
+            const int s0 = ro[(size_t)r], len = ro[(size_t)r + 1] - s0;
+            if (hgt > 0) {
+                const int ps = ro[(size_t)p], mm = std::min(len, plen);
+                bool same = true;
+                for (int q = 0; q < mm && same; ++q)
+                    same = ci[(size_t)s0 + q] == ci[(size_t)ps + q];
+                if (!same || (len > 64 && plen <= 64))  // (k_build_blocks' rules, incl. its 64-column stop)
+                    break;
+                if (len > plen) {
+                    p = r;
+                    plen = len;
+                }
+            }
+        }
+        const int c = std::max(1, (plen + 63) / 64);
+        const long long it = (long long)(r - g) + (ro[(size_t)r] - ro[(size_t)g]);
+        if (chunks > 0 && (chunks + c > kBlkTileChunks || items + it > items_cap)) {
+            hb.push_back(make_int2(g, ro[(size_t)g]));
+            chunks = 0;
+            items = 0;
+        }
+        chunks += c;
+        items += it;
+    }
+    hb.push_back(make_int2(h->m, h->nnz));
+    if (hb.size() > 2 && hb[hb.size() - 2].x == h->m)
+        hb.erase(hb.end() - 2);
+    const TilePlan *np = nullptr;
+    const mspmv_status st = build_plan(h, 1, &np, 0, &hb);
+    if (st != MSPMV_OK) {
+        auto it = h->plans.find(kRunPlanKey);
+        if (it != h->plans.end()) {
+            free_plan(it->second);
+            h->plans.erase(it);
+        }
+        (void)hipGetLastError();
+        set_error("");
+        return MSPMV_OK;
+    }
+    TilePlan &rp = h->plans.find(kRunPlanKey)->second;
+    if (ensure_modes(h, rp, 1) != MSPMV_OK || !rp.blk_spmv || rp.num_tiles_reg != rp.num_tiles) {
+        // the runs must all be register tiles
+        auto it = h->plans.find(kRunPlanKey);
+        free_plan(it->second);
+        h->plans.erase(it);
+        (void)hipGetLastError();
+        set_error("");
+        return MSPMV_OK;
+    }
+    h->spmv_runs = 1;
+    return MSPMV_OK;
+}
+
 static mspmv_status spmv_plan(mspmv_handle_s *h, const TilePlan **out)
 {
     const TilePlan *wg = nullptr;
@@ -552,7 +678,13 @@ static mspmv_status spmv_plan(mspmv_handle_s *h, const TilePlan **out)
         }
         h->spmv_onewave = want ? 1 : 0;
     }
-    *out = h->spmv_onewave == 1 ? &h->plans.find(-64 * spmv_items_per_thread())->second : wg;
+    if (h->spmv_onewave == 1) {
+        *out = &h->plans.find(-64 * spmv_items_per_thread())->second;
+        return MSPMV_OK;
+    }
+    if (h->spmv_runs < 0)
+        ST_TRY(spmv_runs_decide(h, wg));
+    *out = h->spmv_runs == 1 ? &h->plans.find(kRunPlanKey)->second : wg;
     return MSPMV_OK;
 }
 
@@ -930,6 +1062,7 @@ mspmv_status mspmv_set_cu_limit(mspmv_handle h, int num_cus)
         h->plans.clear();
         h->spmv_onewave = -1;
         h->spmv_slab = -1;
+        h->spmv_runs = -1;
         for (int &v : h->spmm_slab)
             v = -1;
         h->num_cus = n;

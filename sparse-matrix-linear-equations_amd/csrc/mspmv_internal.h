@@ -113,6 +113,7 @@ struct TilePlan {
     int blk_rows_max = 8;               // the tallest run (rows of one node) over the descriptors
     bool blk_spmv = false;              // the plain SpMV runs k_spmv_blk (most tiles register run tiles;
                                         // the rest take its register fallback)
+    int blk_two_rounds = 0;             // node-block tiles of more than one round of run slots (> kBlkTileChunks)
     std::vector<unsigned char> h_blk_reg;  // [num_tiles] 1: the plain SpMV reduces the tile in registers
                                            // (a reordered sum: mspmv_tile_modes reports 255)
     SlabData *slab = nullptr;           // column-slab plan (tiles = blocks; mspmv_slab.hip), else null
@@ -209,6 +210,9 @@ struct mspmv_handle_s {
     // plain single-RHS SpMV on the column-slab plan (mspmv_slab.hip, plan key kSlabPlanKey): -1 not
     // decided yet, 0 no, 1 yes (spmv_plan; MSPMV_SPMV_SLAB)
     int spmv_slab = -1;
+    // plain single-RHS SpMV on the run-balanced node-block plan (key kRunPlanKey; mspmv_api.hip
+    // spmv_runs_decide): -1 not decided yet, 0 no, 1 yes
+    int spmv_runs = -1;
     // plain SpMM of width L (index l_index(L)) on a column-slab plan (key slab_mm_key(L)): -1 not
     // decided yet, 0 no, 1 yes (mspmv_api.hip spmm_slab_decide; MSPMV_SPMM_SLAB)
     int spmm_slab[5] = {-1, -1, -1, -1, -1};
@@ -236,6 +240,7 @@ namespace mspmv {
 
 // ---- column-slab SpMV (mspmv_slab.hip) ---------------------------------------------
 constexpr int kSlabPlanKey = -1;
+constexpr int kRunPlanKey = -2;  // the run-balanced node-block SpMV plan (mspmv_api.hip spmv_runs_decide)
 // Builds the column-slab plan into *p (blocks, split rows, reordered stream); MSPMV_ERR_UNSUPPORTED
 // when the matrix does not fit the form (rows per block) or its blocks would hold fewer than
 // min_nnz_per_block nonzeros on average; p is freed by the caller on any error.
@@ -271,6 +276,9 @@ hipError_t launch_pack_cols16(const int *d_cols, const int2 *d_bounds, int num_t
 bool spmv_blocks_enabled();
 // SpMM (L >= 2) through the single-RHS node-block plan (k_spmm_blk) when all its tiles are register tiles.
 bool spmm_blk_enabled();
+// Rows per run: at most 6, the column-pair SpMV kernel's value registers (k_spmv_blk<.., 6>); a node
+// of 7 or 8 unknowns becomes two runs (a 6-DOF FEM node, pwtk's, is one).
+constexpr int kBlkRunRows = 6;
 constexpr int kBlkPerTile = 64;  // == kBlkMax in the kernels: descriptor capacity of a tile
 // Chunks per tile k_build_blocks may describe for the plain SpMV's column-pair kernel (two rounds of
 // its eight half-wave run slots), and the one-round limit of k_spmv_tile's node-block paths.

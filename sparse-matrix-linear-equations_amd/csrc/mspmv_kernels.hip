@@ -474,9 +474,7 @@ __global__ __launch_bounds__(kBlock) void k_build_dict(const int *__restrict__ c
 //   z, w: the h row lengths, 8 bits each (rows of a run are <= 255 long)
 constexpr int kBlkMax = 64;  // descriptors a tile may have (the plan stores them at a stride of 16, 32 or 64)
 constexpr int kBlkRows = 8;
-// Rows per run: at most 6, the column-pair SpMV kernel's value registers (k_spmv_blk<.., 6>); a node
-// of 7 or 8 unknowns becomes two runs (a 6-DOF FEM node, pwtk's, is one).
-constexpr int kBlkRunRows = 6;
+// (kBlkRunRows, mspmv_internal.h: rows per run)
 // (kBlkTileChunks, mspmv_internal.h: the chunks of a tile the LDS-staged and column-owner paths of
 // k_spmv_tile take -- one round of its four waves, more measured slower than striped staging; tiles
 // of up to kBlkPlanChunks run only in the column-pair kernel, which loops over rounds.)
@@ -521,7 +519,9 @@ __global__ void k_build_blocks(const int *__restrict__ row_offsets, const int *_
                 bool same = true;
                 for (int q = 0; q < m && same; ++q)
                     same = cols[s + q] == cols[ps + q];
-                if (!same)
+                // a row that would widen a pattern of <= 64 columns past 64 starts a new run: the run
+                // stays one chunk (a register run tile) -- spmv_runs_decide's host restatement relies on it
+                if (!same || (len > 64 && plen <= 64))
                     break;
                 if (len > plen) {
                     p = r;

@@ -378,3 +378,37 @@ def test_blocks_mixed_plan_spmm(orc, name, L):
     with mspmv.GpuCsr(a) as g:
         Y = g.spmm(X)
         check_parity_chunked(a, g, Y, orc.csr_spmm_t(a, X), X, L)
+
+
+@pytest.mark.parametrize("runs", ["0", "1", "auto"])
+@pytest.mark.parametrize("name", ["regular", "perturbed_small", "perturbed_heavy"])
+def test_blocks_run_plan(orc, monkeypatch, name, runs):
+    """The run-balanced node-block plan (mspmv_api.hip spmv_runs_decide: tiles cut at run starts, <= 8
+    run chunks each, so k_spmv_blk takes every tile in one round of its half-wave slots): automatic on
+    every all-register node-block plan, off with MSPMV_SPMV_RUNS=0.  Parity against SpmvGold under the
+    plan the product ran on, and the L = 16 node-block SpMM on it against OmpCsrSpmmT; bitwise repeats;
+    its boundaries are row starts."""
+    if runs == "auto":
+        monkeypatch.delenv("MSPMV_SPMV_RUNS", raising=False)
+    else:
+        monkeypatch.setenv("MSPMV_SPMV_RUNS", runs)
+    make = mixed_cases().get(name) or (lambda: mspmv.CsrMatrix.synth_fem_blocked(21792, 1152443, 6, 170, seed=3))
+    a = make()
+    x = np.random.default_rng(21).uniform(-1, 1, a.num_cols)
+    X = np.random.default_rng(22).uniform(-1, 1, (a.num_cols, 16))
+    with mspmv.GpuCsr(a) as g:
+        plan = g.tile_plan(1)
+        y = g.spmv(x)
+        y2 = g.spmv(x)
+        kname = g.kernel_name()
+        check_parity(a, y, orc.spmv_gold(a, x), x, plan, 1)
+        Y = g.spmm(X)
+        check_parity(a, Y, orc.csr_spmm_t(a, X), X, g.tile_plan(16), 16)
+        mname = g.spmm_kernel_name(16)
+        assert g.tile_plan(16)["num_tiles"] == plan["num_tiles"] or name.startswith("perturbed") or runs == "0"
+    assert y.tobytes() == y2.tobytes()
+    assert kname.startswith("k_spmv_blk<0,"), kname
+    b = plan["bounds"]
+    on_rows = np.array_equal(a.row_offsets[b[:, 0]], b[:, 1])
+    if runs != "0":  # automatic on every all-register node-block plan
+        assert on_rows and plan["num_carries"] == 0

@@ -18,7 +18,7 @@ shapes = {
 }
 runs = {"cant": (16,), "pwtk": (2, 4, 8, 16), "nlpkkt": (8,)}
 out = {"lib": os.path.basename(os.environ.get("MSPMV_LIB", "libmspmv.so"))}
-for name, make in shapes.items():
+for name, make in [(k, v) for k, v in shapes.items() if not os.environ.get("PROBE_ONLY") or k in os.environ["PROBE_ONLY"].split()]:
     a = make()
     with mspmv.GpuCsr(a) as g:
         for L in runs[name]:

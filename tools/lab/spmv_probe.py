@@ -38,6 +38,7 @@ for name in (sys.argv[1:] or os.environ.get("PROBE_SHAPES", "").split() or list(
     plan = gs[0].tile_plan(1)
     print(json.dumps({"shape": name, "lib": os.path.basename(os.environ.get("MSPMV_LIB", "libmspmv.so")),
                       "kernel": gs[0].kernel_name(), "nnz": a.num_nonzeros, "tiles": plan["num_tiles"],
+                      "tiles_all": [g.tile_plan(1)["num_tiles"] for g in gs],
                       "block_tiles": gs[0].plan_block_tiles(1), "carries": plan["num_carries"],
                       "kernel_us": round(kern * 1e3, 2), "step_us": round(step * 1e3, 2), "kernels_per_step": kps,
                       "frac": round(nb / (kern * 1e-3) / 1e9 / HBM, 4)}), flush=True)
