@@ -487,7 +487,7 @@ def run_cg_multi(d, dev):
             call_ms, kern_ms, _ = g.time_spmm(dx1, dy1, 1, 40)
             nb = spmv_bytes(n, n, nk.num_nonzeros)
             spmv_large = {"workload": f"SpMV fp64 1 RHS, nlpkkt120-sized 27-pt matrix m={n} nnz={nk.num_nonzeros}",
-                          "kernel_ms": round(kern_ms, 5), "gflops": round(2.0 * nk.num_nonzeros / kern_ms / 1e6, 1),
+                          "kernel": g.kernel_name(), "kernel_ms": round(kern_ms, 5), "gflops": round(2.0 * nk.num_nonzeros / kern_ms / 1e6, 1),
                           "bytes_per_launch": nb, "achieved_GBps": round(nb / kern_ms / 1e6, 1),
                           "frac": round(nb / kern_ms / 1e6 / HBM_PEAK_GBS, 4)}
         mode = "1 GPU"

@@ -101,6 +101,8 @@ static void free_plan(TilePlan &p)
     dev_free(p.d_blk);
     free_slab(p.slab);
     p.slab = nullptr;
+    free_dia(p.dia);
+    p.dia = nullptr;
 }
 
 // Build (once) the tile plan for L right-hand sides, validating on the host every bound the
@@ -134,10 +136,77 @@ static mspmv_status spmv_plan(mspmv_handle_s *h, const TilePlan **out);
 static mspmv_status spmm_slab_decide(mspmv_handle_s *h, int L);
 static mspmv_status spmv_runs_decide(mspmv_handle_s *h, const TilePlan *wg);
 
+// Offset-window plan (mspmv_dia.hip) for the plain SpMV / SpMM of every width and the split CG's SpMM:
+// taken when every 64-row window of the matrix lists its columns at <= kDiaMaxK common offsets col - row
+// and the nonzeros fill >= kDiaAutoFill of the windows' rows x offsets overall (>= kDiaWindowFill in each
+// window): structured-grid stencils, whose boundary planes miss a third of the offsets.  MSPMV_DIA=0
+// never, =1 whenever every window fits at any fill; read at each handle's decision.
+constexpr double kDiaAutoFill = 0.85;
+constexpr double kDiaWindowFill = 0.3;
+static int dia_switch()
+{
+    const char *e = getenv("MSPMV_DIA");
+    return e && *e ? (atoi(e) != 0 ? 1 : 0) : -1;
+}
+
+static mspmv_status dia_decide(mspmv_handle_s *h)
+{
+    h->dia = 0;
+    const int sw = dia_switch();
+    if (sw == 0)
+        return MSPMV_OK;
+    TilePlan p;
+    const mspmv_status st = build_dia_plan(h, p, sw == 1 ? 0.0 : kDiaAutoFill, sw == 1 ? 0.0 : kDiaWindowFill);
+    if (st != MSPMV_OK) {
+        free_plan(p);
+        if (sw < 0 || st == MSPMV_ERR_UNSUPPORTED) {  // optional plan: the tile plans stay
+            set_error("");
+            (void)hipGetLastError();
+            return MSPMV_OK;
+        }
+        return st;
+    }
+    h->plans.emplace(kDiaPlanKey, p);
+    h->dia = 1;
+    return MSPMV_OK;
+}
+
+// The L-wide products take the windows only when asked (MSPMV_DIA_SPMM=1): on the nlpkkt120-size
+// 27-point shape the L = 8 window kernel measured 470-513 us against 443 us on the tiles, even on the
+// parabolic_fem shape (r05q); the single-RHS product is where the windows win (221 -> 189 us, 11.2 ->
+// 7.7 us, r05p).
+bool mspmv::dia_spmm_enabled()
+{
+    const char *e = getenv("MSPMV_DIA_SPMM");
+    return e && *e && atoi(e) != 0;
+}
+
+// The offset-window plan for a product of width L when the handle takes one (deciding on first use),
+// else null.
+static mspmv_status dia_plan(mspmv_handle_s *h, const TilePlan **out, int L = 1)
+{
+    *out = nullptr;
+    if (L > 1 && !dia_spmm_enabled())
+        return MSPMV_OK;
+    if (h->dia < 0)
+        ST_TRY(dia_decide(h));
+    if (h->dia == 1)
+        *out = &h->plans.find(kDiaPlanKey)->second;
+    return MSPMV_OK;
+}
+
 // plain: the caller runs the plain product (y = A x / Y = A X), whose single-RHS form may take a
 // one-wave plan of its own (spmv_plan); CG, dot-mode and sharded callers use the workgroup plan.
 static mspmv_status get_plan(mspmv_handle_s *h, int L, const TilePlan **out, bool plain = false)
 {
+    if (plain) {
+        const TilePlan *dp = nullptr;
+        ST_TRY(dia_plan(h, &dp, L));
+        if (dp) {
+            *out = dp;
+            return MSPMV_OK;
+        }
+    }
     if (plain && L == 1)
         return spmv_plan(h, out);
     if (L > 1 && spmm_blk_enabled()) {
@@ -651,6 +720,9 @@ static mspmv_status spmv_runs_decide(mspmv_handle_s *h, const TilePlan *wg)
 
 static mspmv_status spmv_plan(mspmv_handle_s *h, const TilePlan **out)
 {
+    ST_TRY(dia_plan(h, out));
+    if (*out)
+        return MSPMV_OK;
     const TilePlan *wg = nullptr;
     ST_TRY(get_plan(h, 1, &wg));
     if (h->spmv_slab < 0)
@@ -1063,6 +1135,7 @@ mspmv_status mspmv_set_cu_limit(mspmv_handle h, int num_cus)
         h->spmv_onewave = -1;
         h->spmv_slab = -1;
         h->spmv_runs = -1;
+        h->dia = -1;
         for (int &v : h->spmm_slab)
             v = -1;
         h->num_cus = n;
@@ -1111,10 +1184,13 @@ static int native_chunk(int left)
 // rows (the SpMM tolerance of the tests).
 static mspmv_status spmm_chunks(mspmv_handle_s *h, const double *d_X, double *d_Y, int L)
 {
+    const TilePlan *dp = nullptr;  // the offset-window plan serves every width it is enabled for
+    ST_TRY(dia_plan(h, &dp, 2));
     for (int c0 = 0; c0 < L;) {
         const int w = native_chunk(L - c0);
-        const TilePlan *plan = nullptr;
-        ST_TRY(get_plan(h, w, &plan));
+        const TilePlan *plan = dp;
+        if (!plan)
+            ST_TRY(get_plan(h, w, &plan));
         HIP_TRY(launch_spmm(h, *plan, d_X + c0, d_Y + c0, w, nullptr, L));
         c0 += w;
     }
@@ -1352,11 +1428,12 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
         return MSPMV_OK;
     const TilePlan *plan = nullptr, *mplan = nullptr, *splan = nullptr;
     ST_TRY(get_plan(h, L, &plan));
-    if (!hm && !ic && cg_split_iteration(L) && (L == 8 || L == 16)) {
-        // the split iteration's plain SpMM runs on the handle's column-slab plan when the plain product
-        // takes one: decided here, before any graph capture (it may copy the matrix to the host)
+    if (!hm && !ic && cg_split_iteration(L)) {
+        // the split iteration's plain SpMM runs on the handle's offset-window or column-slab plan when
+        // the plain product takes one: decided here, before any graph capture (it may copy the matrix to
+        // the host); launch_cg_iteration_split finds it by the handle's decisions
         ST_TRY(get_plan(h, L, &splan, true));
-        if (!splan->slab)
+        if (!splan->slab && !splan->dia)
             splan = nullptr;
     }
     if (hm) {

@@ -62,6 +62,21 @@ struct SlabMmCfg {
 };
 constexpr int kSlabMmMaxChunks = 127;  // chunks per block (their descriptors sit in LDS)
 
+// Offset windows (mspmv_dia.hip): 64-row windows whose rows list their columns at <= kDiaMaxK common
+// offsets col - row, values lane-major per window.
+constexpr int kDiaMaxK = 32;
+struct DiaData {
+    int windows = 0;
+    int max_k = 0;
+    int masked_windows = 0;                  // windows with a row missing some offset (presence masks)
+    long long sum_k = 0;                     // value panels of 64 doubles
+    double fill = 0.0;                       // nonzeros / (64 sum_k)
+    int4 *d_hdr = nullptr;                   // [windows] {K, offset base, value base, mask base or -1}
+    int *d_off = nullptr;                    // [sum_k]
+    unsigned long long *d_mask = nullptr;    // [K of the masked windows]
+    double *d_vt = nullptr;                  // [sum_k][64]
+};
+
 // A merge-path tile plan for one nominal tile size (merge items per tile).
 //
 // Tile t covers the merge-path diagonals between boundary t and t+1.  A boundary whose
@@ -117,6 +132,7 @@ struct TilePlan {
     std::vector<unsigned char> h_blk_reg;  // [num_tiles] 1: the plain SpMV reduces the tile in registers
                                            // (a reordered sum: mspmv_tile_modes reports 255)
     SlabData *slab = nullptr;           // column-slab plan (tiles = blocks; mspmv_slab.hip), else null
+    DiaData *dia = nullptr;             // offset-window plan (tiles = 64-row windows; mspmv_dia.hip), else null
 };
 
 // Device-resident CG scalars (one set per right-hand side column).
@@ -216,6 +232,9 @@ struct mspmv_handle_s {
     // plain SpMM of width L (index l_index(L)) on a column-slab plan (key slab_mm_key(L)): -1 not
     // decided yet, 0 no, 1 yes (mspmv_api.hip spmm_slab_decide; MSPMV_SPMM_SLAB)
     int spmm_slab[5] = {-1, -1, -1, -1, -1};
+    // plain SpMV / SpMM (every width) and the split CG's SpMM on the offset-window plan (key kDiaPlanKey;
+    // mspmv_api.hip dia_decide): -1 not decided yet, 0 no, 1 yes
+    int dia = -1;
 };
 
 // IC(0) factor on the device (mspmv_ic0_create): L and its transpose for the two sync-free
@@ -257,6 +276,20 @@ hipError_t launch_slab_mm(mspmv_handle_s *h, const TilePlan &plan, const double 
                           const CgControl *ctrl);
 std::string slab_mm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan);
 mspmv_status plan_split_rows(TilePlan &p, const std::vector<int2> &hb, const std::vector<unsigned char> &hs);
+
+// ---- offset windows (mspmv_dia.hip) -------------------------------------------------
+constexpr int kDiaPlanKey = -3;
+// Builds the offset-window plan into *p; MSPMV_ERR_UNSUPPORTED when some window does not fit (a row
+// longer than kDiaMaxK, more distinct offsets than that, fewer than min_window_fill x rows x K
+// nonzeros, or columns not strictly ascending) or the matrix's nonzeros fill less than min_fill of the
+// panels; p is freed by the caller on any error.
+mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, double min_window_fill);
+void free_dia(DiaData *d);
+// Y = A X (L = 1, 2, 4, 8, 16; ld: panel stride, 0 = L); ctrl (CG): return at once when ctrl->done
+hipError_t launch_dia(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L, int ld,
+                      const CgControl *ctrl);
+std::string dia_kernel_name(const mspmv_handle_s *h, int L);
+bool dia_spmm_enabled();  // MSPMV_DIA_SPMM=1: the L-wide products on the windows too (mspmv_api.hip)
 
 // ---- launchers (mspmv_kernels.hip) --------------------------------------------------
 void set_error(const std::string &msg);

@@ -3146,6 +3146,8 @@ int blk_kr(const TilePlan &p) { return p.blk_rows_max <= 6 ? 6 : 8; }
 
 std::string spmv_kernel_name(const mspmv_handle_s *h)
 {
+    if (h->dia == 1)
+        return dia_kernel_name(h, 1);
     if (h->spmv_slab == 1)
         return slab_kernel_name(h);
     const std::string nt = stream_nt(h) ? "true" : "false";
@@ -3173,6 +3175,8 @@ std::string spmm_kernel_name(const mspmv_handle_s *h, const TilePlan &plan, int 
 {
     if (L == 1)
         return spmv_kernel_name(h);
+    if (plan.dia)
+        return dia_kernel_name(h, L);
     if (plan.slab)
         return slab_mm_kernel_name(h, plan);
     const std::string nt = stream_nt(h) ? "true" : "false";
@@ -3451,6 +3455,8 @@ hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const 
 {
     if (plan.num_tiles == 0)
         return hipSuccess;
+    if (plan.dia)  // offset windows: every width on one plan
+        return launch_dia(h, plan, d_X, d_Y, L, ld, nullptr);
     if (plan.slab) {  // a column-slab plan: the plain SpMV's (spmv_plan) or an L-wide SpMM's (get_plan)
         if (plan.slab->L != L)
             return hipErrorInvalidValue;
@@ -3800,7 +3806,11 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
         // (on the column-slab plan when the handle's plain L-wide product took one: spmm_slab_decide)
         const auto sp = (L == 8 || L == 16) && h->spmm_slab[l_index(L)] == 1 ? h->plans.find(slab_mm_key(L))
                                                                               : h->plans.end();
-        if (sp != h->plans.end()) {
+        const auto dp = h->dia == 1 && (L == 1 || dia_spmm_enabled()) ? h->plans.find(kDiaPlanKey) : h->plans.end();
+        if (dp != h->plans.end()) {  // offset windows (mspmv_dia.hip): structured-grid rows
+            if ((e = launch_dia(h, dp->second, h->d_p0, h->d_ap, L, L, h->d_ctrl)) != hipSuccess)
+                return e;
+        } else if (sp != h->plans.end()) {
             if ((e = launch_slab_mm(h, sp->second, h->d_p0, h->d_ap, L, L, h->d_ctrl)) != hipSuccess)
                 return e;
         } else {

@@ -39,6 +39,18 @@ def gpu_available():
     return True
 
 
+# Modules that run the library's default plan choice.  The others exercise the tile kernels' own
+# features (reductions, node blocks, dictionaries, slabs, plan queries) on stencil-shaped matrices too,
+# which by default take the offset-window plan (csrc/mspmv_dia.hip): they pin MSPMV_DIA=0.
+DEFAULT_PLAN_MODULES = {"test_gpu_dia.py", "test_gpu_fullsize.py", "test_gpu_cg.py"}
+
+
+@pytest.fixture(autouse=True)
+def _tile_plans_for_tile_tests(request, monkeypatch):
+    if request.node.fspath.basename not in DEFAULT_PLAN_MODULES:
+        monkeypatch.setenv("MSPMV_DIA", "0")
+
+
 def pytest_collection_modifyitems(config, items):
     """Run test_gpu_fullsize.py (one test per BASELINE config at its full size) first, then the
     rest in file order: a round-end run cut short still has covered every config."""

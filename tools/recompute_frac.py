@@ -173,7 +173,7 @@ def main(src, dst):
                 # SURVEY 8(d)'s named 70 % case: the nlpkkt120-size single-RHS SpMV timed in the same leg
                 # (back-to-back launches) against its rows in this trace
                 sl = bench["spmv_nlpkkt120_size"]
-                sp = [r for r in rows if r["kernel"].startswith("k_spmv") and r["calls"] >= 40]
+                sp = [r for r in rows if r["kernel"].startswith(("k_spmv", "k_spmm_dia<1,")) and r["calls"] >= 40]
                 if sp:
                     r = max(sp, key=lambda q: q["grid"])
                     own = lj0.get("spmv_nlpkkt120_size") if isinstance(lj0, dict) else None
