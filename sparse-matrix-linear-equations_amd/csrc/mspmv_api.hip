@@ -171,14 +171,14 @@ static mspmv_status dia_decide(mspmv_handle_s *h)
     return MSPMV_OK;
 }
 
-// The L-wide products take the windows only when asked (MSPMV_DIA_SPMM=1): on the nlpkkt120-size
-// 27-point shape the L = 8 window kernel measured 470-513 us against 443 us on the tiles, even on the
-// parabolic_fem shape (r05q); the single-RHS product is where the windows win (221 -> 189 us, 11.2 ->
-// 7.7 us, r05p).
+// The L-wide products take the windows too unless MSPMV_DIA_SPMM=0: with the offsets taken run by run
+// through LDS they beat the merge tiles at every width on the stencil shapes (nlpkkt120 size L = 2 / 4 / 8
+// / 16: 268 / 295 / 372 / 677 us against 336 / 375 / 441 / 753; parabolic_fem shape 10.5 / 13.5 / 19.2 /
+// 37 against 15.4 / 16 / 21.8 / 37.5 us; configs[4]'s CG 0.786 -> 0.704 ms per iteration, r05x).
 bool mspmv::dia_spmm_enabled()
 {
     const char *e = getenv("MSPMV_DIA_SPMM");
-    return e && *e && atoi(e) != 0;
+    return !(e && *e && atoi(e) == 0);
 }
 
 // The offset-window plan for a product of width L when the handle takes one (deciding on first use),

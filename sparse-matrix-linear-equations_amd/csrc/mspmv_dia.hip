@@ -3,12 +3,13 @@
 // A window is 64 consecutive rows.  Where the rows of a window list their columns at a few common
 // offsets from the row index (col - row: a finite-difference or finite-volume stencil, the 27-point
 // nlpkkt120-size shape, parabolic_fem's 7-point triangles), the window is stored as its sorted offset
-// list D (K <= kDiaMaxK entries) and a K x 64 panel of values, lane-major: value k of the window's row
-// l at vt[k][l] (0 where row l has no column at offset D[k]; a 64-bit presence mask per (window, k)
-// then says which rows hold it).  One wave computes one window with lane = row: for k = 0 .. K-1 it
-// loads vt[k][lane] (512 contiguous bytes) and x[row + D[k]] (64 consecutive rows: contiguous), so
-// there is no column stream (8 B per nonzero from HBM instead of 10-12), no gather of scattered lines,
-// no LDS and no cross-lane reduction.  Each row is summed from 0.0 in D order, which is its CSR order
+// list D (K <= kDiaMaxK entries) and its values lane-major in pairs of offsets: values 2p and 2p+1 of
+// the window's row l at vt[p][l][0..1] (0 where row l has no column at offset D[k]; a 64-bit presence
+// mask per (window, k) then says which rows hold it).  One wave computes one window with lane = row:
+// per two offsets it loads vt[p][lane] (16 B per lane, 1 KB per wave instruction: 8-B loads streamed
+// the panels at 5.2 TB/s, r05u) and x[row + D[k]] (64 consecutive rows: contiguous), so there is no
+// column stream (8 B per nonzero from HBM instead of 10-12), no gather of scattered lines, no LDS and
+// no cross-lane reduction.  Each row is summed from 0.0 in D order, which is its CSR order
 // (the planner requires every row's columns strictly ascending), as mul then add: bit-identical to
 // SpmvGold (cpu_spmv.cpp:241-265) and, per column, to the reference's row-by-row SpMM
 // (work_2025/spmm/cpu_spmm.cpp), whose merge-path OmpMergeCsrmv / OmpMergeCsrmm
@@ -47,8 +48,13 @@ struct DiaArgs {
     int windows;
     int groups;                      // workgroups (windows / 4, rounded up)
     int m;
+    int n;                           // columns (X rows)
     int ld;                          // panel row stride (L-wide products)
 };
+
+// Runs of consecutive offsets (d, d+1, ..., d+g-1; g <= kDiaRun) read the same X panel rows shifted by
+// one row per offset: form 5 stages the run's 64 + g - 1 rows once in LDS.
+constexpr int kDiaRun = 4;
 
 template <bool NT>
 __device__ __forceinline__ double dia_ld(const double *p)
@@ -59,20 +65,30 @@ __device__ __forceinline__ double dia_ld(const double *p)
         return *p;
 }
 
-// Values in flight per lane: U consecutive offsets of the window are loaded before any is summed.
-constexpr int dia_unroll(int L) { return L <= 2 ? 8 : L <= 8 ? 4 : 2; }
+template <bool NT>
+__device__ __forceinline__ v2d_t dia_ld2(const v2d_t *p)
+{
+    if constexpr (NT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
 
-// Lab forms of the L-wide kernel (MSPMV_DIA_FORM, A/B only; default 1): 0 lanes (column pair, row)
-// with each lane's rows' values loaded directly, U = dia_unroll(L); 1 the values loaded once per offset
-// (lane = row) and passed by shuffles; 2 one row per lane (L/2 double2 loads per offset); 3 form 2
-// with half the unroll; 4 form 0 with half the unroll.  nlpkkt120 size, L = 8 (r05q): 497 / 470 / 586
-// / 598 / 513 us -- value-load instructions and X lines per instruction both cost.
-constexpr int dia_form_unroll(int L, int FORM) { return (FORM == 3 || FORM == 4) ? (dia_unroll(L) > 1 ? dia_unroll(L) / 2 : 1) : dia_unroll(L); }
-
-template <int L, bool NT, int FORM = 0>
+// The window's metadata -- offsets, presence masks, run lengths -- is loaded once into lanes (lane k:
+// offset k) and read as wave-uniform values with v_readlane: no memory operation per offset, so no
+// scalar-load chain before each x load and no vmcnt wait that would drain a prefetch (r05s).
+//
+// L = 1: lane = row, U offsets in flight (U/2 pair loads of the panel, U x loads).
+// L > 1 (X row-major, L/2 lanes per panel row, a lane holding L/2 rows of the window): the window's
+// offsets taken run by run (d, d+1, ..., d+g-1, g <= kDiaRun: a stencil's x-line neighbours), each run's
+// 64 + g - 1 panel rows loaded ONCE -- 1 KB contiguous per wave instruction -- and staged in LDS, where
+// the g offsets read them shifted by one row each; the next run's rows and values are loaded while this
+// run is summed.  A row's value for offset k comes from the lane holding the row (lane = row) by a
+// shuffle.  nlpkkt120 size, L = 8 (r05q-r05t): 369-374 us against 440 on the
+// merge tiles; gathering every offset's rows directly (no LDS) 460-497 us, one row per lane 586 us.
+template <int L, bool NT>
 __global__ __launch_bounds__(kDiaThreads) void k_spmm_dia(DiaArgs a)
 {
-    constexpr int U = L == 1 ? dia_unroll(1) : dia_form_unroll(L, FORM);
     const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int w = xcd_tile(blockIdx.x, a.groups) * kDiaWaves + wv;
     if (w >= a.windows)
@@ -81,129 +97,152 @@ __global__ __launch_bounds__(kDiaThreads) void k_spmm_dia(DiaArgs a)
         return;
     const int lane = threadIdx.x & 63;
     const int4 hd = a.hdr[w];
-    const int K = hd.x;
-    const int *__restrict__ off = a.off + hd.y;
-    const double *__restrict__ vt = a.vt + (size_t)hd.z * 64;
+    const int K = __builtin_amdgcn_readfirstlane(hd.x);
+    const bool masked = __builtin_amdgcn_readfirstlane(hd.w) >= 0;
+    const int lk = min(lane, K - 1);
+    const int offv = a.off[__builtin_amdgcn_readfirstlane(hd.y) + lk];
+    const unsigned long long mkv = masked ? a.mask[__builtin_amdgcn_readfirstlane(hd.w) + lk] : ~0ull;
+    // value pairs of this window: pair p of lane l (offsets 2p, 2p+1 of row l) at vp[p * 64 + l]
+    const v2d_t *__restrict__ vp = reinterpret_cast<const v2d_t *>(a.vt) + (size_t)__builtin_amdgcn_readfirstlane(hd.z) * 64;
+    const int KP = (K + 1) >> 1;
     const long long r0 = (long long)w * 64;
-    const bool masked = hd.w >= 0;
-    const unsigned long long *__restrict__ mk = a.mask + (masked ? hd.w : 0);
+    auto off_at = [&](int k) { return __builtin_amdgcn_readlane(offv, k); };
+    auto mask_at = [&](int k) {
+        const unsigned lo = __builtin_amdgcn_readlane((unsigned)mkv, k);
+        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(mkv >> 32), k);
+        return ((unsigned long long)hi << 32) | lo;
+    };
+    auto pair_at = [&](int p) { return dia_ld2<NT>(vp + (size_t)min(p, KP - 1) * 64 + lane); };
 
     if constexpr (L == 1) {
+        constexpr int U = 8;
         const long long r = r0 + lane;
         double acc = 0.0;
-        if (!masked) {  // every row of the window holds every offset: no selects, no clamps
-            for (int k0 = 0; k0 < K; k0 += U) {
-                double v[U], xv[U];
+        for (int k0 = 0; k0 < K; k0 += U) {
+            v2d_t v[U / 2];
+            double xv[U];
+            bool on[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int kk = min(k0 + u, K - 1);
-                    v[u] = dia_ld<NT>(vt + (size_t)kk * 64 + lane);
-                    xv[u] = a.x[r + off[kk]];
-                }
+            for (int u = 0; u < U / 2; ++u)
+                v[u] = pair_at((k0 >> 1) + u);
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (k0 + u < K)
-                        acc += v[u] * xv[u];
+            for (int u = 0; u < U; ++u) {
+                const int kk = min(k0 + u, K - 1);
+                on[u] = !masked || ((mask_at(kk) >> lane) & 1ull);
+                xv[u] = a.x[on[u] ? r + off_at(kk) : 0];
             }
-        } else {
-            for (int k0 = 0; k0 < K; k0 += U) {
-                double v[U], xv[U];
-                bool on[U];
+            // acc starts at +0.0 and never becomes -0.0, so adding +0.0 for an absent entry is the
+            // identity: the sum is the row's CSR-order sum bit for bit
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const int kk = min(k0 + u, K - 1);
-                    on[u] = (mk[kk] >> lane) & 1ull;
-                    v[u] = dia_ld<NT>(vt + (size_t)kk * 64 + lane);
-                    xv[u] = a.x[on[u] ? r + off[kk] : 0];
-                }
-                // acc starts at +0.0 and never becomes -0.0, so adding +0.0 for an absent entry is
-                // the identity: the sum is the row's CSR-order sum bit for bit
-#pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (k0 + u < K)
-                        acc += on[u] ? v[u] * xv[u] : 0.0;
-            }
+            for (int u = 0; u < U; ++u)
+                if (k0 + u < K)
+                    acc += on[u] ? (u & 1 ? v[u >> 1].y : v[u >> 1].x) * xv[u] : 0.0;
         }
         if (r < a.m)
             __builtin_nontemporal_store(acc, a.y + r);
-    } else if constexpr (FORM == 2 || FORM == 3) {
-        constexpr int GL = L / 2;
-        const long long r = r0 + lane;
-        double2 acc[GL];
-#pragma unroll
-        for (int j = 0; j < GL; ++j)
-            acc[j] = make_double2(0.0, 0.0);
-        for (int k0 = 0; k0 < K; k0 += U) {
-            double v[U];
-            double2 xv[U][GL];
-            bool on[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int kk = min(k0 + u, K - 1);
-                on[u] = masked ? ((mk[kk] >> lane) & 1ull) != 0 : true;
-                v[u] = dia_ld<NT>(vt + (size_t)kk * 64 + lane);
-                const double *xr = a.x + (on[u] ? r + off[kk] : 0) * a.ld;
-#pragma unroll
-                for (int j = 0; j < GL; ++j)
-                    xv[u][j] = *reinterpret_cast<const double2 *>(xr + 2 * j);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (k0 + u >= K)
-                    break;
-#pragma unroll
-                for (int j = 0; j < GL; ++j) {
-                    acc[j].x += on[u] ? v[u] * xv[u][j].x : 0.0;
-                    acc[j].y += on[u] ? v[u] * xv[u][j].y : 0.0;
-                }
-            }
-        }
-        if (r < a.m) {
-#pragma unroll
-            for (int j = 0; j < GL; ++j)
-                __builtin_nontemporal_store(v2d_t{acc[j].x, acc[j].y}, reinterpret_cast<v2d_t *>(a.y + r * a.ld + 2 * j));
-        }
     } else {
         constexpr int GL = L / 2;    // lanes per panel row
         constexpr int RS = 64 / GL;  // panel rows per wave instruction
+        constexpr int SPAN = 64 + kDiaRun - 1;
+        __shared__ v2d_t s_x[kDiaWaves][SPAN * GL];
+        v2d_t *sx = s_x[wv];
         const int c = lane % GL, rl = lane / GL;
         const double *__restrict__ xb = a.x + 2 * c;
-        double2 acc[GL];
+        const long long nmax = a.n - 1;
+        // run length from each offset k (lane k): consecutive offsets, <= kDiaRun, within the list
+        int runv = 1;
+        {
+            int step = 1;
 #pragma unroll
-        for (int q = 0; q < GL; ++q)
-            acc[q] = make_double2(0.0, 0.0);
-        for (int k0 = 0; k0 < K; k0 += U) {
-            double v[U][GL];
-            double2 xv[U][GL];
-            unsigned long long mw[U];
+            for (int j = 1; j < kDiaRun; ++j) {
+                const int nxt = __shfl_down(offv, j);
+                step = step && lane + j < K && nxt == offv + j;
+                runv += step;
+            }
+        }
+        v2d_t nx[GL], ne;
+        double nv[kDiaRun];
+        // offset k's value of row `lane`: one element of the pair panels (the L-wide products' values are a
+        // small part of their traffic; 8-B loads keep the run's values in registers without pair selects)
+        const double *__restrict__ vd = reinterpret_cast<const double *>(vp) + 2 * lane;
+        const size_t lrow = (size_t)rl * a.ld;  // this lane's first span row, as an element offset
+        auto fetch = [&](int k) {  // the run's panel span (clamped into X: rows outside it serve absent entries only)
+            const long long d0 = off_at(k);
+            const long long s0 = r0 + d0;  // the span's first row (wave-uniform)
+            if (s0 >= 0 && s0 + 64 + kDiaRun - 2 <= nmax) {  // inside X: a scalar base and per-lane constants
+                const double *sb = xb + s0 * a.ld;
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int kk = min(k0 + u, K - 1);
-                const long long d = off[kk];
-                mw[u] = masked ? mk[kk] : ~0ull;
-                double vl = 0.0;
-                if constexpr (FORM == 1)
-                    vl = dia_ld<NT>(vt + (size_t)kk * 64 + lane);
+                for (int q = 0; q < GL; ++q)
+                    nx[q] = *reinterpret_cast<const v2d_t *>(sb + lrow + (size_t)(RS * q) * a.ld);
+                ne = *reinterpret_cast<const v2d_t *>(sb + (size_t)(64 + min(rl, kDiaRun - 2)) * a.ld);
+            } else {
 #pragma unroll
                 for (int q = 0; q < GL; ++q) {
-                    const int row = rl + RS * q;
-                    if constexpr (FORM == 1)
-                        v[u][q] = __shfl(vl, row);
-                    else
-                        v[u][q] = dia_ld<NT>(vt + (size_t)kk * 64 + row);
-                    const long long xr = ((mw[u] >> row) & 1ull) ? r0 + row + d : 0;
-                    xv[u][q] = *reinterpret_cast<const double2 *>(xb + xr * a.ld);
+                    const long long xr = min(max(s0 + rl + RS * q, 0LL), nmax);
+                    nx[q] = *reinterpret_cast<const v2d_t *>(xb + xr * a.ld);
                 }
+                const long long xe = min(max(s0 + 64 + min(rl, kDiaRun - 2), 0LL), nmax);
+                ne = *reinterpret_cast<const v2d_t *>(xb + xe * a.ld);
             }
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (k0 + u >= K)
-                    break;
+            for (int j = 0; j < kDiaRun; ++j) {
+                const int kk = min(k + j, K - 1);
+                nv[j] = dia_ld<NT>(vd + (size_t)(kk >> 1) * 128 + (kk & 1));
+            }
+        };
+        // Lanes read panel rows other lanes of the wave wrote.  The hardware runs a wave's DS operations in
+        // order; the compiler, reasoning per lane, could move a read of another lane's row above the write
+        // (or the next run's writes above this run's reads): wave-scope fences around the hand-off.
+        auto wave_sync = [] {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        };
+        v2d_t acc[GL];
 #pragma unroll
-                for (int q = 0; q < GL; ++q) {
-                    const bool on = (mw[u] >> (rl + RS * q)) & 1ull;
-                    acc[q].x += on ? v[u][q] * xv[u][q].x : 0.0;
-                    acc[q].y += on ? v[u][q] * xv[u][q].y : 0.0;
+        for (int q = 0; q < GL; ++q)
+            acc[q] = v2d_t{0.0, 0.0};
+        fetch(0);
+        for (int k = 0; k < K;) {
+            wave_sync();
+#pragma unroll
+            for (int q = 0; q < GL; ++q)
+                sx[(rl + RS * q) * GL + c] = nx[q];
+            if (rl < kDiaRun - 1)
+                sx[(64 + rl) * GL + c] = ne;
+            wave_sync();
+            double cv[kDiaRun];
+#pragma unroll
+            for (int j = 0; j < kDiaRun; ++j)
+                cv[j] = nv[j];
+            const int gk = __builtin_amdgcn_readlane(runv, k), kc = k;
+            k += gk;
+            if (k < K)  // the next run's loads fly while this one is summed
+                fetch(k);
+#pragma unroll
+            for (int j = 0; j < kDiaRun; ++j) {
+                if (j >= gk)
+                    break;
+                const unsigned long long mw = masked ? mask_at(kc + j) : ~0ull;
+                if (mw == ~0ull) {  // every row holds this offset (wave-uniform): no selects
+#pragma unroll
+                    for (int q = 0; q < GL; ++q) {
+                        const int row = rl + RS * q;
+                        const double v = __shfl(cv[j], row);
+                        const v2d_t xv = sx[(row + j) * GL + c];
+                        acc[q].x += v * xv.x;
+                        acc[q].y += v * xv.y;
+                    }
+                } else {
+#pragma unroll
+                    for (int q = 0; q < GL; ++q) {
+                        const int row = rl + RS * q;
+                        const double v = __shfl(cv[j], row);
+                        const v2d_t xv = sx[(row + j) * GL + c];
+                        const bool on = (mw >> row) & 1ull;
+                        acc[q].x += on ? v * xv.x : 0.0;
+                        acc[q].y += on ? v * xv.y : 0.0;
+                    }
                 }
             }
         }
@@ -211,8 +250,7 @@ __global__ __launch_bounds__(kDiaThreads) void k_spmm_dia(DiaArgs a)
         for (int q = 0; q < GL; ++q) {
             const long long r = r0 + rl + RS * q;
             if (r < a.m)
-                __builtin_nontemporal_store(v2d_t{acc[q].x, acc[q].y},
-                                            reinterpret_cast<v2d_t *>(a.y + r * a.ld + 2 * c));
+                __builtin_nontemporal_store(acc[q], reinterpret_cast<v2d_t *>(a.y + r * a.ld + 2 * c));
         }
     }
 }
@@ -239,7 +277,7 @@ __global__ __launch_bounds__(kDiaThreads) void k_dia_fill(const int *__restrict_
         while (k < hd.x && D[k] < d)
             ++k;
         if (k < hd.x)
-            vt[((size_t)hd.z + k) * 64 + lane] = vals[j];
+            vt[((size_t)hd.z + (k >> 1)) * 128 + 2 * lane + (k & 1)] = vals[j];
         ++k;
     }
 }
@@ -279,24 +317,25 @@ static mspmv_status dia_upload(T **d, const std::vector<T> &hsrc)
     return MSPMV_OK;
 }
 
-mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, double min_window_fill)
+// The planning itself, on host arrays (build_dia_plan after downloading them; mspmv_offset_windows for
+// inspection).  false: the plan does not hold.
+struct DiaHostPlan {
+    int windows = 0, max_k = 0, masked = 0;
+    long long sum_k = 0, sum_pairs = 0;
+    std::vector<int> kw;                     // [windows] K
+    std::vector<int4> hdr;                   // [windows] {K, offset base, pair panel base, mask base or -1}
+    std::vector<int> offs;                   // [sum_k]
+    std::vector<unsigned long long> masks;   // [K of the masked windows]
+};
+
+static bool dia_plan_host(const int *ro, const int *ci, int m, long long nnz, double min_fill, double min_window_fill,
+                          DiaHostPlan &out)
 {
-    const int m = h->m;
-    if (m <= 0 || h->nnz <= 0)
-        return MSPMV_ERR_UNSUPPORTED;
-    std::vector<int> ro((size_t)m + 1);
-    if (hipMemcpy(ro.data(), h->d_row_offsets, sizeof(int) * ro.size(), hipMemcpyDeviceToHost) != hipSuccess) {
-        set_error("offset-window plan: row offsets download failed");
-        return MSPMV_ERR_HIP;
-    }
+    if (m <= 0 || nnz <= 0)
+        return false;
     for (int r = 0; r < m; ++r)  // a row longer than the list: no window can hold it
-        if (ro[(size_t)r + 1] - ro[(size_t)r] > kDiaMaxK)
-            return MSPMV_ERR_UNSUPPORTED;
-    std::vector<int> ci((size_t)h->nnz);
-    if (hipMemcpy(ci.data(), h->d_cols, sizeof(int) * ci.size(), hipMemcpyDeviceToHost) != hipSuccess) {
-        set_error("offset-window plan: column download failed");
-        return MSPMV_ERR_HIP;
-    }
+        if (ro[r + 1] - ro[r] > kDiaMaxK)
+            return false;
     const int W = (m + 63) / 64;
     std::vector<int> kw((size_t)W, 0), dl((size_t)W * kDiaMaxK, 0);
     std::vector<unsigned char> full((size_t)W, 0);
@@ -307,12 +346,12 @@ mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, dou
             continue;
         const int r0 = w * 64, r1 = std::min(m, r0 + 64);
         std::vector<int> d;
-        d.reserve((size_t)(ro[(size_t)r1] - ro[(size_t)r0]));
+        d.reserve((size_t)(ro[r1] - ro[r0]));
         bool ok = true;
         for (int r = r0; r < r1 && ok; ++r) {
             long long prev = -(1LL << 40);
-            for (int j = ro[(size_t)r]; j < ro[(size_t)r + 1]; ++j) {
-                const long long o = (long long)ci[(size_t)j] - r;
+            for (int j = ro[r]; j < ro[r + 1]; ++j) {
+                const long long o = (long long)ci[j] - r;
                 if (o <= prev) {  // columns not strictly ascending: the D order would not be the CSR order
                     ok = false;
                     break;
@@ -325,7 +364,7 @@ mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, dou
             std::sort(d.begin(), d.end());
             d.erase(std::unique(d.begin(), d.end()), d.end());
             const int K = (int)d.size();
-            const long long nz = ro[(size_t)r1] - ro[(size_t)r0];
+            const long long nz = ro[r1] - ro[r0];
             ok = K >= 1 && K <= kDiaMaxK && (double)nz >= min_window_fill * (double)(r1 - r0) * K;
             if (ok) {
                 kw[(size_t)w] = K;
@@ -337,25 +376,34 @@ mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, dou
             bad = 1;
     }
     if (bad)
-        return MSPMV_ERR_UNSUPPORTED;
+        return false;
     long long sumk = 0, summ = 0;
     for (int w = 0; w < W; ++w)
         sumk += kw[(size_t)w];
-    if (sumk > 0x7fffffffLL || (double)h->nnz < min_fill * 64.0 * (double)sumk)
-        return MSPMV_ERR_UNSUPPORTED;  // the panels would stream too many zeros overall
-    std::vector<int4> hdr((size_t)W);
-    std::vector<int> offs;
-    offs.reserve((size_t)sumk);
+    if (sumk > 0x7fffffffLL || (double)nnz < min_fill * 64.0 * (double)sumk)
+        return false;  // the panels would stream too many zeros overall
+    out.hdr.assign((size_t)W, make_int4(0, 0, 0, 0));
+    out.offs.clear();
+    out.offs.reserve((size_t)sumk);
     sumk = 0;
+    long long sump = 0;  // value pair panels (64 x 16 B): (K + 1) / 2 per window
     for (int w = 0; w < W; ++w) {
         const int K = kw[(size_t)w];
-        hdr[(size_t)w] = make_int4(K, (int)sumk, (int)sumk, full[(size_t)w] ? -1 : (int)summ);
-        offs.insert(offs.end(), dl.begin() + (size_t)w * kDiaMaxK, dl.begin() + (size_t)w * kDiaMaxK + K);
+        if (sump > 0x7fffffffLL / 64)
+            return false;
+        out.hdr[(size_t)w] = make_int4(K, (int)sumk, (int)sump, full[(size_t)w] ? -1 : (int)summ);
+        sump += (K + 1) / 2;
+        out.offs.insert(out.offs.end(), dl.begin() + (size_t)w * kDiaMaxK, dl.begin() + (size_t)w * kDiaMaxK + K);
         sumk += K;
         if (!full[(size_t)w])
             summ += K;
+        out.max_k = std::max(out.max_k, K);
+        out.masked += !full[(size_t)w];
     }
-    std::vector<unsigned long long> masks((size_t)summ, 0ull);
+    out.masks.assign((size_t)summ, 0ull);
+    const std::vector<int4> &hdr = out.hdr;
+    const std::vector<int> &offs = out.offs;
+    std::vector<unsigned long long> &masks = out.masks;
 #pragma omp parallel for schedule(static)
     for (int w = 0; w < W; ++w) {
         const int4 hd = hdr[(size_t)w];
@@ -365,8 +413,8 @@ mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, dou
         const int r0 = w * 64, r1 = std::min(m, r0 + 64);
         for (int r = r0; r < r1; ++r) {
             int k = 0;
-            for (int j = ro[(size_t)r]; j < ro[(size_t)r + 1]; ++j) {
-                const int o = ci[(size_t)j] - r;
+            for (int j = ro[r]; j < ro[r + 1]; ++j) {
+                const int o = ci[j] - r;
                 while (D[k] < o)
                     ++k;
                 masks[(size_t)hd.w + k] |= 1ull << (r - r0);
@@ -374,26 +422,57 @@ mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, dou
             }
         }
     }
+    out.windows = W;
+    out.sum_k = sumk;
+    out.sum_pairs = sump;
+    out.kw = std::move(kw);
+    return true;
+}
+
+mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, double min_window_fill)
+{
+    const int m = h->m;
+    if (m <= 0 || h->nnz <= 0)
+        return MSPMV_ERR_UNSUPPORTED;
+    std::vector<int> ro((size_t)m + 1);
+    if (hipMemcpy(ro.data(), h->d_row_offsets, sizeof(int) * ro.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error("offset-window plan: row offsets download failed");
+        return MSPMV_ERR_HIP;
+    }
+    for (int r = 0; r < m; ++r)  // the cheap precheck before the columns are copied: rows too long
+        if (ro[(size_t)r + 1] - ro[(size_t)r] > kDiaMaxK)
+            return MSPMV_ERR_UNSUPPORTED;
+    std::vector<int> ci((size_t)h->nnz);
+    if (hipMemcpy(ci.data(), h->d_cols, sizeof(int) * ci.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error("offset-window plan: column download failed");
+        return MSPMV_ERR_HIP;
+    }
+    DiaHostPlan hp;
+    if (!dia_plan_host(ro.data(), ci.data(), m, h->nnz, min_fill, min_window_fill, hp))
+        return MSPMV_ERR_UNSUPPORTED;
+    const int W = hp.windows;
+    const std::vector<int4> &hdr = hp.hdr;
+    const std::vector<int> &offs = hp.offs;
+    const std::vector<unsigned long long> &masks = hp.masks;
+    const long long sumk = hp.sum_k, sump = hp.sum_pairs;
     auto *dd = new DiaData();
     p.dia = dd;
     dd->windows = W;
     dd->sum_k = sumk;
-    dd->masked_windows = 0;
-    for (int w = 0; w < W; ++w) {
-        dd->max_k = std::max(dd->max_k, kw[(size_t)w]);
-        dd->masked_windows += !full[(size_t)w];
-    }
+    dd->sum_pairs = sump;
+    dd->masked_windows = hp.masked;
+    dd->max_k = hp.max_k;
     dd->fill = (double)h->nnz / (64.0 * (double)sumk);
     mspmv_status st;
     if ((st = dia_upload(&dd->d_hdr, hdr)) != MSPMV_OK || (st = dia_upload(&dd->d_off, offs)) != MSPMV_OK ||
         (st = dia_upload(&dd->d_mask, masks)) != MSPMV_OK)
         return st;
-    if (hipMalloc((void **)&dd->d_vt, sizeof(double) * 64 * (size_t)sumk) != hipSuccess) {
+    if (hipMalloc((void **)&dd->d_vt, sizeof(double) * 128 * (size_t)sump) != hipSuccess) {
         dd->d_vt = nullptr;
         set_error("offset-window plan: value panel allocation failed");
         return MSPMV_ERR_OOM;
     }
-    hipError_t e = hipMemsetAsync(dd->d_vt, 0, sizeof(double) * 64 * (size_t)sumk, h->stream);
+    hipError_t e = hipMemsetAsync(dd->d_vt, 0, sizeof(double) * 128 * (size_t)sump, h->stream);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_dia_fill, dim3((unsigned)((W + kDiaWaves - 1) / kDiaWaves)), dim3(kDiaThreads), 0,
                            h->stream, h->d_row_offsets, h->d_cols, h->d_vals, dd->d_hdr, dd->d_off, W, m, dd->d_vt);
@@ -433,39 +512,14 @@ mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, dou
     return MSPMV_OK;
 }
 
-static int dia_form()
-{
-    static const int f = [] {
-        const char *e = getenv("MSPMV_DIA_FORM");
-        return e && *e ? atoi(e) : 1;
-    }();
-    return f;
-}
-
-template <int L, int FORM>
-static void dia_launch_form(const DiaArgs &a, hipStream_t s, bool nt)
-{
-    const dim3 grid((unsigned)a.groups), block(kDiaThreads);
-    if (nt)
-        hipLaunchKernelGGL((k_spmm_dia<L, true, FORM>), grid, block, 0, s, a);
-    else
-        hipLaunchKernelGGL((k_spmm_dia<L, false, FORM>), grid, block, 0, s, a);
-}
-
 template <int L>
 static void dia_launch_L(const DiaArgs &a, hipStream_t s, bool nt)
 {
-    if constexpr (L == 1) {
-        dia_launch_form<1, 0>(a, s, nt);
-    } else {
-        switch (dia_form()) {
-        case 1: dia_launch_form<L, 1>(a, s, nt); break;
-        case 2: dia_launch_form<L, 2>(a, s, nt); break;
-        case 3: dia_launch_form<L, 3>(a, s, nt); break;
-        case 4: dia_launch_form<L, 4>(a, s, nt); break;
-        default: dia_launch_form<L, 0>(a, s, nt); break;
-        }
-    }
+    const dim3 grid((unsigned)a.groups), block(kDiaThreads);
+    if (nt)
+        hipLaunchKernelGGL((k_spmm_dia<L, true>), grid, block, 0, s, a);
+    else
+        hipLaunchKernelGGL((k_spmm_dia<L, false>), grid, block, 0, s, a);
 }
 
 hipError_t launch_dia(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L, int ld,
@@ -487,6 +541,7 @@ hipError_t launch_dia(mspmv_handle_s *h, const TilePlan &plan, const double *d_X
     a.windows = dd->windows;
     a.groups = (dd->windows + kDiaWaves - 1) / kDiaWaves;
     a.m = h->m;
+    a.n = h->n;
     a.ld = ld > 0 ? ld : L;
     const bool nt = stream_nt(h);
     switch (L) {
@@ -502,8 +557,46 @@ hipError_t launch_dia(mspmv_handle_s *h, const TilePlan &plan, const double *d_X
 
 std::string dia_kernel_name(const mspmv_handle_s *h, int L)
 {
-    const int f = L == 1 ? 0 : dia_form();
-    return "k_spmm_dia<" + std::to_string(L) + "," + (stream_nt(h) ? "true" : "false") + "," + std::to_string(f) + ">";
+    return "k_spmm_dia<" + std::to_string(L) + "," + (stream_nt(h) ? "true" : "false") + ">";
 }
 
 }  // namespace mspmv
+
+extern "C" mspmv_status mspmv_offset_windows(const mspmv_csr_d *a, double min_fill, double min_window_fill, int *ok,
+                                            int *num_windows, long long *sum_offsets, int *masked_windows,
+                                            int *k_per_window)
+{
+    using namespace mspmv;
+    if (!a || !ok || a->num_rows < 0 || a->num_cols < 0 || a->num_nonzeros < 0 || !a->row_offsets ||
+        (a->num_nonzeros > 0 && !a->column_indices)) {
+        set_error("offset_windows: bad matrix or null output");
+        return MSPMV_ERR_INVALID;
+    }
+    const int m = a->num_rows;
+    const int *ro = a->row_offsets;
+    if (ro[0] != 0 || ro[m] != a->num_nonzeros) {
+        set_error("offset_windows: row offsets must run from 0 to num_nonzeros");
+        return MSPMV_ERR_INVALID;
+    }
+    for (int r = 0; r < m; ++r)
+        if (ro[r + 1] < ro[r]) {
+            set_error("offset_windows: row offsets not monotone");
+            return MSPMV_ERR_INVALID;
+        }
+    for (long long j = 0; j < a->num_nonzeros; ++j)
+        if (a->column_indices[j] < 0 || a->column_indices[j] >= a->num_cols) {
+            set_error("offset_windows: column index out of range");
+            return MSPMV_ERR_INVALID;
+        }
+    DiaHostPlan hp;
+    *ok = dia_plan_host(ro, a->column_indices, m, a->num_nonzeros, min_fill, min_window_fill, hp) ? 1 : 0;
+    if (num_windows)
+        *num_windows = *ok ? hp.windows : 0;
+    if (sum_offsets)
+        *sum_offsets = *ok ? hp.sum_k : 0;
+    if (masked_windows)
+        *masked_windows = *ok ? hp.masked : 0;
+    if (k_per_window && *ok)
+        std::copy(hp.kw.begin(), hp.kw.end(), k_per_window);
+    return MSPMV_OK;
+}

@@ -69,12 +69,13 @@ struct DiaData {
     int windows = 0;
     int max_k = 0;
     int masked_windows = 0;                  // windows with a row missing some offset (presence masks)
-    long long sum_k = 0;                     // value panels of 64 doubles
+    long long sum_k = 0;                     // offsets over the windows
+    long long sum_pairs = 0;                 // value pair panels: (K + 1) / 2 per window
     double fill = 0.0;                       // nonzeros / (64 sum_k)
-    int4 *d_hdr = nullptr;                   // [windows] {K, offset base, value base, mask base or -1}
+    int4 *d_hdr = nullptr;                   // [windows] {K, offset base, pair panel base, mask base or -1}
     int *d_off = nullptr;                    // [sum_k]
     unsigned long long *d_mask = nullptr;    // [K of the masked windows]
-    double *d_vt = nullptr;                  // [sum_k][64]
+    double *d_vt = nullptr;                  // [sum_pairs][64 lanes][2]: offsets 2p, 2p+1 of each row
 };
 
 // A merge-path tile plan for one nominal tile size (merge items per tile).
@@ -289,7 +290,7 @@ void free_dia(DiaData *d);
 hipError_t launch_dia(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L, int ld,
                       const CgControl *ctrl);
 std::string dia_kernel_name(const mspmv_handle_s *h, int L);
-bool dia_spmm_enabled();  // MSPMV_DIA_SPMM=1: the L-wide products on the windows too (mspmv_api.hip)
+bool dia_spmm_enabled();  // the L-wide products on the windows too unless MSPMV_DIA_SPMM=0 (mspmv_api.hip)
 
 // ---- launchers (mspmv_kernels.hip) --------------------------------------------------
 void set_error(const std::string &msg);

@@ -112,6 +112,7 @@ _SIGS = {
     "mspmv_plan_block_tiles": (_I, [_P, _I, _PI]),
     "mspmv_tile_modes": (_I, [_P, _I, _P]),
     "mspmv_tile_lanes": (_I, [_P, _I, _PI]),
+    "mspmv_offset_windows": (_I, [ctypes.POINTER(_CsrD), _D, _D, _PI, _PI, ctypes.POINTER(ctypes.c_longlong), _PI, _P]),
     "mspmv_spmv_kernel_name": (ctypes.c_char_p, [_P]),
     "mspmv_spmm_kernel_name": (ctypes.c_char_p, [_P, _I]),
     "mspmv_cg_kernel_name": (ctypes.c_char_p, [_P]),
@@ -620,6 +621,20 @@ def pcg_ic0(g: "GpuCsr", ic: GpuIc0, B: np.ndarray, max_iters: int, tolerance: f
                                   _ptr(hist) if hist_cap else None, hist_cap)
     _check(st, "dpcg_ic0_multi", allow=(4,))
     return X, it.value, hist[: min(it.value, hist_cap)], st
+
+
+def offset_windows(a: CsrMatrix, min_fill: float = 0.85, min_window_fill: float = 0.3):
+    """Host-side offset-window planning (mspmv_offset_windows; no device): None when the matrix does
+    not fit the plan, else {"windows", "sum_offsets", "masked_windows", "k"} (k: offsets per 64-row
+    window).  The library's automatic choice uses the default thresholds."""
+    ok, nw, mw = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    sk = ctypes.c_longlong()
+    k = np.zeros(max((a.num_rows + 63) // 64, 1), np.int32)
+    _check(lib.mspmv_offset_windows(ctypes.byref(a._c()), min_fill, min_window_fill, ctypes.byref(ok), ctypes.byref(nw),
+                                    ctypes.byref(sk), ctypes.byref(mw), _ptr(k)), "offset_windows")
+    if not ok.value:
+        return None
+    return {"windows": nw.value, "sum_offsets": sk.value, "masked_windows": mw.value, "k": k[: nw.value]}
 
 
 def spai_values(a: CsrMatrix) -> np.ndarray:

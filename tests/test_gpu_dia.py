@@ -7,9 +7,9 @@ add, so every row -- and every column of an SpMM -- is bit-identical to the orac
 demands exactly that.  Shapes: 27-point and 2-D stencils (the nlpkkt120 and parabolic_fem shapes,
 windows straddling grid lines: presence masks), a tridiagonal band (every window full), a partial last
 window, rectangular panels, empty rows and rows missing offsets (forced with MSPMV_DIA=1), an x holding
-inf where no row reads it.  The L-wide products take the windows only with MSPMV_DIA_SPMM=1 (the tiles
-measured faster at L = 8 on the 27-point shape, r05q); with it the block CG runs its SpMM on the
-windows and is held to the oracle's CGSolveMultiple (no_pretreatment.hpp:32-197) like the tile path.
+inf where no row reads it.  The L-wide products take the windows too (MSPMV_DIA_SPMM=0 opts them out),
+and the block CG runs its SpMM on the windows, held to the oracle's CGSolveMultiple
+(no_pretreatment.hpp:32-197) like the tile path.
 """
 import numpy as np
 import pytest
@@ -30,7 +30,7 @@ def _need_gpu(gpu_available):
 @pytest.fixture(autouse=True)
 def _windows_every_width(monkeypatch):
     monkeypatch.delenv("MSPMV_DIA", raising=False)
-    monkeypatch.setenv("MSPMV_DIA_SPMM", "1")
+    monkeypatch.delenv("MSPMV_DIA_SPMM", raising=False)
 
 
 def band(m, offsets, seed, n=None, drop=0.0):
@@ -206,7 +206,7 @@ def test_dia_default_choice(monkeypatch):
         with mspmv.GpuCsr(make()) as g:
             for L in (1, 8):
                 assert g.spmm_kernel_name(L).startswith("k_spmm_dia<") == dia, (name, L, g.spmm_kernel_name(L))
-    monkeypatch.delenv("MSPMV_DIA_SPMM")  # by default only the single-RHS product takes the windows
+    monkeypatch.setenv("MSPMV_DIA_SPMM", "0")  # the L-wide products opted out: only the SpMV takes the windows
     with mspmv.GpuCsr(CASES["stencil27"]()) as g:
         assert g.kernel_name().startswith("k_spmm_dia<1,")
         assert not g.spmm_kernel_name(8).startswith("k_spmm_dia<")

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Offset windows vs tiles (run under MSPMV_DIA=0 / unset): kernel times by HIP events on the
 structured-grid shapes -- the nlpkkt120-size 27-point matrix (L = 1 and 8, never cache-resident) and
-the parabolic_fem shape (L = 1 and 8, cold after a 512 MiB flush) -- and the kernel each ran.
+the parabolic_fem shape (L = 1 and 8, cold after a 512 MiB flush) -- and the kernel each ran; PROBE_L
+lists other widths.
 One JSON line."""
 import json
 import os
@@ -25,7 +26,7 @@ for name, (make, flush) in shapes.items():
         continue
     a = make()
     with mspmv.GpuCsr(a) as g:
-        for L in (1, 8):
+        for L in [int(v) for v in os.environ.get("PROBE_L", "1 8").split()]:
             X = np.random.default_rng(3).uniform(0, 1, (a.num_cols, L))
             dX = mspmv.DeviceBuffer.from_array(X)
             dY = mspmv.DeviceBuffer(8 * a.num_rows * L)
