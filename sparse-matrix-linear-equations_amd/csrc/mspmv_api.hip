@@ -762,6 +762,7 @@ static mspmv_status spmv_plan(mspmv_handle_s *h, const TilePlan **out)
 
 namespace mspmv {
 mspmv_status plan_for(mspmv_handle_s *h, int L, const TilePlan **out) { return get_plan(h, L, out); }
+mspmv_status dia_plan_for(mspmv_handle_s *h, int L, const TilePlan **out) { return dia_plan(h, out, L); }
 }  // namespace mspmv
 
 static mspmv_status validate_host_csr(const mspmv_csr_d *a)
@@ -1444,7 +1445,10 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
     bool stalled = false;
     const int nblk = pipelined ? cg1_blocks(h->m) : cg_update_blocks((long long)h->m * L, h->num_cus);
     const int cap = hist ? std::max(hist_cap, 0) : 0;
-    ST_TRY(ensure_cg_workspace(h, L, nblk, std::max(plan->num_tiles, mplan ? mplan->num_tiles : 0), cap));
+    // partials: one per tile of the plan, or per window of the offset-window plan (its dot mode)
+    ST_TRY(ensure_cg_workspace(h, L, nblk,
+                               std::max({plan->num_tiles, mplan ? mplan->num_tiles : 0, splan ? splan->num_tiles : 0}),
+                               cap));
     const int use_cap = hist ? cap : 0;
     if (pipelined) {
         // the whole solve as one register-resident launch, where the matrix fits (mspmv_cg_resident.hip)

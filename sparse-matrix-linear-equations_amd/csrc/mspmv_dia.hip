@@ -45,6 +45,8 @@ struct DiaArgs {
     const double *x;
     double *y;
     const CgControl *ctrl;           // CG: return at once when ctrl->done
+    double *partials;                // dot mode: x.(A x) per column per window, [windows][L] (launch_fold_dot)
+    const double *xr;                // dot mode: x at this matrix's rows (x + row_off * ld for a row-range view)
     int windows;
     int groups;                      // workgroups (windows / 4, rounded up)
     int m;
@@ -86,7 +88,10 @@ __device__ __forceinline__ v2d_t dia_ld2(const v2d_t *p)
 // run is summed.  A row's value for offset k comes from the lane holding the row (lane = row) by a
 // shuffle.  nlpkkt120 size, L = 8 (r05q-r05t): 369-374 us against 440 on the
 // merge tiles; gathering every offset's rows directly (no LDS) 460-497 us, one row per lane 586 us.
-template <int L, bool NT>
+// DOT (the block CG's SpMM): each window also writes its rows' x.(A x) per column to a.partials (the x
+// rows reloaded after the products -- they were staged moments before, cache hits), summed by
+// launch_fold_dot, which replaces the separate p.Ap pass (k_pcg_dot) over p and Ap.
+template <int L, bool NT, bool DOT = false>
 __global__ __launch_bounds__(kDiaThreads) void k_spmm_dia(DiaArgs a)
 {
     const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -140,6 +145,14 @@ __global__ __launch_bounds__(kDiaThreads) void k_spmm_dia(DiaArgs a)
         }
         if (r < a.m)
             __builtin_nontemporal_store(acc, a.y + r);
+        if constexpr (DOT) {
+            double d = r < a.m ? a.xr[r] * acc : 0.0;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1)
+                d += __shfl_xor(d, off);
+            if (lane == 0)
+                a.partials[w] = d;
+        }
     } else {
         constexpr int GL = L / 2;    // lanes per panel row
         constexpr int RS = 64 / GL;  // panel rows per wave instruction
@@ -251,6 +264,25 @@ __global__ __launch_bounds__(kDiaThreads) void k_spmm_dia(DiaArgs a)
             const long long r = r0 + rl + RS * q;
             if (r < a.m)
                 __builtin_nontemporal_store(acc[q], reinterpret_cast<v2d_t *>(a.y + r * a.ld + 2 * c));
+        }
+        if constexpr (DOT) {  // column pair c: the lane's rows in q order, then the wave's rows by a fixed butterfly
+            v2d_t d = v2d_t{0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < GL; ++q) {
+                const long long r = r0 + rl + RS * q;
+                if (r < a.m) {
+                    const v2d_t xv = *reinterpret_cast<const v2d_t *>(a.xr + 2 * c + r * a.ld);
+                    d.x += xv.x * acc[q].x;
+                    d.y += xv.y * acc[q].y;
+                }
+            }
+#pragma unroll
+            for (int off = 32; off >= GL; off >>= 1) {
+                d.x += __shfl_xor(d.x, off);
+                d.y += __shfl_xor(d.y, off);
+            }
+            if (rl == 0)
+                *reinterpret_cast<v2d_t *>(a.partials + (size_t)w * L + 2 * c) = d;
         }
     }
 }
@@ -516,14 +548,20 @@ template <int L>
 static void dia_launch_L(const DiaArgs &a, hipStream_t s, bool nt)
 {
     const dim3 grid((unsigned)a.groups), block(kDiaThreads);
-    if (nt)
+    if (a.partials) {
+        if (nt)
+            hipLaunchKernelGGL((k_spmm_dia<L, true, true>), grid, block, 0, s, a);
+        else
+            hipLaunchKernelGGL((k_spmm_dia<L, false, true>), grid, block, 0, s, a);
+    } else if (nt) {
         hipLaunchKernelGGL((k_spmm_dia<L, true>), grid, block, 0, s, a);
-    else
+    } else {
         hipLaunchKernelGGL((k_spmm_dia<L, false>), grid, block, 0, s, a);
+    }
 }
 
 hipError_t launch_dia(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L, int ld,
-                      const CgControl *ctrl)
+                      const CgControl *ctrl, double *partials, long long row_off, hipStream_t stream)
 {
     const DiaData *dd = plan.dia;
     if (!dd)
@@ -538,18 +576,21 @@ hipError_t launch_dia(mspmv_handle_s *h, const TilePlan &plan, const double *d_X
     a.x = d_X;
     a.y = d_Y;
     a.ctrl = ctrl;
+    a.partials = partials;
     a.windows = dd->windows;
+    a.xr = d_X + row_off * (ld > 0 ? ld : L);
     a.groups = (dd->windows + kDiaWaves - 1) / kDiaWaves;
     a.m = h->m;
     a.n = h->n;
     a.ld = ld > 0 ? ld : L;
     const bool nt = stream_nt(h);
+    hipStream_t s = stream ? stream : h->stream;
     switch (L) {
-    case 1: dia_launch_L<1>(a, h->stream, nt); break;
-    case 2: dia_launch_L<2>(a, h->stream, nt); break;
-    case 4: dia_launch_L<4>(a, h->stream, nt); break;
-    case 8: dia_launch_L<8>(a, h->stream, nt); break;
-    case 16: dia_launch_L<16>(a, h->stream, nt); break;
+    case 1: dia_launch_L<1>(a, s, nt); break;
+    case 2: dia_launch_L<2>(a, s, nt); break;
+    case 4: dia_launch_L<4>(a, s, nt); break;
+    case 8: dia_launch_L<8>(a, s, nt); break;
+    case 16: dia_launch_L<16>(a, s, nt); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -746,13 +746,21 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
     // each part's dot-mode tiles write their p.Ap partials at the part's offset, one fold sums
     // the three in tile order
     const TilePlan *pp[3] = {nullptr, nullptr, nullptr};
+    // offset windows (mspmv_dia.hip) where the rows take them -- the unsplit local rows, or a part whose
+    // columns keep a constant offset from its rows (the interior: owned columns only); their dot mode
+    // writes one p.Ap partial per window into the same fold (MSPMV_DIA_DOT=0: tiles everywhere)
+    const TilePlan *dlocal = nullptr, *dpart[3] = {nullptr, nullptr, nullptr};
     int toff[4] = {0, 0, 0, 0};
     const bool split = d->part[1] != nullptr;
+    if (dia_dot_fused() && !split)
+        D_ST(dia_plan_for(d->local, L, &dlocal));
     for (int q = 0; q < 3 && split; ++q) {
         D_ST(plan_for(d->part[q], L, &pp[q]));
-        toff[q + 1] = toff[q] + pp[q]->num_tiles;
+        if (dia_dot_fused())
+            D_ST(dia_plan_for(d->part[q], L, &dpart[q]));
+        toff[q + 1] = toff[q] + (dpart[q] ? dpart[q]->num_tiles : pp[q]->num_tiles);
     }
-    D_ST(ensure_buffers(d, L, nblk, std::max(plan->num_tiles, toff[3]), cap));
+    D_ST(ensure_buffers(d, L, nblk, std::max({plan->num_tiles, dlocal ? dlocal->num_tiles : 0, toff[3]}), cap));
     hipStream_t s = d->local->stream;
     DistVecArgs va{};
     va.n_elems = elems;
@@ -786,21 +794,31 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
         D_HIP(launch_dist_vec_mirror(2, a, L, nblk, d->d_pext, s));       // p = r + beta p
         if (!split) {
             D_ST(halo_exchange(d, L, d->d_ctrl));                           // p halo rows
-            D_HIP(launch_spmm_dot(d->local, *plan, d->d_pext, d->d_ap, L, d->d_ctrl, d->d_partials, d->d_gtickets,
-                                  pAp));
+            if (dlocal) {
+                D_HIP(launch_dia(d->local, *dlocal, d->d_pext, d->d_ap, L, L, d->d_ctrl, d->d_partials));
+                D_HIP(launch_fold_dot(dlocal->num_tiles, L, d->d_partials, d->d_gtickets, pAp, nullptr, nullptr,
+                                      d->d_ctrl, -1, s));
+            } else {
+                D_HIP(launch_spmm_dot(d->local, *plan, d->d_pext, d->d_ap, L, d->d_ctrl, d->d_partials, d->d_gtickets,
+                                      pAp));
+            }
         } else {
+            const int rofs[3] = {0, d->int_lo, d->int_hi};
+            auto part_dot = [&](int q, hipStream_t st) -> hipError_t {
+                double *ap = d->d_ap + (size_t)rofs[q] * L, *part = d->d_partials + (size_t)toff[q] * L;
+                return dpart[q] ? launch_dia(d->part[q], *dpart[q], d->d_pext, ap, L, L, d->d_ctrl, part, rofs[q], st)
+                                : launch_spmm_dot_tiles(d->part[q], *pp[q], d->d_pext, ap, L, d->d_ctrl, part, st,
+                                                        rofs[q]);
+            };
             // the interior (owned columns only) on its own stream beside the exchange
             mspmv_handle mid = d->part[1];
             D_HIP(hipEventRecord(d->ev[0], s));
             D_HIP(hipStreamWaitEvent(mid->stream, d->ev[0], 0));
-            D_HIP(launch_spmm_dot_tiles(mid, *pp[1], d->d_pext, d->d_ap + (size_t)d->int_lo * L, L, d->d_ctrl,
-                                        d->d_partials + (size_t)toff[1] * L, mid->stream, d->int_lo));
+            D_HIP(part_dot(1, mid->stream));
             D_HIP(hipEventRecord(d->ev[1], mid->stream));
             D_ST(halo_exchange(d, L, d->d_ctrl));                           // p halo rows
-            const int rofs[3] = {0, d->int_lo, d->int_hi};
             for (int q = 0; q < 3; q += 2)
-                D_HIP(launch_spmm_dot_tiles(d->part[q], *pp[q], d->d_pext, d->d_ap + (size_t)rofs[q] * L, L,
-                                            d->d_ctrl, d->d_partials + (size_t)toff[q] * L, s, rofs[q]));
+                D_HIP(part_dot(q, s));
             D_HIP(hipStreamWaitEvent(s, d->ev[1], 0));
             D_HIP(launch_fold_dot(toff[3], L, d->d_partials, d->d_gtickets, pAp, nullptr, nullptr, d->d_ctrl, -1, s));
         }
@@ -828,7 +846,8 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
     std::memcpy(&tk, &tolerance, sizeof tk);
     const std::vector<const void *> key = {
         d_X_own, d->d_pext, d->d_send, d->d_r, d->d_ap, d->d_partials, d->d_gtickets, d->d_scal, d->d_conv,
-        d->d_red, d->d_ctrl, va.hist, plan, pp[0], pp[1], pp[2], tk, reinterpret_cast<const void *>((intptr_t)L),
+        d->d_red, d->d_ctrl, va.hist, plan, pp[0], pp[1], pp[2], dlocal, dpart[0], dpart[1], dpart[2], tk,
+        reinterpret_cast<const void *>((intptr_t)L),
         reinterpret_cast<const void *>((intptr_t)nblk), reinterpret_cast<const void *>((intptr_t)cap),
         reinterpret_cast<const void *>((intptr_t)K)};
     // one batch: the cached graph when it matches (capturing it now if this object has run an eager

@@ -286,11 +286,17 @@ constexpr int kDiaPlanKey = -3;
 // panels; p is freed by the caller on any error.
 mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, double min_window_fill);
 void free_dia(DiaData *d);
-// Y = A X (L = 1, 2, 4, 8, 16; ld: panel stride, 0 = L); ctrl (CG): return at once when ctrl->done
+// Y = A X (L = 1, 2, 4, 8, 16; ld: panel stride, 0 = L); ctrl (CG): return at once when ctrl->done;
+// partials (dot mode): also X.(A X) per column per window into partials[windows][L] (launch_fold_dot),
+// with the matrix's rows at X row row_off (a row-range view); stream: 0 = the handle's
 hipError_t launch_dia(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L, int ld,
-                      const CgControl *ctrl);
+                      const CgControl *ctrl, double *partials = nullptr, long long row_off = 0,
+                      hipStream_t stream = nullptr);
 std::string dia_kernel_name(const mspmv_handle_s *h, int L);
 bool dia_spmm_enabled();  // the L-wide products on the windows too unless MSPMV_DIA_SPMM=0 (mspmv_api.hip)
+// The handle's offset-window plan for width L (decided on first use), or null (mspmv_api.hip)
+mspmv_status dia_plan_for(mspmv_handle_s *h, int L, const TilePlan **out);
+bool dia_dot_fused();     // the window SpMM takes p.Ap in its dot mode unless MSPMV_DIA_DOT=0 (mspmv_kernels.hip)
 
 // ---- launchers (mspmv_kernels.hip) --------------------------------------------------
 void set_error(const std::string &msg);

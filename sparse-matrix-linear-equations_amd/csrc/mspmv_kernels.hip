@@ -3772,6 +3772,14 @@ static bool cg_dot_pass(int L)
     return mode != 0 && L >= 1;
 }
 
+// The block CG's SpMM on the offset windows takes p.Ap in its dot mode (MSPMV_DIA_DOT=0: the plain window
+// SpMM and the separate pass, as the tiles do).
+bool dia_dot_fused()
+{
+    const char *e = getenv("MSPMV_DIA_DOT");
+    return !(e && *e && atoi(e) == 0);
+}
+
 static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &plan, double *d_x, int L, int nblk,
                                             double tol)
 {
@@ -3799,15 +3807,23 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
     va.rev = 0;
     if (e != hipSuccess)
         return e;
-    if (cg_dot_pass(L)) {
+    const auto dp = h->dia == 1 && (L == 1 || dia_spmm_enabled()) ? h->plans.find(kDiaPlanKey) : h->plans.end();
+    if (dp != h->plans.end() && dia_dot_fused()) {
+        // offset windows (mspmv_dia.hip) in dot mode: Ap and one p.Ap partial per window, folded with the
+        // non-finite-alpha stop -- no separate pass over p and Ap
+        if ((e = launch_dia(h, dp->second, h->d_p0, h->d_ap, L, L, h->d_ctrl, h->d_partials)) != hipSuccess)
+            return e;
+        if ((e = launch_fold_dot(dp->second.num_tiles, L, h->d_partials, h->d_gtickets, h->d_red, h->d_scal,
+                                 h->d_conv, h->d_ctrl, -1, h->stream)) != hipSuccess)
+            return e;
+    } else if (cg_dot_pass(L)) {
         // the plain SpMM (its tile kernel holds fewer registers than the dot mode's, so more
         // workgroups per CU, and never spills), stopped by the control word, then p.Ap in one
         // streaming pass over p and Ap with the fold's breakdown checks (k_pcg_dot mode 2)
-        // (on the column-slab plan when the handle's plain L-wide product took one: spmm_slab_decide)
+        // (on the offset-window or column-slab plan when the handle's plain L-wide product took one)
         const auto sp = (L == 8 || L == 16) && h->spmm_slab[l_index(L)] == 1 ? h->plans.find(slab_mm_key(L))
                                                                               : h->plans.end();
-        const auto dp = h->dia == 1 && (L == 1 || dia_spmm_enabled()) ? h->plans.find(kDiaPlanKey) : h->plans.end();
-        if (dp != h->plans.end()) {  // offset windows (mspmv_dia.hip): structured-grid rows
+        if (dp != h->plans.end()) {
             if ((e = launch_dia(h, dp->second, h->d_p0, h->d_ap, L, L, h->d_ctrl)) != hipSuccess)
                 return e;
         } else if (sp != h->plans.end()) {

@@ -169,14 +169,16 @@ print("SPLIT CG OK")
 """
 
 
-def test_dist_cg_three_stream_split_one_gpu(tmp_path, orc):
+@pytest.mark.parametrize("plan", ["tiles", "windows"])
+def test_dist_cg_three_stream_split_one_gpu(tmp_path, orc, plan):
     """The sharded CG's overlapped iteration (MSPMV_DIST_FORCE_SPLIT=1: head | interior | tail, the
     interior's dot-mode SpMM on its own stream beside the exchange, each part's p.Ap partials at its
     offset, one fold over the three in tile order) at L = 1, 3, 8: iterations, history within 1e-10
-    and X as the oracle's CGSolveMultiple."""
+    and X as the oracle's CGSolveMultiple.  `windows`: every part (a stencil's rows, no halo at world 1)
+    on the offset windows' dot mode (csrc/mspmv_dia.hip), one partial per window."""
     import subprocess
     import mspmv
-    env = dict(os.environ, MSPMV_DIST_FORCE_SPLIT="1")
+    env = dict(os.environ, MSPMV_DIST_FORCE_SPLIT="1", MSPMV_DIA="0" if plan == "tiles" else "")
     r = subprocess.run([sys.executable, "-c", _SPLIT_CG_CHILD, os.path.join(ROOT, "sparse-matrix-linear-equations_amd"),
                         os.path.join(ROOT, "tests"), str(tmp_path)], env=env, capture_output=True, text=True,
                        timeout=300)
@@ -194,10 +196,14 @@ def test_dist_cg_three_stream_split_one_gpu(tmp_path, orc):
         assert np.linalg.norm(Xg - Xo) <= 1e-8 * np.linalg.norm(Xo), L
 
 
-def test_dist_cg_any_width(orc):
+@pytest.mark.parametrize("plan", ["tiles", "windows"])
+def test_dist_cg_any_width(orc, monkeypatch, plan):
     """mspmv_dist_cg_dev at L = 3 and 12: column groups of native widths, every rank (here one) the
-    same groups; iterations, history and X as the oracle's single L-wide CGSolveMultiple."""
+    same groups; iterations, history and X as the oracle's single L-wide CGSolveMultiple.  `windows`:
+    the unsplit local rows on the offset windows' dot mode."""
     import mspmv
+    if plan == "windows":
+        monkeypatch.delenv("MSPMV_DIA", raising=False)
     a = _matrix()
     rb = mspmv.dist_partition(a, 1)
     d = mspmv.DistCsr(mspmv.comm_unique_id(), 1, 0, 0, rb, mspmv.local_rows(a, rb, 0))
