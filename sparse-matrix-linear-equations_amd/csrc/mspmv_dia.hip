@@ -30,6 +30,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 namespace mspmv {
@@ -92,7 +93,8 @@ __device__ __forceinline__ v2d_t dia_ld2(const v2d_t *p)
 // rows reloaded after the products -- they were staged moments before, cache hits), summed by
 // launch_fold_dot, which replaces the separate p.Ap pass (k_pcg_dot) over p and Ap.
 template <int L, bool NT, bool DOT = false>
-__global__ __launch_bounds__(kDiaThreads) void k_spmm_dia(DiaArgs a)
+__global__ __launch_bounds__(kDiaThreads) __attribute__((amdgpu_waves_per_eu(L == 1 ? 8 : 1))) void
+k_spmm_dia(DiaArgs a)
 {
     const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     const int w = xcd_tile(blockIdx.x, a.groups) * kDiaWaves + wv;
@@ -123,7 +125,12 @@ __global__ __launch_bounds__(kDiaThreads) void k_spmm_dia(DiaArgs a)
         constexpr int U = 8;
         const long long r = r0 + lane;
         double acc = 0.0;
-        for (int k0 = 0; k0 < K; k0 += U) {
+        // one batch of U offsets from k0: MASKED selects the absent entries out (acc starts at +0.0 and
+        // never becomes -0.0, so adding +0.0 for them is the identity: the sum is the row's CSR-order
+        // sum bit for bit); GUARD stops at K (the last batch only)
+        auto batch = [&](int k0, auto masked_c, auto guard_c, auto u_c) {
+            constexpr bool MASKED = decltype(masked_c)::value, GUARD = decltype(guard_c)::value;
+            constexpr int U = decltype(u_c)::value;
             v2d_t v[U / 2];
             double xv[U];
             bool on[U];
@@ -132,17 +139,36 @@ __global__ __launch_bounds__(kDiaThreads) void k_spmm_dia(DiaArgs a)
                 v[u] = pair_at((k0 >> 1) + u);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const int kk = min(k0 + u, K - 1);
-                on[u] = !masked || ((mask_at(kk) >> lane) & 1ull);
-                xv[u] = a.x[on[u] ? r + off_at(kk) : 0];
+                const int kk = GUARD ? min(k0 + u, K - 1) : k0 + u;
+                on[u] = MASKED ? ((mask_at(kk) >> lane) & 1ull) != 0 : true;
+                xv[u] = a.x[MASKED ? (on[u] ? r + off_at(kk) : 0) : r + off_at(kk)];
             }
-            // acc starts at +0.0 and never becomes -0.0, so adding +0.0 for an absent entry is the
-            // identity: the sum is the row's CSR-order sum bit for bit
+            // (the guard is a select, not a break: a break let the compiler sink the loads under it and
+            // issue them one round trip at a time -- K = 7 windows 8.0 -> 9.4 us, r05ab)
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (k0 + u < K)
-                    acc += on[u] ? (u & 1 ? v[u >> 1].y : v[u >> 1].x) * xv[u] : 0.0;
-        }
+            for (int u = 0; u < U; ++u) {
+                const double pv = (u & 1 ? v[u >> 1].y : v[u >> 1].x) * xv[u];
+                const bool use = (!MASKED || on[u]) && (!GUARD || k0 + u < K);
+                acc += use ? pv : 0.0;
+            }
+        };
+        // full batches of U, then the rest in one guarded batch of U or U/2 offsets (the 27-point stencil's
+        // 3 left over would otherwise issue 5 clamped duplicate x loads and 2 pair loads per window)
+        using U8 = std::integral_constant<int, U>;
+        using U4 = std::integral_constant<int, U / 2>;
+        const int kfull = K - K % U;
+        auto windows = [&](auto masked_c) {
+            for (int k0 = 0; k0 < kfull; k0 += U)
+                batch(k0, masked_c, std::false_type{}, U8{});
+            if (K - kfull > U / 2)
+                batch(kfull, masked_c, std::true_type{}, U8{});
+            else if (kfull < K)
+                batch(kfull, masked_c, std::true_type{}, U4{});
+        };
+        if (masked)
+            windows(std::true_type{});
+        else
+            windows(std::false_type{});
         if (r < a.m)
             __builtin_nontemporal_store(acc, a.y + r);
         if constexpr (DOT) {
