@@ -540,16 +540,16 @@ constexpr double kSlabAutoBytes = 16.0;
 // slab plan without it and lost: 0.396 against 0.43 on tiles (r04x).
 constexpr double kSlabAutoNnzPerBlock = 12288.0;
 constexpr bool kSlabAuto = true;
-static int slab_switch()  // read at each handle's decision (tests set it per matrix)
+static int slab_switch()  // read at each handle's decision (tests set it per matrix); 2: column groups
 {
     const char *e = getenv("MSPMV_SPMV_SLAB");
-    return e && *e ? (atoi(e) != 0 ? 1 : 0) : -1;
+    return e && *e ? (atoi(e) >= 2 && atoi(e) <= 3 ? atoi(e) : atoi(e) != 0 ? 1 : 0) : -1;
 }
 
 static mspmv_status spmv_slab_decide(mspmv_handle_s *h, const TilePlan *wg)
 {
     const int sw = slab_switch();
-    bool cand = sw == 1;
+    bool cand = sw >= 1;
     if (sw < 0 && kSlabAuto)
         cand = wg->lanes == kBlock && wg->num_tiles >= 64 && !wg->blk_spmv && 2 * wg->num_tiles_dict >= wg->num_tiles;
     h->spmv_slab = 0;
@@ -559,7 +559,7 @@ static mspmv_status spmv_slab_decide(mspmv_handle_s *h, const TilePlan *wg)
     // automatic: the blocks-per-nonzero test runs inside the builder before anything past the bounds is
     // copied or allocated, and any failure (an allocation near capacity included) means "no slab plan":
     // the workgroup plan is ready, so the product must not fail for an optional plan
-    const mspmv_status st = build_slab_plan(h, p, sw < 0 ? kSlabAutoNnzPerBlock : 0.0);
+    const mspmv_status st = build_slab_plan(h, p, sw < 0 ? kSlabAutoNnzPerBlock : 0.0, sw == 2 ? 1 : 0, sw >= 2);
     if (st != MSPMV_OK && (sw < 0 || st == MSPMV_ERR_UNSUPPORTED)) {
         free_plan(p);
         set_error("");

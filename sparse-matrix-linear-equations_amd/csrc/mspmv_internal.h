@@ -34,12 +34,34 @@ constexpr int kSlabChunk = 2048;    // nonzeros per chunk (4 per thread)
 constexpr int kSlabEntries = 1024;  // row runs per chunk
 constexpr int kSlabBlocksPerCu = 2; // resident blocks per CU (LDS: 76 KB per block)
 constexpr int kSlabMaxChunks = 255; // chunks per block (their descriptors sit in LDS)
+// The SpMV's block shapes: 0 the band configuration above (merge-path blocks, two per CU); 1 the
+// column-group configuration for x too wide for any block to reuse a slab (power-law rows over random
+// columns): one block per CU, each block a (row block, column group) pair -- whole rows, the columns of
+// kSlabGroups consecutive slab ranges -- so a block stages a quarter of x, not all of it; the groups'
+// partial row sums are folded by the row block's last block to finish.
+struct SlabCfg {
+    int threads;  // per block
+    int cols;     // columns per slab (LDS: cols x 8 B)
+    int rows;     // rows ending in one block
+    int chunk;    // nonzeros per chunk
+    int entries;  // row runs per chunk
+    int per_cu;   // resident blocks per CU
+};
+constexpr SlabCfg kSlabCfgs[2] = {{kSlabThreads, kSlabCols, kSlabRows, kSlabChunk, kSlabEntries, kSlabBlocksPerCu},
+                                  {1024, 8192, 4095, 4096, 2048, 1}};
+constexpr int kSlabGroups = 4;
+constexpr int kSlabLongRun = 64;  // runs longer than this are summed by whole waves (listed first in a chunk)
 struct SlabData {
     int L = 1;                          // 1: the SpMV's plan (k_spmv_slab); 8 / 16: an SpMM plan (k_spmm_slab)
-    int cfg = 0;                        // SpMM: the kernel configuration the plan was cut for (slab_mm_cfg)
+    int cfg = 0;                        // the kernel configuration the plan was cut for (SpMV: kSlabCfgs;
+                                        // SpMM: slab_mm_cfg)
+    int groups = 1;                     // SpMV column groups (cfg 1): blocks = row blocks x groups
+    double *d_part = nullptr;           // [groups][m] the groups' partial row sums (groups > 1)
+    unsigned *d_gcnt = nullptr;         // [row blocks] tickets of the fold (self-resetting)
     int num_chunks = 0, num_entries = 0;
     int4 *d_blk = nullptr;              // [blocks] {first row, rows ending in the block, chunk0, chunk1}
-    int4 *d_chunk = nullptr;            // [chunks + 1] SpMV: {stream start, length | lanes_log2 << 16, slab, entry0};
+    int4 *d_chunk = nullptr;            // [chunks + 1] SpMV: {stream start, length | lanes_log2 << 13 | long runs << 16,
+                                        // slab, entry0};
                                         // SpMM: {stream start, length | lanes_log2 << 13 | columns << 16,
                                         // first column of the chunk's segment, entry0}
     uint2 *d_ent = nullptr;             // [entries] {offset in chunk | length << 16, row in block}
@@ -264,10 +286,12 @@ constexpr int kRunPlanKey = -2;  // the run-balanced node-block SpMV plan (mspmv
 // Builds the column-slab plan into *p (blocks, split rows, reordered stream); MSPMV_ERR_UNSUPPORTED
 // when the matrix does not fit the form (rows per block) or its blocks would hold fewer than
 // min_nnz_per_block nonzeros on average; p is freed by the caller on any error.
-mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p, double min_nnz_per_block = 0.0);
+// cfg: the block shape (kSlabCfgs); groups (always for cfg 1): column-group blocks instead of merge-path ones.
+mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p, double min_nnz_per_block = 0.0, int cfg = 0,
+                             bool groups = false);
 void free_slab(SlabData *s);
 hipError_t launch_slab(mspmv_handle_s *h, const TilePlan &plan, const double *d_x, double *d_y);
-std::string slab_kernel_name(const mspmv_handle_s *h);
+std::string slab_kernel_name(const mspmv_handle_s *h);  // the handle's plain-SpMV slab plan's kernel
 // Column-slab SpMM plans (L = 8, 16), keyed apart from every tile plan.
 inline int slab_mm_key(int L) { return -(1 << 20) - L; }
 const SlabMmCfg &slab_mm_cfg(int L, int which = -1);  // which < 0: the shipped configuration for L

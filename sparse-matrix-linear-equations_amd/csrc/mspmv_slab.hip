@@ -21,6 +21,7 @@
 #include "mspmv_device.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -38,6 +39,10 @@ struct SlabArgs {
     double *y;
     int n;
     int num_tiles;              // blocks
+    int groups;                 // column groups (1: every block holds whole rows' nonzeros)
+    int m;
+    double *part;               // [groups][m] partial row sums (groups > 1)
+    unsigned *gcnt;             // [row blocks] fold tickets
     // split rows (close_split_rows reads these names)
     const int2 *bounds;
     const unsigned char *split;
@@ -56,16 +61,17 @@ __device__ __forceinline__ T slab_stream(const T *p)
     return *p;
 }
 
-template <bool NT>
-__global__ __launch_bounds__(kSlabThreads) void k_spmv_slab(SlabArgs a)
+template <bool NT, int CFG>
+__global__ __launch_bounds__(kSlabCfgs[CFG].threads) void k_spmv_slab(SlabArgs a)
 {
-    constexpr int TB = kSlabThreads;
-    constexpr int IPT = kSlabChunk / TB;    // stream items per thread and chunk
-    constexpr int EPT = kSlabEntries / TB;  // entries per thread and chunk
-    __shared__ double xs[kSlabCols];
-    __shared__ double yacc[kSlabRows + 1];
-    __shared__ double prod[kSlabChunk];
-    __shared__ uint2 sent[kSlabEntries];
+    constexpr SlabCfg C = kSlabCfgs[CFG];
+    constexpr int TB = C.threads;
+    constexpr int IPT = C.chunk / TB;    // stream items per thread and chunk
+    constexpr int EPT = C.entries / TB;  // entries per thread and chunk
+    __shared__ double xs[C.cols];
+    __shared__ double yacc[C.rows + 1];
+    __shared__ double prod[C.chunk];
+    __shared__ uint2 sent[C.entries];
     __shared__ int4 schunk[kSlabMaxChunks + 1];
     const int tid = threadIdx.x;
     const int b = xcd_tile(blockIdx.x, a.num_tiles);
@@ -93,7 +99,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_spmv_slab(SlabArgs a)
     };
     auto fetch = [&](int ci, Regs &r) {
         const int4 cd = chunk(ci);
-        const int len = cd.y & 0xffff;
+        const int len = cd.y & 0x1fff;
         const int e0 = cd.w, ne = chunk(ci + 1).w - e0;
 #pragma unroll
         for (int j = 0; j < IPT; ++j) {
@@ -107,10 +113,10 @@ __global__ __launch_bounds__(kSlabThreads) void k_spmv_slab(SlabArgs a)
             r.e[j] = k < ne ? a.ent[e0 + k] : make_uint2(0u, 0u);
         }
     };
-    constexpr int XPT = kSlabCols / TB;  // x values per thread and slab
+    constexpr int XPT = C.cols / TB;  // x values per thread and slab
     double xq[XPT];
     auto fetch_x = [&](int slab) {  // a slab of x, into registers (coalesced: lane-consecutive columns)
-        const int c0 = slab * kSlabCols;
+        const int c0 = slab * C.cols;
 #pragma unroll
         for (int j = 0; j < XPT; ++j) {
             const int col = c0 + tid + j * TB;
@@ -124,7 +130,7 @@ __global__ __launch_bounds__(kSlabThreads) void k_spmv_slab(SlabArgs a)
     // next chunk changes it, then the runs summed into yacc.
     auto process = [&](int ci, Regs &r) {
         const int4 cd = chunk(ci);
-        const int len = cd.y & 0xffff, lg = cd.y >> 16;
+        const int len = cd.y & 0x1fff, lg = (cd.y >> 13) & 7, nlong = cd.y >> 16;
         const int ne = chunk(ci + 1).w - cd.w;
         if (cd.z != cur) {  // block-uniform
             cur = cd.z;
@@ -154,8 +160,21 @@ __global__ __launch_bounds__(kSlabThreads) void k_spmv_slab(SlabArgs a)
                 fetch_x(ns);
         }
         __syncthreads();
+        // long runs (listed first) by whole waves: a run thousands long (a power-law hub row) must not
+        // sit on a few lanes of a group sized for the chunk's short runs
+        for (int q = tid >> 6; q < nlong; q += TB >> 6) {  // wave-uniform
+            const uint2 en = sent[q];
+            const int off = (int)(en.x & 0xffffu), el = (int)(en.x >> 16);
+            double s = 0.0;
+            for (int k = off + (tid & 63); k < off + el; k += 64)
+                s += prod[k];
+            for (int o = 32; o > 0; o >>= 1)
+                s += __shfl_xor(s, o);
+            if ((tid & 63) == 0)
+                yacc[en.y] += s;
+        }
         const int G = 1 << lg, lane = tid & (G - 1);
-        for (int q = tid >> lg; q < ne; q += TB >> lg) {  // uniform within a group
+        for (int q = nlong + (tid >> lg); q < ne; q += TB >> lg) {  // uniform within a group
             const uint2 en = sent[q];
             const int off = (int)(en.x & 0xffffu), el = (int)(en.x >> 16);
             double s = 0.0;
@@ -179,6 +198,30 @@ __global__ __launch_bounds__(kSlabThreads) void k_spmv_slab(SlabArgs a)
         process(ci, ra);
         if (ci + 1 < bd.w)
             process(ci + 1, rb);
+    }
+    if (a.groups > 1) {  // block-uniform: a column group's partial row sums, folded by the last group
+        const int G = a.groups, g = b % G, rb = b / G;
+        for (int i = tid; i < nrows; i += TB)
+            store_sc1(&a.part[(size_t)g * a.m + bd.x + i], yacc[i]);
+        __shared__ int s_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this group's partials are out
+        __syncthreads();
+        if (tid == 0)
+            s_last = __hip_atomic_fetch_add(&a.gcnt[rb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                     (unsigned)(G - 1);
+        __syncthreads();
+        if (!s_last)
+            return;
+        // the row block's last group to finish: y = the groups' partials in group order (fixed order)
+        for (int i = tid; i < nrows; i += TB) {
+            double s = 0.0;
+            for (int q = 0; q < G; ++q)
+                s += q == g ? yacc[i] : load_sc1(&a.part[(size_t)q * a.m + bd.x + i]);
+            a.y[bd.x + i] = s;
+        }
+        if (tid == 0)
+            __hip_atomic_store(&a.gcnt[rb], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
     }
     // rows ending in the block; its first row goes to the head slot when it completes a split row
     for (int i = tid; i < nrows; i += TB)
@@ -208,18 +251,31 @@ hipError_t launch_slab(mspmv_handle_s *h, const TilePlan &plan, const double *d_
     a.carry_val = plan.d_carry_val;
     a.head_val = plan.d_carry_val + (size_t)std::max(plan.num_tiles, 1) * plan.carry_L;
     a.head_pub = a.head_val + (size_t)std::max(plan.num_tiles, 1) * plan.carry_L;
+    a.groups = s.groups;
+    a.m = h->m;
+    a.part = s.d_part;
+    a.gcnt = s.d_gcnt;
     if (plan.num_tiles == 0)
         return hipSuccess;
-    if (stream_nt(h))
-        hipLaunchKernelGGL(k_spmv_slab<true>, dim3(plan.num_tiles), dim3(kSlabThreads), 0, h->stream, a);
+    const bool nt = stream_nt(h);
+    const dim3 grid(plan.num_tiles);
+    const dim3 b1(kSlabCfgs[1].threads), b0(kSlabCfgs[0].threads);
+    if (s.cfg == 1 && nt)
+        hipLaunchKernelGGL((k_spmv_slab<true, 1>), grid, b1, 0, h->stream, a);
+    else if (s.cfg == 1)
+        hipLaunchKernelGGL((k_spmv_slab<false, 1>), grid, b1, 0, h->stream, a);
+    else if (nt)
+        hipLaunchKernelGGL((k_spmv_slab<true, 0>), grid, b0, 0, h->stream, a);
     else
-        hipLaunchKernelGGL(k_spmv_slab<false>, dim3(plan.num_tiles), dim3(kSlabThreads), 0, h->stream, a);
+        hipLaunchKernelGGL((k_spmv_slab<false, 0>), grid, b0, 0, h->stream, a);
     return hipGetLastError();
 }
 
 std::string slab_kernel_name(const mspmv_handle_s *h)
 {
-    return std::string("k_spmv_slab<") + (stream_nt(h) ? "true" : "false") + ">";
+    const auto it = h->plans.find(kSlabPlanKey);
+    const int cfg = it != h->plans.end() && it->second.slab ? it->second.slab->cfg : 0;
+    return std::string("k_spmv_slab<") + (stream_nt(h) ? "true" : "false") + "," + std::to_string(cfg) + ">";
 }
 
 template <typename T>
@@ -239,6 +295,8 @@ void free_slab(SlabData *s)
     slab_free(s->d_ent);
     slab_free(s->d_val);
     slab_free(s->d_col);
+    slab_free(s->d_part);
+    slab_free(s->d_gcnt);
     delete s;
 }
 
@@ -261,8 +319,9 @@ static mspmv_status slab_upload(T **d, const std::vector<T> &hsrc, size_t pad = 
     return MSPMV_OK;
 }
 
-// Per block: its nonzeros [n0, n1) in slab-major order (stable within a slab: CSR order), cut into
-// chunks of one slab, <= kSlabChunk nonzeros and <= kSlabEntries runs of one row.
+// Per block: its nonzeros [n0, n1) with columns in [clo, chi) in slab-major order (stable within a
+// slab: CSR order), placed at stream position base, cut into chunks of one slab, <= C.chunk nonzeros
+// and <= C.entries runs of one row.
 struct SlabBlockOut {
     std::vector<int4> chunks;  // entry0 relative to the block
     std::vector<uint2> ents;
@@ -270,37 +329,46 @@ struct SlabBlockOut {
 };
 
 static void slab_block(const std::vector<int> &ro, const std::vector<int> &ci, const std::vector<double> &va,
-                       int r0, int n0, int r1, int n1, double *oval, unsigned short *ocol, SlabBlockOut &out)
+                       int r0, int n0, int r1, int n1, int clo, int chi, int base, const SlabCfg &C, double *oval,
+                       unsigned short *ocol, SlabBlockOut &out)
 {
-    const int cnt = n1 - n0;
+    const int W = C.cols;
+    const int rlast = n1 > ro[(size_t)r1] ? r1 : r1 - 1;  // the trailing partial row, when there is one
+    std::vector<int> ks, kr;  // the block's nonzeros in the column range, CSR order, and their local rows
+    for (int r = r0; r <= rlast; ++r) {
+        const int k0 = std::max(ro[(size_t)r], n0), k1 = std::min(ro[(size_t)r + 1], n1);
+        for (int k = k0; k < k1; ++k)
+            if (ci[(size_t)k] >= clo && ci[(size_t)k] < chi) {
+                ks.push_back(k);
+                kr.push_back(r - r0);
+            }
+    }
+    const int cnt = (int)ks.size();
     if (cnt <= 0)
         return;
     int smin = 0x7fffffff, smax = -1;
-    for (int k = n0; k < n1; ++k) {
-        const int s = ci[(size_t)k] / kSlabCols;
+    for (int k : ks) {
+        const int s = ci[(size_t)k] / W;
         smin = std::min(smin, s);
         smax = std::max(smax, s);
     }
     const int ns = smax - smin + 1;
     std::vector<int> off((size_t)ns + 1, 0);
-    for (int k = n0; k < n1; ++k)
-        ++off[(size_t)(ci[(size_t)k] / kSlabCols - smin) + 1];
+    for (int k : ks)
+        ++off[(size_t)(ci[(size_t)k] / W - smin) + 1];
     for (int s = 0; s < ns; ++s) {
         out.slabs += off[(size_t)s + 1] > 0;
         off[(size_t)s + 1] += off[(size_t)s];
     }
     std::vector<int> row((size_t)cnt);  // local row of each reordered nonzero
     std::vector<int> put(off.begin(), off.end() - 1);
-    const int rlast = n1 > ro[(size_t)r1] ? r1 : r1 - 1;  // the trailing partial row, when there is one
-    for (int r = r0; r <= rlast; ++r) {
-        const int k0 = std::max(ro[(size_t)r], n0), k1 = std::min(ro[(size_t)r + 1], n1);
-        for (int k = k0; k < k1; ++k) {
-            const int s = ci[(size_t)k] / kSlabCols;
-            const int q = put[(size_t)(s - smin)]++;
-            oval[(size_t)n0 + q] = va[(size_t)k];
-            ocol[(size_t)n0 + q] = (unsigned short)(ci[(size_t)k] - s * kSlabCols);
-            row[(size_t)q] = r - r0;
-        }
+    for (int i = 0; i < cnt; ++i) {
+        const int k = ks[(size_t)i];
+        const int s = ci[(size_t)k] / W;
+        const int q = put[(size_t)(s - smin)]++;
+        oval[(size_t)base + q] = va[(size_t)k];
+        ocol[(size_t)base + q] = (unsigned short)(ci[(size_t)k] - s * W);
+        row[(size_t)q] = kr[(size_t)i];
     }
     for (int s = 0; s < ns; ++s) {
         int q = off[(size_t)s];
@@ -308,31 +376,41 @@ static void slab_block(const std::vector<int> &ro, const std::vector<int> &ci, c
         while (q < qe) {  // chunks of this slab
             const int start = q, e0 = (int)out.ents.size();
             int ne = 0;
-            while (q < qe && q - start < kSlabChunk) {
+            while (q < qe && q - start < C.chunk) {
                 int k = q;
-                while (k < qe && k - start < kSlabChunk && row[(size_t)k] == row[(size_t)q])
+                while (k < qe && k - start < C.chunk && row[(size_t)k] == row[(size_t)q])
                     ++k;
-                if (ne == kSlabEntries)
+                if (ne == C.entries)
                     break;
                 out.ents.push_back(make_uint2((unsigned)(q - start) | ((unsigned)(k - q) << 16), (unsigned)row[(size_t)q]));
                 ++ne;
                 q = k;
             }
             const int len = q - start;
-            // lanes per run: the fewest latency steps -- rounds of runs over the workgroup x (the run's
-            // products per lane + its butterfly + ~8 steps of LDS round trips); the older rule, the
+            // runs longer than kSlabLongRun first (whole waves sum them), then the short ones
+            std::stable_partition(out.ents.begin() + e0, out.ents.end(),
+                                  [](const uint2 &e) { return (int)(e.x >> 16) > kSlabLongRun; });
+            int nlong = 0, slen = 0;
+            for (int i = e0; i < (int)out.ents.size(); ++i) {
+                const int el = (int)(out.ents[(size_t)i].x >> 16);
+                nlong += el > kSlabLongRun;
+                slen += el > kSlabLongRun ? 0 : el;
+            }
+            const int ns_ = ne - nlong;
+            // lanes per short run: the fewest latency steps -- rounds of runs over the workgroup x (the
+            // run's products per lane + its butterfly + ~8 steps of LDS round trips); the older rule, the
             // smallest G with 4 G >= the mean run, took two rounds where one does (44 -> 40 us, r04w)
-            const int mean = (len + ne - 1) / ne;
+            const int mean = ns_ > 0 ? (slen + ns_ - 1) / ns_ : 1;
             int lg = 0, best = 1 << 30;
             for (int l = 0; l <= 6; ++l) {
-                const int rounds = (ne + (kSlabThreads >> l) - 1) / (kSlabThreads >> l);
+                const int rounds = (ns_ + (C.threads >> l) - 1) / (C.threads >> l);
                 const int cost = rounds * ((mean + (1 << l) - 1) / (1 << l) + 2 * l + 8);
                 if (cost < best) {
                     best = cost;
                     lg = l;
                 }
             }
-            out.chunks.push_back(make_int4(n0 + start, len | (lg << 16), smin + s, e0));
+            out.chunks.push_back(make_int4(base + start, len | (lg << 13) | (nlong << 16), smin + s, e0));
         }
     }
 }
@@ -418,10 +496,171 @@ static mspmv_status slab_host_matrix(mspmv_handle_s *h, std::vector<int> &ro, st
     return MSPMV_OK;
 }
 
-mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p, double min_nnz_per_block)
+// The blocks' reordered streams, chunks and entries to the device, then the plan's split rows (their
+// carries and heads: three [T][16] slots, as the tile plans) and tile modes 255.
+static mspmv_status slab_finish(mspmv_handle_s *h, TilePlan &p, int cfg, int groups,
+                                const std::vector<int4> &blk, const std::vector<SlabBlockOut> &outs,
+                                const std::vector<double> &oval, const std::vector<unsigned short> &ocol,
+                                const std::vector<int2> &hb, const std::vector<unsigned char> &hs)
+{
+    const int T = p.num_tiles;
+    std::vector<int4> dblk(blk), chunks;
+    std::vector<uint2> ents;
+    long long staged = 0;
+    for (int t = 0; t < T; ++t) {
+        const SlabBlockOut &o = outs[(size_t)t];
+        if ((int)o.chunks.size() > kSlabMaxChunks)  // more chunks than one block's LDS table holds
+            return MSPMV_ERR_UNSUPPORTED;
+        const int c0 = (int)chunks.size(), ebase = (int)ents.size();
+        for (int4 c : o.chunks) {
+            c.w += ebase;
+            chunks.push_back(c);
+        }
+        ents.insert(ents.end(), o.ents.begin(), o.ents.end());
+        dblk[(size_t)t].z = c0;
+        dblk[(size_t)t].w = (int)chunks.size();
+        staged += (long long)o.slabs * kSlabCfgs[cfg].cols * 8;
+    }
+    chunks.push_back(make_int4(0, 0, 0, (int)ents.size()));  // sentinel: the last chunk's entry end
+    SlabData *s = new SlabData();
+    s->cfg = cfg;
+    s->groups = groups;
+    s->num_chunks = (int)chunks.size() - 1;
+    s->num_entries = (int)ents.size();
+    s->x_bytes_per_nnz = (double)staged / (double)h->nnz;
+    p.slab = s;
+    mspmv_status st;
+    if ((st = slab_upload(&s->d_blk, dblk)) != MSPMV_OK || (st = slab_upload(&s->d_chunk, chunks)) != MSPMV_OK ||
+        (st = slab_upload(&s->d_ent, ents)) != MSPMV_OK || (st = slab_upload(&s->d_val, oval, kNnzPad)) != MSPMV_OK ||
+        (st = slab_upload(&s->d_col, ocol, kNnzPad)) != MSPMV_OK)
+        return st;
+    if (groups > 1) {
+        const std::vector<unsigned> zero((size_t)T / groups, 0u);
+        if ((st = slab_upload(&s->d_gcnt, zero)) != MSPMV_OK)
+            return st;
+        if (hipMalloc((void **)&s->d_part, sizeof(double) * (size_t)groups * h->m) != hipSuccess) {
+            s->d_part = nullptr;
+            set_error("column-slab plan: hipMalloc failed");
+            return MSPMV_ERR_HIP;
+        }
+    }
+    p.carry_L = 16;
+    if (hipMalloc((void **)&p.d_carry_val, sizeof(double) * (size_t)T * 16 * 3) != hipSuccess ||
+        hipMalloc((void **)&p.d_modes[0], (size_t)T) != hipSuccess) {
+        set_error("column-slab plan: hipMalloc failed");
+        return MSPMV_ERR_HIP;
+    }
+    if (hipMemset(p.d_modes[0], 255, (size_t)T) != hipSuccess) {
+        set_error("column-slab plan: memset failed");
+        return MSPMV_ERR_HIP;
+    }
+    return plan_split_rows(p, hb, hs);
+}
+
+// Column-group blocks (kSlabCfgs[1]): whole-row blocks of ~(m + nnz) / R merge items (<= C.rows rows),
+// R = the resident blocks / groups, each crossed with the groups' column ranges (consecutive slabs);
+// block t = row block t / G, group t % G.  The reported bounds give each row block to its first group
+// (the others span nothing), so the plan reads as monotone merge-path tiles.
+static mspmv_status build_slab_group_plan(mspmv_handle_s *h, TilePlan &p, double min_nnz_per_block, int cfg)
+{
+    const SlabCfg &C = kSlabCfgs[cfg];
+    const int nslabs = (h->n + C.cols - 1) / C.cols;
+    const char *ge = getenv("MSPMV_SLAB_GROUPS");  // lab: the column-group count
+    const int G = std::max(1, std::min(ge && *ge ? atoi(ge) : kSlabGroups, nslabs));
+    const int spg = (nslabs + G - 1) / G;  // slabs per group
+    const long long R0 = std::max(1, h->num_cus * C.per_cu / G);
+    std::vector<int> ro, ci;
+    std::vector<double> va;
+    mspmv_status st0;
+    ro.resize((size_t)h->m + 1);
+    if (hipMemcpy(ro.data(), h->d_row_offsets, sizeof(int) * ro.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error("column-slab plan: row offsets download failed");
+        return MSPMV_ERR_HIP;
+    }
+    const long long target = ((long long)h->m + h->nnz + R0 - 1) / R0;
+    std::vector<int> rbs{0};
+    long long items = 0;
+    int rows = 0;
+    for (int r = 0; r < h->m; ++r) {
+        if (rows == C.rows) {
+            rbs.push_back(r);
+            items = 0;
+            rows = 0;
+        }
+        items += 1 + (long long)ro[(size_t)r + 1] - ro[(size_t)r];
+        ++rows;
+        if (items >= target && r + 1 < h->m) {  // cut after the row that reaches the target: <= R0 blocks
+            rbs.push_back(r + 1);
+            items = 0;
+            rows = 0;
+        }
+    }
+    rbs.push_back(h->m);
+    const int R = (int)rbs.size() - 1;
+    const long long Tl = (long long)R * G;
+    if (Tl > 64LL * h->num_cus || (double)h->nnz < min_nnz_per_block * (double)Tl)  // before the copy
+        return MSPMV_ERR_UNSUPPORTED;
+    const int T = (int)Tl;
+    if ((st0 = slab_host_matrix(h, ro, ci, va)) != MSPMV_OK)
+        return st0;
+    auto crange = [&](int g, int &lo, int &hi) {
+        lo = std::min(h->n, g * spg * C.cols);
+        hi = g == G - 1 ? 0x7fffffff : std::min(h->n, (g + 1) * spg * C.cols);
+    };
+    // stream positions: block t's nonzeros after those of blocks 0 .. t-1
+    std::vector<long long> cnt((size_t)T + 1, 0);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int rb = 0; rb < R; ++rb) {
+        for (int k = ro[(size_t)rbs[(size_t)rb]]; k < ro[(size_t)rbs[(size_t)rb + 1]]; ++k) {
+            const int g = std::min(G - 1, ci[(size_t)k] / (spg * C.cols));
+            ++cnt[(size_t)rb * G + g + 1];
+        }
+    }
+    for (int t = 0; t < T; ++t)
+        cnt[(size_t)t + 1] += cnt[(size_t)t];
+    std::vector<double> oval((size_t)h->nnz);
+    std::vector<unsigned short> ocol((size_t)h->nnz);
+    std::vector<SlabBlockOut> outs((size_t)T);
+    std::vector<int4> blk((size_t)T);
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int t = 0; t < T; ++t) {
+        const int rb = t / G, g = t % G, r0 = rbs[(size_t)rb], r1 = rbs[(size_t)rb + 1];
+        int lo, hi;
+        crange(g, lo, hi);
+        slab_block(ro, ci, va, r0, ro[(size_t)r0], r1, ro[(size_t)r1], lo, hi, (int)cnt[(size_t)t], C, oval.data(),
+                   ocol.data(), outs[(size_t)t]);
+        blk[(size_t)t] = make_int4(r0, r1 - r0, 0, 0);
+    }
+    std::vector<int2> hb((size_t)T + 1);
+    for (int t = 0; t < T; ++t) {
+        const int r = rbs[(size_t)(t / G) + (t % G == 0 ? 0 : 1)];
+        hb[(size_t)t] = make_int2(r, ro[(size_t)r]);
+    }
+    hb[(size_t)T] = make_int2(h->m, h->nnz);
+    const std::vector<unsigned char> hs((size_t)T + 1, 0);
+    if (hipMalloc((void **)&p.d_bounds, sizeof(int2) * hb.size()) != hipSuccess ||
+        hipMalloc((void **)&p.d_split, hs.size()) != hipSuccess) {
+        set_error("column-slab plan: hipMalloc failed");
+        return MSPMV_ERR_HIP;
+    }
+    if (hipMemcpy(p.d_bounds, hb.data(), sizeof(int2) * hb.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p.d_split, hs.data(), hs.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("column-slab plan: upload failed");
+        return MSPMV_ERR_HIP;
+    }
+    p.num_tiles = T;
+    p.lanes = C.threads;
+    p.tile_items = (int)std::min<long long>(target, 0x7fffffff);
+    p.snap = 0;
+    return slab_finish(h, p, cfg, G, blk, outs, oval, ocol, hb, hs);
+}
+
+mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p, double min_nnz_per_block, int cfg, bool groups)
 {
     if (h->m <= 0 || h->nnz <= 0)
         return MSPMV_ERR_UNSUPPORTED;
+    if (cfg == 1 || groups)
+        return build_slab_group_plan(h, p, min_nnz_per_block, cfg);
     std::vector<int2> hb;
     std::vector<unsigned char> hs;
     long long step = 0;
@@ -445,52 +684,15 @@ mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p, double min_nnz_per_
     std::vector<double> oval((size_t)h->nnz);
     std::vector<unsigned short> ocol((size_t)h->nnz);
     std::vector<SlabBlockOut> outs((size_t)T);
+    std::vector<int4> blk((size_t)T);
 #pragma omp parallel for schedule(dynamic, 4)
     for (int t = 0; t < T; ++t) {
         const int2 b0 = hb[(size_t)t], b1 = hb[(size_t)t + 1];
-        slab_block(ro, ci, va, b0.x, b0.y, b1.x, b1.y, oval.data(), ocol.data(), outs[(size_t)t]);
+        slab_block(ro, ci, va, b0.x, b0.y, b1.x, b1.y, 0, 0x7fffffff, b0.y, kSlabCfgs[0], oval.data(), ocol.data(),
+                   outs[(size_t)t]);
+        blk[(size_t)t] = make_int4(b0.x, b1.x - b0.x, 0, 0);
     }
-    SlabData *s = new SlabData();
-    std::vector<int4> blk((size_t)T), chunks;
-    std::vector<uint2> ents;
-    long long staged = 0;
-    for (int t = 0; t < T; ++t) {
-        const SlabBlockOut &o = outs[(size_t)t];
-        const int c0 = (int)chunks.size(), ebase = (int)ents.size();
-        for (int4 c : o.chunks) {
-            c.w += ebase;
-            chunks.push_back(c);
-        }
-        ents.insert(ents.end(), o.ents.begin(), o.ents.end());
-        blk[(size_t)t] = make_int4(hb[(size_t)t].x, hb[(size_t)t + 1].x - hb[(size_t)t].x, c0, (int)chunks.size());
-        if ((int)o.chunks.size() > kSlabMaxChunks) {  // more slabs than one block's LDS table holds
-            delete s;
-            return MSPMV_ERR_UNSUPPORTED;
-        }
-        staged += (long long)o.slabs * kSlabCols * 8;
-    }
-    chunks.push_back(make_int4(0, 0, 0, (int)ents.size()));  // sentinel: the last chunk's entry end
-    s->num_chunks = (int)chunks.size() - 1;
-    s->num_entries = (int)ents.size();
-    s->x_bytes_per_nnz = (double)staged / (double)h->nnz;
-    p.slab = s;
-    mspmv_status st;
-    if ((st = slab_upload(&s->d_blk, blk)) != MSPMV_OK || (st = slab_upload(&s->d_chunk, chunks)) != MSPMV_OK ||
-        (st = slab_upload(&s->d_ent, ents)) != MSPMV_OK || (st = slab_upload(&s->d_val, oval, kNnzPad)) != MSPMV_OK ||
-        (st = slab_upload(&s->d_col, ocol, kNnzPad)) != MSPMV_OK)
-        return st;
-    // split rows, their carries and heads (three [T][16] slots, as the tile plans), tile modes 255
-    p.carry_L = 16;
-    if (hipMalloc((void **)&p.d_carry_val, sizeof(double) * (size_t)T * 16 * 3) != hipSuccess ||
-        hipMalloc((void **)&p.d_modes[0], (size_t)T) != hipSuccess) {
-        set_error("column-slab plan: hipMalloc failed");
-        return MSPMV_ERR_HIP;
-    }
-    if (hipMemset(p.d_modes[0], 255, (size_t)T) != hipSuccess) {
-        set_error("column-slab plan: memset failed");
-        return MSPMV_ERR_HIP;
-    }
-    return plan_split_rows(p, hb, hs);
+    return slab_finish(h, p, 0, 1, blk, outs, oval, ocol, hb, hs);
 }
 
 

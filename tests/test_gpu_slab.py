@@ -1,7 +1,8 @@
 """Column-slab SpMV (mspmv_slab.hip): blocks of a CU's share of the merge path, each block's nonzeros
 reordered by 4,096-column slab of x (staged in LDS), rows accumulated in LDS in slab order.
 
-Forced with MSPMV_SPMV_SLAB=1 (read when a handle first decides its plain-SpMV plan) on shapes with
+Forced with MSPMV_SPMV_SLAB=1 (merge-path blocks) and =2 (column-group blocks whose partial row sums the
+row block's last group folds; read when a handle first decides its plain-SpMV plan) on shapes with
 scattered, skewed, split, empty and rectangular rows; checked against the oracle's SpmvGold
 (cpu_spmv.cpp:241-265) within the reordering bound (the slab order is a reordered CSR sum:
 mspmv_tile_modes reports every block as 255), bit-identical on repeats and under a CU limit's
@@ -17,9 +18,11 @@ from gpu_common import check_parity
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture
-def slab_on(monkeypatch):
-    monkeypatch.setenv("MSPMV_SPMV_SLAB", "1")
+@pytest.fixture(params=["1", "2"], ids=["band", "groups"])
+def slab_on(monkeypatch, request):
+    """1: merge-path blocks (kSlabCfgs[0]); 2: column-group blocks (kSlabCfgs[1], partials folded)."""
+    monkeypatch.setenv("MSPMV_SPMV_SLAB", request.param)
+    return request.param
 
 
 def scatter_band(m, per_row, band, seed):
@@ -57,6 +60,7 @@ def test_slab_parity(orc, slab_on, name):
     with mspmv.GpuCsr(a) as g:
         y = g.spmv(x)
         assert g.kernel_name().startswith("k_spmv_slab<"), g.kernel_name()
+        assert g.kernel_name().endswith(",1>" if slab_on == "2" else ",0>"), g.kernel_name()
         plan = g.tile_plan(1)
         assert np.all(plan["modes"] == 255)
         check_parity(a, y, gold, x, plan, 1)
