@@ -543,8 +543,30 @@ constexpr bool kSlabAuto = true;
 static int slab_switch()  // read at each handle's decision (tests set it per matrix); 2: column groups
 {
     const char *e = getenv("MSPMV_SPMV_SLAB");
-    return e && *e ? (atoi(e) >= 2 && atoi(e) <= 3 ? atoi(e) : atoi(e) != 0 ? 1 : 0) : -1;
+    return e && *e ? (atoi(e) >= 2 && atoi(e) <= 4 ? atoi(e) : atoi(e) != 0 ? 1 : 0) : -1;
 }
+
+// Most of the workgroup plan's tiles are merge walks (row lengths uneven inside most tiles: skewed,
+// power-law rows): the one-wave plan's and the sliced-ELL plan's test.
+static mspmv_status mostly_walks(const TilePlan *wg, bool *out)
+{
+    *out = false;
+    if (wg->lanes != kBlock || wg->num_tiles < 64 || wg->d_blk)
+        return MSPMV_OK;
+    std::vector<unsigned char> hm((size_t)wg->num_tiles);
+    HIP_TRY(hipMemcpy(hm.data(), wg->d_modes[0], hm.size(), hipMemcpyDeviceToHost));
+    long long walk = 0;
+    for (unsigned char v : hm)
+        walk += v == 0;
+    *out = 2 * walk >= (long long)wg->num_tiles;
+    return MSPMV_OK;
+}
+
+// Skewed rows (mostly merge walks) with at least kSellAutoNnzPerBlock nonzeros per column-group block
+// take the sliced-ELL plan (k_spmv_sell) when it stages at most kSlabAutoBytes of x per nonzero: the
+// power-law variant at pwtk size 80 -> 67 us per launch (r05ao-r05aq); smaller skewed matrices keep
+// the one-wave tiles (their blocks would be a few chunks of work each).
+constexpr double kSellAutoNnzPerBlock = 12288.0;
 
 static mspmv_status spmv_slab_decide(mspmv_handle_s *h, const TilePlan *wg)
 {
@@ -553,13 +575,30 @@ static mspmv_status spmv_slab_decide(mspmv_handle_s *h, const TilePlan *wg)
     if (sw < 0 && kSlabAuto)
         cand = wg->lanes == kBlock && wg->num_tiles >= 64 && !wg->blk_spmv && 2 * wg->num_tiles_dict >= wg->num_tiles;
     h->spmv_slab = 0;
+    if (!cand && sw < 0 && kSlabAuto) {  // skewed rows: the sliced-ELL plan, when it pays
+        bool skew = false;
+        ST_TRY(mostly_walks(wg, &skew));
+        if (skew && (double)h->nnz >= kSellAutoNnzPerBlock * h->num_cus) {
+            TilePlan p;
+            const mspmv_status st = build_slab_plan(h, p, kSellAutoNnzPerBlock, 2, true);
+            if (st == MSPMV_OK && p.slab->x_bytes_per_nnz <= kSlabAutoBytes) {
+                h->plans.emplace(kSlabPlanKey, p);
+                h->spmv_slab = 1;
+                return MSPMV_OK;
+            }
+            free_plan(p);  // optional plan: any failure keeps the tiles
+            set_error("");
+            (void)hipGetLastError();
+        }
+        return MSPMV_OK;
+    }
     if (!cand)
         return MSPMV_OK;
     TilePlan p;
     // automatic: the blocks-per-nonzero test runs inside the builder before anything past the bounds is
     // copied or allocated, and any failure (an allocation near capacity included) means "no slab plan":
     // the workgroup plan is ready, so the product must not fail for an optional plan
-    const mspmv_status st = build_slab_plan(h, p, sw < 0 ? kSlabAutoNnzPerBlock : 0.0, sw == 2 ? 1 : 0, sw >= 2);
+    const mspmv_status st = build_slab_plan(h, p, sw < 0 ? kSlabAutoNnzPerBlock : 0.0, sw == 2 ? 1 : sw == 4 ? 2 : 0, sw >= 2);
     if (st != MSPMV_OK && (sw < 0 || st == MSPMV_ERR_UNSUPPORTED)) {
         free_plan(p);
         set_error("");
@@ -733,14 +772,7 @@ static mspmv_status spmv_plan(mspmv_handle_s *h, const TilePlan **out)
     }
     if (h->spmv_onewave < 0) {
         bool want = false;
-        if (wg->lanes == kBlock && wg->num_tiles >= 64 && !wg->d_blk) {
-            std::vector<unsigned char> hm((size_t)wg->num_tiles);
-            HIP_TRY(hipMemcpy(hm.data(), wg->d_modes[0], hm.size(), hipMemcpyDeviceToHost));
-            long long walk = 0;
-            for (unsigned char v : hm)
-                walk += v == 0;
-            want = 2 * walk >= (long long)wg->num_tiles;  // most tiles merge walks
-        }
+        ST_TRY(mostly_walks(wg, &want));
         if (want) {
             const TilePlan *np = nullptr;
             const int key = -64 * spmv_items_per_thread();  // build_plan's key for one-wave plans

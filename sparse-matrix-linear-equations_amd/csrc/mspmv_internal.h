@@ -47,9 +47,18 @@ struct SlabCfg {
     int entries;  // row runs per chunk
     int per_cu;   // resident blocks per CU
 };
-constexpr SlabCfg kSlabCfgs[2] = {{kSlabThreads, kSlabCols, kSlabRows, kSlabChunk, kSlabEntries, kSlabBlocksPerCu},
-                                  {1024, 8192, 4095, 4096, 2048, 1}};
+// 2: the column-group blocks of 1 in sliced-ELL form (k_spmv_sell): per (block, slab) the short runs, sorted
+// by length, in slices of 64 whose values sit column-major (lane = run), long runs apart.
+constexpr SlabCfg kSlabCfgs[3] = {{kSlabThreads, kSlabCols, kSlabRows, kSlabChunk, kSlabEntries, kSlabBlocksPerCu},
+                                  {1024, 8192, 4095, 4096, 2048, 1},
+                                  {1024, 8192, 4095, 0, 0, 1}};
 constexpr int kSlabGroups = 4;
+constexpr int kSlabMaxGroups = 8;
+constexpr int kSellShortRun = 8;     // sliced-ELL: runs up to this long sit one per lane in slices of 64,
+constexpr int kSellLongRun = 64;     // up to this long 8 per slice (8 lanes each), longer ones by whole waves
+                                     // in pieces of <= 512
+constexpr int kSellMaxPieces = 1024;  // long-run pieces per (block, slab) segment (their sums sit in LDS)
+constexpr int kSellMaxSegs = 255;     // segments per block (their descriptors sit in LDS)
 constexpr int kSlabLongRun = 64;  // runs longer than this are summed by whole waves (listed first in a chunk)
 struct SlabData {
     int L = 1;                          // 1: the SpMV's plan (k_spmv_slab); 8 / 16: an SpMM plan (k_spmm_slab)
@@ -58,6 +67,11 @@ struct SlabData {
     int groups = 1;                     // SpMV column groups (cfg 1): blocks = row blocks x groups
     double *d_part = nullptr;           // [groups][m] the groups' partial row sums (groups > 1)
     unsigned *d_gcnt = nullptr;         // [row blocks] tickets of the fold (self-resetting)
+    // sliced-ELL (cfg 2): d_chunk holds the (block, slab) segments {slab, slice0, slice1, piece0} (+ sentinel)
+    int2 *d_slice = nullptr;            // [slices] {value base, slots per lane | medium << 16}
+    unsigned *d_sent = nullptr;         // [slices][64] row in block | run length << 16 (0: no run)
+    int4 *d_long = nullptr;             // [long-run pieces] {value base, length <= 512, row in block,
+                                        //  the run's first piece in the segment | pieces << 16}
     int num_chunks = 0, num_entries = 0;
     int4 *d_blk = nullptr;              // [blocks] {first row, rows ending in the block, chunk0, chunk1}
     int4 *d_chunk = nullptr;            // [chunks + 1] SpMV: {stream start, length | lanes_log2 << 13 | long runs << 16,

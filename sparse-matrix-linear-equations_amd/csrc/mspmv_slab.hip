@@ -43,6 +43,9 @@ struct SlabArgs {
     int m;
     double *part;               // [groups][m] partial row sums (groups > 1)
     unsigned *gcnt;             // [row blocks] fold tickets
+    const int2 *slice;          // sliced-ELL (k_spmv_sell): SlabData::d_slice, d_sent, d_long
+    const unsigned *sent;
+    const int4 *lng;
     // split rows (close_split_rows reads these names)
     const int2 *bounds;
     const unsigned char *split;
@@ -59,6 +62,41 @@ __device__ __forceinline__ T slab_stream(const T *p)
     if (NT)
         return __builtin_nontemporal_load(p);
     return *p;
+}
+
+// A column group's partial row sums (agent scope), then, by the row block's last group to finish (a
+// ticket per row block, reset by it), y = the groups' partials added in group order (fixed order).
+template <int TB>
+__device__ __forceinline__ void group_out(const SlabArgs &a, int b, int r0, int nrows, const double *yacc)
+{
+    const int tid = threadIdx.x;
+    const int G = a.groups, g = b % G, rb = b / G;
+    for (int i = tid; i < nrows; i += TB)
+        store_sc1(&a.part[(size_t)g * a.m + r0 + i], yacc[i]);
+    __shared__ int s_last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this group's partials are out
+    __syncthreads();
+    if (tid == 0)
+        s_last = __hip_atomic_fetch_add(&a.gcnt[rb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                 (unsigned)(G - 1);
+    __syncthreads();
+    if (!s_last)
+        return;
+    // (agent-scope loads, all issued before the sum; __threadfence() pairs instead cost 100+ us, r05ao)
+    for (int i = tid; i < nrows; i += TB) {
+        double pv[kSlabMaxGroups];
+#pragma unroll
+        for (int q = 0; q < kSlabMaxGroups; ++q)
+            pv[q] = q < G && q != g ? load_sc1(&a.part[(size_t)q * a.m + r0 + i]) : 0.0;
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < kSlabMaxGroups; ++q)
+            if (q < G)
+                s += q == g ? yacc[i] : pv[q];
+        a.y[r0 + i] = s;
+    }
+    if (tid == 0)
+        __hip_atomic_store(&a.gcnt[rb], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <bool NT, int CFG>
@@ -199,28 +237,8 @@ __global__ __launch_bounds__(kSlabCfgs[CFG].threads) void k_spmv_slab(SlabArgs a
         if (ci + 1 < bd.w)
             process(ci + 1, rb);
     }
-    if (a.groups > 1) {  // block-uniform: a column group's partial row sums, folded by the last group
-        const int G = a.groups, g = b % G, rb = b / G;
-        for (int i = tid; i < nrows; i += TB)
-            store_sc1(&a.part[(size_t)g * a.m + bd.x + i], yacc[i]);
-        __shared__ int s_last;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this group's partials are out
-        __syncthreads();
-        if (tid == 0)
-            s_last = __hip_atomic_fetch_add(&a.gcnt[rb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                     (unsigned)(G - 1);
-        __syncthreads();
-        if (!s_last)
-            return;
-        // the row block's last group to finish: y = the groups' partials in group order (fixed order)
-        for (int i = tid; i < nrows; i += TB) {
-            double s = 0.0;
-            for (int q = 0; q < G; ++q)
-                s += q == g ? yacc[i] : load_sc1(&a.part[(size_t)q * a.m + bd.x + i]);
-            a.y[bd.x + i] = s;
-        }
-        if (tid == 0)
-            __hip_atomic_store(&a.gcnt[rb], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.groups > 1) {  // block-uniform
+        group_out<TB>(a, b, bd.x, nrows, yacc);
         return;
     }
     // rows ending in the block; its first row goes to the head slot when it completes a split row
@@ -229,6 +247,198 @@ __global__ __launch_bounds__(kSlabCfgs[CFG].threads) void k_spmv_slab(SlabArgs a
     if (tail && tid == 0)
         store_sc1(&a.carry_val[b], yacc[nrows]);
     close_split_rows<TB>(a, b, fx, 1, 1);
+}
+
+// Sliced-ELL form of the column-group blocks (kSlabCfgs[2]): per (block, slab) segment, the slab of x is
+// staged in LDS once (the next segment's slab prefetched in registers meanwhile), then each wave takes
+// slices of 64 runs -- lane = run, the run's values column-major in the slice, so every load of the
+// stream is coalesced and no product passes through LDS; the next slice's values and the one after's
+// header and runs are loaded while this one computes -- continuing its row's sum from yacc in the run's CSR order (a row's
+// runs follow slab order: within a group the row sum is the CSR-order sum when its columns ascend).
+// Runs longer than kSellLongRun come in pieces of <= 512 values, one wave each (8 loads per lane, xor
+// butterfly) into lpart; after a barrier each run's pieces are added to its row in piece order.
+template <bool NT>
+__global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
+{
+    constexpr SlabCfg C = kSlabCfgs[2];
+    constexpr int TB = C.threads, NW = TB / 64, XPT = C.cols / TB;
+    __shared__ double xs[C.cols];
+    __shared__ double yacc[C.rows + 1];
+    __shared__ double lpart[kSellMaxPieces];
+    __shared__ int4 sseg[kSellMaxSegs + 1];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int b = xcd_tile(blockIdx.x, a.num_tiles);
+    const int4 bd = a.blk[b];  // {first row, rows, segment0, segment1}
+    const int nrows = bd.y;
+    // the block's segment descriptors (and the next one's piece start) in LDS: a scalar load at each
+    // segment's head put its round trip in every segment (~2 us each, r05ao)
+    if (tid <= bd.w - bd.z)
+        sseg[tid] = a.chunk[bd.z + tid];
+    for (int i = tid; i < nrows; i += TB)
+        yacc[i] = 0.0;
+    __syncthreads();
+    auto segd = [&](int sg) {  // block-uniform
+        const int4 c = sseg[sg - bd.z];
+        return make_int4(__builtin_amdgcn_readfirstlane(c.x), __builtin_amdgcn_readfirstlane(c.y),
+                         __builtin_amdgcn_readfirstlane(c.z), __builtin_amdgcn_readfirstlane(c.w));
+    };
+    double xq[XPT];
+    auto fetch_x = [&](int slab) {
+        const int c0 = slab * C.cols;
+#pragma unroll
+        for (int j = 0; j < XPT; ++j) {
+            const int col = c0 + tid + j * TB;
+            xq[j] = col < a.n ? a.x[col] : 0.0;
+        }
+    };
+    struct Sl {
+        double v[8];
+        unsigned short c[8];
+    };
+    auto meta = [&](int qq, int2 &hq, unsigned &ev) {  // qq < 0: none
+        hq = qq >= 0 ? a.slice[qq] : make_int2(0, 0);
+        ev = qq >= 0 ? a.sent[(size_t)qq * 64 + lane] : 0u;
+    };
+    auto load8 = [&](const int2 &hq, Sl &d) {
+        const double *vp = a.val + hq.x + lane;
+        const unsigned short *cp = a.col + hq.x + lane;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const bool in = j < (hq.y & 0xffff);  // wave-uniform: the slice's slots
+            d.v[j] = in ? slab_stream<NT>(vp + 64 * j) : 0.0;
+            d.c[j] = in ? slab_stream<NT>(cp + 64 * j) : (unsigned short)0;
+        }
+    };
+    // the wave's slice after slice q of segment s: q + NW in s, else its first one in s + 1 (-1: none)
+    auto nxt = [&](int q, int s, int &qn, int &sn) {
+        qn = -1;
+        sn = s;
+        if (q < 0)
+            return;
+        if (q + NW < segd(s).z) {
+            qn = q + NW;
+            return;
+        }
+        if (s + 1 < bd.w) {
+            const int4 ns = segd(s + 1);
+            if (ns.y + wave < ns.z) {
+                qn = ns.y + wave;
+                sn = s + 1;
+            }
+        }
+    };
+    int qa = -1, sa = -1, qb = -1, sb = -1;
+    int2 h0 = make_int2(0, 0), h1 = make_int2(0, 0);
+    unsigned e0 = 0, e1 = 0;
+    Sl d0, d1;
+    if (bd.z < bd.w)
+        fetch_x(segd(bd.z).x);
+    for (int sg = bd.z; sg < bd.w; ++sg) {  // block-uniform
+        const int4 seg = segd(sg);
+        const int p0 = seg.w, p1 = segd(sg + 1).w;
+        __syncthreads();  // the previous segment's readers of xs (and its folds) are done
+#pragma unroll
+        for (int j = 0; j < XPT; ++j)
+            xs[tid + j * TB] = xq[j];
+        __syncthreads();
+        if (sg + 1 < bd.w)
+            fetch_x(segd(sg + 1).x);
+        // long runs first (their loads in flight behind the slices of other waves): pieces of <= 512 values
+        for (int u = p0 + wave; u < p1; u += NW) {  // wave-uniform
+            const int4 pc = a.lng[u];
+            double v[8];
+            unsigned short c[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int k = lane + 64 * j;
+                v[j] = k < pc.y ? slab_stream<NT>(a.val + pc.x + k) : 0.0;
+                c[j] = k < pc.y ? slab_stream<NT>(a.col + pc.x + k) : (unsigned short)0;
+            }
+            double s = 0.0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const double pv = v[j] * xs[c[j]];
+                s += lane + 64 * j < pc.y ? pv : 0.0;
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1)
+                s += __shfl_xor(s, o);
+            if (lane == 0)
+                lpart[u - p0] = s;
+        }
+        // slices, software-pipelined per wave and across segments: while slice qa computes, the wave's
+        // next slice's values and the one after's header and runs are in flight -- at a segment's end
+        // those are the next segment's first slices, so the pipeline refills during the x-stage barriers
+        if (sa != sg) {  // prime: the wave's first slice of this segment
+            qa = seg.y + wave < seg.z ? seg.y + wave : -1;
+            sa = sg;
+            meta(qa, h0, e0);
+            load8(h0, d0);
+            nxt(qa, sa, qb, sb);
+            meta(qb, h1, e1);
+        }
+        while (qa >= 0 && sa == sg) {  // wave-uniform
+            load8(h1, d1);
+            int qc, sc;
+            int2 h2;
+            unsigned e2;
+            nxt(qb, sb, qc, sc);
+            meta(qc, h2, e2);
+            const int row = (int)(e0 & 0xffffu), len = (int)(e0 >> 16);
+            if (!(h0.y >> 16)) {  // wave-uniform: a slice of 64 short runs, lane = run, in CSR order
+                double acc = len > 0 ? yacc[row] : 0.0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const double pv = d0.v[j] * xs[d0.c[j]];
+                    acc += j < len ? pv : 0.0;  // acc never -0.0 (sums start at +0.0): adding +0.0 is exact
+                }
+                if (len > 0)
+                    yacc[row] = acc;
+            } else {  // 8 medium runs, 8 lanes each: lane-strided sums, a fixed xor butterfly
+                double s = 0.0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const double pv = d0.v[j] * xs[d0.c[j]];
+                    s += 8 * j + (lane & 7) < len ? pv : 0.0;
+                }
+                s += __shfl_xor(s, 1);
+                s += __shfl_xor(s, 2);
+                s += __shfl_xor(s, 4);
+                if ((lane & 7) == 0 && len > 0)
+                    yacc[row] += s;
+            }
+            qa = qb;
+            sa = sb;
+            h0 = h1;
+            e0 = e1;
+            d0 = d1;
+            qb = qc;
+            sb = sc;
+            h1 = h2;
+            e1 = e2;
+        }
+        if (p1 > p0) {  // block-uniform: each run's pieces, in order, onto its row
+            __syncthreads();
+            for (int i = tid; i < p1 - p0; i += TB) {
+                const int4 pc = a.lng[p0 + i];
+                const int first = pc.w & 0xffff, np = pc.w >> 16;
+                if (i == first) {
+                    double s = yacc[pc.z];
+                    for (int q = 0; q < np; ++q)
+                        s += lpart[first + q];
+                    yacc[pc.z] = s;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (a.groups > 1) {  // block-uniform
+        group_out<TB>(a, b, bd.x, nrows, yacc);
+        return;
+    }
+    for (int i = tid; i < nrows; i += TB)
+        a.y[bd.x + i] = yacc[i];
 }
 
 hipError_t launch_slab(mspmv_handle_s *h, const TilePlan &plan, const double *d_x, double *d_y)
@@ -255,10 +465,20 @@ hipError_t launch_slab(mspmv_handle_s *h, const TilePlan &plan, const double *d_
     a.m = h->m;
     a.part = s.d_part;
     a.gcnt = s.d_gcnt;
+    a.slice = s.d_slice;
+    a.sent = s.d_sent;
+    a.lng = s.d_long;
     if (plan.num_tiles == 0)
         return hipSuccess;
     const bool nt = stream_nt(h);
     const dim3 grid(plan.num_tiles);
+    if (s.cfg == 2) {
+        if (nt)
+            hipLaunchKernelGGL((k_spmv_sell<true>), grid, dim3(kSlabCfgs[2].threads), 0, h->stream, a);
+        else
+            hipLaunchKernelGGL((k_spmv_sell<false>), grid, dim3(kSlabCfgs[2].threads), 0, h->stream, a);
+        return hipGetLastError();
+    }
     const dim3 b1(kSlabCfgs[1].threads), b0(kSlabCfgs[0].threads);
     if (s.cfg == 1 && nt)
         hipLaunchKernelGGL((k_spmv_slab<true, 1>), grid, b1, 0, h->stream, a);
@@ -275,6 +495,8 @@ std::string slab_kernel_name(const mspmv_handle_s *h)
 {
     const auto it = h->plans.find(kSlabPlanKey);
     const int cfg = it != h->plans.end() && it->second.slab ? it->second.slab->cfg : 0;
+    if (cfg == 2)
+        return std::string("k_spmv_sell<") + (stream_nt(h) ? "true" : "false") + ">";
     return std::string("k_spmv_slab<") + (stream_nt(h) ? "true" : "false") + "," + std::to_string(cfg) + ">";
 }
 
@@ -297,6 +519,9 @@ void free_slab(SlabData *s)
     slab_free(s->d_col);
     slab_free(s->d_part);
     slab_free(s->d_gcnt);
+    slab_free(s->d_slice);
+    slab_free(s->d_sent);
+    slab_free(s->d_long);
     delete s;
 }
 
@@ -557,6 +782,205 @@ static mspmv_status slab_finish(mspmv_handle_s *h, TilePlan &p, int cfg, int gro
     return plan_split_rows(p, hb, hs);
 }
 
+// Sliced-ELL layout of one column-group block (rows [r0, r1), columns [lo, hi)): per slab touched, in
+// slab order, its runs of one row (CSR order); runs longer than kSellLongRun stored contiguously and
+// listed apart in pieces of <= 512 values, the others sorted by length (longest first, rows ascending among equals) and cut into
+// slices of 64, value j of the slice's run i at slot j * 64 + i (slots past a run's length: zeros, never
+// added).  Bases relative to the block.
+struct SellBlockOut {
+    std::vector<int4> segs;
+    std::vector<int2> slices;
+    std::vector<unsigned> sents;
+    std::vector<int4> longs;
+    std::vector<double> val;
+    std::vector<unsigned short> col;
+    long long staged = 0;
+    bool too_many = false;  // a segment with more long-run pieces than the kernel's LDS table holds
+};
+
+static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, const std::vector<double> &va, int r0,
+                       int r1, int lo, int hi, SellBlockOut &o)
+{
+    const int W = kSlabCfgs[2].cols;
+    std::vector<int> ks, kr;
+    int smin = 0x7fffffff, smax = -1;
+    for (int r = r0; r < r1; ++r)
+        for (int k = ro[(size_t)r]; k < ro[(size_t)r + 1]; ++k)
+            if (ci[(size_t)k] >= lo && ci[(size_t)k] < hi) {
+                ks.push_back(k);
+                kr.push_back(r - r0);
+                smin = std::min(smin, ci[(size_t)k] / W);
+                smax = std::max(smax, ci[(size_t)k] / W);
+            }
+    if (ks.empty())
+        return;
+    const int ns = smax - smin + 1;
+    std::vector<int> off((size_t)ns + 1, 0);
+    for (int k : ks)
+        ++off[(size_t)(ci[(size_t)k] / W - smin) + 1];
+    for (int s = 0; s < ns; ++s)
+        off[(size_t)s + 1] += off[(size_t)s];
+    std::vector<int> ord(ks.size()), put(off.begin(), off.end() - 1);
+    for (size_t i = 0; i < ks.size(); ++i)
+        ord[(size_t)put[(size_t)(ci[(size_t)ks[i]] / W - smin)]++] = (int)i;  // stable: CSR order per slab
+    struct Run {
+        int row, first, len;
+    };
+    for (int s = 0; s < ns; ++s) {
+        const int q0 = off[(size_t)s], q1 = off[(size_t)s + 1];
+        if (q0 == q1)
+            continue;
+        std::vector<Run> runs;
+        for (int q = q0; q < q1;) {
+            int e = q;
+            while (e < q1 && kr[(size_t)ord[(size_t)e]] == kr[(size_t)ord[(size_t)q]])
+                ++e;
+            runs.push_back({kr[(size_t)ord[(size_t)q]], q, e - q});
+            q = e;
+        }
+        const int slab = smin + s;
+        auto put_val = [&](size_t at, int q) {
+            const int k = ks[(size_t)ord[(size_t)q]];
+            o.val[at] = va[(size_t)k];
+            o.col[at] = (unsigned short)(ci[(size_t)k] - slab * W);
+        };
+        const int slice0 = (int)o.slices.size(), long0 = (int)o.longs.size();
+        std::vector<Run> shorts, mediums;
+        for (const Run &r : runs) {
+            if (r.len > kSellShortRun && r.len <= kSellLongRun) {
+                mediums.push_back(r);
+            } else if (r.len > kSellLongRun) {  // pieces of <= 512 values: {base, length, row, first | count << 16}
+                const size_t base = o.val.size();
+                o.val.resize(base + r.len, 0.0);
+                o.col.resize(base + r.len, 0);
+                for (int j = 0; j < r.len; ++j)
+                    put_val(base + j, r.first + j);
+                const int np = (r.len + 511) / 512, first = (int)o.longs.size() - long0;
+                for (int q = 0; q < np; ++q)
+                    o.longs.push_back(make_int4((int)base + 512 * q, std::min(512, r.len - 512 * q), r.row,
+                                                first | (np << 16)));
+            } else {
+                shorts.push_back(r);
+            }
+        }
+        if ((int)o.longs.size() - long0 > kSellMaxPieces)
+            o.too_many = true;
+        std::stable_sort(shorts.begin(), shorts.end(), [](const Run &x, const Run &y) { return x.len > y.len; });
+        for (size_t i0 = 0; i0 < shorts.size(); i0 += 64) {
+            const int n = (int)std::min<size_t>(64, shorts.size() - i0);
+            const int Lm = shorts[i0].len;
+            const size_t base = o.val.size();
+            o.val.resize(base + (size_t)Lm * 64, 0.0);
+            o.col.resize(base + (size_t)Lm * 64, 0);
+            for (int i = 0; i < 64; ++i) {
+                if (i >= n) {
+                    o.sents.push_back(0u);
+                    continue;
+                }
+                const Run &r = shorts[i0 + (size_t)i];
+                for (int j = 0; j < r.len; ++j)
+                    put_val(base + (size_t)j * 64 + i, r.first + j);
+                o.sents.push_back((unsigned)r.row | ((unsigned)r.len << 16));
+            }
+            o.slices.push_back(make_int2((int)base, Lm));
+        }
+        // medium runs: 8 per slice, 8 lanes each -- value j of the slice's run r at slot j / 8, lane
+        // 8 r + j % 8 (header length | 1 << 16: slots per lane, the medium flag)
+        std::stable_sort(mediums.begin(), mediums.end(), [](const Run &x, const Run &y) { return x.len > y.len; });
+        for (size_t i0 = 0; i0 < mediums.size(); i0 += 8) {
+            const int n = (int)std::min<size_t>(8, mediums.size() - i0);
+            const int Lm = (mediums[i0].len + 7) / 8;
+            const size_t base = o.val.size();
+            o.val.resize(base + (size_t)Lm * 64, 0.0);
+            o.col.resize(base + (size_t)Lm * 64, 0);
+            for (int i = 0; i < 8; ++i) {
+                const Run *r = i < n ? &mediums[i0 + (size_t)i] : nullptr;
+                if (r)
+                    for (int j = 0; j < r->len; ++j)
+                        put_val(base + (size_t)(j / 8) * 64 + 8 * i + j % 8, r->first + j);
+                for (int l = 0; l < 8; ++l)
+                    o.sents.push_back(r ? (unsigned)r->row | ((unsigned)r->len << 16) : 0u);
+            }
+            o.slices.push_back(make_int2((int)base, Lm | (1 << 16)));
+        }
+        o.segs.push_back(make_int4(slab, slice0, (int)o.slices.size(), long0));
+        o.staged += (long long)W * 8;
+    }
+}
+
+static mspmv_status sell_finish(mspmv_handle_s *h, TilePlan &p, const std::vector<int> &rbs, int G, int spg,
+                                const std::vector<int> &ro, const std::vector<int> &ci, const std::vector<double> &va,
+                                const std::vector<int2> &hb, const std::vector<unsigned char> &hs)
+{
+    const int W = kSlabCfgs[2].cols, T = p.num_tiles;
+    std::vector<SellBlockOut> outs((size_t)T);
+#pragma omp parallel for schedule(dynamic, 2)
+    for (int t = 0; t < T; ++t) {
+        const int rb = t / G, g = t % G;
+        const int lo = std::min(h->n, g * spg * W), hi = g == G - 1 ? 0x7fffffff : std::min(h->n, (g + 1) * spg * W);
+        sell_block(ro, ci, va, rbs[(size_t)rb], rbs[(size_t)rb + 1], lo, hi, outs[(size_t)t]);
+    }
+    std::vector<int4> blk((size_t)T), segs, longs;
+    std::vector<int2> slices;
+    std::vector<unsigned> sents;
+    std::vector<double> val;
+    std::vector<unsigned short> col;
+    long long staged = 0;
+    for (int t = 0; t < T; ++t) {
+        const SellBlockOut &o = outs[(size_t)t];
+        if (o.too_many || (int)o.segs.size() > kSellMaxSegs || val.size() + o.val.size() > (size_t)0x7fffff00)
+            return MSPMV_ERR_UNSUPPORTED;
+        const int vb = (int)val.size(), sb = (int)slices.size(), lb = (int)longs.size(), g0 = (int)segs.size();
+        for (int4 s : o.segs)
+            segs.push_back(make_int4(s.x, s.y + sb, s.z + sb, s.w + lb));
+        for (int2 s : o.slices)
+            slices.push_back(make_int2(s.x + vb, s.y));
+        for (int4 l : o.longs)
+            longs.push_back(make_int4(l.x + vb, l.y, l.z, l.w));
+        sents.insert(sents.end(), o.sents.begin(), o.sents.end());
+        val.insert(val.end(), o.val.begin(), o.val.end());
+        col.insert(col.end(), o.col.begin(), o.col.end());
+        const int rb = t / G;
+        blk[(size_t)t] = make_int4(rbs[(size_t)rb], rbs[(size_t)rb + 1] - rbs[(size_t)rb], g0, (int)segs.size());
+        staged += o.staged;
+    }
+    segs.push_back(make_int4(0, 0, 0, (int)longs.size()));  // sentinel: the last segment's long-run end
+    SlabData *s = new SlabData();
+    s->cfg = 2;
+    s->groups = G;
+    s->num_chunks = (int)segs.size() - 1;
+    s->num_entries = (int)longs.size();
+    s->x_bytes_per_nnz = (double)staged / (double)h->nnz;
+    p.slab = s;
+    mspmv_status st;
+    if ((st = slab_upload(&s->d_blk, blk)) != MSPMV_OK || (st = slab_upload(&s->d_chunk, segs)) != MSPMV_OK ||
+        (st = slab_upload(&s->d_slice, slices)) != MSPMV_OK || (st = slab_upload(&s->d_sent, sents)) != MSPMV_OK ||
+        (st = slab_upload(&s->d_long, longs)) != MSPMV_OK || (st = slab_upload(&s->d_val, val, kNnzPad)) != MSPMV_OK ||
+        (st = slab_upload(&s->d_col, col, kNnzPad)) != MSPMV_OK)
+        return st;
+    if (G > 1) {
+        const std::vector<unsigned> zero((size_t)T / G, 0u);
+        if ((st = slab_upload(&s->d_gcnt, zero)) != MSPMV_OK)
+            return st;
+        if (hipMalloc((void **)&s->d_part, sizeof(double) * (size_t)G * h->m) != hipSuccess) {
+            s->d_part = nullptr;
+            set_error("column-slab plan: hipMalloc failed");
+            return MSPMV_ERR_HIP;
+        }
+    }
+    p.carry_L = 16;
+    if (hipMalloc((void **)&p.d_carry_val, sizeof(double) * (size_t)T * 16 * 3) != hipSuccess ||
+        hipMalloc((void **)&p.d_modes[0], (size_t)T) != hipSuccess) {
+        set_error("column-slab plan: hipMalloc failed");
+        return MSPMV_ERR_HIP;
+    }
+    if (hipMemset(p.d_modes[0], 255, (size_t)T) != hipSuccess) {
+        set_error("column-slab plan: memset failed");
+        return MSPMV_ERR_HIP;
+    }
+    return plan_split_rows(p, hb, hs);
+}
+
 // Column-group blocks (kSlabCfgs[1]): whole-row blocks of ~(m + nnz) / R merge items (<= C.rows rows),
 // R = the resident blocks / groups, each crossed with the groups' column ranges (consecutive slabs);
 // block t = row block t / G, group t % G.  The reported bounds give each row block to its first group
@@ -566,7 +990,7 @@ static mspmv_status build_slab_group_plan(mspmv_handle_s *h, TilePlan &p, double
     const SlabCfg &C = kSlabCfgs[cfg];
     const int nslabs = (h->n + C.cols - 1) / C.cols;
     const char *ge = getenv("MSPMV_SLAB_GROUPS");  // lab: the column-group count
-    const int G = std::max(1, std::min(ge && *ge ? atoi(ge) : kSlabGroups, nslabs));
+    const int G = std::max(1, std::min(std::min(ge && *ge ? atoi(ge) : kSlabGroups, kSlabMaxGroups), nslabs));
     const int spg = (nslabs + G - 1) / G;  // slabs per group
     const long long R0 = std::max(1, h->num_cus * C.per_cu / G);
     std::vector<int> ro, ci;
@@ -577,24 +1001,39 @@ static mspmv_status build_slab_group_plan(mspmv_handle_s *h, TilePlan &p, double
         set_error("column-slab plan: row offsets download failed");
         return MSPMV_ERR_HIP;
     }
-    const long long target = ((long long)h->m + h->nnz + R0 - 1) / R0;
-    std::vector<int> rbs{0};
-    long long items = 0;
-    int rows = 0;
-    for (int r = 0; r < h->m; ++r) {
-        if (rows == C.rows) {
-            rbs.push_back(r);
-            items = 0;
-            rows = 0;
+    // whole-row blocks of at most C.rows rows, R0 of them with the smallest possible largest block (in
+    // rows + nonzeros): the least bound B whose greedy cut needs <= R0 blocks (binary search), so a hub
+    // row sets B only as far as its own length
+    auto cut = [&](long long B, std::vector<int> *out) {
+        long long items = 0, blocks = 1;
+        int rows = 0;
+        for (int r = 0; r < h->m; ++r) {
+            const long long it = 1 + (long long)ro[(size_t)r + 1] - ro[(size_t)r];
+            if (rows > 0 && (rows == C.rows || items + it > B)) {
+                if (out)
+                    out->push_back(r);
+                ++blocks;
+                items = 0;
+                rows = 0;
+            }
+            items += it;
+            ++rows;
         }
-        items += 1 + (long long)ro[(size_t)r + 1] - ro[(size_t)r];
-        ++rows;
-        if (items >= target && r + 1 < h->m) {  // cut after the row that reaches the target: <= R0 blocks
-            rbs.push_back(r + 1);
-            items = 0;
-            rows = 0;
-        }
+        return blocks;
+    };
+    long long lo_b = ((long long)h->m + h->nnz + R0 - 1) / R0, hi_b = (long long)h->m + h->nnz;
+    for (int r = 0; r < h->m; ++r)
+        lo_b = std::max(lo_b, 1 + (long long)ro[(size_t)r + 1] - ro[(size_t)r]);
+    while (lo_b < hi_b) {
+        const long long mid = lo_b + (hi_b - lo_b) / 2;
+        if (cut(mid, nullptr) <= R0)
+            hi_b = mid;
+        else
+            lo_b = mid + 1;
     }
+    const long long target = lo_b;
+    std::vector<int> rbs{0};
+    cut(target, &rbs);
     rbs.push_back(h->m);
     const int R = (int)rbs.size() - 1;
     const long long Tl = (long long)R * G;
@@ -603,6 +1042,29 @@ static mspmv_status build_slab_group_plan(mspmv_handle_s *h, TilePlan &p, double
     const int T = (int)Tl;
     if ((st0 = slab_host_matrix(h, ro, ci, va)) != MSPMV_OK)
         return st0;
+    std::vector<int2> hb((size_t)T + 1);
+    for (int t = 0; t < T; ++t) {
+        const int r = rbs[(size_t)(t / G) + (t % G == 0 ? 0 : 1)];
+        hb[(size_t)t] = make_int2(r, ro[(size_t)r]);
+    }
+    hb[(size_t)T] = make_int2(h->m, h->nnz);
+    const std::vector<unsigned char> hs((size_t)T + 1, 0);
+    if (hipMalloc((void **)&p.d_bounds, sizeof(int2) * hb.size()) != hipSuccess ||
+        hipMalloc((void **)&p.d_split, hs.size()) != hipSuccess) {
+        set_error("column-slab plan: hipMalloc failed");
+        return MSPMV_ERR_HIP;
+    }
+    if (hipMemcpy(p.d_bounds, hb.data(), sizeof(int2) * hb.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(p.d_split, hs.data(), hs.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        set_error("column-slab plan: upload failed");
+        return MSPMV_ERR_HIP;
+    }
+    p.num_tiles = T;
+    p.lanes = C.threads;
+    p.tile_items = (int)std::min<long long>(target, 0x7fffffff);
+    p.snap = 0;
+    if (cfg == 2)
+        return sell_finish(h, p, rbs, G, spg, ro, ci, va, hb, hs);
     auto crange = [&](int g, int &lo, int &hi) {
         lo = std::min(h->n, g * spg * C.cols);
         hi = g == G - 1 ? 0x7fffffff : std::min(h->n, (g + 1) * spg * C.cols);
@@ -631,27 +1093,6 @@ static mspmv_status build_slab_group_plan(mspmv_handle_s *h, TilePlan &p, double
                    ocol.data(), outs[(size_t)t]);
         blk[(size_t)t] = make_int4(r0, r1 - r0, 0, 0);
     }
-    std::vector<int2> hb((size_t)T + 1);
-    for (int t = 0; t < T; ++t) {
-        const int r = rbs[(size_t)(t / G) + (t % G == 0 ? 0 : 1)];
-        hb[(size_t)t] = make_int2(r, ro[(size_t)r]);
-    }
-    hb[(size_t)T] = make_int2(h->m, h->nnz);
-    const std::vector<unsigned char> hs((size_t)T + 1, 0);
-    if (hipMalloc((void **)&p.d_bounds, sizeof(int2) * hb.size()) != hipSuccess ||
-        hipMalloc((void **)&p.d_split, hs.size()) != hipSuccess) {
-        set_error("column-slab plan: hipMalloc failed");
-        return MSPMV_ERR_HIP;
-    }
-    if (hipMemcpy(p.d_bounds, hb.data(), sizeof(int2) * hb.size(), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(p.d_split, hs.data(), hs.size(), hipMemcpyHostToDevice) != hipSuccess) {
-        set_error("column-slab plan: upload failed");
-        return MSPMV_ERR_HIP;
-    }
-    p.num_tiles = T;
-    p.lanes = C.threads;
-    p.tile_items = (int)std::min<long long>(target, 0x7fffffff);
-    p.snap = 0;
     return slab_finish(h, p, cfg, G, blk, outs, oval, ocol, hb, hs);
 }
 
@@ -659,7 +1100,7 @@ mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p, double min_nnz_per_
 {
     if (h->m <= 0 || h->nnz <= 0)
         return MSPMV_ERR_UNSUPPORTED;
-    if (cfg == 1 || groups)
+    if (cfg >= 1 || groups)
         return build_slab_group_plan(h, p, min_nnz_per_block, cfg);
     std::vector<int2> hb;
     std::vector<unsigned char> hs;

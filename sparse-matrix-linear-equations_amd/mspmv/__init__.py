@@ -504,8 +504,12 @@ class GpuCsr:
         _check(lib.mspmv_dspmm(self.h, _ptr(X), _ptr(Y), L), "dspmm")
         return Y
 
-    def spmm_dev(self, dX: DeviceBuffer, dY: DeviceBuffer, L: int = 1):
+    def spmm_dev(self, dX: DeviceBuffer, dY: DeviceBuffer, L: int = 1, sync: bool = True):
+        """Y = A X on device buffers: mspmv_dspmm_dev runs on the handle's (non-blocking) stream, so the
+        result is complete only after a sync -- done here unless sync=False."""
         _check(lib.mspmv_dspmm_dev(self.h, dX.ptr, dY.ptr, L), "dspmm_dev")
+        if sync:
+            self.sync()
 
     def time_spmm(self, dX: DeviceBuffer, dY: DeviceBuffer, L: int, reps: int, flush_bytes: int = 0):
         """(avg ms per call, avg ms of the tile kernel, kernels per call), HIP events."""

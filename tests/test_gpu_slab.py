@@ -1,13 +1,14 @@
 """Column-slab SpMV (mspmv_slab.hip): blocks of a CU's share of the merge path, each block's nonzeros
 reordered by 4,096-column slab of x (staged in LDS), rows accumulated in LDS in slab order.
 
-Forced with MSPMV_SPMV_SLAB=1 (merge-path blocks) and =2 (column-group blocks whose partial row sums the
-row block's last group folds; read when a handle first decides its plain-SpMV plan) on shapes with
+Forced with MSPMV_SPMV_SLAB=1 (merge-path blocks), =2 (column-group blocks whose partial row sums the
+row block's last group folds) and =4 (the column-group blocks in sliced-ELL form, k_spmv_sell; read when a
+handle first decides its plain-SpMV plan) on shapes with
 scattered, skewed, split, empty and rectangular rows; checked against the oracle's SpmvGold
 (cpu_spmv.cpp:241-265) within the reordering bound (the slab order is a reordered CSR sum:
 mspmv_tile_modes reports every block as 255), bit-identical on repeats and under a CU limit's
-rebuilt plan against the oracle again.  The default choice (scattered band: slab; FEM, stencil,
-cant: tiles) is checked on its own.
+rebuilt plan against the oracle again.  The default choice (scattered band: slab; large power-law:
+sliced-ELL column groups; FEM, stencil, cant, small power-law: tiles) is checked on its own.
 """
 import numpy as np
 import pytest
@@ -18,11 +19,19 @@ from gpu_common import check_parity
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["1", "2"], ids=["band", "groups"])
+SLAB_KERNEL = {"1": "k_spmv_slab<{nt},0>", "2": "k_spmv_slab<{nt},1>", "4": "k_spmv_sell<{nt}>"}
+
+
+@pytest.fixture(params=["1", "2", "4"], ids=["band", "groups", "sell"])
 def slab_on(monkeypatch, request):
-    """1: merge-path blocks (kSlabCfgs[0]); 2: column-group blocks (kSlabCfgs[1], partials folded)."""
+    """1: merge-path blocks (kSlabCfgs[0]); 2: column-group blocks (kSlabCfgs[1], partials folded);
+    4: the column-group blocks in sliced-ELL form (k_spmv_sell)."""
     monkeypatch.setenv("MSPMV_SPMV_SLAB", request.param)
     return request.param
+
+
+def slab_kernel_ok(name, mode):
+    return name in (SLAB_KERNEL[mode].format(nt="true"), SLAB_KERNEL[mode].format(nt="false"))
 
 
 def scatter_band(m, per_row, band, seed):
@@ -59,8 +68,7 @@ def test_slab_parity(orc, slab_on, name):
     gold = orc.spmv_gold(a, x)
     with mspmv.GpuCsr(a) as g:
         y = g.spmv(x)
-        assert g.kernel_name().startswith("k_spmv_slab<"), g.kernel_name()
-        assert g.kernel_name().endswith(",1>" if slab_on == "2" else ",0>"), g.kernel_name()
+        assert slab_kernel_ok(g.kernel_name(), slab_on), g.kernel_name()
         plan = g.tile_plan(1)
         assert np.all(plan["modes"] == 255)
         check_parity(a, y, gold, x, plan, 1)
@@ -88,7 +96,7 @@ def test_slab_device_buffers_and_cg_unaffected(orc, slab_on):
         dx, dy = mspmv.DeviceBuffer.from_array(x), mspmv.DeviceBuffer(8 * spd.num_rows)
         g.spmm_dev(dx, dy, 1)
         y = dy.download(spd.num_rows)
-        assert g.kernel_name().startswith("k_spmv_slab<")
+        assert slab_kernel_ok(g.kernel_name(), slab_on), g.kernel_name()
         check_parity(spd, y, orc.spmv_gold(spd, x), x, g.tile_plan(1), 1)
         b = np.random.default_rng(3).uniform(-1, 1, spd.num_rows)
         xs, it, _, st = g.cg_single(b, 400, 1e-10)
@@ -99,14 +107,31 @@ def test_slab_device_buffers_and_cg_unaffected(orc, slab_on):
         dy.free()
 
 
-def test_slab_default_choice(monkeypatch):
+def test_slab_default_choice(orc, monkeypatch):
+    """The default plain-SpMV choice: scattered band -> slab blocks; power-law rows at >= 12,288
+    nonzeros per CU -> the sliced-ELL column groups (checked against the oracle here too); a smaller
+    power-law matrix -> one-wave tiles; FEM, stencil, cant -> tiles."""
     monkeypatch.delenv("MSPMV_SPMV_SLAB", raising=False)
     want = {
-        "scatter": (lambda: scatter_band(217918, 53, 10000, 77), True),
-        "fem": (lambda: mspmv.CsrMatrix.synth_fem_blocked(21792, 1152443, 6, 170, seed=3), False),
-        "stencil": (lambda: mspmv.CsrMatrix.synth_stencil(1, 40 * 30 * 30, 40, 30, 30, seed=1, diag_shift=1e-2), False),
-        "cant": (lambda: scatter_band(62451, 64, 2000, 1), False),  # small blocks: tiles win (r04x)
+        "scatter": (lambda: scatter_band(217918, 53, 10000, 77), "k_spmv_slab<"),
+        "powerlaw": (lambda: mspmv.CsrMatrix.synth_powerlaw(120000, 120000, 4000000, exponent=1.2, seed=9),
+                     "k_spmv_sell<"),
+        "powerlaw_small": (lambda: mspmv.CsrMatrix.synth_powerlaw(60000, 60000, 1800000, exponent=1.2, seed=7),
+                           "k_spmv_tile<"),
+        "fem": (lambda: mspmv.CsrMatrix.synth_fem_blocked(21792, 1152443, 6, 170, seed=3), None),
+        "stencil": (lambda: mspmv.CsrMatrix.synth_stencil(1, 40 * 30 * 30, 40, 30, 30, seed=1, diag_shift=1e-2), None),
+        "cant": (lambda: scatter_band(62451, 64, 2000, 1), None),  # small blocks: tiles win (r04x)
     }
-    for name, (make, slab) in want.items():
-        with mspmv.GpuCsr(make()) as g:
-            assert g.kernel_name().startswith("k_spmv_slab<") == slab, (name, g.kernel_name())
+    for name, (make, prefix) in want.items():
+        a = make()
+        with mspmv.GpuCsr(a) as g:
+            k = g.kernel_name()
+            if prefix is None:
+                assert not k.startswith(("k_spmv_slab<", "k_spmv_sell<")), (name, k)
+            else:
+                assert k.startswith(prefix), (name, k)
+            if name == "powerlaw":
+                x = np.random.default_rng(4).uniform(-1, 1, a.num_cols)
+                y = g.spmv(x)
+                check_parity(a, y, orc.spmv_gold(a, x), x, g.tile_plan(1), 1)
+                assert y.tobytes() == g.spmv(x).tobytes()
