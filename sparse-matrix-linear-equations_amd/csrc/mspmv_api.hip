@@ -564,7 +564,7 @@ static mspmv_status mostly_walks(const TilePlan *wg, bool *out)
 
 // Skewed rows (mostly merge walks) with at least kSellAutoNnzPerBlock nonzeros per column-group block
 // take the sliced-ELL plan (k_spmv_sell) when it stages at most kSlabAutoBytes of x per nonzero: the
-// power-law variant at pwtk size 80 -> 67 us per launch (r05ao-r05aq); smaller skewed matrices keep
+// power-law variant at pwtk size 80 -> 55 us per launch (r05ao-r05as); smaller skewed matrices keep
 // the one-wave tiles (their blocks would be a few chunks of work each).
 constexpr double kSellAutoNnzPerBlock = 12288.0;
 

@@ -51,7 +51,7 @@ struct SlabCfg {
 // by length, in slices of 64 whose values sit column-major (lane = run), long runs apart.
 constexpr SlabCfg kSlabCfgs[3] = {{kSlabThreads, kSlabCols, kSlabRows, kSlabChunk, kSlabEntries, kSlabBlocksPerCu},
                                   {1024, 8192, 4095, 4096, 2048, 1},
-                                  {1024, 8192, 4095, 0, 0, 1}};
+                                  {1024, 14336, 4095, 0, 0, 1}};
 constexpr int kSlabGroups = 4;
 constexpr int kSlabMaxGroups = 8;
 constexpr int kSellShortRun = 8;     // sliced-ELL: runs up to this long sit one per lane in slices of 64,
