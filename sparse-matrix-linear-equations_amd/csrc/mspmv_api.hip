@@ -298,7 +298,7 @@ mspmv_status plan_split_rows(TilePlan &p, const std::vector<int2> &hb, const std
         return st;
     hipError_t e = hipMemcpy(p.d_fix, fix.data(), sizeof(int4) * fix.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess)
-        e = hipMemset(p.d_fix_cnt, 0, sizeof(unsigned) * T);
+        e = memset_sync(p.d_fix_cnt, 0, sizeof(unsigned) * T);
     if (e != hipSuccess) {
         set_error(std::string("tile plan upload: ") + hipGetErrorString(e));
         return MSPMV_ERR_HIP;
@@ -880,8 +880,8 @@ static mspmv_status create_common(const mspmv_csr_d *a, int device, bool from_de
     } else {
         if ((st = dev_alloc(&h->d_cols, padded)) != MSPMV_OK || (st = dev_alloc(&h->d_vals, padded)) != MSPMV_OK)
             return fail(st);
-        if (hipMemset(h->d_cols, 0, sizeof(int) * padded) != hipSuccess ||
-            hipMemset(h->d_vals, 0, sizeof(double) * padded) != hipSuccess) {
+        if (memset_sync(h->d_cols, 0, sizeof(int) * padded) != hipSuccess ||
+            memset_sync(h->d_vals, 0, sizeof(double) * padded) != hipSuccess) {
             set_error("hipMemset of padded CSR arrays failed");
             return fail(MSPMV_ERR_HIP);
         }
@@ -911,7 +911,7 @@ static mspmv_status create_common(const mspmv_csr_d *a, int device, bool from_de
         if ((st = dev_alloc(&d_bad, 1)) != MSPMV_OK)
             return fail(st);
         int bad = 0;
-        hipError_t e = hipMemset(d_bad, 0, sizeof(int));
+        hipError_t e = memset_sync(d_bad, 0, sizeof(int));
         if (e == hipSuccess) {
             hipLaunchKernelGGL(k_check_cols, dim3(1024), dim3(256), 0, h->stream, h->d_cols, (long long)h->nnz, h->n,
                                d_bad);
@@ -1346,7 +1346,9 @@ static mspmv_status ensure_cg_workspace(mspmv_handle_s *h, int L, int nblk, int 
         dev_free(h->d_gtickets);
         h->gtickets_cap = 0;
         ST_TRY(dev_alloc(&h->d_gtickets, gtickets_capacity(slots)));
-        HIP_TRY(hipMemset(h->d_gtickets, 0, sizeof(unsigned) * gtickets_capacity(slots)));
+        // on the handle's stream: it is non-blocking, so a null-stream memset is not ordered before the
+        // folds queued on it next
+        HIP_TRY(hipMemsetAsync(h->d_gtickets, 0, sizeof(unsigned) * gtickets_capacity(slots), h->stream));
         h->gtickets_cap = gtickets_capacity(slots);
     }
     if (L > h->scal_cap) {
@@ -2028,7 +2030,7 @@ mspmv_status mspmv_time_stream_read(int device, size_t bytes, int reps, double *
     HIP_TRY(hipMalloc(&buf, bytes));
     hipStream_t s = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    hipError_t e = hipMemset(buf, 0, bytes);
+    hipError_t e = memset_sync(buf, 0, bytes);
     if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     if (e == hipSuccess)
@@ -2346,7 +2348,7 @@ mspmv_status mspmv_memcpy_d2d(void *d_dst, const void *d_src, size_t bytes)
 
 mspmv_status mspmv_memset_dev(void *d_dst, int byte_value, size_t bytes)
 {
-    HIP_TRY(hipMemset(d_dst, byte_value, bytes));
+    HIP_TRY(memset_sync(d_dst, byte_value, bytes));
     return MSPMV_OK;
 }
 

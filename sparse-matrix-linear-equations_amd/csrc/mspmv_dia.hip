@@ -550,12 +550,12 @@ mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, dou
     if (e == hipSuccess && hipMalloc((void **)&p.d_split, (size_t)W + 1) != hipSuccess)
         e = hipErrorOutOfMemory;
     if (e == hipSuccess)
-        e = hipMemset(p.d_split, 0, (size_t)W + 1);
+        e = memset_sync(p.d_split, 0, (size_t)W + 1);
     for (int i = 0; i < 5 && e == hipSuccess; ++i) {
         if (hipMalloc((void **)&p.d_modes[i], (size_t)W) != hipSuccess)
             e = hipErrorOutOfMemory;
         else
-            e = hipMemset(p.d_modes[i], 1, (size_t)W);
+            e = memset_sync(p.d_modes[i], 1, (size_t)W);
     }
     if (e == hipSuccess)
         e = hipStreamSynchronize(h->stream);

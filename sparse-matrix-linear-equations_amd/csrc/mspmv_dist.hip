@@ -533,7 +533,8 @@ mspmv_status ensure_buffers(mspmv_dist_s *d, int L, int nblk, int num_tiles, int
         dfree(d->d_gtickets);
         d->gtickets_cap = 0;
         D_ST(dalloc(&d->d_gtickets, gtickets_capacity(slots)));
-        D_HIP(hipMemset(d->d_gtickets, 0, sizeof(unsigned) * gtickets_capacity(slots)));
+        // on the local stream (non-blocking: a null-stream memset is not ordered before the folds on it)
+        D_HIP(hipMemsetAsync(d->d_gtickets, 0, sizeof(unsigned) * gtickets_capacity(slots), d->local->stream));
         d->gtickets_cap = gtickets_capacity(slots);
     }
     if (hist_cap > d->hist_cap) {

@@ -10,6 +10,15 @@
 
 #include "mspmv.h"
 
+// hipMemset on the legacy null stream, then wait for it: every handle's stream is non-blocking, so a
+// null-stream fill is not ordered before the next launch on it otherwise (a fold's tickets or a plan's
+// modes could be read before they are written)
+static inline hipError_t memset_sync(void *p, int value, size_t bytes)
+{
+    const hipError_t e = hipMemset(p, value, bytes);
+    return e == hipSuccess ? hipStreamSynchronize(nullptr) : e;
+}
+
 namespace mspmv {
 
 constexpr int kBlock = 256;  // 4 x 64-lane waves per workgroup

@@ -536,7 +536,7 @@ static mspmv_status slab_upload(T **d, const std::vector<T> &hsrc, size_t pad = 
     }
     hipError_t e = hsrc.empty() ? hipSuccess : hipMemcpy(*d, hsrc.data(), sizeof(T) * hsrc.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess && pad)
-        e = hipMemset(*d + hsrc.size(), 0, sizeof(T) * pad);
+        e = memset_sync(*d + hsrc.size(), 0, sizeof(T) * pad);
     if (e != hipSuccess) {
         set_error(std::string("column-slab plan upload: ") + hipGetErrorString(e));
         return MSPMV_ERR_HIP;
@@ -775,7 +775,7 @@ static mspmv_status slab_finish(mspmv_handle_s *h, TilePlan &p, int cfg, int gro
         set_error("column-slab plan: hipMalloc failed");
         return MSPMV_ERR_HIP;
     }
-    if (hipMemset(p.d_modes[0], 255, (size_t)T) != hipSuccess) {
+    if (memset_sync(p.d_modes[0], 255, (size_t)T) != hipSuccess) {
         set_error("column-slab plan: memset failed");
         return MSPMV_ERR_HIP;
     }
@@ -974,7 +974,7 @@ static mspmv_status sell_finish(mspmv_handle_s *h, TilePlan &p, const std::vecto
         set_error("column-slab plan: hipMalloc failed");
         return MSPMV_ERR_HIP;
     }
-    if (hipMemset(p.d_modes[0], 255, (size_t)T) != hipSuccess) {
+    if (memset_sync(p.d_modes[0], 255, (size_t)T) != hipSuccess) {
         set_error("column-slab plan: memset failed");
         return MSPMV_ERR_HIP;
     }
@@ -1652,7 +1652,7 @@ mspmv_status build_slab_mm_plan(mspmv_handle_s *h, int L, TilePlan &p)
         set_error("column-slab SpMM plan: hipMalloc failed");
         return MSPMV_ERR_HIP;
     }
-    if (hipMemset(p.d_modes[l_index(L)], 255, (size_t)T) != hipSuccess) {
+    if (memset_sync(p.d_modes[l_index(L)], 255, (size_t)T) != hipSuccess) {
         set_error("column-slab SpMM plan: memset failed");
         return MSPMV_ERR_HIP;
     }
