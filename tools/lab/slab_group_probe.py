@@ -20,6 +20,8 @@ M, NNZ = 217918, 11524432
 shapes = {
     "powerlaw": lambda: mspmv.CsrMatrix.synth_powerlaw(M, M, NNZ, 1.2, 3),
     "band": lambda: mspmv.CsrMatrix.synth_banded(M, M * 53, 10000, seed=77),
+    # the default-choice test's power-law matrix (tests/test_gpu_slab.py)
+    "powerlaw4m": lambda: mspmv.CsrMatrix.synth_powerlaw(120000, 120000, 4000000, exponent=1.2, seed=9),
 }
 modes = os.environ.get("PROBE_MODES", " 2").split(" ")
 only = os.environ.get("PROBE_ONLY", "").split()
