@@ -300,14 +300,18 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
         hq = qq >= 0 ? a.slice[qq] : make_int2(0, 0);
         ev = qq >= 0 ? a.sent[(size_t)qq * 64 + lane] : 0u;
     };
-    auto load8 = [&](const int2 &hq, Sl &d) {
-        const double *vp = a.val + hq.x + lane;
-        const unsigned short *cp = a.col + hq.x + lane;
+    auto load8 = [&](const int2 &hq, Sl &d) {  // slot pairs: one 16-B value load, one 4-B column load
+        const v2d_t *vp = reinterpret_cast<const v2d_t *>(a.val + hq.x) + lane;
+        const unsigned *cp = reinterpret_cast<const unsigned *>(a.col + hq.x) + lane;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const bool in = j < (hq.y & 0xffff);  // wave-uniform: the slice's slots
-            d.v[j] = in ? slab_stream<NT>(vp + 64 * j) : 0.0;
-            d.c[j] = in ? slab_stream<NT>(cp + 64 * j) : (unsigned short)0;
+        for (int p = 0; p < 4; ++p) {
+            const bool in = 2 * p < (hq.y & 0xffff);  // wave-uniform: the slice's slot pairs
+            const v2d_t v = in ? slab_stream<NT>(vp + 64 * p) : v2d_t{0.0, 0.0};
+            const unsigned c = in ? slab_stream<NT>(cp + 64 * p) : 0u;
+            d.v[2 * p] = v.x;
+            d.v[2 * p + 1] = v.y;
+            d.c[2 * p] = (unsigned short)(c & 0xffffu);
+            d.c[2 * p + 1] = (unsigned short)(c >> 16);
         }
     };
     // the wave's slice after slice q of segment s: q + NW in s, else its first one in s + 1 (-1: none)
@@ -785,7 +789,8 @@ static mspmv_status slab_finish(mspmv_handle_s *h, TilePlan &p, int cfg, int gro
 // Sliced-ELL layout of one column-group block (rows [r0, r1), columns [lo, hi)): per slab touched, in
 // slab order, its runs of one row (CSR order); runs longer than kSellLongRun stored contiguously and
 // listed apart in pieces of <= 512 values, the others sorted by length (longest first, rows ascending among equals) and cut into
-// slices of 64, value j of the slice's run i at slot j * 64 + i (slots past a run's length: zeros, never
+// slices of 64, value j of the slice's run i at slot j of lane i -- slots in pairs, pair p of lane i at
+// 2 (64 p + i): one 16-B value load and one 4-B column load per pair (slots past a run's length: zeros, never
 // added).  Bases relative to the block.
 struct SellBlockOut {
     std::vector<int4> segs;
@@ -851,8 +856,8 @@ static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, c
                 mediums.push_back(r);
             } else if (r.len > kSellLongRun) {  // pieces of <= 512 values: {base, length, row, first | count << 16}
                 const size_t base = o.val.size();
-                o.val.resize(base + r.len, 0.0);
-                o.col.resize(base + r.len, 0);
+                o.val.resize(base + r.len + (r.len & 1), 0.0);  // even bases: the slices' pair loads
+                o.col.resize(base + r.len + (r.len & 1), 0);
                 for (int j = 0; j < r.len; ++j)
                     put_val(base + j, r.first + j);
                 const int np = (r.len + 511) / 512, first = (int)o.longs.size() - long0;
@@ -870,8 +875,8 @@ static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, c
             const int n = (int)std::min<size_t>(64, shorts.size() - i0);
             const int Lm = shorts[i0].len;
             const size_t base = o.val.size();
-            o.val.resize(base + (size_t)Lm * 64, 0.0);
-            o.col.resize(base + (size_t)Lm * 64, 0);
+            o.val.resize(base + (size_t)(Lm + (Lm & 1)) * 64, 0.0);
+            o.col.resize(base + (size_t)(Lm + (Lm & 1)) * 64, 0);
             for (int i = 0; i < 64; ++i) {
                 if (i >= n) {
                     o.sents.push_back(0u);
@@ -879,25 +884,25 @@ static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, c
                 }
                 const Run &r = shorts[i0 + (size_t)i];
                 for (int j = 0; j < r.len; ++j)
-                    put_val(base + (size_t)j * 64 + i, r.first + j);
+                    put_val(base + (size_t)(j / 2) * 128 + 2 * i + (j & 1), r.first + j);
                 o.sents.push_back((unsigned)r.row | ((unsigned)r.len << 16));
             }
             o.slices.push_back(make_int2((int)base, Lm));
         }
-        // medium runs: 8 per slice, 8 lanes each -- value j of the slice's run r at slot j / 8, lane
+        // medium runs: 8 per slice, 8 lanes each (slot pairs as above) -- value j of the slice's run r at slot j / 8, lane
         // 8 r + j % 8 (header length | 1 << 16: slots per lane, the medium flag)
         std::stable_sort(mediums.begin(), mediums.end(), [](const Run &x, const Run &y) { return x.len > y.len; });
         for (size_t i0 = 0; i0 < mediums.size(); i0 += 8) {
             const int n = (int)std::min<size_t>(8, mediums.size() - i0);
             const int Lm = (mediums[i0].len + 7) / 8;
             const size_t base = o.val.size();
-            o.val.resize(base + (size_t)Lm * 64, 0.0);
-            o.col.resize(base + (size_t)Lm * 64, 0);
+            o.val.resize(base + (size_t)(Lm + (Lm & 1)) * 64, 0.0);
+            o.col.resize(base + (size_t)(Lm + (Lm & 1)) * 64, 0);
             for (int i = 0; i < 8; ++i) {
                 const Run *r = i < n ? &mediums[i0 + (size_t)i] : nullptr;
                 if (r)
                     for (int j = 0; j < r->len; ++j)
-                        put_val(base + (size_t)(j / 8) * 64 + 8 * i + j % 8, r->first + j);
+                        put_val(base + (size_t)(j / 16) * 128 + 2 * (8 * i + j % 8) + (j / 8) % 2, r->first + j);
                 for (int l = 0; l < 8; ++l)
                     o.sents.push_back(r ? (unsigned)r->row | ((unsigned)r->len << 16) : 0u);
             }
