@@ -2,7 +2,7 @@
 the SuiteSparse matrices, which are not available offline), through the C-ABI.
 
 * SpMV (configs[0..1]: cant, pwtk, rma10 shapes; the parabolic_fem and nlpkkt120 sizes of
-  configs[3..4]) against the oracle's SpmvGold restatement (cpu_spmv.cpp:241-265): rows the
+  configs[3..4]; the power-law variant at pwtk size) against the oracle's SpmvGold restatement (cpu_spmv.cpp:241-265): rows the
   kernel sums sequentially bit-identical, all others within 2 (len+1) eps (|A||x|)_i; merge
   coordinates at P = 256 bit-exact with MergePathSearch (cpu_spmv.cpp:208-235).
 * SpMM, 16-column panel (configs[2]) on the cant and pwtk shapes against the row-split
@@ -39,6 +39,8 @@ def full_cases():
         "rma10": lambda: mspmv.CsrMatrix.synth_banded(46835, 2374001, 3000, seed=2),
         "parabolic_fem": lambda: mspmv.CsrMatrix.synth_stencil(0, 525825, 725, diag_shift=1e-4),
         "nlpkkt120": lambda: mspmv.CsrMatrix.synth_stencil(1, 160 * 135 * 164, 160, 135, 164, diag_shift=1e-2),
+        # SURVEY 8(d)'s skewed variant, bench.py's spmv_shapes power-law leg (the sliced-ELL SpMV)
+        "powerlaw": lambda: mspmv.CsrMatrix.synth_powerlaw(PWTK["m"], PWTK["m"], PWTK["nnz"], 1.2, 3),
     }
 
 
@@ -50,6 +52,9 @@ def test_spmv_full_size(orc, name):
         y = g.spmv(x)
         check_parity(a, y, orc.spmv_gold(a, x), x, g.tile_plan(1), 1)
         np.testing.assert_array_equal(g.merge_coords(256), orc.merge_coords(a, 256))
+        if name == "powerlaw":
+            assert g.kernel_name().startswith("k_spmv_sell<"), g.kernel_name()
+            assert y.tobytes() == g.spmv(x).tobytes()  # fixed order: repeats bit-identical
 
 
 @pytest.mark.parametrize("name", ["cant", "pwtk"])
