@@ -22,6 +22,14 @@ Extra fields: the scattered-band stress shape, CG iterations/s for configs[3] (s
 parabolic_fem shape) and configs[4] (8-RHS block CG, nlpkkt120 size; at N > 1 row-sharded over
 all ranks with RCCL halo exchange + dot all-reduces).
 
+Launch: `python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment starts its own N
+ranks -- before it imports mspmv or touches a GPU, the parent runs `python -m torch.distributed.run
+--nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 --master-port <free> bench.py <same args>` as a
+child process (never an exec), relays rank 0's JSON line and exits with the launcher's status (non-zero
+when any rank fails).  Under torch.distributed.run (WORLD_SIZE set) it runs as one rank.  --dry-run: every
+rank joins the gloo group, reports its WORLD_SIZE / RANK, and rank 0 prints them without touching a GPU
+(tests/test_bench_launch.py checks the launch on CPU).
+
 Multi-GPU (--gpus N via torch.distributed.run; run_sharded_headline): weak scaling with a real
 exchange step -- each matrix of the batch is ONE FEM-blocked matrix of N x 217,918 rows, sharded by
 merge-path row blocks; every rank generates only its pwtk-sized block, and each SpMV exchanges the
@@ -42,6 +50,44 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "sparse-matrix-linear-equations_amd")]
+
+
+def launch_ranks():
+    """`--gpus N` (N > 1) outside a torch.distributed launch: start the N ranks as a child launcher
+    process and relay rank 0's JSON line; returns the exit status (None: run here as one process).
+    Runs before mspmv is imported, so this parent never initialises a GPU."""
+    if "WORLD_SIZE" in os.environ:
+        return None
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    known, _ = pre.parse_known_args()
+    if known.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={known.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
+    proc = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    lines = [ln for ln in proc.stdout.splitlines() if ln.startswith("{")]
+    for ln in proc.stdout.splitlines():
+        if not ln.startswith("{"):
+            print(ln, file=sys.stderr)  # anything else the ranks printed: kept, off the JSON channel
+    if lines:
+        print(lines[-1], flush=True)
+    if proc.returncode != 0:
+        print(f"bench.py: the {known.gpus}-rank launch exited with status {proc.returncode}", file=sys.stderr)
+        return proc.returncode or 1
+    return 0 if lines else 1
+
+
+if __name__ == "__main__":
+    _rc = launch_ranks()
+    if _rc is not None:
+        sys.exit(_rc)
 
 import mspmv  # noqa: E402
 
@@ -643,9 +689,23 @@ def main():
     ap.add_argument("--only", choices=["spmm16", "spmv_shapes", "cg_single", "cg_multi", "pwtk_perturbed"],
                     help="run one side measurement alone and print its JSON (profiling: rocprofv3 then sees only "
                          "that leg's launches; tools/profile_legs.sh)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch check only: every rank joins the gloo group and reports WORLD_SIZE / RANK; "
+                         "no GPU is touched")
     args = ap.parse_args()
 
     d = Dist(args.gpus)
+    if args.dry_run:
+        ranks = [(d.rank, d.world)]
+        if d.td:
+            ranks = [None] * d.world
+            d.td.all_gather_object(ranks, (d.rank, d.world))
+        if d.rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": args.gpus, "world_size": d.world,
+                              "ranks": [{"rank": r, "world_size": w} for r, w in ranks]}), flush=True)
+        if d.td:
+            d.td.destroy_process_group()
+        return
     if args.only:
         dev = d.local
         do_cpu = not args.no_cpu

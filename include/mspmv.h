@@ -43,8 +43,11 @@ typedef enum mspmv_status {
     MSPMV_ERR_RCCL = 5,          /* a collective failed */
     MSPMV_ERR_UNSUPPORTED = 6,   /* e.g. L outside the compiled set */
     MSPMV_ERR_IO = 7,            /* MatrixMarket read/parse failure */
-    MSPMV_ERR_STALL = 8          /* IC(0) apply: a triangular-solve dependency never became ready
+    MSPMV_ERR_STALL = 8,         /* IC(0) apply: a triangular-solve dependency never became ready
                                     (the solve stopped; X is not a solution) */
+    MSPMV_ERR_FAULT = 9          /* a cross-workgroup fold ticket drew past its group: its array was
+                                    not zero when the launch began, so a fold summed partials not yet
+                                    written or never ran (results invalid; a CG solve stops) */
 } mspmv_status;
 
 /* Mirror of CsrMatrix<double,int> fields, sparse_matrix.h:648-653.  row_offsets has
@@ -305,6 +308,22 @@ MSPMV_API const char *mspmv_spmm_kernel_name(mspmv_handle h, int L);
  * matrix register/LDS-resident on every CU, one cooperative launch per solve), "pipelined (...)"
  * (single RHS, two kernels per iteration), or the split multi-RHS / PCG forms.  "" before any. */
 MSPMV_API const char *mspmv_cg_kernel_name(mspmv_handle h);
+
+/* ---- fault detection ----------------------------------------------------------------- */
+/* The kernels' cross-workgroup folds (CG dot products, rows split between tiles, column groups) are
+ * closed by the last arrival on a self-resetting ticket.  An arrival that draws past its group (the
+ * ticket was not 0 when the launch began) raises a fault word.  CG solves return MSPMV_ERR_FAULT
+ * themselves; for products, the host-pointer calls check after their copy-back and *_dev callers
+ * call this: it synchronizes the handle's stream, clears the word and returns MSPMV_ERR_FAULT if any
+ * product since the last check raised it.  No reference counterpart (OpenMP reductions need none). */
+MSPMV_API mspmv_status mspmv_check_faults(mspmv_handle h);
+/* Test hook: the next CG solve on h fills its fold tickets with `value` before its first iteration
+ * (MSPMV_POISON_FILL), optionally zeroes them again after the first iteration is enqueued
+ * (MSPMV_POISON_LATE_ZERO: the ordering of round 5's unordered null-stream memset) and optionally
+ * records the fault without stopping (MSPMV_POISON_NO_STOP: the solve runs to its stop test and then
+ * returns MSPMV_ERR_FAULT with the iteration count it reached).  One solve only. */
+enum { MSPMV_POISON_FILL = 1, MSPMV_POISON_LATE_ZERO = 2, MSPMV_POISON_NO_STOP = 4 };
+MSPMV_API mspmv_status mspmv_test_poison_tickets(mspmv_handle h, unsigned value, int flags);
 
 /* ---- device memory helpers (so hosts need no HIP headers) ---------------------------- */
 MSPMV_API mspmv_status mspmv_device_malloc(int device, size_t bytes, void **d_ptr);

@@ -93,6 +93,10 @@ MSPMV_API mspmv_status mspmv_dist_time_local_dev(mspmv_dist d, double *d_Y_own, 
 MSPMV_API mspmv_status mspmv_dist_cg_dev(mspmv_dist d, const double *d_B_own, double *d_X_own, int L,
                                          int max_iters, double tolerance, int *iters, double *max_err_hist,
                                          int hist_cap);
+/* Test hook, as mspmv_test_poison_tickets (mspmv.h) for the next sharded CG solve on this rank.  A
+ * ticket fault does not stop a rank's kernels; the fault word is all-reduced (max) after every batch
+ * of iterations, so every rank stops at the same batch and returns MSPMV_ERR_FAULT. */
+MSPMV_API mspmv_status mspmv_dist_test_poison_tickets(mspmv_dist d, unsigned value, int flags);
 
 #ifdef __cplusplus
 }

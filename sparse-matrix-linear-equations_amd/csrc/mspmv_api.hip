@@ -886,6 +886,12 @@ static mspmv_status create_common(const mspmv_csr_d *a, int device, bool from_de
             return fail(MSPMV_ERR_HIP);
         }
     }
+    if ((st = dev_alloc(&h->d_fault, 1)) != MSPMV_OK)
+        return fail(st);
+    if (memset_sync(h->d_fault, 0, sizeof(unsigned)) != hipSuccess) {
+        set_error("hipMemset of the fault word failed");
+        return fail(MSPMV_ERR_HIP);
+    }
     const hipMemcpyKind kind = from_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     std::vector<int> host_ro;
     const int *ro = a->row_offsets;
@@ -1059,6 +1065,7 @@ mspmv_status mspmv_destroy(mspmv_handle h)
     dev_free(h->d_conv);
     dev_free(h->d_ctrl);
     dev_free(h->d_hist);
+    dev_free(h->d_fault);
     if (h->cg_exec)
         (void)hipGraphExecDestroy(h->cg_exec);
     if (h->cg_graph)
@@ -1308,12 +1315,38 @@ mspmv_status mspmv_dspmm(mspmv_handle h, const double *X, double *Y, int L)
             st = MSPMV_ERR_HIP;
         }
     }
+    if (st == MSPMV_OK)
+        st = mspmv_check_faults(h);
     dev_free(dX);
     dev_free(dY);
     return st;
 }
 
 mspmv_status mspmv_dspmv(mspmv_handle h, const double *x, double *y) { return mspmv_dspmm(h, x, y, 1); }
+
+mspmv_status mspmv_check_faults(mspmv_handle h)
+{
+    ST_TRY(check_handle(h));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    unsigned f = 0;
+    HIP_TRY(hipMemcpy(&f, h->d_fault, sizeof f, hipMemcpyDeviceToHost));
+    if (!f)
+        return MSPMV_OK;
+    HIP_TRY(memset_sync(h->d_fault, 0, sizeof f));
+    set_error("a fold ticket drew past its group (its array was not zero when the launch began): the products "
+              "since the last check are invalid");
+    return MSPMV_ERR_FAULT;
+}
+
+mspmv_status mspmv_test_poison_tickets(mspmv_handle h, unsigned value, int flags)
+{
+    ST_TRY(check_handle(h));
+    if (flags & ~(MSPMV_POISON_FILL | MSPMV_POISON_LATE_ZERO | MSPMV_POISON_NO_STOP))
+        return invalid("test_poison_tickets: unknown flag");
+    h->poison_value = value;
+    h->poison_flags = flags;
+    return MSPMV_OK;
+}
 
 // ---- CG ------------------------------------------------------------------------------------
 static mspmv_status ensure_cg_workspace(mspmv_handle_s *h, int L, int nblk, int num_tiles, int hist_cap)
@@ -1471,6 +1504,7 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
         if (!splan->slab && !splan->dia)
             splan = nullptr;
     }
+    const bool dot_fused = dia_dot_fused();  // once per solve (an environment switch; in the graph key)
     if (hm) {
         ST_TRY(get_plan(hm, L, &mplan));
         HIP_TRY(hipStreamSynchronize(hm->stream));  // hm's SpMMs are enqueued on h's stream
@@ -1507,6 +1541,17 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
     const int saved_cap = h->hist_cap;
     h->hist_cap = use_cap;  // kernels record only what the caller asked for
     HIP_TRY(hipMemsetAsync(h->d_ctrl, 0, sizeof(CgControl), h->stream));
+    // test hook (mspmv_test_poison_tickets): dirty fold tickets at the first fold, as an unordered zeroing
+    // of freshly allocated (recycled) memory leaves them
+    const int poison = h->poison_flags;
+    h->poison_flags = 0;
+    // the fold tickets reset themselves, but a solve that stopped early or faulted may leave some
+    // raised: every solve starts from zeroed ones (a few KB, on the solve's stream)
+    HIP_TRY(hipMemsetAsync(h->d_gtickets, 0, sizeof(unsigned) * h->gtickets_cap, h->stream));
+    if (poison & MSPMV_POISON_FILL)
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)h->d_gtickets, (int)h->poison_value, h->gtickets_cap, h->stream));
+    if (poison & MSPMV_POISON_NO_STOP)
+        HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)&h->d_ctrl->fault_no_stop, 1, 1, h->stream));
     // Split-row tickets reset themselves when every tile sharing a row reaches close_split_rows; a CG
     // SpMM returns at its stop test before that (all tiles alike, but an aborted launch might not), so
     // every solve starts from zeroed tickets
@@ -1526,13 +1571,20 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
             return launch_pcg_iteration(h, hm, *plan, *mplan, d_x, L, nblk, tol);
         if (ic)
             return launch_pcg_ic0_iteration(h, ic, *plan, d_x, L, nblk, tol);
-        return launch_cg_iteration(h, *plan, d_x, L, i & 1, nblk, tol);
+        return launch_cg_iteration(h, *plan, splan, dot_fused, d_x, L, i & 1, nblk, tol);
+    };
+    int iterations_enqueued = 0;
+    auto iterate_hook = [&](int i) -> hipError_t {
+        hipError_t e = iterate(i);
+        if (e == hipSuccess && (poison & MSPMV_POISON_LATE_ZERO) && ++iterations_enqueued == 1)
+            e = hipMemsetAsync(h->d_gtickets, 0, sizeof(unsigned) * h->gtickets_cap, h->stream);  // the late zeroing
+        return e;
     };
 
     const int K = cg_batch_iters(h->m, h->nnz, L);  // iterations per graph replay (even: p buffers alternate)
     mspmv_status st = MSPMV_OK;
     hipGraphExec_t exec = nullptr;
-    if (max_iters >= K) {
+    if (max_iters >= K && !(poison & MSPMV_POISON_LATE_ZERO)) {
         // The graph bakes in every buffer, the plan, L, the tolerance and the history size:
         // reuse the handle's graph while all of them are unchanged (instantiation costs ms).
         const void *tk = nullptr;
@@ -1547,7 +1599,7 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
             ic ? (const void *)ic->d_lva : nullptr,
             reinterpret_cast<const void *>((uintptr_t)(hm ? hm->gen : 0)),
             reinterpret_cast<const void *>((uintptr_t)(ic ? ic->gen : 0)),
-            reinterpret_cast<const void *>((intptr_t)K)};
+            reinterpret_cast<const void *>((intptr_t)K), reinterpret_cast<const void *>((intptr_t)dot_fused)};
         if (!h->cg_exec || h->cg_graph_key != key) {
             if (h->cg_exec)
                 (void)hipGraphExecDestroy(h->cg_exec);
@@ -1593,7 +1645,7 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
                 e = hipGraphLaunch(exec, h->stream);
             else
                 for (int i = 0; i < k && e == hipSuccess; ++i)
-                    e = iterate(i);
+                    e = iterate_hook(i);
             if (e == hipSuccess)
                 e = hipMemcpyAsync(&h->h_ctrl[slot], h->d_ctrl, sizeof(CgControl), hipMemcpyDeviceToHost, h->stream);
             if (e == hipSuccess)
@@ -1653,6 +1705,11 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
         if (nh > 0)
             HIP_TRY(hipMemcpy(hist, h->d_hist, sizeof(double) * nh, hipMemcpyDeviceToHost));
     }
+    if (fin.fault) {
+        set_error("CG: a reduction ticket drew past its group (the ticket array was not zero when a fold began): "
+                  "the solve stopped, X is not a solution");
+        return MSPMV_ERR_FAULT;
+    }
     if (fin.breakdown == 2) {
         if (iters)
             *iters = fin.iter;
@@ -1692,6 +1749,7 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
     std::vector<std::vector<double>> gh;
     std::vector<int> git;
     int total = 0;
+    bool faulted = false;  // a group's solve met a ticket fault (reported at the end)
     bool broke = false;  // a group's CG broke down: keep solving the other groups, report it at the end
     for (int c0 = 0; c0 < L && st == MSPMV_OK;) {
         const int w = native_chunk(L - c0);
@@ -1706,6 +1764,9 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
         st = cg_solve_native(h, gb, gx, w, max_iters, tol, &it, cap ? hg.data() : nullptr, cap, hm, ic);
         if (st == MSPMV_ERR_BREAKDOWN) {
             broke = true;
+            st = MSPMV_OK;
+        } else if (st == MSPMV_ERR_FAULT) {  // the other groups still run (each solve re-zeroes its tickets)
+            faulted = true;
             st = MSPMV_OK;
         }
         if (st == MSPMV_OK) {
@@ -1724,7 +1785,10 @@ static mspmv_status cg_solve_dev(mspmv_handle_s *h, const double *d_b, double *d
     }
     dev_free(gb);
     dev_free(gx);
-    if (st == MSPMV_OK && broke) {
+    if (st == MSPMV_OK && faulted) {
+        set_error("CG: a reduction ticket drew past its group in at least one column group: X is not a solution");
+        st = MSPMV_ERR_FAULT;
+    } else if (st == MSPMV_OK && broke) {
         set_error("CG breakdown: p.Ap gave a non-finite alpha in at least one column (frozen; the other "
                   "columns were solved)");
         st = MSPMV_ERR_BREAKDOWN;

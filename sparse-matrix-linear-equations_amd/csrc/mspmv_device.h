@@ -2,7 +2,7 @@
 // (mspmv_slab.hip): agent-scope stores and loads, the XCD-contiguous tile mapping, and the closing of
 // rows split between tiles.  Included by HIP sources only.
 #pragma once
-#include <hip/hip_runtime.h>
+#include "mspmv_internal.h"
 
 namespace mspmv {
 
@@ -30,6 +30,32 @@ __device__ __forceinline__ void store_sc1_2(double *p, double2 v)
 {
     store_sc1(p, v.x);
     store_sc1(p + 1, v.y);
+}
+
+// One arrival on a self-resetting ticket (call from one thread; tickets guard the cross-workgroup folds:
+// reduce_slots, publish_partials, close_split_rows, the slab kernels' column groups).  The fetch_add is a
+// release at agent scope: it orders this workgroup's earlier stores (agent-scope, drained) before the
+// arrival.  The arrival that draws `last` -- the group's final one -- takes an agent-scope acquire fence
+// before it reads the others' stores; the other arrivals read nothing, so they skip it (an acquire on
+// every arrival would invalidate the L2's non-coherent lines once per workgroup).  Tickets start at 0
+// and the final arrival resets them, so a group draws exactly 0 .. last.  A draw > last means the ticket
+// was not 0 when the group began -- its array not zeroed, or zeroed out of stream order, before the
+// launch (round 5's 70-vs-43 iterations): the draw of `last` then falls on an arrival that
+// is not the final one (a fold of partials not yet written) or on none (no fold: the consumer reads a
+// stale total).  That draw raises kFaultTicket in *fault (nullable), which a solve returns as
+// MSPMV_ERR_FAULT (a plain product: mspmv_check_faults).
+// *faulted (nullable) tells the caller this arrival raised the fault.
+__device__ __forceinline__ bool ticket_arrive(unsigned *tk, unsigned last, unsigned *fault, bool *faulted = nullptr)
+{
+    const unsigned v = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (v > last && fault)
+        __hip_atomic_fetch_or(fault, kFaultTicket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (faulted)
+        *faulted = v > last;
+    if (v != last)
+        return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return true;
 }
 
 // Split rows, closed inside the tile kernel (replaces r03's k_fixup launch).  A row longer than the
@@ -70,11 +96,9 @@ __device__ __forceinline__ void close_split_rows(const A &a, int t, int4 fx, int
     }
     if (threadIdx.x == 0) {
         int f0 = -1, f1 = -1;
-        if (fx.x >= 0 &&
-            __hip_atomic_fetch_add(&a.fix_cnt[fx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)fx.y)
+        if (fx.x >= 0 && ticket_arrive(&a.fix_cnt[fx.x], (unsigned)fx.y, a.fault))
             f0 = fx.x;
-        if (fx.z > 0 &&
-            __hip_atomic_fetch_add(&a.fix_cnt[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)fx.z)
+        if (fx.z > 0 && ticket_arrive(&a.fix_cnt[t], (unsigned)fx.z, a.fault))
             f1 = t;
         s_fin[0] = f0;
         s_fin[1] = f1;

@@ -122,6 +122,9 @@ struct mspmv_dist_s {
     hipGraphExec_t cg_exec = nullptr;
     std::vector<const void *> cg_key;
     bool cg_warm = false;
+    // test hook (mspmv_dist_test_poison_tickets): the next CG solve's fold tickets start dirty
+    unsigned poison_value = 0;
+    int poison_flags = 0;
 };
 
 extern "C" {
@@ -691,7 +694,7 @@ mspmv_status mspmv_dist_cg_dev(mspmv_dist d, const double *d_B_own, double *d_X_
     std::vector<std::vector<double>> gh;
     std::vector<int> git;
     int total = 0;
-    bool broke = false;
+    bool broke = false, faulted = false;
     for (int c0 = 0; c0 < L && st == MSPMV_OK;) {
         int w = 16;
         while (w > L - c0)
@@ -705,6 +708,9 @@ mspmv_status mspmv_dist_cg_dev(mspmv_dist d, const double *d_B_own, double *d_X_
         st = dist_cg_native(d, gb, gx, w, max_iters, tolerance, &it, cap ? hg.data() : nullptr, cap);
         if (st == MSPMV_ERR_BREAKDOWN) {
             broke = true;
+            st = MSPMV_OK;
+        } else if (st == MSPMV_ERR_FAULT) {  // the other groups still run (each solve re-zeroes its tickets)
+            faulted = true;
             st = MSPMV_OK;
         }
         if (st == MSPMV_OK && d->n_own &&
@@ -727,6 +733,9 @@ mspmv_status mspmv_dist_cg_dev(mspmv_dist d, const double *d_B_own, double *d_X_
                 v = std::max(v, gh[g][(size_t)std::min(k, git[g] - 1)]);
         max_err_hist[k] = v;
     }
+    if (st == MSPMV_OK && faulted)
+        return fail_msg(MSPMV_ERR_FAULT, "dist CG: a reduction ticket drew past its group in at least one column "
+                                         "group: X is not a solution");
     if (st == MSPMV_OK && broke)
         return fail_msg(MSPMV_ERR_BREAKDOWN, "dist CG breakdown: non-finite alpha in at least one column (frozen)");
     return st;
@@ -781,6 +790,21 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
     double *pAp = d->d_red, *rr = d->d_red + L;
     // init: x = 0, r = p = b; all-reduce b.b; scalars
     D_HIP(hipMemsetAsync(d->d_ctrl, 0, sizeof(CgControl), s));
+    // a ticket fault does not stop the device side of a sharded solve: every rank must stop at the same
+    // batch, so the host stops on the all-reduced fault word (below)
+    D_HIP(hipMemsetD32Async((hipDeviceptr_t)&d->d_ctrl->fault_no_stop, 1, 1, s));
+    // split-row tickets reset themselves when every tile sharing a row closes it; a CG SpMM that returns
+    // at its stop test leaves them as they were, so every solve starts from zeroed ones
+    for (const TilePlan *tp : {plan, pp[0], pp[1], pp[2], dlocal, dpart[0], dpart[1], dpart[2]})
+        if (tp && tp->d_fix_cnt)
+            D_HIP(hipMemsetAsync(tp->d_fix_cnt, 0, sizeof(unsigned) * (size_t)tp->num_tiles, s));
+    // test hook: fold tickets dirty at the first fold (round 5's unordered zeroing of recycled memory)
+    const int poison = d->poison_flags;
+    d->poison_flags = 0;
+    // fold tickets: zeroed at every solve's start (a solve that stopped early or faulted may leave some raised)
+    D_HIP(hipMemsetAsync(d->d_gtickets, 0, sizeof(unsigned) * d->gtickets_cap, s));
+    if (poison & MSPMV_POISON_FILL)
+        D_HIP(hipMemsetD32Async((hipDeviceptr_t)d->d_gtickets, (int)d->poison_value, d->gtickets_cap, s));
     {
         DistVecArgs a = va;
         a.p = d_B_own;
@@ -831,6 +855,13 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
         D_HIP(launch_dist_vec_mirror(4, a, L, 1, nullptr, s));             // stop test, beta
         return MSPMV_OK;
     };
+    int iterations_enqueued = 0;
+    auto iteration_hook = [&]() -> mspmv_status {
+        D_ST(iteration());
+        if ((poison & MSPMV_POISON_LATE_ZERO) && ++iterations_enqueued == 1)  // the late zeroing
+            D_HIP(hipMemsetAsync(d->d_gtickets, 0, sizeof(unsigned) * d->gtickets_cap, s));
+        return MSPMV_OK;
+    };
     // batches of K iterations, the control word of batch b inspected while b+1 is queued
     const int K = cg_batch_iters(d->n_own, d->local->nnz, L);
     // MSPMV_DIST_GRAPH: 1 on, 0 off; unset: on for a single rank (tested bit-identical to eager),
@@ -841,7 +872,7 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
         const char *e = getenv("MSPMV_DIST_GRAPH");
         return e ? (atoi(e) != 0 ? 1 : 0) : -1;
     }();
-    const bool use_graph = graph_env >= 0 ? graph_env == 1 : d->nranks == 1;
+    const bool use_graph = (graph_env >= 0 ? graph_env == 1 : d->nranks == 1) && !(poison & MSPMV_POISON_LATE_ZERO);
     const void *tk = nullptr;
     static_assert(sizeof(tk) == sizeof(tolerance), "tolerance bits as a key word");
     std::memcpy(&tk, &tolerance, sizeof tk);
@@ -893,7 +924,7 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
             return hipGraphLaunch(d->cg_exec, s) == hipSuccess ? MSPMV_OK
                                                                : fail_msg(MSPMV_ERR_HIP, "dist CG: graph launch failed");
         for (int i = 0; i < k; ++i)
-            D_ST(iteration());
+            D_ST(iteration_hook());
         return MSPMV_OK;
     };
     hipEvent_t evs[2] = {nullptr, nullptr};
@@ -907,6 +938,12 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
             st = batch(k);
             if (st != MSPMV_OK)
                 break;
+            // every rank's fault word -> the max over ranks, so all ranks stop at the same batch
+            if (d->nranks > 1 &&
+                ncclAllReduce(&d->d_ctrl->fault, &d->d_ctrl->fault, 1, ncclUint32, ncclMax, d->comm, s) != ncclSuccess) {
+                st = fail_msg(MSPMV_ERR_RCCL, "dist CG: fault word all-reduce failed");
+                break;
+            }
             if (hipMemcpyAsync(&d->h_ctrl[slot], d->d_ctrl, sizeof(CgControl), hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipEventRecord(evs[slot], s) != hipSuccess) {
                 st = fail_msg(MSPMV_ERR_HIP, "dist CG: control copy failed");
@@ -925,7 +962,8 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
             }
             --pending;
             d->cg_warm = true;  // a batch has run: RCCL's connections exist, later batches may be captured
-            const bool done = d->h_ctrl[oldest].done != 0;
+            const bool done = d->h_ctrl[oldest].done != 0 ||
+                              (d->h_ctrl[oldest].fault != 0 && !(poison & MSPMV_POISON_NO_STOP));
             oldest ^= 1;
             if (done)
                 break;
@@ -951,8 +989,22 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
         if (nh > 0)
             D_HIP(hipMemcpy(max_err_hist, d->d_hist, sizeof(double) * nh, hipMemcpyDeviceToHost));
     }
+    if (fin.fault)
+        return fail_msg(MSPMV_ERR_FAULT, "dist CG: a reduction ticket drew past its group (the ticket array was not "
+                                         "zero when a fold began): X is not a solution");
     if (fin.breakdown)
         return fail_msg(MSPMV_ERR_BREAKDOWN, "dist CG breakdown: non-finite alpha at iteration " + std::to_string(it));
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_dist_test_poison_tickets(mspmv_dist d, unsigned value, int flags)
+{
+    if (!d)
+        return fail_msg(MSPMV_ERR_INVALID, "null dist");
+    if (flags & ~(MSPMV_POISON_FILL | MSPMV_POISON_LATE_ZERO | MSPMV_POISON_NO_STOP))
+        return fail_msg(MSPMV_ERR_INVALID, "dist_test_poison_tickets: unknown flag");
+    d->poison_value = value;
+    d->poison_flags = flags;
     return MSPMV_OK;
 }
 

@@ -22,6 +22,7 @@ static inline hipError_t memset_sync(void *p, int value, size_t bytes)
 namespace mspmv {
 
 constexpr int kBlock = 256;  // 4 x 64-lane waves per workgroup
+constexpr unsigned kFaultTicket = 1u;  // fault word bit: a fold ticket drew past its group (ticket_arrive)
 constexpr int kNnzPad = 16;  // padding elements after the last nonzero of the device arrays
 constexpr int kSnapDiv = 8;
 constexpr int kSlotGroup = 32;     // fan-in of the CG partial-reduction tree (reduce_slots)
@@ -200,8 +201,11 @@ struct CgControl {
     int iter_par[2]; // single-RHS pipelined CG: iteration index handed to the next SpMV, by parity
     int x_pending;   // multi-RHS split CG: x += alpha p of the last update not applied yet (k_cg_update
                      // sets it, the next p update applies the term, the fold after it clears it)
-    unsigned reserved;
+    unsigned fault;          // kFault* bits raised by the kernels (take_ticket): the solve's result is invalid
+    unsigned fault_no_stop;  // sharded CG: a fault does not set done on the device (the host stops on the
+                             // all-reduced fault word, so every rank stops at the same batch)
 };
+
 
 // Register-resident single-RHS CG (mspmv_cg_resident.hip): the ELL layout of the matrix's row
 // blocks, one per CU, built once per handle when the matrix fits (ok).
@@ -254,6 +258,12 @@ struct mspmv_handle_s {
     double *d_hist = nullptr;
     int hist_cap = 0;
     int scal_cap = 0;
+    // kFault* bits the plain products raise (ticket_arrive: split-row and column-group tickets), read
+    // and cleared by mspmv_check_faults (the host-pointer products call it; CG solves use d_ctrl's)
+    unsigned *d_fault = nullptr;
+    // test hook (mspmv_test_poison_tickets): the next CG solve fills its fold tickets with this value
+    unsigned poison_value = 0;
+    int poison_flags = 0;  // 0: none pending; MSPMV_POISON_* bits
     // CG iteration graph (K iterations), reused while everything it was captured with is unchanged
     hipGraph_t cg_graph = nullptr;
     hipGraphExec_t cg_exec = nullptr;
@@ -410,8 +420,10 @@ bool supported_L(int L);
 
 // CG pieces
 hipError_t launch_cg_init(mspmv_handle_s *h, const double *d_b, double *d_x, int L, double tol, int nblk);
-hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *d_x, int L, int parity, int nblk,
-                               double tol);
+// splan / dot_fused: the split iteration's plain-product plan and window dot mode, resolved once per
+// solve by cg_solve_native (launch_cg_iteration_split)
+hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, const TilePlan *splan, bool dot_fused,
+                               double *d_x, int L, int parity, int nblk, double tol);
 int cg_update_blocks(long long elems, int num_cus);
 // Iterations per CG batch / graph replay for an m-row, nnz-nonzero matrix and L columns (mspmv_api.hip).
 int cg_batch_iters(long long m, long long nnz, int L);

@@ -149,9 +149,22 @@ __device__ __forceinline__ void fold_cols(const double *base, int count, double 
 // block does).  Tickets reset themselves for the next launch.  Why a tree of small groups on
 // separate 256-B lines: agent-scope atomics on one address serialise at the memory side
 // (~10 ns each), so 2 k blocks on one ticket cost ~22 us; fan-in 32 keeps each chain short.
+// One arrival on a fold group's ticket (thread 0 only; ticket_arrive).  A fault also stops a single-GPU
+// solve (done); a sharded one does not (fault_no_stop: the ranks' stop decisions must stay identical, so
+// its host stops on the all-reduced fault word at a batch boundary instead).
+__device__ __forceinline__ bool take_ticket(unsigned *tk, int gsize, CgControl *ctrl)
+{
+    bool faulted = false;
+    if (ticket_arrive(tk, (unsigned)gsize - 1, ctrl ? &ctrl->fault : nullptr, &faulted))
+        return true;
+    if (faulted && ctrl && !__hip_atomic_load(&ctrl->fault_no_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        __hip_atomic_store(&ctrl->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+}
+
 template <int L>
 __device__ __forceinline__ bool reduce_slots(double *partials, unsigned *tickets, int slot, int nslots,
-                                             double *s_tmp, double *s_out, int *s_flag)
+                                             double *s_tmp, double *s_out, int *s_flag, CgControl *ctrl)
 {
     const int tid = threadIdx.x;
     double *lvl = partials;
@@ -161,10 +174,8 @@ __device__ __forceinline__ bool reduce_slots(double *partials, unsigned *tickets
         const int ngroups = (count + kSlotGroup - 1) / kSlotGroup;
         const int gsize = min(kSlotGroup, count - g * kSlotGroup);
         unsigned *tk = &tickets[(size_t)g * kTicketStride];
-        if (tid == 0) {
-            const unsigned v = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            *s_flag = v == (unsigned)gsize - 1;
-        }
+        if (tid == 0)
+            *s_flag = take_ticket(tk, gsize, ctrl);
         __syncthreads();
         if (!*s_flag)
             return false;
@@ -220,7 +231,7 @@ __device__ __forceinline__ double part_sum(const PartRegs<NR> &r, double *s_red)
 // (reduce_slots' tickets), down to the level consumer_level() names.
 template <int L>
 __device__ __forceinline__ void publish_partials(double *partials, unsigned *tickets, int slot, int nslots, int stop,
-                                                 double *s_tmp, double *s_out, int *s_flag)
+                                                 double *s_tmp, double *s_out, int *s_flag, CgControl *ctrl)
 {
     const int tid = threadIdx.x;
     double *lvl = partials;
@@ -230,10 +241,8 @@ __device__ __forceinline__ void publish_partials(double *partials, unsigned *tic
         const int ngroups = (count + kSlotGroup - 1) / kSlotGroup;
         const int gsize = min(kSlotGroup, count - g * kSlotGroup);
         unsigned *tk = &tickets[(size_t)g * kTicketStride];
-        if (tid == 0) {
-            const unsigned v = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            *s_flag = v == (unsigned)gsize - 1;
-        }
+        if (tid == 0)
+            *s_flag = take_ticket(tk, gsize, ctrl);
         __syncthreads();
         if (!*s_flag)
             return;
@@ -629,6 +638,8 @@ struct TileArgs {
     double *__restrict__ carry_val;    // [tile][L] split-row partials, agent-scope stores (close_split_rows)
     const int4 *fix;                   // TilePlan::d_fix / d_fix_cnt (null: the plan splits no row)
     unsigned *fix_cnt;
+    unsigned *fault;                   // where a ticket overrun is raised (ticket_arrive): the CG's control word,
+                                       // else the handle's fault word (mspmv_check_faults)
     double *head_val;                  // [tile][L]: the first row of a tile that completes a split row
     double *head_pub;                  // [tile][L]: the same, republished with agent scope (close_split_rows)
     double *y0;                        // per tile (set by the kernel): where row 0 of the tile goes --
@@ -1524,7 +1535,7 @@ __device__ __forceinline__ void cg1_publish(const TileArgs &a, SM &sm, int slot,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    publish_partials<1>(a.partials, a.gtickets, slot, nslots, kConsumeTile, sm.prod, sm.red, &sm.last);
+    publish_partials<1>(a.partials, a.gtickets, slot, nslots, kConsumeTile, sm.prod, sm.red, &sm.last, a.ctrl);
 }
 
 // Single right-hand side, one tile per workgroup of TB threads.  TILE = TB*IPT merge items
@@ -2454,7 +2465,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_dot(const double *part, int T, 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    if (!reduce_slots<L>(lvl, tickets, blockIdx.x, gridDim.x, s_tmp, s_out, &s_last))
+    if (!reduce_slots<L>(lvl, tickets, blockIdx.x, gridDim.x, s_tmp, s_out, &s_last, ctrl))
         return;
     if (tid < L) {
         const double d = s_out[tid];
@@ -2614,7 +2625,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_init(CgVecArgs a)
         acc.x += b * b;
     }
     colpair_block_reduce<L>(acc, s_red2, a.partials + (size_t)blockIdx.x * L);
-    if (!reduce_slots<L>(a.partials, a.gtickets, blockIdx.x, gridDim.x, s_colred, s_out, &s_last))
+    if (!reduce_slots<L>(a.partials, a.gtickets, blockIdx.x, gridDim.x, s_colred, s_out, &s_last, a.ctrl))
         return;
     if (a.red_out) {
         if (tid < L)
@@ -2716,7 +2727,7 @@ __global__ __launch_bounds__(kBlock) void k_cg_update(CgVecArgs a)
         acc.x += r * r;
     }
     colpair_block_reduce<L>(acc, s_red2, a.partials + (size_t)blockIdx.x * L);
-    if (!reduce_slots<L>(a.partials, a.gtickets, blockIdx.x, gridDim.x, s_colred, s_out, &s_last))
+    if (!reduce_slots<L>(a.partials, a.gtickets, blockIdx.x, gridDim.x, s_colred, s_out, &s_last, a.ctrl))
         return;
     if (a.red_out) {
         if (tid < L)
@@ -2964,7 +2975,7 @@ __global__ __launch_bounds__(kBlock) void k_pcg_dot(CgVecArgs a, int mode)
     if ((a.n_elems & 1) && blockIdx.x == 0 && tid == 0)
         acc.x += a.r[a.n_elems - 1] * a.p[a.n_elems - 1];
     colpair_block_reduce<L>(acc, s_red2, a.partials + (size_t)blockIdx.x * L);
-    if (!reduce_slots<L>(a.partials, a.gtickets, blockIdx.x, gridDim.x, s_colred, s_out, &s_last))
+    if (!reduce_slots<L>(a.partials, a.gtickets, blockIdx.x, gridDim.x, s_colred, s_out, &s_last, a.ctrl))
         return;
     if (mode == 2) {  // split CG: p.Ap (a.r = p, a.p = Ap) -> red_out, breakdown per column
         if (tid < L) {
@@ -3323,6 +3334,7 @@ static TileArgs make_args(mspmv_handle_s *h, const TilePlan &plan, const double 
     a.carry_val = plan.d_carry_val;
     a.fix = plan.num_carries ? plan.d_fix : nullptr;  // split rows: closed by the tile kernels
     a.fix_cnt = plan.d_fix_cnt;
+    a.fault = h->d_fault;
     a.head_val = plan.d_carry_val + (size_t)std::max(plan.num_tiles, 1) * plan.carry_L;
     a.head_pub = a.head_val + (size_t)std::max(plan.num_tiles, 1) * plan.carry_L;
     a.num_tiles = plan.num_tiles;
@@ -3780,8 +3792,11 @@ bool dia_dot_fused()
     return !(e && *e && atoi(e) == 0);
 }
 
-static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &plan, double *d_x, int L, int nblk,
-                                            double tol)
+// splan: the plan the solve chose for the plain L-wide product (cg_solve_native: the offset-window or
+// column-slab plan, else null -> the tiles of `plan`); dot_fused: the window SpMM takes p.Ap in its dot
+// mode (resolved once per solve, and part of the CG graph's key).
+static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &plan, const TilePlan *splan,
+                                            bool dot_fused, double *d_x, int L, int nblk, double tol)
 {
     CgVecArgs va{};
     va.n_elems = (long long)h->m * L;
@@ -3807,31 +3822,31 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
     va.rev = 0;
     if (e != hipSuccess)
         return e;
-    const auto dp = h->dia == 1 && (L == 1 || dia_spmm_enabled()) ? h->plans.find(kDiaPlanKey) : h->plans.end();
-    if (dp != h->plans.end() && dia_dot_fused()) {
+    const TilePlan *dp = splan && splan->dia ? splan : nullptr;
+    const TilePlan *sp = splan && splan->slab ? splan : nullptr;
+    if (dp && dot_fused) {
         // offset windows (mspmv_dia.hip) in dot mode: Ap and one p.Ap partial per window, folded with the
         // non-finite-alpha stop -- no separate pass over p and Ap
-        if ((e = launch_dia(h, dp->second, h->d_p0, h->d_ap, L, L, h->d_ctrl, h->d_partials)) != hipSuccess)
+        if ((e = launch_dia(h, *dp, h->d_p0, h->d_ap, L, L, h->d_ctrl, h->d_partials)) != hipSuccess)
             return e;
-        if ((e = launch_fold_dot(dp->second.num_tiles, L, h->d_partials, h->d_gtickets, h->d_red, h->d_scal,
-                                 h->d_conv, h->d_ctrl, -1, h->stream)) != hipSuccess)
+        if ((e = launch_fold_dot(dp->num_tiles, L, h->d_partials, h->d_gtickets, h->d_red, h->d_scal, h->d_conv,
+                                 h->d_ctrl, -1, h->stream)) != hipSuccess)
             return e;
     } else if (cg_dot_pass(L)) {
         // the plain SpMM (its tile kernel holds fewer registers than the dot mode's, so more
         // workgroups per CU, and never spills), stopped by the control word, then p.Ap in one
         // streaming pass over p and Ap with the fold's breakdown checks (k_pcg_dot mode 2)
         // (on the offset-window or column-slab plan when the handle's plain L-wide product took one)
-        const auto sp = (L == 8 || L == 16) && h->spmm_slab[l_index(L)] == 1 ? h->plans.find(slab_mm_key(L))
-                                                                              : h->plans.end();
-        if (dp != h->plans.end()) {
-            if ((e = launch_dia(h, dp->second, h->d_p0, h->d_ap, L, L, h->d_ctrl)) != hipSuccess)
+        if (dp) {
+            if ((e = launch_dia(h, *dp, h->d_p0, h->d_ap, L, L, h->d_ctrl)) != hipSuccess)
                 return e;
-        } else if (sp != h->plans.end()) {
-            if ((e = launch_slab_mm(h, sp->second, h->d_p0, h->d_ap, L, L, h->d_ctrl)) != hipSuccess)
+        } else if (sp) {
+            if ((e = launch_slab_mm(h, *sp, h->d_p0, h->d_ap, L, L, h->d_ctrl)) != hipSuccess)
                 return e;
         } else {
             TileArgs ta = make_args(h, plan, h->d_p0, h->d_ap, L);
             ta.ctrl = h->d_ctrl;
+            ta.fault = &h->d_ctrl->fault;
             if ((e = launch_tile<kModeSpmv>(ta, L, h->stream, stream_nt(h))) != hipSuccess)
                 return e;
         }
@@ -3880,11 +3895,11 @@ bool cg_split_iteration(int L)
     return L >= 2 || mode != 0;
 }
 
-hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *d_x, int L, int parity, int nblk,
-                               double tol)
+hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, const TilePlan *splan, bool dot_fused,
+                               double *d_x, int L, int parity, int nblk, double tol)
 {
     if (cg_split_iteration(L))
-        return launch_cg_iteration_split(h, plan, d_x, L, nblk, tol);
+        return launch_cg_iteration_split(h, plan, splan, dot_fused, d_x, L, nblk, tol);
     double *rp_old = parity ? h->d_p1 : h->d_p0;  // {r_k, p_{k-1}} interleaved (cg_rp)
     double *rp_new = parity ? h->d_p0 : h->d_p1;  // receives p_k, then r_{k+1}
     TileArgs ta = make_args(h, plan, rp_old, h->d_ap, 1);
@@ -3892,6 +3907,7 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, double *
     ta.xsol = d_x;
     ta.scal = h->d_scal;
     ta.ctrl = h->d_ctrl;
+    ta.fault = &h->d_ctrl->fault;
     ta.partials = h->d_partials;
     ta.gtickets = h->d_gtickets;
     ta.part_in = h->d_partials_b;
@@ -3965,6 +3981,7 @@ hipError_t launch_spmm_dot_tiles(mspmv_handle_s *h, const TilePlan &plan, const 
     TileArgs ta = make_args(h, plan, d_X, d_Y, L);
     ta.xr = d_X + row_off * L;  // the handle's rows start at row row_off of X
     ta.ctrl = ctrl;
+    ta.fault = ctrl ? &ctrl->fault : h->d_fault;
     ta.partials = partials;
     return launch_tile<kModeDot>(ta, L, s, stream_nt(h));
 }

@@ -54,6 +54,7 @@ struct SlabArgs {
     double *carry_val;
     double *head_val;
     double *head_pub;
+    unsigned *fault;            // the handle's fault word (ticket_arrive)
 };
 
 template <bool NT, typename T>
@@ -77,8 +78,7 @@ __device__ __forceinline__ void group_out(const SlabArgs &a, int b, int r0, int 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this group's partials are out
     __syncthreads();
     if (tid == 0)
-        s_last = __hip_atomic_fetch_add(&a.gcnt[rb], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                 (unsigned)(G - 1);
+        s_last = ticket_arrive(&a.gcnt[rb], (unsigned)(G - 1), a.fault);
     __syncthreads();
     if (!s_last)
         return;
@@ -462,6 +462,7 @@ hipError_t launch_slab(mspmv_handle_s *h, const TilePlan &plan, const double *d_
     a.split = plan.d_split;
     a.fix = plan.num_carries ? plan.d_fix : nullptr;
     a.fix_cnt = plan.d_fix_cnt;
+    a.fault = h->d_fault;
     a.carry_val = plan.d_carry_val;
     a.head_val = plan.d_carry_val + (size_t)std::max(plan.num_tiles, 1) * plan.carry_L;
     a.head_pub = a.head_val + (size_t)std::max(plan.num_tiles, 1) * plan.carry_L;
@@ -1183,6 +1184,7 @@ struct SlabMmArgs {
     double *carry_val;
     double *head_val;
     double *head_pub;
+    unsigned *fault;            // the handle's fault word (ticket_arrive)
 };
 
 // Configurations (one kernel instance each): LDS = 2 x cols x L x 8 (two segment buffers) + (rows + 1) x
@@ -1481,6 +1483,7 @@ hipError_t launch_slab_mm(mspmv_handle_s *h, const TilePlan &plan, const double 
     a.split = plan.d_split;
     a.fix = plan.num_carries ? plan.d_fix : nullptr;
     a.fix_cnt = plan.d_fix_cnt;
+    a.fault = ctrl ? &const_cast<CgControl *>(ctrl)->fault : h->d_fault;
     a.carry_val = plan.d_carry_val;
     a.head_val = plan.d_carry_val + (size_t)std::max(plan.num_tiles, 1) * plan.carry_L;
     a.head_pub = a.head_val + (size_t)std::max(plan.num_tiles, 1) * plan.carry_L;

@@ -32,8 +32,11 @@ SIMPLE, MERGE, NONZERO_SPLIT = 0, 1, 2  # SpmmKernel, work_2025/types.hpp:11-16
 
 STATUS = {
     0: "OK", 1: "INVALID", 2: "HIP", 3: "OOM", 4: "BREAKDOWN", 5: "RCCL", 6: "UNSUPPORTED", 7: "IO",
-    8: "STALL",
+    8: "STALL", 9: "FAULT",
 }
+FAULT = 9  # a fold ticket drew past its group (mspmv_check_faults): results invalid, always raised
+# unless a caller asks for it (the poisoned-ticket tests)
+POISON_FILL, POISON_LATE_ZERO, POISON_NO_STOP = 1, 2, 4  # mspmv_test_poison_tickets flags
 # CG calls return their status beside X: BREAKDOWN (4) is a per-column numerical event (the
 # frozen columns are reported, the others solved), so it is returned, not raised; everything
 # else -- STALL (8, an IC(0) triangular solve that never progressed) included -- raises.
@@ -80,6 +83,9 @@ _SIGS = {
     "mspmv_shape": (_I, [_P, _PI, _PI, _PI]),
     "mspmv_setup_ms": (_D, [_P]),
     "mspmv_sync": (_I, [_P]),
+    "mspmv_check_faults": (_I, [_P]),
+    "mspmv_test_poison_tickets": (_I, [_P, ctypes.c_uint, _I]),
+    "mspmv_dist_test_poison_tickets": (_I, [_P, ctypes.c_uint, _I]),
     "mspmv_set_cu_limit": (_I, [_P, _I]),
     "mspmv_merge_coords": (_I, [_P, _I, ctypes.POINTER(Coord)]),
     "mspmv_dspmv": (_I, [_P, _P, _P]),
@@ -427,6 +433,15 @@ class GpuCsr:
     def sync(self):
         _check(lib.mspmv_sync(self.h), "sync")
 
+    def check_faults(self):
+        """mspmv_check_faults: raises MspmvError(FAULT) if a product since the last check drew a ticket
+        past its group."""
+        _check(lib.mspmv_check_faults(self.h), "check_faults")
+
+    def test_poison_tickets(self, value: int, flags: int = POISON_FILL):
+        """Test hook: the next CG solve's fold tickets start at `value` (mspmv_test_poison_tickets)."""
+        _check(lib.mspmv_test_poison_tickets(self.h, value, flags), "test_poison_tickets")
+
     def set_cu_limit(self, num_cus: int):
         """Run this handle's work on num_cus compute units (<= 0: all) -- mspmv_set_cu_limit."""
         _check(lib.mspmv_set_cu_limit(self.h, int(num_cus)), "set_cu_limit")
@@ -529,7 +544,8 @@ class GpuCsr:
         _check(st, "dcg_single", allow=(4,))
         return x, it.value, hist[: min(it.value, hist_cap)], st
 
-    def cg_multi(self, B: np.ndarray, max_iters: int, tolerance: float, kernel: int = MERGE, hist_cap: int = 0):
+    def cg_multi(self, B: np.ndarray, max_iters: int, tolerance: float, kernel: int = MERGE, hist_cap: int = 0,
+                 allow_fault: bool = False):
         B = np.ascontiguousarray(B, np.float64)
         L = B.shape[1]
         X = np.empty_like(B)
@@ -537,7 +553,7 @@ class GpuCsr:
         hist = np.zeros(max(hist_cap, 1), np.float64)
         st = lib.mspmv_dcg_multi(self.h, _ptr(B), _ptr(X), L, max_iters, tolerance, kernel, ctypes.byref(it),
                                  _ptr(hist) if hist_cap else None, hist_cap)
-        _check(st, "dcg_multi", allow=(4,))
+        _check(st, "dcg_multi", allow=(4, FAULT) if allow_fault else (4,))
         return X, it.value, hist[: min(it.value, hist_cap)], st
 
     def cg_dev(self, dB: DeviceBuffer, dX: DeviceBuffer, L: int, max_iters: int, tolerance: float,
@@ -892,13 +908,17 @@ class DistCsr:
         return ms.value
 
     def cg_dev(self, dB: DeviceBuffer, dX: DeviceBuffer, L: int, max_iters: int, tolerance: float,
-               hist_cap: int = 0):
+               hist_cap: int = 0, allow_fault: bool = False):
         it = ctypes.c_int()
         hist = np.zeros(max(hist_cap, 1))
         st = lib.mspmv_dist_cg_dev(self.h, dB.ptr, dX.ptr, L, max_iters, tolerance, ctypes.byref(it),
                                    _ptr(hist) if hist_cap else None, hist_cap)
-        _check(st, "dist_cg_dev", allow=(4,))
+        _check(st, "dist_cg_dev", allow=(4, FAULT) if allow_fault else (4,))
         return it.value, hist[: min(it.value, hist_cap)], st
+
+    def test_poison_tickets(self, value: int, flags: int = POISON_FILL):
+        """Test hook: the next sharded CG solve's fold tickets start at `value`."""
+        _check(lib.mspmv_dist_test_poison_tickets(self.h, value, flags), "dist_test_poison_tickets")
 
     def close(self):
         if getattr(self, "h", None):
