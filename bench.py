@@ -123,6 +123,7 @@ def pmc_traffic(kernel, bytes_launch):
 PWTK = dict(m=217918, nnz=11524432, block=6, half_band_nodes=1700)
 PARABOLIC_FEM = dict(m=525825, width=725, shift=1e-4)
 NLPKKT120 = dict(dims=(160, 135, 164), shift=1e-2, L=8)
+KKT120 = dict(dims=(120, 120, 123), eps=1e-2)  # 2 x 120 x 120 x 123 = nlpkkt120's 3,542,400 rows
 
 
 def spmv_bytes(m, n, nnz):
@@ -334,6 +335,112 @@ def run_spmv_shapes(dev, cpu_seconds, do_cpu):
     return out
 
 
+class env_set:
+    """Environment switches for the handles created inside the block (the plan decisions read them per
+    handle: MSPMV_DIA, MSPMV_SPMV_RUNS)."""
+
+    def __init__(self, **kv):
+        self.kv, self.old = kv, {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = os.environ.get(k)
+            os.environ[k] = v
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def time_batch_on(mats, dxs, dys, dev, steps, **env):
+    """Per-launch kernel ms of a batch of plain SpMVs on handles created under `env`, and the kernel name."""
+    with env_set(**env):
+        gs = [mspmv.GpuCsr(a, device=dev) for a in mats]
+    try:
+        mspmv.time_spmm_batch(gs, dxs, dys, 1, 5)
+        _, kern_ms, _ = mspmv.time_spmm_batch(gs, dxs, dys, 1, steps)
+        return kern_ms, gs[0].kernel_name()
+    finally:
+        for g in gs:
+            g.close()
+
+
+def merge_path_entry(kern_ms, kname, nb, nnz, what):
+    return {"plan": what, "kernel": kname, "kernel_ms": round(kern_ms, 5),
+            "gflops": round(2.0 * nnz / kern_ms / 1e6, 1), "bytes_per_launch": nb,
+            "frac": round(nb / kern_ms / 1e6 / HBM_PEAK_GBS, 4)}
+
+
+def run_merge_path_generic(dev, batch=4, steps=50):
+    """The headline batch on the plain merge-path tiles with no node blocks (k_spmv_tile; run by bench.py
+    as a child process under MSPMV_SPMV_BLOCKS=0, a per-process switch)."""
+    mats = [mspmv.CsrMatrix.synth_fem_blocked(PWTK["m"], PWTK["nnz"], PWTK["block"], PWTK["half_band_nodes"],
+                                              seed=1 + i) for i in range(batch)]
+    dxs = [mspmv.DeviceBuffer.from_array(np.random.default_rng(2 + i).uniform(0.0, 1.0, a.num_cols), dev)
+           for i, a in enumerate(mats)]
+    dys = [mspmv.DeviceBuffer(8 * a.num_rows, dev) for a in mats]
+    k, name = time_batch_on(mats, dxs, dys, dev, steps, MSPMV_SPMV_RUNS="0")
+    a0 = mats[0]
+    return merge_path_entry(k, name, spmv_bytes(a0.num_rows, a0.num_cols, a0.num_nonzeros), a0.num_nonzeros,
+                            "merge-path tiles of 2,048 merge items, striped staging, no node blocks (MSPMV_SPMV_BLOCKS=0)")
+
+
+def merge_path_generic_child(dev):
+    """run_merge_path_generic in a child process (MSPMV_SPMV_BLOCKS is read once per process)."""
+    import subprocess
+    env = dict(os.environ, MSPMV_SPMV_BLOCKS="0")
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "--only", "merge_path_generic", "--device", str(dev)],
+                       env=env, capture_output=True, text=True, timeout=300)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": (r.stderr or "no output")[-300:]}
+    d = json.loads(lines[-1])
+    d.pop("leg", None)
+    return d
+
+
+def run_window_shapes(dev, steps=40):
+    """Shapes the offset windows were not designed on, at the nlpkkt120 size, SpMV cold-free
+    back to back (1 GB+ per launch: never Infinity-Cache resident): the 27-point stencil with 1 % of the
+    rows holding an off-pattern column and 0.1 % holding eight (rows of 35), and a KKT saddle point
+    [[H, B^T], [B, -eps I]] (nlpkkt120's block structure: 27-point H, 7-point B; 34 offsets in the upper
+    rows).  The default plan (windows plus a remainder) beside the merge-path tiles (MSPMV_DIA=0)."""
+    out = {}
+    shapes = {
+        "stencil27_perturbed": (lambda: mspmv.CsrMatrix.synth_stencil_perturbed(
+            NLPKKT120["dims"], seed=5, diag_shift=NLPKKT120["shift"], extra_frac=0.01, long_frac=0.001),
+            "nlpkkt120-size 27-point stencil, 1 % of rows one off-pattern column, 0.1 % eight"),
+        "kkt": (lambda: mspmv.CsrMatrix.synth_kkt(KKT120["dims"], seed=6, eps=KKT120["eps"]),
+                "KKT saddle point [[H, B^T], [B, -eps I]], 27-point H, 7-point B, 2 x 120 x 120 x 123 rows"),
+    }
+    for name, (make, what) in shapes.items():
+        a = make()
+        n, nnz = a.num_rows, a.num_nonzeros
+        nb = spmv_bytes(n, a.num_cols, nnz)
+        w = mspmv.offset_windows(a)
+        dx = mspmv.DeviceBuffer.from_array(np.random.default_rng(7).uniform(0, 1, a.num_cols), dev)
+        dy = mspmv.DeviceBuffer(8 * n, dev)
+        r = {"workload": what, "m": n, "nnz": nnz, "bytes_per_launch": nb,
+             "window_remainder_entries": w["remainder"] if w else None,
+             "window_sum_offsets": w["sum_offsets"] if w else None}
+        for plan, env in (("default", {}), ("merge_path", {"MSPMV_DIA": "0"})):
+            with env_set(**env):
+                g = mspmv.GpuCsr(a, device=dev)
+            with g:
+                g.time_spmm(dx, dy, 1, 5)
+                _, k, _ = g.time_spmm(dx, dy, 1, steps)
+                r[plan] = {"kernel": g.kernel_name(), "kernel_ms": round(k, 5), "gflops": round(2.0 * nnz / k / 1e6, 1),
+                           "frac": round(nb / k / 1e6 / HBM_PEAK_GBS, 4), "setup_ms": round(g.setup_ms, 2)}
+        r["frac"] = r["default"]["frac"]
+        dx.free()
+        dy.free()
+        out[name] = r
+    return out
+
+
 def run_pwtk_perturbed(dev, batch=4, steps=50):
     """The headline's FEM shape made imperfect (the node-block plan must not be all-or-
     nothing): pwtk's m and nnz, ~2 % of the nodes with 5 or 7 unknowns instead of 6 and ~1 % of the
@@ -536,6 +643,13 @@ def run_cg_multi(d, dev):
                           "kernel": g.kernel_name(), "kernel_ms": round(kern_ms, 5), "gflops": round(2.0 * nk.num_nonzeros / kern_ms / 1e6, 1),
                           "bytes_per_launch": nb, "achieved_GBps": round(nb / kern_ms / 1e6, 1),
                           "frac": round(nb / kern_ms / 1e6 / HBM_PEAK_GBS, 4)}
+            with env_set(MSPMV_DIA="0"):  # north_star's merge-based figure: the same matrix on the merge-path tiles
+                gm = mspmv.GpuCsr(nk, device=dev)
+            with gm:
+                gm.time_spmm(dx1, dy1, 1, 5)
+                _, mk, _ = gm.time_spmm(dx1, dy1, 1, 40)
+                spmv_large["merge_path"] = merge_path_entry(mk, gm.kernel_name(), nb, nk.num_nonzeros,
+                                                            "merge-path tiles (MSPMV_DIA=0)")
         mode = "1 GPU"
     else:
         rb = mspmv.dist_partition(nk, d.world)
@@ -686,7 +800,9 @@ def main():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the hot-matrix and scatter-band side measurements (profiling runs: the "
                          "headline kernel's rocprofv3 average then covers exactly the timed launches)")
-    ap.add_argument("--only", choices=["spmm16", "spmv_shapes", "cg_single", "cg_multi", "pwtk_perturbed"],
+    ap.add_argument("--device", type=int, default=None, help="--only legs: the HIP device (default LOCAL_RANK)")
+    ap.add_argument("--only", choices=["spmm16", "spmv_shapes", "cg_single", "cg_multi", "pwtk_perturbed",
+                                       "merge_path_generic", "window_shapes"],
                     help="run one side measurement alone and print its JSON (profiling: rocprofv3 then sees only "
                          "that leg's launches; tools/profile_legs.sh)")
     ap.add_argument("--dry-run", action="store_true",
@@ -707,9 +823,13 @@ def main():
             d.td.destroy_process_group()
         return
     if args.only:
-        dev = d.local
+        dev = d.local if args.device is None else args.device
         do_cpu = not args.no_cpu
-        if args.only == "spmm16":
+        if args.only == "merge_path_generic":
+            r = run_merge_path_generic(dev)
+        elif args.only == "window_shapes":
+            r = run_window_shapes(dev)
+        elif args.only == "spmm16":
             r = run_spmm16(dev, min(args.cpu_seconds, 5.0), do_cpu)
         elif args.only == "spmv_shapes":
             r = run_spmv_shapes(dev, min(args.cpu_seconds, 3.0), do_cpu)
@@ -803,6 +923,18 @@ def main():
                                                         "one contiguous slice per workgroup, 4 workgroups per CU, "
                                                         "20 passes, HIP events (the best of the read shapes in "
                                                         "tools/read_ceiling.hip)")
+        if not args.no_extras:
+            # north_star's figure is merge-based CsrMV: the same batch on the merge-path tile plan (node blocks
+            # in registers, tiles cut at 2,048 merge items) beside the default run-balanced plan, and on the
+            # generic merge-path tiles (no node blocks) in a child process
+            mk, mname = time_batch_on(mats, dxs, dys, dev, 50, MSPMV_SPMV_RUNS="0")
+            result["merge_path"] = {
+                "note": "the headline batch on merge-path plans (the default plan above is run-balanced: tiles cut at "
+                        "FEM node-run starts, DESIGN 4.2)",
+                "node_blocks": merge_path_entry(mk, mname, bytes_launch, a0.num_nonzeros,
+                                                "merge-path tiles of 2,048 merge items, node blocks in registers "
+                                                "(MSPMV_SPMV_RUNS=0)"),
+                "generic": merge_path_generic_child(dev) if d.world == 1 else None}
         if hot_ms is not None:
             result["hot_single_matrix"] = {"ms_per_call": round(hot_ms, 5), "kernel_ms": round(hot_kern, 5),
                                            "GBps_vs_algorithmic": round(bytes_launch / (hot_kern * 1e-3) / 1e9, 1),
@@ -836,6 +968,7 @@ def main():
             result["spmv_pwtk_perturbed"] = run_pwtk_perturbed(dev)
             result["spmm16"] = run_spmm16(dev, min(args.cpu_seconds, 5.0), d.world == 1 and not args.no_cpu)
             result["spmv_shapes"] = run_spmv_shapes(dev, min(args.cpu_seconds, 3.0), d.world == 1 and not args.no_cpu)
+            result["window_shapes"] = run_window_shapes(dev)
 
         if d.rank == 0 and d.world == 1 and not args.no_cpu:
             y_cpu, cb = cpu_baseline(a0, xs[0], args.cpu_seconds)

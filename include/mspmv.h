@@ -285,16 +285,20 @@ MSPMV_API mspmv_status mspmv_tile_modes(mspmv_handle h, int L, unsigned char *mo
  * need to tell the rows summed sequentially from the split ones. */
 MSPMV_API mspmv_status mspmv_tile_lanes(mspmv_handle h, int L, int *lanes);
 /* Offset windows (host planning only, no device needed): whether a CSR matrix fits the plan the plain
- * SpMV takes by default for structured-grid rows -- 64-row windows whose rows list their columns at
- * <= 32 common offsets col - row, every row's columns ascending.  min_fill /
- * min_window_fill: the nonzeros' share of the windows' rows x offsets overall / in each window (the
- * library's automatic choice uses 0.85 / 0.30).  *ok = 1 when the plan holds; then *num_windows =
- * ceil(m / 64), *sum_offsets = the offsets over all windows, *masked_windows = windows where some row
- * lacks an offset (or that hold fewer than 64 rows); k_per_window (nullable, num_windows entries)
+ * SpMV takes by default for structured-grid rows -- 64-row windows, each keeping the offsets col - row
+ * that at least 8 of its rows hold (all rows when it has fewer; <= 64 offsets, the most frequent),
+ * dropping its rarest while its kept entries fill less than min_window_fill of rows x offsets; every
+ * other entry goes to the plan's remainder (summed after the row's offsets).  Every row's columns
+ * must ascend strictly.  The plan holds when the kept entries fill >= min_fill of the
+ * windows' 64 x sum K slots and the remainder is at most 5 % of the nonzeros (any share when min_fill
+ * is 0: the forced plan).  The library's automatic choice uses 0.85 / 0.30.  *ok = 1 when the plan
+ * holds; then *num_windows = ceil(m / 64), *sum_offsets = the offsets over all windows,
+ * *masked_windows = windows where some row lacks a kept offset (or that hold fewer than 64 rows),
+ * *remainder (nullable) = the remainder's entries; k_per_window (nullable, num_windows entries)
  * receives each window's offset count.  Outputs other than *ok are 0 when the plan does not hold. */
 MSPMV_API mspmv_status mspmv_offset_windows(const mspmv_csr_d *a, double min_fill, double min_window_fill, int *ok,
                                             int *num_windows, long long *sum_offsets, int *masked_windows,
-                                            int *k_per_window);
+                                            int *k_per_window, long long *remainder);
 /* The single-RHS SpMV kernel instantiation launched for this matrix (tuning read once from
  * the MSPMV_SPMV_* environment; nontemporal matrix loads above 128 MiB), e.g.
  * "k_spmv_tile<8,0,true>" -- the name rocprofv3 reports.  Valid until the next call on this

@@ -70,6 +70,21 @@ MSPMV_API mspmv_status mspmv_synth_stencil(int kind, int m, int dim0, int dim1, 
                                            double diag_shift, int *row_offsets, int *cols, double *vals,
                                            long long *nnz_out);
 
+/* The kind-1 27-point SPD stencil on dim0 x dim1 x dim2 made imperfect (a shape the
+ * offset windows were not designed on): each row gains one column at a random position within
+ * +-2 dim0 dim1 of the diagonal with probability extra_frac, and eight such columns with probability
+ * long_frac (rows of up to 36 entries); added values -U(0,1), columns sorted per row.  Not symmetric. */
+MSPMV_API mspmv_status mspmv_synth_stencil_perturbed(int dim0, int dim1, int dim2, unsigned long long seed,
+                                                     double diag_shift, double extra_frac, double long_frac,
+                                                     int *row_offsets, int *cols, double *vals, long long *nnz_out);
+
+/* KKT-shaped saddle-point matrix, nlpkkt120's block structure [[H, B^T], [B, -eps I]] with grid blocks:
+ * H = the SPD 27-point stencil (kind 1, diag_shift) on the N = dim0 dim1 dim2 grid, B = a 7-point grid
+ * operator (diagonal 1 + U(0,1), neighbours -U(0,1)/6).  m = 2 N (120 x 120 x 123: nlpkkt120's
+ * 3,542,400 rows); rows < N hold 27 + 7 entries, rows >= N 7 + 1.  Symmetric indefinite. */
+MSPMV_API mspmv_status mspmv_synth_kkt(int dim0, int dim1, int dim2, unsigned long long seed, double diag_shift,
+                                       double eps, int *row_offsets, int *cols, double *vals, long long *nnz_out);
+
 #ifdef __cplusplus
 }
 #endif

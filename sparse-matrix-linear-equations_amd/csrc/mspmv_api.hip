@@ -1677,7 +1677,7 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
     if (st == MSPMV_OK && max_iters > 0 && !hm && !ic) {
         // pipelined: the last iteration's stop test (a no-op once the solve has stopped); both
         // forms: the deferred x += alpha p of the last update
-        hipError_t ef = pipelined ? launch_cg1_finish(h, d_x, max_iters & 1, nblk) : launch_cg_xflush(h, d_x, L, nblk);
+        hipError_t ef = pipelined ? launch_cg1_finish(h, d_x, max_iters & 1, nblk) : launch_cg_xflush(h, d_x, L, nblk, splan, dot_fused);
         if (ef != hipSuccess) {
             set_error(std::string("CG finish launch: ") + hipGetErrorString(ef));
             st = MSPMV_ERR_HIP;

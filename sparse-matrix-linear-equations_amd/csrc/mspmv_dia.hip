@@ -19,10 +19,13 @@
 // each); a wave instruction reads 64/(L/2) consecutive panel rows -- 1 KB contiguous -- and a lane
 // holds L/2 rows of the window.
 //
-// The plan is all or nothing: every window of the matrix must fit (K <= kDiaMaxK, its nonzeros >=
-// min_window_fill x rows x K) and the whole matrix fill its panels (nonzeros >= min_fill x 64 x sum K:
-// the zeros of rows missing an offset -- grid boundaries -- are streamed too); anything else keeps
-// the tile plans.
+// Windows plus a remainder (round 6; round 5's plan was all or nothing): each window keeps the offsets
+// most of its rows hold (dia_plan_host: >= kDiaKeepRows rows, <= kDiaMaxK = 64 of them, its panels >=
+// min_window_fill full), and every other entry -- an off-pattern column, a row longer than the list --
+// goes to a remainder CSR over the same rows that the kernels add after the row's offsets.  The plan
+// holds when the remainder is <= kDiaMaxRemFrac of the nonzeros and the kept entries fill >= min_fill
+// of the panels (the zeros of rows missing an offset -- grid boundaries -- are streamed too); anything
+// else keeps the tile plans.
 #include "mspmv_device.h"
 #include "mspmv_internal.h"
 
@@ -48,6 +51,17 @@ struct DiaArgs {
     const CgControl *ctrl;           // CG: return at once when ctrl->done
     double *partials;                // dot mode: x.(A x) per column per window, [windows][L] (launch_fold_dot)
     const double *xr;                // dot mode: x at this matrix's rows (x + row_off * ld for a row-range view)
+    // block CG, p update fused (k_spmm_dia_wg PUPD): x above is p_old; the spans staged are
+    // p = r + beta p_old (CgScalars::beta per column), the window's own rows of p go to pnew and take
+    // the deferred x += alpha p_old (CgScalars::alpha, when ctrl->x_pending: CgVecArgs::lazy_x)
+    const double *r;
+    double *pnew;
+    double *xsol;
+    const CgScalars *scal;
+    // the remainder (entries off the window's offset list): a CSR over all rows, summed after the offsets
+    const int *rem_ptr;
+    const int *rem_col;
+    const double *rem_val;
     int windows;
     int groups;                      // workgroups (windows / 4, rounded up)
     int m;
@@ -104,11 +118,12 @@ k_spmm_dia(DiaArgs a)
         return;
     const int lane = threadIdx.x & 63;
     const int4 hd = a.hdr[w];
-    const int K = __builtin_amdgcn_readfirstlane(hd.x);
+    const int K = __builtin_amdgcn_readfirstlane(hd.x) & 0xffff;
+    const bool has_rem = (__builtin_amdgcn_readfirstlane(hd.x) >> 16) != 0;
     const bool masked = __builtin_amdgcn_readfirstlane(hd.w) >= 0;
-    const int lk = min(lane, K - 1);
-    const int offv = a.off[__builtin_amdgcn_readfirstlane(hd.y) + lk];
-    const unsigned long long mkv = masked ? a.mask[__builtin_amdgcn_readfirstlane(hd.w) + lk] : ~0ull;
+    const int lk = max(min(lane, K - 1), 0);
+    const int offv = K ? a.off[__builtin_amdgcn_readfirstlane(hd.y) + lk] : 0;
+    const unsigned long long mkv = masked && K ? a.mask[__builtin_amdgcn_readfirstlane(hd.w) + lk] : ~0ull;
     // value pairs of this window: pair p of lane l (offsets 2p, 2p+1 of row l) at vp[p * 64 + l]
     const v2d_t *__restrict__ vp = reinterpret_cast<const v2d_t *>(a.vt) + (size_t)__builtin_amdgcn_readfirstlane(hd.z) * 64;
     const int KP = (K + 1) >> 1;
@@ -169,6 +184,12 @@ k_spmm_dia(DiaArgs a)
             windows(std::true_type{});
         else
             windows(std::false_type{});
+        if (has_rem && r < a.m) {  // the row's remainder entries, in CSR order, after its offsets
+            double ar = 0.0;
+            for (int j = a.rem_ptr[r]; j < a.rem_ptr[r + 1]; ++j)
+                ar += a.rem_val[j] * a.x[a.rem_col[j]];
+            acc = acc + ar;  // + 0.0 for a row without any: acc is never -0.0, so the identity
+        }
         if (r < a.m)
             __builtin_nontemporal_store(acc, a.y + r);
         if constexpr (DOT) {
@@ -241,7 +262,8 @@ k_spmm_dia(DiaArgs a)
 #pragma unroll
         for (int q = 0; q < GL; ++q)
             acc[q] = v2d_t{0.0, 0.0};
-        fetch(0);
+        if (K > 0)
+            fetch(0);
         for (int k = 0; k < K;) {
             wave_sync();
 #pragma unroll
@@ -285,6 +307,23 @@ k_spmm_dia(DiaArgs a)
                 }
             }
         }
+        if (has_rem) {  // the rows' remainder entries, in CSR order, after their offsets
+#pragma unroll
+            for (int q = 0; q < GL; ++q) {
+                const long long r = r0 + rl + RS * q;
+                if (r >= a.m)
+                    continue;
+                v2d_t ar = v2d_t{0.0, 0.0};
+                for (int j = a.rem_ptr[r]; j < a.rem_ptr[r + 1]; ++j) {
+                    const double v = a.rem_val[j];
+                    const v2d_t xv = *reinterpret_cast<const v2d_t *>(xb + (size_t)a.rem_col[j] * a.ld);
+                    ar[0] += v * xv[0];
+                    ar[1] += v * xv[1];
+                }
+                acc[q][0] = acc[q][0] + ar[0];
+                acc[q][1] = acc[q][1] + ar[1];
+            }
+        }
 #pragma unroll
         for (int q = 0; q < GL; ++q) {
             const long long r = r0 + rl + RS * q;
@@ -313,31 +352,269 @@ k_spmm_dia(DiaArgs a)
     }
 }
 
-// Plan time: each window's values into its lane-major panel (the offsets were checked on the host:
-// every row's offsets ascend and each is in the window's list).
+// L = 8, 16: one window per WORKGROUP (four waves) instead of per wave.  The wave form holds L/2 rows
+// of the window per lane (126 VGPRs at L = 8: 4 waves per SIMD, each a serial chain of runs; 28 % of its
+// wave cycles waiting on memory, the rest issue and LDS latency -- r05ad counters).  Here thread t
+// holds row t / (L/2) (L = 8; rows t / 8 and t / 8 + 32 at L = 16) of the window and column pair t % (L/2):
+// the four waves stage each run's span of 64 + g - 1 panel rows in LDS together (one 16-B element per
+// thread and row slot, double-buffered, ONE workgroup barrier per run), each thread loads its own
+// rows' values (no shuffles) and sums its row in CSR order (offsets ascending, mul then add): the
+// products are the wave form's bit for bit.
+// PUPD (the block CG's iteration, CGSolveMultiple no_pretreatment.hpp:93-177 with the p update of
+// :177 moved ahead of the next SpMM): the spans staged are p = r + beta p_old (the reference's
+// update_p_multiple expression, per column), so the separate p update pass (k_dist_pupdate: r, p, x
+// read, p, x written) is gone; the window's own rows of p are written to pnew (ping-pong buffers:
+// other windows still read p_old) and take the deferred x += alpha p_old.
+// DOT: p.(A p) per column per window into partials (launch_fold_dot), p = the staged p (PUPD) or xr.
+template <int L, bool NT, bool DOT, bool PUPD>
+__global__ __launch_bounds__(kDiaThreads) void k_spmm_dia_wg(DiaArgs a)
+{
+    static_assert(L == 8 || L == 16, "workgroup windows: L = 8 or 16");
+    constexpr int GL = L / 2;                       // threads per panel row
+    constexpr int RPI = kDiaThreads / GL;            // panel rows per workgroup instruction
+    constexpr int NR = 64 / RPI;                     // window rows per thread
+    constexpr int SPAN = 64 + kDiaRun - 1;
+    constexpr int EDGE = (kDiaRun - 1) * GL;         // span elements past row 63
+    static_assert(EDGE <= kDiaThreads, "edge rows: one element per thread");
+    __shared__ v2d_t sx[2][SPAN * GL];
+    __shared__ v2d_t s_dot[kDiaWaves][GL];
+    const int w = xcd_tile(blockIdx.x, a.windows);
+    if (a.ctrl && a.ctrl->done)
+        return;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int c = tid % GL, rl = tid / GL;
+    const int4 hd = a.hdr[w];
+    const int K = __builtin_amdgcn_readfirstlane(hd.x) & 0xffff;
+    const bool has_rem = (__builtin_amdgcn_readfirstlane(hd.x) >> 16) != 0;
+    const bool masked = __builtin_amdgcn_readfirstlane(hd.w) >= 0;
+    const int lk = max(min(lane, K - 1), 0);
+    const int offv = K ? a.off[__builtin_amdgcn_readfirstlane(hd.y) + lk] : 0;
+    const unsigned long long mkv = masked && K ? a.mask[__builtin_amdgcn_readfirstlane(hd.w) + lk] : ~0ull;
+    auto off_at = [&](int k) { return __builtin_amdgcn_readlane(offv, k); };
+    auto mask_at = [&](int k) {
+        const unsigned lo = __builtin_amdgcn_readlane((unsigned)mkv, k);
+        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(mkv >> 32), k);
+        return ((unsigned long long)hi << 32) | lo;
+    };
+    int runv = 1;  // run length from offset k (lane k): consecutive offsets, <= kDiaRun, within the list
+    {
+        int step = 1;
+#pragma unroll
+        for (int j = 1; j < kDiaRun; ++j) {
+            const int nxt = __shfl_down(offv, j);
+            step = step && lane + j < K && nxt == offv + j;
+            runv += step;
+        }
+    }
+    const long long r0 = (long long)w * 64;
+    const long long nmax = a.n - 1;
+    const double *__restrict__ vb = a.vt + (size_t)__builtin_amdgcn_readfirstlane(hd.z) * 128;
+    double2 beta = make_double2(0.0, 0.0), alpha = make_double2(0.0, 0.0);
+    bool lag = false;
+    if constexpr (PUPD) {
+        beta = make_double2(a.scal[2 * c].beta, a.scal[2 * c + 1].beta);
+        alpha = make_double2(a.scal[2 * c].alpha, a.scal[2 * c + 1].alpha);
+        lag = a.ctrl->x_pending != 0;
+    }
+    // span element (span row sr, column pair c): p_old, or r + beta p_old
+    auto span_ld = [&](long long xrow) -> v2d_t {
+        const size_t o = (size_t)xrow * a.ld + 2 * c;
+        const v2d_t q = *reinterpret_cast<const v2d_t *>(a.x + o);
+        if constexpr (PUPD) {
+            const v2d_t rv = *reinterpret_cast<const v2d_t *>(a.r + o);
+            return v2d_t{rv[0] + beta.x * q[0], rv[1] + beta.y * q[1]};
+        } else {
+            return q;
+        }
+    };
+    v2d_t nx[NR], ne = v2d_t{0.0, 0.0};
+    double nv[kDiaRun][NR];
+    auto fetch = [&](int k) {  // run k's span (rows clamped into X: outside it they serve absent entries only)
+        const long long s0 = r0 + off_at(k);
+#pragma unroll
+        for (int q = 0; q < NR; ++q)
+            nx[q] = span_ld(min(max(s0 + rl + RPI * q, 0LL), nmax));
+        if (tid < EDGE)
+            ne = span_ld(min(max(s0 + 64 + tid / GL, 0LL), nmax));
+#pragma unroll
+        for (int j = 0; j < kDiaRun; ++j) {
+            const int kk = min(k + j, K - 1);
+#pragma unroll
+            for (int q = 0; q < NR; ++q)
+                nv[j][q] = dia_ld<NT>(vb + (size_t)(kk >> 1) * 128 + 2 * (rl + RPI * q) + (kk & 1));
+        }
+    };
+    auto stage = [&](int buf) {
+#pragma unroll
+        for (int q = 0; q < NR; ++q)
+            sx[buf][(rl + RPI * q) * GL + c] = nx[q];
+        if (tid < EDGE)
+            sx[buf][64 * GL + tid] = ne;
+    };
+    v2d_t acc[NR];
+#pragma unroll
+    for (int q = 0; q < NR; ++q)
+        acc[q] = v2d_t{0.0, 0.0};
+    if (K > 0) {
+        fetch(0);
+        stage(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int k = 0; k < K;) {
+        double cv[kDiaRun][NR];
+#pragma unroll
+        for (int j = 0; j < kDiaRun; ++j)
+#pragma unroll
+            for (int q = 0; q < NR; ++q)
+                cv[j][q] = nv[j][q];
+        const int gk = __builtin_amdgcn_readlane(runv, k), kc = k;
+        k += gk;
+        if (k < K)  // the next run's span and values fly while this one is summed
+            fetch(k);
+#pragma unroll
+        for (int j = 0; j < kDiaRun; ++j) {
+            if (j >= gk)
+                break;
+            const unsigned long long mw = masked ? mask_at(kc + j) : ~0ull;
+#pragma unroll
+            for (int q = 0; q < NR; ++q) {
+                const int row = rl + RPI * q;
+                const v2d_t xv = sx[buf][(row + j) * GL + c];
+                const double v = cv[j][q];
+                if (mw == ~0ull) {  // every row holds this offset (workgroup-uniform): no selects
+                    acc[q][0] += v * xv[0];
+                    acc[q][1] += v * xv[1];
+                } else {
+                    const bool on = (mw >> row) & 1ull;
+                    acc[q][0] += on ? v * xv[0] : 0.0;
+                    acc[q][1] += on ? v * xv[1] : 0.0;
+                }
+            }
+        }
+        if (k < K)
+            stage(buf ^ 1);
+        __syncthreads();  // run kc's reads of sx[buf] and the next span's writes to sx[buf ^ 1] are done
+        buf ^= 1;
+    }
+    if (has_rem) {  // the rows' remainder entries, in CSR order, after their offsets (p at their columns)
+#pragma unroll
+        for (int q = 0; q < NR; ++q) {
+            const long long r = r0 + rl + RPI * q;
+            if (r >= a.m)
+                continue;
+            v2d_t ar = v2d_t{0.0, 0.0};
+            for (int j = a.rem_ptr[r]; j < a.rem_ptr[r + 1]; ++j) {
+                const double v = a.rem_val[j];
+                const v2d_t xv = span_ld(a.rem_col[j]);
+                ar[0] += v * xv[0];
+                ar[1] += v * xv[1];
+            }
+            acc[q][0] = acc[q][0] + ar[0];
+            acc[q][1] = acc[q][1] + ar[1];
+        }
+    }
+    v2d_t d = v2d_t{0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+        const long long r = r0 + rl + RPI * q;
+        if (r >= a.m)
+            continue;
+        const size_t o = (size_t)r * a.ld + 2 * c;
+        __builtin_nontemporal_store(acc[q], reinterpret_cast<v2d_t *>(a.y + o));
+        v2d_t pv;
+        if constexpr (PUPD) {  // the window's own rows: p = r + beta p_old to pnew, x += alpha p_old
+            const v2d_t q0 = *reinterpret_cast<const v2d_t *>(a.x + o);
+            const v2d_t rv = *reinterpret_cast<const v2d_t *>(a.r + o);
+            pv = v2d_t{rv[0] + beta.x * q0[0], rv[1] + beta.y * q0[1]};
+            *reinterpret_cast<v2d_t *>(a.pnew + o) = pv;
+            if (lag) {
+                const v2d_t xo = __builtin_nontemporal_load(reinterpret_cast<const v2d_t *>(a.xsol + o));
+                __builtin_nontemporal_store(v2d_t{xo[0] + alpha.x * q0[0], xo[1] + alpha.y * q0[1]},
+                                            reinterpret_cast<v2d_t *>(a.xsol + o));
+            }
+        } else if constexpr (DOT) {
+            pv = *reinterpret_cast<const v2d_t *>(a.xr + o);
+        }
+        if constexpr (DOT) {
+            d[0] += pv[0] * acc[q][0];
+            d[1] += pv[1] * acc[q][1];
+        }
+    }
+    if constexpr (DOT) {  // column pair c: rows in q order, the wave's rows by a fixed butterfly, waves in order
+#pragma unroll
+        for (int off = 32; off >= GL; off >>= 1) {
+            d[0] += __shfl_xor(d[0], off);
+            d[1] += __shfl_xor(d[1], off);
+        }
+        if (lane < GL)
+            s_dot[wv][lane] = d;
+        __syncthreads();
+        if (tid < GL) {
+            v2d_t t = s_dot[0][tid];
+#pragma unroll
+            for (int u = 1; u < kDiaWaves; ++u) {
+                t[0] += s_dot[u][tid][0];
+                t[1] += s_dot[u][tid][1];
+            }
+            *reinterpret_cast<v2d_t *>(a.partials + (size_t)w * L + 2 * tid) = t;
+        }
+    }
+}
+
+// Plan time: each window's values into its lane-major panel.  One workgroup per window streams the
+// window's CSR entries coalesced (its row offsets and offset list in LDS; an entry finds its row and its
+// offset index by binary searches there); entries off the list are the remainder's (k_dia_rem_fill).  The
+// round-5 form (one lane per row walking its own entries) read 64 scattered lines per wave instruction:
+// 23.8 GB moved to fill 1.2 GB of panels on the nlpkkt120 size.
 __global__ __launch_bounds__(kDiaThreads) void k_dia_fill(const int *__restrict__ ro, const int *__restrict__ ci,
                                                          const double *__restrict__ vals, const int4 *__restrict__ hdr,
                                                          const int *__restrict__ off, int windows, int m,
                                                          double *__restrict__ vt)
 {
-    const int w = blockIdx.x * kDiaWaves + ((int)threadIdx.x >> 6);
-    if (w >= windows)
-        return;
-    const int lane = threadIdx.x & 63;
-    const int r = w * 64 + lane;
-    if (r >= m)
-        return;
+    __shared__ int s_ro[65];
+    __shared__ int s_d[kDiaMaxK];
+    const int w = blockIdx.x;
+    const int r0 = w * 64, nr = min(m - r0, 64);
     const int4 hd = hdr[w];
-    const int *D = off + hd.y;
-    int k = 0;
-    for (int j = ro[r]; j < ro[r + 1]; ++j) {
-        const int d = ci[j] - r;
-        while (k < hd.x && D[k] < d)
-            ++k;
-        if (k < hd.x)
-            vt[((size_t)hd.z + (k >> 1)) * 128 + 2 * lane + (k & 1)] = vals[j];
-        ++k;
+    const int K = hd.x & 0xffff;
+    const int tid = threadIdx.x;
+    if (tid <= nr)
+        s_ro[tid] = ro[r0 + tid];
+    if (tid < K)
+        s_d[tid] = off[hd.y + tid];
+    __syncthreads();
+    if (K == 0)
+        return;
+    double *__restrict__ panel = vt + (size_t)hd.z * 128;
+    for (int j = s_ro[0] + tid; j < s_ro[nr]; j += kDiaThreads) {
+        int lo = 0, hi = nr - 1;  // the row: the last i with s_ro[i] <= j
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_ro[mid] <= j)
+                lo = mid;
+            else
+                hi = mid - 1;
+        }
+        const int d = ci[j] - (r0 + lo);
+        int a = 0, b = K;  // lower bound of d in the offset list
+        while (a < b) {
+            const int mid = (a + b) >> 1;
+            if (s_d[mid] < d)
+                a = mid + 1;
+            else
+                b = mid;
+        }
+        if (a < K && s_d[a] == d)
+            panel[(size_t)(a >> 1) * 128 + 2 * lo + (a & 1)] = vals[j];
     }
+}
+
+__global__ void k_dia_rem_fill(const double *__restrict__ vals, const int *__restrict__ src, long long n,
+                               double *__restrict__ out)
+{
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        out[i] = vals[src[i]];
 }
 
 template <typename T>
@@ -356,6 +633,9 @@ void free_dia(DiaData *d)
     dia_free(d->d_off);
     dia_free(d->d_mask);
     dia_free(d->d_vt);
+    dia_free(d->d_rem_ptr);
+    dia_free(d->d_rem_col);
+    dia_free(d->d_rem_val);
     delete d;
 }
 
@@ -377,114 +657,238 @@ static mspmv_status dia_upload(T **d, const std::vector<T> &hsrc)
 
 // The planning itself, on host arrays (build_dia_plan after downloading them; mspmv_offset_windows for
 // inspection).  false: the plan does not hold.
+//
+// Windows plus a remainder (round 6; the round-5 plan was all or nothing): a window keeps the offsets
+// that at least kDiaKeepRows of its rows hold (all of its rows when it has fewer), the kDiaMaxK most
+// frequent when more qualify (ties: the smaller offset), and drops its rarest kept offsets while its
+// kept entries fill less than min_window_fill of rows x K.  Every other entry -- an off-pattern column,
+// a row longer than the list, a whole window of scattered columns -- goes to the REMAINDER: a CSR of the
+// same rows (rem_ptr over all rows, rem_col, rem_src = the entry's CSR position), summed after the
+// window's offsets (rows with remainder entries are within the reordering bound; the others keep the
+// CSR-order sum bit for bit).  The plan holds when every row's columns ascend strictly, the remainder is
+// at most max_rem_frac of the nonzeros and the kept entries fill >= min_fill of 64 x sum K.
+constexpr int kDiaKeepRows = 8;
+
 struct DiaHostPlan {
-    int windows = 0, max_k = 0, masked = 0;
-    long long sum_k = 0, sum_pairs = 0;
+    int windows = 0, max_k = 0, masked = 0, rem_windows = 0;
+    long long sum_k = 0, sum_pairs = 0, rem = 0;
     std::vector<int> kw;                     // [windows] K
-    std::vector<int4> hdr;                   // [windows] {K, offset base, pair panel base, mask base or -1}
+    std::vector<int4> hdr;                   // [windows] {K | has_rem << 16, offset base, pair panel base, mask base or -1}
     std::vector<int> offs;                   // [sum_k]
     std::vector<unsigned long long> masks;   // [K of the masked windows]
+    std::vector<int> rem_ptr;                // [m + 1] (empty when rem == 0)
+    std::vector<int> rem_col, rem_src;       // [rem]
 };
 
+// One window's kept offsets (ascending) and their entry count; false when some row's columns do not
+// ascend strictly.  ci[j - cbase] is the column of CSR entry j.
+static bool window_offsets(const int *ro, const int *ci, long long cbase, int r0, int r1, double min_window_fill,
+                           std::vector<std::pair<int, int>> &keep, long long &kept)
+{
+    std::vector<int> d;
+    d.reserve((size_t)(ro[r1] - ro[r0]));
+    for (int r = r0; r < r1; ++r) {
+        long long prev = -(1LL << 40);
+        for (int j = ro[r]; j < ro[r + 1]; ++j) {
+            const long long o = (long long)ci[j - cbase] - r;
+            if (o <= prev)  // columns not strictly ascending: the D order would not be the CSR order
+                return false;
+            prev = o;
+            d.push_back((int)o);
+        }
+    }
+    // offsets with their row counts (a row holds an offset at most once: columns strictly ascend)
+    std::sort(d.begin(), d.end());
+    std::vector<std::pair<int, int>> cnt;  // (offset, rows)
+    for (size_t i = 0; i < d.size();) {
+        size_t e = i;
+        while (e < d.size() && d[e] == d[i])
+            ++e;
+        cnt.emplace_back(d[i], (int)(e - i));
+        i = e;
+    }
+    const int keep_min = std::min(kDiaKeepRows, r1 - r0);
+    keep.clear();
+    for (const auto &c : cnt)
+        if (c.second >= keep_min)
+            keep.push_back(c);
+    // the most frequent first (ties: the smaller offset), at most kDiaMaxK, then drop the rarest while the
+    // window's panels would be too empty
+    std::stable_sort(keep.begin(), keep.end(),
+                     [](const std::pair<int, int> &a, const std::pair<int, int> &b) { return a.second > b.second; });
+    if ((int)keep.size() > kDiaMaxK)
+        keep.resize(kDiaMaxK);
+    kept = 0;
+    for (const auto &c : keep)
+        kept += c.second;
+    while (!keep.empty() && (double)kept < min_window_fill * (double)(r1 - r0) * (double)keep.size()) {
+        kept -= keep.back().second;
+        keep.pop_back();
+    }
+    std::sort(keep.begin(), keep.end());  // ascending offsets: each row's kept entries in CSR order
+    return true;
+}
+
 static bool dia_plan_host(const int *ro, const int *ci, int m, long long nnz, double min_fill, double min_window_fill,
-                          DiaHostPlan &out)
+                          double max_rem_frac, DiaHostPlan &out)
 {
     if (m <= 0 || nnz <= 0)
         return false;
-    for (int r = 0; r < m; ++r)  // a row longer than the list: no window can hold it
-        if (ro[r + 1] - ro[r] > kDiaMaxK)
-            return false;
     const int W = (m + 63) / 64;
     std::vector<int> kw((size_t)W, 0), dl((size_t)W * kDiaMaxK, 0);
-    std::vector<unsigned char> full((size_t)W, 0);
+    std::vector<long long> kept_nz((size_t)W, 0);
+    std::vector<int> rem_rows((size_t)m, 0);  // remainder entries per row
     int bad = 0;
 #pragma omp parallel for schedule(static) reduction(| : bad)
     for (int w = 0; w < W; ++w) {
         if (bad)
             continue;
         const int r0 = w * 64, r1 = std::min(m, r0 + 64);
-        std::vector<int> d;
-        d.reserve((size_t)(ro[r1] - ro[r0]));
-        bool ok = true;
-        for (int r = r0; r < r1 && ok; ++r) {
-            long long prev = -(1LL << 40);
-            for (int j = ro[r]; j < ro[r + 1]; ++j) {
-                const long long o = (long long)ci[j] - r;
-                if (o <= prev) {  // columns not strictly ascending: the D order would not be the CSR order
-                    ok = false;
-                    break;
-                }
-                prev = o;
-                d.push_back((int)o);
-            }
-        }
-        if (ok) {
-            std::sort(d.begin(), d.end());
-            d.erase(std::unique(d.begin(), d.end()), d.end());
-            const int K = (int)d.size();
-            const long long nz = ro[r1] - ro[r0];
-            ok = K >= 1 && K <= kDiaMaxK && (double)nz >= min_window_fill * (double)(r1 - r0) * K;
-            if (ok) {
-                kw[(size_t)w] = K;
-                std::copy(d.begin(), d.end(), dl.begin() + (size_t)w * kDiaMaxK);
-                full[(size_t)w] = (r1 - r0 == 64 && nz == 64LL * K) ? 1 : 0;
-            }
-        }
-        if (!ok)
+        std::vector<std::pair<int, int>> keep;
+        long long nz = 0;
+        if (!window_offsets(ro, ci, 0, r0, r1, min_window_fill, keep, nz)) {
             bad = 1;
+            continue;
+        }
+        kw[(size_t)w] = (int)keep.size();
+        kept_nz[(size_t)w] = nz;
+        for (size_t k = 0; k < keep.size(); ++k)
+            dl[(size_t)w * kDiaMaxK + k] = keep[k].first;
+        // remainder entries per row
+        const int *D = &dl[(size_t)w * kDiaMaxK];
+        const int K = (int)keep.size();
+        for (int r = r0; r < r1; ++r) {
+            int k = 0, nrem = 0;
+            for (int j = ro[r]; j < ro[r + 1]; ++j) {
+                const int o = ci[j] - r;
+                while (k < K && D[k] < o)
+                    ++k;
+                if (k < K && D[k] == o)
+                    ++k;
+                else
+                    ++nrem;
+            }
+            rem_rows[(size_t)r] = nrem;
+        }
     }
     if (bad)
         return false;
-    long long sumk = 0, summ = 0;
-    for (int w = 0; w < W; ++w)
+    long long sumk = 0, kept = 0, rem = 0;
+    for (int w = 0; w < W; ++w) {
         sumk += kw[(size_t)w];
-    if (sumk > 0x7fffffffLL || (double)nnz < min_fill * 64.0 * (double)sumk)
-        return false;  // the panels would stream too many zeros overall
+        kept += kept_nz[(size_t)w];
+    }
+    rem = nnz - kept;
+    if (sumk == 0 || sumk > 0x7fffffffLL || (double)kept < min_fill * 64.0 * (double)sumk ||
+        (double)rem > max_rem_frac * (double)nnz)
+        return false;  // the panels would stream too many zeros overall, or too much would be left over
     out.hdr.assign((size_t)W, make_int4(0, 0, 0, 0));
     out.offs.clear();
     out.offs.reserve((size_t)sumk);
-    sumk = 0;
-    long long sump = 0;  // value pair panels (64 x 16 B): (K + 1) / 2 per window
+    long long summ = 0, sump = 0, sk = 0;  // value pair panels (64 x 16 B): (K + 1) / 2 per window
+    std::vector<unsigned char> wrem((size_t)W, 0);
+    for (int w = 0; w < W; ++w) {
+        const int r0 = w * 64, r1 = std::min(m, r0 + 64);
+        for (int r = r0; r < r1; ++r)
+            wrem[(size_t)w] |= rem_rows[(size_t)r] > 0;
+    }
     for (int w = 0; w < W; ++w) {
         const int K = kw[(size_t)w];
+        const int r0 = w * 64, r1 = std::min(m, r0 + 64);
         if (sump > 0x7fffffffLL / 64)
             return false;
-        out.hdr[(size_t)w] = make_int4(K, (int)sumk, (int)sump, full[(size_t)w] ? -1 : (int)summ);
+        const bool full = r1 - r0 == 64 && kept_nz[(size_t)w] == 64LL * K;
+        out.hdr[(size_t)w] = make_int4(K | (wrem[(size_t)w] ? 1 << 16 : 0), (int)sk, (int)sump, full ? -1 : (int)summ);
         sump += (K + 1) / 2;
         out.offs.insert(out.offs.end(), dl.begin() + (size_t)w * kDiaMaxK, dl.begin() + (size_t)w * kDiaMaxK + K);
-        sumk += K;
-        if (!full[(size_t)w])
+        sk += K;
+        if (!full)
             summ += K;
         out.max_k = std::max(out.max_k, K);
-        out.masked += !full[(size_t)w];
+        out.masked += !full;
+        out.rem_windows += wrem[(size_t)w];
     }
     out.masks.assign((size_t)summ, 0ull);
+    if (rem > 0) {
+        out.rem_ptr.assign((size_t)m + 1, 0);
+        for (int r = 0; r < m; ++r)
+            out.rem_ptr[(size_t)r + 1] = out.rem_ptr[(size_t)r] + rem_rows[(size_t)r];
+        out.rem_col.assign((size_t)rem, 0);
+        out.rem_src.assign((size_t)rem, 0);
+    }
     const std::vector<int4> &hdr = out.hdr;
     const std::vector<int> &offs = out.offs;
     std::vector<unsigned long long> &masks = out.masks;
 #pragma omp parallel for schedule(static)
     for (int w = 0; w < W; ++w) {
         const int4 hd = hdr[(size_t)w];
-        if (hd.w < 0)
-            continue;
-        const int *D = &offs[(size_t)hd.y];
+        const int K = hd.x & 0xffff;
+        const int *D = K ? &offs[(size_t)hd.y] : nullptr;
         const int r0 = w * 64, r1 = std::min(m, r0 + 64);
+        if (hd.w < 0 && !(hd.x >> 16))
+            continue;  // every row holds every offset and nothing is left over
         for (int r = r0; r < r1; ++r) {
             int k = 0;
+            int q = rem > 0 ? out.rem_ptr[(size_t)r] : 0;
             for (int j = ro[r]; j < ro[r + 1]; ++j) {
                 const int o = ci[j] - r;
-                while (D[k] < o)
+                while (k < K && D[k] < o)
                     ++k;
-                masks[(size_t)hd.w + k] |= 1ull << (r - r0);
-                ++k;
+                if (k < K && D[k] == o) {
+                    if (hd.w >= 0)
+                        masks[(size_t)hd.w + k] |= 1ull << (r - r0);
+                    ++k;
+                } else {
+                    out.rem_col[(size_t)q] = ci[j];
+                    out.rem_src[(size_t)q] = j;
+                    ++q;
+                }
             }
         }
     }
     out.windows = W;
-    out.sum_k = sumk;
+    out.sum_k = sk;
     out.sum_pairs = sump;
+    out.rem = rem;
     out.kw = std::move(kw);
     return true;
+}
+
+// The cheap test before the whole column array is copied to the host: up to kDiaSamples windows spread
+// over the matrix, planned as dia_plan_host plans them (their columns downloaded alone); the plan is
+// not attempted when their entries would leave twice the remainder allowed or fill the panels clearly
+// less than min_fill (FEM node blocks, random bands and power-law rows fail here in microseconds).
+constexpr int kDiaSamples = 64;
+static mspmv_status dia_sample_ok(const mspmv_handle_s *h, const std::vector<int> &ro, double min_fill,
+                                  double min_window_fill, double max_rem_frac, bool *ok)
+{
+    const int m = h->m, W = (m + 63) / 64;
+    const int S = std::min(W, kDiaSamples);
+    long long total = 0, kept = 0, slots = 0;
+    std::vector<int> buf;
+    std::vector<std::pair<int, int>> keep;
+    for (int i = 0; i < S; ++i) {
+        const int w = (int)((long long)i * W / S);
+        const int r0 = w * 64, r1 = std::min(m, r0 + 64);
+        const long long j0 = ro[(size_t)r0], j1 = ro[(size_t)r1];
+        buf.resize((size_t)std::max(j1 - j0, 1LL));
+        if (j1 > j0 && hipMemcpy(buf.data(), h->d_cols + j0, sizeof(int) * (size_t)(j1 - j0), hipMemcpyDeviceToHost) !=
+                           hipSuccess) {
+            set_error("offset-window plan: sample download failed");
+            return MSPMV_ERR_HIP;
+        }
+        long long kw = 0;
+        if (!window_offsets(ro.data(), buf.data(), j0, r0, r1, min_window_fill, keep, kw)) {
+            *ok = false;
+            return MSPMV_OK;
+        }
+        total += j1 - j0;
+        kept += kw;
+        slots += 64LL * (long long)keep.size();
+    }
+    *ok = total > 0 && slots > 0 && (double)(total - kept) <= 2.0 * max_rem_frac * (double)total &&
+          (double)kept >= 0.9 * min_fill * (double)slots;
+    return MSPMV_OK;
 }
 
 mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, double min_window_fill)
@@ -492,22 +896,27 @@ mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, dou
     const int m = h->m;
     if (m <= 0 || h->nnz <= 0)
         return MSPMV_ERR_UNSUPPORTED;
+    const double max_rem = min_fill > 0.0 ? kDiaMaxRemFrac : 1.0;  // forced (MSPMV_DIA=1): any remainder
     std::vector<int> ro((size_t)m + 1);
     if (hipMemcpy(ro.data(), h->d_row_offsets, sizeof(int) * ro.size(), hipMemcpyDeviceToHost) != hipSuccess) {
         set_error("offset-window plan: row offsets download failed");
         return MSPMV_ERR_HIP;
     }
-    for (int r = 0; r < m; ++r)  // the cheap precheck before the columns are copied: rows too long
-        if (ro[(size_t)r + 1] - ro[(size_t)r] > kDiaMaxK)
-            return MSPMV_ERR_UNSUPPORTED;
+    bool sample_ok = true;
+    const mspmv_status sst = dia_sample_ok(h, ro, min_fill, min_window_fill, max_rem, &sample_ok);
+    if (sst != MSPMV_OK)
+        return sst;
+    if (!sample_ok)
+        return MSPMV_ERR_UNSUPPORTED;
     std::vector<int> ci((size_t)h->nnz);
     if (hipMemcpy(ci.data(), h->d_cols, sizeof(int) * ci.size(), hipMemcpyDeviceToHost) != hipSuccess) {
         set_error("offset-window plan: column download failed");
         return MSPMV_ERR_HIP;
     }
     DiaHostPlan hp;
-    if (!dia_plan_host(ro.data(), ci.data(), m, h->nnz, min_fill, min_window_fill, hp))
+    if (!dia_plan_host(ro.data(), ci.data(), m, h->nnz, min_fill, min_window_fill, max_rem, hp))
         return MSPMV_ERR_UNSUPPORTED;
+    std::vector<int>().swap(ci);
     const int W = hp.windows;
     const std::vector<int4> &hdr = hp.hdr;
     const std::vector<int> &offs = hp.offs;
@@ -520,11 +929,36 @@ mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, dou
     dd->sum_pairs = sump;
     dd->masked_windows = hp.masked;
     dd->max_k = hp.max_k;
-    dd->fill = (double)h->nnz / (64.0 * (double)sumk);
+    dd->rem = hp.rem;
+    dd->rem_windows = hp.rem_windows;
+    dd->fill = (double)(h->nnz - hp.rem) / (64.0 * (double)sumk);
     mspmv_status st;
     if ((st = dia_upload(&dd->d_hdr, hdr)) != MSPMV_OK || (st = dia_upload(&dd->d_off, offs)) != MSPMV_OK ||
         (st = dia_upload(&dd->d_mask, masks)) != MSPMV_OK)
         return st;
+    if (hp.rem > 0) {
+        if ((st = dia_upload(&dd->d_rem_ptr, hp.rem_ptr)) != MSPMV_OK ||
+            (st = dia_upload(&dd->d_rem_col, hp.rem_col)) != MSPMV_OK)
+            return st;
+        int *d_src = nullptr;
+        if ((st = dia_upload(&d_src, hp.rem_src)) != MSPMV_OK) {
+            dia_free(d_src);
+            return st;
+        }
+        if (hipMalloc((void **)&dd->d_rem_val, sizeof(double) * (size_t)hp.rem) != hipSuccess) {
+            dd->d_rem_val = nullptr;
+            dia_free(d_src);
+            set_error("offset-window plan: remainder allocation failed");
+            return MSPMV_ERR_OOM;
+        }
+        hipLaunchKernelGGL(k_dia_rem_fill, dim3(1024), dim3(256), 0, h->stream, h->d_vals, d_src, hp.rem, dd->d_rem_val);
+        const hipError_t e = hipStreamSynchronize(h->stream);
+        dia_free(d_src);
+        if (e != hipSuccess) {
+            set_error(std::string("offset-window plan: remainder fill: ") + hipGetErrorString(e));
+            return MSPMV_ERR_HIP;
+        }
+    }
     if (hipMalloc((void **)&dd->d_vt, sizeof(double) * 128 * (size_t)sump) != hipSuccess) {
         dd->d_vt = nullptr;
         set_error("offset-window plan: value panel allocation failed");
@@ -532,16 +966,20 @@ mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, dou
     }
     hipError_t e = hipMemsetAsync(dd->d_vt, 0, sizeof(double) * 128 * (size_t)sump, h->stream);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_dia_fill, dim3((unsigned)((W + kDiaWaves - 1) / kDiaWaves)), dim3(kDiaThreads), 0,
-                           h->stream, h->d_row_offsets, h->d_cols, h->d_vals, dd->d_hdr, dd->d_off, W, m, dd->d_vt);
+        hipLaunchKernelGGL(k_dia_fill, dim3((unsigned)W), dim3(kDiaThreads), 0, h->stream, h->d_row_offsets, h->d_cols,
+                           h->d_vals, dd->d_hdr, dd->d_off, W, m, dd->d_vt);
         e = hipGetLastError();
     }
     // the plan as the tile-plan queries see it: one "tile" per window, whole rows, every row summed in
-    // CSR order (mode 1: bit-identical), no split rows
+    // CSR order (mode 1: bit-identical) -- except in windows with remainder entries, summed after the
+    // offsets (mode 255: within the reordering bound) -- and no split rows
     std::vector<int2> hb((size_t)W + 1);
+    std::vector<unsigned char> modes((size_t)W);
     for (int w = 0; w <= W; ++w) {
         const int r = std::min(m, w * 64);
         hb[(size_t)w] = make_int2(r, ro[(size_t)r]);
+        if (w < W)
+            modes[(size_t)w] = (hdr[(size_t)w].x >> 16) ? 255 : 1;
     }
     if (e == hipSuccess && hipMalloc((void **)&p.d_bounds, sizeof(int2) * hb.size()) != hipSuccess)
         e = hipErrorOutOfMemory;
@@ -555,7 +993,7 @@ mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, dou
         if (hipMalloc((void **)&p.d_modes[i], (size_t)W) != hipSuccess)
             e = hipErrorOutOfMemory;
         else
-            e = memset_sync(p.d_modes[i], 1, (size_t)W);
+            e = hipMemcpy(p.d_modes[i], modes.data(), (size_t)W, hipMemcpyHostToDevice);
     }
     if (e == hipSuccess)
         e = hipStreamSynchronize(h->stream);
@@ -570,9 +1008,35 @@ mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, dou
     return MSPMV_OK;
 }
 
+// L = 8, 16 on the workgroup form (k_spmm_dia_wg) unless MSPMV_DIA_WG=0 (A/B against the wave form)
+static bool dia_wg_enabled()
+{
+    static const bool on = [] {
+        const char *e = getenv("MSPMV_DIA_WG");
+        return !(e && *e && atoi(e) == 0);
+    }();
+    return on;
+}
+
 template <int L>
 static void dia_launch_L(const DiaArgs &a, hipStream_t s, bool nt)
 {
+    if constexpr (L == 8 || L == 16) {
+        if (dia_wg_enabled()) {
+            const dim3 grid((unsigned)a.windows), block(kDiaThreads);
+            if (a.partials) {
+                if (nt)
+                    hipLaunchKernelGGL((k_spmm_dia_wg<L, true, true, false>), grid, block, 0, s, a);
+                else
+                    hipLaunchKernelGGL((k_spmm_dia_wg<L, false, true, false>), grid, block, 0, s, a);
+            } else if (nt) {
+                hipLaunchKernelGGL((k_spmm_dia_wg<L, true, false, false>), grid, block, 0, s, a);
+            } else {
+                hipLaunchKernelGGL((k_spmm_dia_wg<L, false, false, false>), grid, block, 0, s, a);
+            }
+            return;
+        }
+    }
     const dim3 grid((unsigned)a.groups), block(kDiaThreads);
     if (a.partials) {
         if (nt)
@@ -604,6 +1068,9 @@ hipError_t launch_dia(mspmv_handle_s *h, const TilePlan &plan, const double *d_X
     a.ctrl = ctrl;
     a.partials = partials;
     a.windows = dd->windows;
+    a.rem_ptr = dd->d_rem_ptr;
+    a.rem_col = dd->d_rem_col;
+    a.rem_val = dd->d_rem_val;
     a.xr = d_X + row_off * (ld > 0 ? ld : L);
     a.groups = (dd->windows + kDiaWaves - 1) / kDiaWaves;
     a.m = h->m;
@@ -622,8 +1089,60 @@ hipError_t launch_dia(mspmv_handle_s *h, const TilePlan &plan, const double *d_X
     return hipGetLastError();
 }
 
+// The block CG's fused iteration SpMM (k_spmm_dia_wg PUPD + DOT): Ap = A p with p = r + beta p_old staged
+// on the fly, p's own rows to pnew, the deferred x += alpha p_old, p.Ap partials per window.
+hipError_t launch_dia_cg(mspmv_handle_s *h, const TilePlan &plan, const double *p_old, const double *r, double *pnew,
+                         double *ap, double *x, int L, CgControl *ctrl, const CgScalars *scal, double *partials)
+{
+    const DiaData *dd = plan.dia;
+    if (!dd || !(L == 8 || L == 16) || !partials || !ctrl || !scal)
+        return hipErrorInvalidValue;
+    if (dd->windows == 0)
+        return hipSuccess;
+    DiaArgs a{};
+    a.hdr = dd->d_hdr;
+    a.off = dd->d_off;
+    a.mask = dd->d_mask;
+    a.vt = dd->d_vt;
+    a.x = p_old;
+    a.y = ap;
+    a.ctrl = ctrl;
+    a.partials = partials;
+    a.windows = dd->windows;
+    a.rem_ptr = dd->d_rem_ptr;
+    a.rem_col = dd->d_rem_col;
+    a.rem_val = dd->d_rem_val;
+    a.xr = p_old;
+    a.groups = (dd->windows + kDiaWaves - 1) / kDiaWaves;
+    a.m = h->m;
+    a.n = h->n;
+    a.ld = L;
+    a.r = r;
+    a.pnew = pnew;
+    a.xsol = x;
+    a.scal = scal;
+    const dim3 grid((unsigned)dd->windows), block(kDiaThreads);
+    const bool nt = stream_nt(h);
+    if (L == 8) {
+        if (nt)
+            hipLaunchKernelGGL((k_spmm_dia_wg<8, true, true, true>), grid, block, 0, h->stream, a);
+        else
+            hipLaunchKernelGGL((k_spmm_dia_wg<8, false, true, true>), grid, block, 0, h->stream, a);
+    } else {
+        if (nt)
+            hipLaunchKernelGGL((k_spmm_dia_wg<16, true, true, true>), grid, block, 0, h->stream, a);
+        else
+            hipLaunchKernelGGL((k_spmm_dia_wg<16, false, true, true>), grid, block, 0, h->stream, a);
+    }
+    return hipGetLastError();
+}
+
+bool dia_cg_fused_available(int L) { return (L == 8 || L == 16) && dia_wg_enabled(); }
+
 std::string dia_kernel_name(const mspmv_handle_s *h, int L)
 {
+    if ((L == 8 || L == 16) && dia_wg_enabled())
+        return "k_spmm_dia_wg<" + std::to_string(L) + "," + (stream_nt(h) ? "true" : "false") + ">";
     return "k_spmm_dia<" + std::to_string(L) + "," + (stream_nt(h) ? "true" : "false") + ">";
 }
 
@@ -631,7 +1150,7 @@ std::string dia_kernel_name(const mspmv_handle_s *h, int L)
 
 extern "C" mspmv_status mspmv_offset_windows(const mspmv_csr_d *a, double min_fill, double min_window_fill, int *ok,
                                             int *num_windows, long long *sum_offsets, int *masked_windows,
-                                            int *k_per_window)
+                                            int *k_per_window, long long *remainder)
 {
     using namespace mspmv;
     if (!a || !ok || a->num_rows < 0 || a->num_cols < 0 || a->num_nonzeros < 0 || !a->row_offsets ||
@@ -656,7 +1175,10 @@ extern "C" mspmv_status mspmv_offset_windows(const mspmv_csr_d *a, double min_fi
             return MSPMV_ERR_INVALID;
         }
     DiaHostPlan hp;
-    *ok = dia_plan_host(ro, a->column_indices, m, a->num_nonzeros, min_fill, min_window_fill, hp) ? 1 : 0;
+    *ok = dia_plan_host(ro, a->column_indices, m, a->num_nonzeros, min_fill, min_window_fill,
+                        min_fill > 0.0 ? kDiaMaxRemFrac : 1.0, hp) ? 1 : 0;
+    if (remainder)
+        *remainder = *ok ? hp.rem : 0;
     if (num_windows)
         *num_windows = *ok ? hp.windows : 0;
     if (sum_offsets)

@@ -110,7 +110,8 @@ constexpr int kSlabMmMaxChunks = 127;  // chunks per block (their descriptors si
 
 // Offset windows (mspmv_dia.hip): 64-row windows whose rows list their columns at <= kDiaMaxK common
 // offsets col - row, values lane-major per window.
-constexpr int kDiaMaxK = 32;
+constexpr double kDiaMaxRemFrac = 0.05;  // at most this share of the nonzeros in the windows' remainder
+constexpr int kDiaMaxK = 64;  // one offset per lane of the window's wave (metadata read by v_readlane)
 struct DiaData {
     int windows = 0;
     int max_k = 0;
@@ -122,6 +123,11 @@ struct DiaData {
     int *d_off = nullptr;                    // [sum_k]
     unsigned long long *d_mask = nullptr;    // [K of the masked windows]
     double *d_vt = nullptr;                  // [sum_pairs][64 lanes][2]: offsets 2p, 2p+1 of each row
+    long long rem = 0;                       // remainder entries (off the windows' offset lists)
+    int rem_windows = 0;                     // windows holding some
+    int *d_rem_ptr = nullptr;                // [m + 1] (null when rem == 0)
+    int *d_rem_col = nullptr;                // [rem]
+    double *d_rem_val = nullptr;             // [rem]
 };
 
 // A merge-path tile plan for one nominal tile size (merge items per tile).
@@ -350,6 +356,11 @@ hipError_t launch_dia(mspmv_handle_s *h, const TilePlan &plan, const double *d_X
                       const CgControl *ctrl, double *partials = nullptr, long long row_off = 0,
                       hipStream_t stream = nullptr);
 std::string dia_kernel_name(const mspmv_handle_s *h, int L);
+// The block CG's iteration SpMM with the p update fused (k_spmm_dia_wg: Ap = A p, p = r + beta p_old staged
+// from p_old and r, p's rows to pnew, the deferred x += alpha p_old, p.Ap partials per window); L = 8, 16
+hipError_t launch_dia_cg(mspmv_handle_s *h, const TilePlan &plan, const double *p_old, const double *r, double *pnew,
+                         double *ap, double *x, int L, CgControl *ctrl, const CgScalars *scal, double *partials);
+bool dia_cg_fused_available(int L);
 bool dia_spmm_enabled();  // the L-wide products on the windows too unless MSPMV_DIA_SPMM=0 (mspmv_api.hip)
 // The handle's offset-window plan for width L (decided on first use), or null (mspmv_api.hip)
 mspmv_status dia_plan_for(mspmv_handle_s *h, int L, const TilePlan **out);
@@ -445,7 +456,8 @@ void resident_free(ResidentCg *r);
 hipError_t launch_cg_resident(mspmv_handle_s *h, ResidentCg *r, const double *d_b, double *d_x, int max_iters,
                               double tol, unsigned long long *d_stamps = nullptr, int stamp_iters = 0);
 // Split (multi-RHS) CG: the last deferred x += alpha p after the loop (a no-op when none is pending).
-hipError_t launch_cg_xflush(mspmv_handle_s *h, double *d_x, int L, int nblk);
+// splan / dot_fused as launch_cg_iteration (the fused form's p alternates buffers).
+hipError_t launch_cg_xflush(mspmv_handle_s *h, double *d_x, int L, int nblk, const TilePlan *splan, bool dot_fused);
 // Offset (doubles) and count of the partials level a consumer sums: levels of a fan-in
 // kSlotGroup tree are folded while more than `stop` partials would remain.
 inline void consumer_level(int nslots, int stop, int L, long long *off, int *count)

@@ -2852,10 +2852,12 @@ __global__ __launch_bounds__(kBlock) void k_dist_pupdate(CgVecArgs a, double *p)
 // once, and a stop in the fold (every column converged or broken) follows a p update that applied
 // the term and a fold that cleared the flag.
 template <int L>
-__global__ __launch_bounds__(kBlock) void k_cg_xflush(CgVecArgs a, const double *p)
+__global__ __launch_bounds__(kBlock) void k_cg_xflush(CgVecArgs a, const double *p, const double *p_odd)
 {
     if (!a.ctrl->x_pending)
         return;
+    if (p_odd && (a.ctrl->iter & 1))  // fused p update: iteration i wrote its p to buffer (i + 1) & 1
+        p = p_odd;
     const long long stride = (long long)gridDim.x * kBlock;
     for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < a.n_elems; i += stride)
         a.x[i] = a.x[i] + a.scal[L == 1 ? 0 : (int)(i % L)].alpha * p[i];
@@ -3795,8 +3797,16 @@ bool dia_dot_fused()
 // splan: the plan the solve chose for the plain L-wide product (cg_solve_native: the offset-window or
 // column-slab plan, else null -> the tiles of `plan`); dot_fused: the window SpMM takes p.Ap in its dot
 // mode (resolved once per solve, and part of the CG graph's key).
+// Fused form (offset windows in dot mode, L = 8 / 16): the p update runs inside the window SpMM
+// (launch_dia_cg), p alternating between d_p0 and d_p1 by iteration parity -- three launches per
+// iteration (SpMM, fold, update) instead of four.
+static bool cg_split_pupd_fused(const TilePlan *splan, bool dot_fused, int L)
+{
+    return splan && splan->dia && dot_fused && dia_cg_fused_available(L);
+}
+
 static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &plan, const TilePlan *splan,
-                                            bool dot_fused, double *d_x, int L, int nblk, double tol)
+                                            bool dot_fused, double *d_x, int L, int parity, int nblk, double tol)
 {
     CgVecArgs va{};
     va.n_elems = (long long)h->m * L;
@@ -3817,8 +3827,20 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
         const char *e = getenv("MSPMV_CG_REV");
         return e ? atoi(e) : 1;
     }();
+    hipError_t e;
+    if (cg_split_pupd_fused(splan, dot_fused, L)) {
+        double *pold = parity ? h->d_p1 : h->d_p0, *pnew = parity ? h->d_p0 : h->d_p1;
+        if ((e = launch_dia_cg(h, *splan, pold, h->d_r, pnew, h->d_ap, d_x, L, h->d_ctrl, h->d_scal, h->d_partials)) !=
+            hipSuccess)
+            return e;
+        if ((e = launch_fold_dot(splan->num_tiles, L, h->d_partials, h->d_gtickets, h->d_red, h->d_scal, h->d_conv,
+                                 h->d_ctrl, -1, h->stream)) != hipSuccess)
+            return e;
+        va.red_in = h->d_red;
+        return dispatch_vec(false, va, L, nblk, h->stream);
+    }
     va.rev = rev;  // the p update (after the forward update) sweeps backwards
-    hipError_t e = launch_dist_vec(2, va, L, nblk, h->d_p0, h->stream);
+    e = launch_dist_vec(2, va, L, nblk, h->d_p0, h->stream);
     va.rev = 0;
     if (e != hipSuccess)
         return e;
@@ -3865,20 +3887,22 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
     return dispatch_vec(false, va, L, nblk, h->stream);
 }
 
-// After the split iteration's loop: the x += alpha p still pending (CgVecArgs::lazy_x).
-hipError_t launch_cg_xflush(mspmv_handle_s *h, double *d_x, int L, int nblk)
+// After the split iteration's loop: the x += alpha p still pending (CgVecArgs::lazy_x).  The fused
+// form's last p is in d_p0 or d_p1 by the iteration count's parity (chosen on the device).
+hipError_t launch_cg_xflush(mspmv_handle_s *h, double *d_x, int L, int nblk, const TilePlan *splan, bool dot_fused)
 {
+    const double *p_odd = cg_split_pupd_fused(splan, dot_fused, L) ? h->d_p1 : nullptr;
     CgVecArgs va{};
     va.n_elems = (long long)h->m * L;
     va.x = d_x;
     va.scal = h->d_scal;
     va.ctrl = h->d_ctrl;
     switch (L) {
-    case 1: hipLaunchKernelGGL((k_cg_xflush<1>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
-    case 2: hipLaunchKernelGGL((k_cg_xflush<2>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
-    case 4: hipLaunchKernelGGL((k_cg_xflush<4>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
-    case 8: hipLaunchKernelGGL((k_cg_xflush<8>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
-    case 16: hipLaunchKernelGGL((k_cg_xflush<16>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
+    case 1: hipLaunchKernelGGL((k_cg_xflush<1>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0, p_odd); break;
+    case 2: hipLaunchKernelGGL((k_cg_xflush<2>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0, p_odd); break;
+    case 4: hipLaunchKernelGGL((k_cg_xflush<4>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0, p_odd); break;
+    case 8: hipLaunchKernelGGL((k_cg_xflush<8>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0, p_odd); break;
+    case 16: hipLaunchKernelGGL((k_cg_xflush<16>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0, p_odd); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -3899,7 +3923,7 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, const Ti
                                double *d_x, int L, int parity, int nblk, double tol)
 {
     if (cg_split_iteration(L))
-        return launch_cg_iteration_split(h, plan, splan, dot_fused, d_x, L, nblk, tol);
+        return launch_cg_iteration_split(h, plan, splan, dot_fused, d_x, L, parity, nblk, tol);
     double *rp_old = parity ? h->d_p1 : h->d_p0;  // {r_k, p_{k-1}} interleaved (cg_rp)
     double *rp_new = parity ? h->d_p0 : h->d_p1;  // receives p_k, then r_{k+1}
     TileArgs ta = make_args(h, plan, rp_old, h->d_ap, 1);

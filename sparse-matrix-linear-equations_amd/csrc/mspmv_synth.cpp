@@ -412,4 +412,185 @@ mspmv_status mspmv_synth_stencil(int kind, int m, int dim0, int dim1, int dim2, 
     return MSPMV_OK;
 }
 
+// The 27-point grid neighbours of point p (self included), in increasing column order.
+static int neigh27(int p, int nx, int ny, int nz, int *out)
+{
+    const int kx = p % nx, jy = (p / nx) % ny, iz = p / (nx * ny);
+    int k = 0;
+    for (int di = -1; di <= 1; ++di)
+        for (int dj = -1; dj <= 1; ++dj)
+            for (int dk = -1; dk <= 1; ++dk) {
+                const int i2 = iz + di, j2 = jy + dj, k2 = kx + dk;
+                if (i2 < 0 || i2 >= nz || j2 < 0 || j2 >= ny || k2 < 0 || k2 >= nx)
+                    continue;
+                out[k++] = (i2 * ny + j2) * nx + k2;
+            }
+    return k;
+}
+
+// The 7-point grid neighbours (self included), increasing.
+static int neigh7(int p, int nx, int ny, int nz, int *out)
+{
+    const int kx = p % nx, jy = (p / nx) % ny, iz = p / (nx * ny);
+    int k = 0;
+    const int plane = nx * ny;
+    if (iz > 0)
+        out[k++] = p - plane;
+    if (jy > 0)
+        out[k++] = p - nx;
+    if (kx > 0)
+        out[k++] = p - 1;
+    out[k++] = p;
+    if (kx < nx - 1)
+        out[k++] = p + 1;
+    if (jy < ny - 1)
+        out[k++] = p + nx;
+    if (iz < nz - 1)
+        out[k++] = p + plane;
+    return k;
+}
+
+// The SPD 27-point value of entry (p, q) as mspmv_synth_stencil kind 1 gives it (diagonal: sum|off| + shift).
+static void stencil27_row(int p, const int *nb, int k, uint64_t seed, double diag_shift, double *v)
+{
+    double diag = diag_shift;
+    int self = -1;
+    for (int t = 0; t < k; ++t) {
+        const int q = nb[t];
+        if (q == p) {
+            self = t;
+            continue;
+        }
+        const uint64_t a = (uint64_t)std::min(p, q), b = (uint64_t)std::max(p, q);
+        const double off = -u01(seed, a * 0x100000001B3ull + b);
+        v[t] = off;
+        diag += -off;
+    }
+    v[self] = diag;
+}
+
+mspmv_status mspmv_synth_stencil_perturbed(int dim0, int dim1, int dim2, unsigned long long seed, double diag_shift,
+                                           double extra_frac, double long_frac, int *row_offsets, int *cols,
+                                           double *vals, long long *nnz_out)
+{
+    if (!row_offsets || dim0 <= 0 || dim1 <= 0 || dim2 <= 0 || !(diag_shift > 0.0) || extra_frac < 0.0 ||
+        long_frac < 0.0)
+        return MSPMV_ERR_INVALID;
+    const long long mm = (long long)dim0 * dim1 * dim2;
+    if (mm > 0x7fffffffLL)
+        return MSPMV_ERR_INVALID;
+    const int m = (int)mm, nx = dim0, ny = dim1, nz = dim2;
+    const uint64_t s2 = seed * 0x9E3779B97F4A7C15ull + 17;
+    auto extras = [&](int p) {
+        return (u01(s2, 2 * (uint64_t)p) < extra_frac ? 1 : 0) + (u01(s2, 2 * (uint64_t)p + 1) < long_frac ? 8 : 0);
+    };
+    std::vector<int> len(m);
+#pragma omp parallel for schedule(static)
+    for (int p = 0; p < m; ++p) {
+        int tmp[27];
+        len[p] = neigh27(p, nx, ny, nz, tmp) + extras(p);
+    }
+    long long total = 0;
+    for (int v : len)
+        total += v;
+    if (total > 0x7fffffffLL)
+        return MSPMV_ERR_INVALID;
+    prefix_from_lengths(len, row_offsets);
+    if (nnz_out)
+        *nnz_out = total;
+    if (!cols || !vals)
+        return MSPMV_OK;
+    const long long R = 2LL * nx * ny;  // extra columns within +-R of the row
+#pragma omp parallel for schedule(static)
+    for (int p = 0; p < m; ++p) {
+        int nb[27 + 9];
+        double v[27 + 9];
+        const int k = neigh27(p, nx, ny, nz, nb);
+        stencil27_row(p, nb, k, seed, diag_shift, v);
+        const int e = extras(p);
+        std::vector<std::pair<int, double>> row;
+        row.reserve((size_t)(k + e));
+        for (int t = 0; t < k; ++t)
+            row.emplace_back(nb[t], v[t]);
+        for (int t = 0; t < e; ++t) {  // a column not in the row yet (walk right from the pick)
+            long long c = p - R + (long long)(u01(s2, (uint64_t)p * 16 + 1000 + t) * (double)(2 * R + 1));
+            c = std::min<long long>(std::max<long long>(c, 0), m - 1);
+            for (;;) {
+                bool taken = false;
+                for (const auto &q : row)
+                    taken = taken || q.first == c;
+                if (!taken)
+                    break;
+                c = c + 1 < m ? c + 1 : 0;
+            }
+            row.emplace_back((int)c, -u01(s2, (uint64_t)p * 16 + 2000 + t));
+        }
+        std::sort(row.begin(), row.end());
+        const int s0 = row_offsets[p];
+        for (size_t t = 0; t < row.size(); ++t) {
+            cols[s0 + t] = row[t].first;
+            vals[s0 + t] = row[t].second;
+        }
+    }
+    return MSPMV_OK;
+}
+
+mspmv_status mspmv_synth_kkt(int dim0, int dim1, int dim2, unsigned long long seed, double diag_shift, double eps,
+                             int *row_offsets, int *cols, double *vals, long long *nnz_out)
+{
+    if (!row_offsets || dim0 <= 0 || dim1 <= 0 || dim2 <= 0 || !(diag_shift > 0.0) || !(eps > 0.0))
+        return MSPMV_ERR_INVALID;
+    const long long NN = (long long)dim0 * dim1 * dim2;
+    if (2 * NN > 0x7fffffffLL)
+        return MSPMV_ERR_INVALID;
+    const int N = (int)NN, m = 2 * N, nx = dim0, ny = dim1, nz = dim2;
+    const uint64_t sb = seed * 0xD1B54A32D192ED03ull + 5;
+    auto bval = [&](int j, int i) {  // B[j][i] (i a 7-point neighbour of j)
+        return i == j ? 1.0 + u01(sb, (uint64_t)j) : -u01(sb, (uint64_t)j * 0x100000001B3ull + (uint64_t)i + 1) / 6.0;
+    };
+    std::vector<int> len(m);
+#pragma omp parallel for schedule(static)
+    for (int p = 0; p < N; ++p) {
+        int t27[27], t7[7];
+        len[p] = neigh27(p, nx, ny, nz, t27) + neigh7(p, nx, ny, nz, t7);
+        len[N + p] = neigh7(p, nx, ny, nz, t7) + 1;
+    }
+    long long total = 0;
+    for (int v : len)
+        total += v;
+    if (total > 0x7fffffffLL)
+        return MSPMV_ERR_INVALID;
+    prefix_from_lengths(len, row_offsets);
+    if (nnz_out)
+        *nnz_out = total;
+    if (!cols || !vals)
+        return MSPMV_OK;
+#pragma omp parallel for schedule(static)
+    for (int p = 0; p < N; ++p) {
+        int nb[27], n7[7];
+        double v[27];
+        const int k = neigh27(p, nx, ny, nz, nb);
+        stencil27_row(p, nb, k, seed, diag_shift, v);
+        const int k7 = neigh7(p, nx, ny, nz, n7);
+        int s0 = row_offsets[p];
+        for (int t = 0; t < k; ++t) {  // [H | B^T]: H's row, then B^T's (B's column p: rows j with p in nb7(j))
+            cols[s0 + t] = nb[t];
+            vals[s0 + t] = v[t];
+        }
+        s0 += k;
+        for (int t = 0; t < k7; ++t) {
+            cols[s0 + t] = N + n7[t];
+            vals[s0 + t] = bval(n7[t], p);
+        }
+        s0 = row_offsets[N + p];  // [B | -eps I]
+        for (int t = 0; t < k7; ++t) {
+            cols[s0 + t] = n7[t];
+            vals[s0 + t] = bval(p, n7[t]);
+        }
+        cols[s0 + k7] = N + p;
+        vals[s0 + k7] = -eps;
+    }
+    return MSPMV_OK;
+}
+
 }  // extern "C"

@@ -118,7 +118,8 @@ _SIGS = {
     "mspmv_plan_block_tiles": (_I, [_P, _I, _PI]),
     "mspmv_tile_modes": (_I, [_P, _I, _P]),
     "mspmv_tile_lanes": (_I, [_P, _I, _PI]),
-    "mspmv_offset_windows": (_I, [ctypes.POINTER(_CsrD), _D, _D, _PI, _PI, ctypes.POINTER(ctypes.c_longlong), _PI, _P]),
+    "mspmv_offset_windows": (_I, [ctypes.POINTER(_CsrD), _D, _D, _PI, _PI, ctypes.POINTER(ctypes.c_longlong), _PI, _P,
+                                  ctypes.POINTER(ctypes.c_longlong)]),
     "mspmv_spmv_kernel_name": (ctypes.c_char_p, [_P]),
     "mspmv_spmm_kernel_name": (ctypes.c_char_p, [_P, _I]),
     "mspmv_cg_kernel_name": (ctypes.c_char_p, [_P]),
@@ -154,6 +155,9 @@ _SIGS = {
     "mspmv_synth_powerlaw": (_I, [_I, _I, ctypes.c_longlong, _D, ctypes.c_ulonglong, _P, _P, _P]),
     "mspmv_synth_stencil": (_I, [_I, _I, _I, _I, _I, ctypes.c_ulonglong, _D, _P, _P, _P,
                                  ctypes.POINTER(ctypes.c_longlong)]),
+    "mspmv_synth_stencil_perturbed": (_I, [_I, _I, _I, ctypes.c_ulonglong, _D, _D, _D, _P, _P, _P,
+                                           ctypes.POINTER(ctypes.c_longlong)]),
+    "mspmv_synth_kkt": (_I, [_I, _I, _I, ctypes.c_ulonglong, _D, _D, _P, _P, _P, ctypes.POINTER(ctypes.c_longlong)]),
 }
 
 
@@ -346,6 +350,37 @@ class CsrMatrix:
         va = np.empty(max(nnz.value, 1), np.float64)
         _check(lib.mspmv_synth_stencil(kind, m, dim0, dim1, dim2, seed, diag_shift, _ptr(ro), _ptr(ci), _ptr(va),
                                        ctypes.byref(nnz)), "synth_stencil")
+        return cls(m, m, int(nnz.value), ro, ci[: nnz.value], va[: nnz.value])
+
+    @classmethod
+    def synth_stencil_perturbed(cls, dims, seed: int = 7, diag_shift: float = 1.0, extra_frac: float = 0.01,
+                                long_frac: float = 0.001) -> "CsrMatrix":
+        """The 27-point stencil with off-pattern columns (mspmv_synth_stencil_perturbed)."""
+        nx, ny, nz = dims
+        m = nx * ny * nz
+        ro = np.empty(m + 1, np.int32)
+        nnz = ctypes.c_longlong(0)
+        args = (nx, ny, nz, seed, diag_shift, extra_frac, long_frac)
+        _check(lib.mspmv_synth_stencil_perturbed(*args, _ptr(ro), None, None, ctypes.byref(nnz)), "synth_perturbed")
+        ci = np.empty(max(nnz.value, 1), np.int32)
+        va = np.empty(max(nnz.value, 1), np.float64)
+        _check(lib.mspmv_synth_stencil_perturbed(*args, _ptr(ro), _ptr(ci), _ptr(va), ctypes.byref(nnz)),
+               "synth_perturbed")
+        return cls(m, m, int(nnz.value), ro, ci[: nnz.value], va[: nnz.value])
+
+    @classmethod
+    def synth_kkt(cls, dims, seed: int = 7, diag_shift: float = 1.0, eps: float = 1e-2) -> "CsrMatrix":
+        """KKT-shaped [[H, B^T], [B, -eps I]] with grid blocks (mspmv_synth_kkt)."""
+        nx, ny, nz = dims
+        m = 2 * nx * ny * nz
+        ro = np.empty(m + 1, np.int32)
+        nnz = ctypes.c_longlong(0)
+        _check(lib.mspmv_synth_kkt(nx, ny, nz, seed, diag_shift, eps, _ptr(ro), None, None, ctypes.byref(nnz)),
+               "synth_kkt")
+        ci = np.empty(max(nnz.value, 1), np.int32)
+        va = np.empty(max(nnz.value, 1), np.float64)
+        _check(lib.mspmv_synth_kkt(nx, ny, nz, seed, diag_shift, eps, _ptr(ro), _ptr(ci), _ptr(va), ctypes.byref(nnz)),
+               "synth_kkt")
         return cls(m, m, int(nnz.value), ro, ci[: nnz.value], va[: nnz.value])
 
 
@@ -645,16 +680,18 @@ def pcg_ic0(g: "GpuCsr", ic: GpuIc0, B: np.ndarray, max_iters: int, tolerance: f
 
 def offset_windows(a: CsrMatrix, min_fill: float = 0.85, min_window_fill: float = 0.3):
     """Host-side offset-window planning (mspmv_offset_windows; no device): None when the matrix does
-    not fit the plan, else {"windows", "sum_offsets", "masked_windows", "k"} (k: offsets per 64-row
-    window).  The library's automatic choice uses the default thresholds."""
+    not fit the plan, else {"windows", "sum_offsets", "masked_windows", "k", "remainder"} (k: offsets
+    per 64-row window; remainder: entries left off the windows' offset lists).  The library's automatic
+    choice uses the default thresholds."""
     ok, nw, mw = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    sk = ctypes.c_longlong()
+    sk, rem = ctypes.c_longlong(), ctypes.c_longlong()
     k = np.zeros(max((a.num_rows + 63) // 64, 1), np.int32)
     _check(lib.mspmv_offset_windows(ctypes.byref(a._c()), min_fill, min_window_fill, ctypes.byref(ok), ctypes.byref(nw),
-                                    ctypes.byref(sk), ctypes.byref(mw), _ptr(k)), "offset_windows")
+                                    ctypes.byref(sk), ctypes.byref(mw), _ptr(k), ctypes.byref(rem)), "offset_windows")
     if not ok.value:
         return None
-    return {"windows": nw.value, "sum_offsets": sk.value, "masked_windows": mw.value, "k": k[: nw.value]}
+    return {"windows": nw.value, "sum_offsets": sk.value, "masked_windows": mw.value, "k": k[: nw.value],
+            "remainder": rem.value}
 
 
 def spai_values(a: CsrMatrix) -> np.ndarray:

@@ -11,6 +11,8 @@ inf where no row reads it.  The L-wide products take the windows too (MSPMV_DIA_
 and the block CG runs its SpMM on the windows, held to the oracle's CGSolveMultiple
 (no_pretreatment.hpp:32-197) like the tile path.
 """
+import re
+
 import numpy as np
 import pytest
 
@@ -31,6 +33,13 @@ def _need_gpu(gpu_available):
 def _windows_every_width(monkeypatch):
     monkeypatch.delenv("MSPMV_DIA", raising=False)
     monkeypatch.delenv("MSPMV_DIA_SPMM", raising=False)
+
+
+def is_dia(name, L=None):
+    """The offset-window kernels: k_spmm_dia<L, ...> (one window per wave) or k_spmm_dia_wg<L, ...> (one
+    window per workgroup, L = 8 / 16)."""
+    m = re.match(r"k_spmm_dia(_wg)?<(\d+),", name)
+    return m is not None and (L is None or int(m.group(2)) == L)
 
 
 def band(m, offsets, seed, n=None, drop=0.0):
@@ -64,7 +73,13 @@ CASES = {
     "tridiag": lambda: band(64 * 500, [-1, 0, 1], 2),                 # every window full
     "partial": lambda: band(64 * 77 + 13, [-70, -3, 0, 2, 9, 70], 3),  # a 13-row last window
     "rect": lambda: band(20000, [0, 5, 17000, 30000], 4, n=50001),    # n > m, far offsets
+    # shapes the windows were not designed on (round 6, windows plus a remainder): off-pattern columns and
+    # rows of 35 entries; a KKT saddle point whose upper rows hold 34 offsets
+    "perturbed27": lambda: mspmv.CsrMatrix.synth_stencil_perturbed((33, 30, 29), seed=2, extra_frac=0.02,
+                                                                   long_frac=0.01),
+    "kkt": lambda: mspmv.CsrMatrix.synth_kkt((20, 21, 22), seed=3),
 }
+REMAINDER = {"perturbed27", "kkt"}  # cases with entries off the windows' offset lists
 # windows whose rows miss offsets and empty rows: taken only when forced (fill below kDiaAutoFill)
 FORCED = {
     "holes": lambda: band(40000, [-200, -1, 0, 1, 200], 5, drop=0.3),
@@ -78,19 +93,28 @@ def _check_product(a, g, L, orc):
         x = rng.uniform(-1, 1, a.num_cols)
         y = g.spmv(x)
         gold = orc.spmv_gold(a, x)
-        assert g.kernel_name().startswith("k_spmm_dia<1,"), g.kernel_name()
+        assert is_dia(g.kernel_name(), 1), g.kernel_name()
         plan = g.tile_plan(1)
-        assert np.all(plan["modes"] == 1)
         n_exact, n = check_parity(a, y, gold, x, plan, 1)
-        assert n_exact == n
+        assert n_exact == _exact_rows(plan)
         assert g.spmv(x).tobytes() == y.tobytes()
         return
     X = rng.uniform(-1, 1, (a.num_cols, L))
     Y = g.spmm(X)
-    assert g.spmm_kernel_name(L).startswith(f"k_spmm_dia<{L},"), g.spmm_kernel_name(L)
-    n_exact, n = check_parity(a, Y, orc.csr_spmm_t(a, X), X, g.tile_plan(L), L)
-    assert n_exact == n
+    assert is_dia(g.spmm_kernel_name(L), L), g.spmm_kernel_name(L)
+    plan = g.tile_plan(L)
+    n_exact, n = check_parity(a, Y, orc.csr_spmm_t(a, X), X, plan, L)
+    assert n_exact == _exact_rows(plan)
     assert g.spmm(X).tobytes() == Y.tobytes()
+
+
+def _exact_rows(plan):
+    """Rows of windows in mode 1 (summed in CSR order: bit-identical); windows holding remainder entries
+    report 255 (their rows within the reordering bound).  No other mode occurs on the windows."""
+    modes, b = plan["modes"], plan["bounds"]
+    assert np.all((modes == 1) | (modes == 255)), np.unique(modes)
+    rows = np.diff(b[:, 0])
+    return int(rows[modes == 1].sum())
 
 
 @pytest.mark.parametrize("L", [1, 2, 4, 8, 16])
@@ -98,6 +122,8 @@ def _check_product(a, g, L, orc):
 def test_dia_parity(orc, monkeypatch, name, L):
     monkeypatch.delenv("MSPMV_DIA", raising=False)
     a = CASES[name]()
+    w = mspmv.offset_windows(a)
+    assert w is not None and (w["remainder"] > 0) == (name in REMAINDER), (name, w and w["remainder"])
     with mspmv.GpuCsr(a) as g:
         _check_product(a, g, L, orc)
 
@@ -108,7 +134,7 @@ def test_dia_forced_parity(orc, monkeypatch, name, L):
     a = FORCED[name]()
     monkeypatch.delenv("MSPMV_DIA", raising=False)
     with mspmv.GpuCsr(a) as g:  # fill below the automatic threshold: the tiles
-        assert not g.spmm_kernel_name(L).startswith("k_spmm_dia<")
+        assert not is_dia(g.spmm_kernel_name(L))
     monkeypatch.setenv("MSPMV_DIA", "1")
     with mspmv.GpuCsr(a) as g:
         _check_product(a, g, L, orc)
@@ -124,7 +150,7 @@ def test_dia_cu_limit_and_inf(orc, monkeypatch):
         y0 = g.spmv(x)
         g.set_cu_limit(32)
         y1 = g.spmv(x)
-        assert g.kernel_name().startswith("k_spmm_dia<1,")
+        assert is_dia(g.kernel_name(), 1)
         g.set_cu_limit(0)
         assert y0.tobytes() == y1.tobytes()
         x[0] = np.inf  # column 0: read by rows 0, 3 and 70 only (offsets 0, -3, -70)
@@ -145,7 +171,7 @@ def test_dia_column_chunks(orc, monkeypatch, L):
     with mspmv.GpuCsr(a) as g:
         Y = g.spmm(X)
         check_parity_chunked(a, g, Y, orc.csr_spmm_t(a, X), X, L)
-        assert g.spmm_kernel_name(L).startswith("k_spmm_dia<")
+        assert is_dia(g.spmm_kernel_name(L))
 
 
 def test_dia_device_buffers(orc, monkeypatch):
@@ -175,7 +201,7 @@ def test_dia_cg_multi_vs_oracle(orc, monkeypatch, L):
     Xo, it_o, ho = orc.cg_multi(a, B, 5000, tol, kernel=1, P=8, hist_cap=5000)
     with mspmv.GpuCsr(a) as g:
         Xg, it_g, hg, st = g.cg_multi(B, 5000, tol, hist_cap=5000)
-        assert g.spmm_kernel_name(L).startswith(f"k_spmm_dia<{L},")
+        assert is_dia(g.spmm_kernel_name(L), L)
         Xg2, it_g2, hg2, st2 = g.cg_multi(B, 5000, tol, hist_cap=5000)  # cached graph: bitwise repeat
     assert st == 0 and st2 == 0
     assert iter_match(it_g, it_o, ho, tol), (it_g, it_o)
@@ -205,16 +231,16 @@ def test_dia_default_choice(monkeypatch):
     for name, (make, dia) in want.items():
         with mspmv.GpuCsr(make()) as g:
             for L in (1, 8):
-                assert g.spmm_kernel_name(L).startswith("k_spmm_dia<") == dia, (name, L, g.spmm_kernel_name(L))
+                assert is_dia(g.spmm_kernel_name(L)) == dia, (name, L, g.spmm_kernel_name(L))
     monkeypatch.setenv("MSPMV_DIA_SPMM", "0")  # the L-wide products opted out: only the SpMV takes the windows
     with mspmv.GpuCsr(CASES["stencil27"]()) as g:
-        assert g.kernel_name().startswith("k_spmm_dia<1,")
-        assert not g.spmm_kernel_name(8).startswith("k_spmm_dia<")
-        assert not g.spmm_kernel_name(2).startswith("k_spmm_dia<")
+        assert is_dia(g.kernel_name(), 1)
+        assert not is_dia(g.spmm_kernel_name(8))
+        assert not is_dia(g.spmm_kernel_name(2))
     monkeypatch.setenv("MSPMV_DIA", "1")
     with mspmv.GpuCsr(unsorted) as g:
-        assert not g.kernel_name().startswith("k_spmm_dia<")
+        assert not is_dia(g.kernel_name())
     monkeypatch.setenv("MSPMV_DIA", "0")
     with mspmv.GpuCsr(CASES["stencil27"]()) as g:
-        assert not g.kernel_name().startswith("k_spmm_dia<")
-        assert not g.spmm_kernel_name(8).startswith("k_spmm_dia<")
+        assert not is_dia(g.kernel_name())
+        assert not is_dia(g.spmm_kernel_name(8))

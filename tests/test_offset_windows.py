@@ -1,9 +1,11 @@
 """Offset-window planning on the host (mspmv_offset_windows; csrc/mspmv_dia.hip dia_plan_host), no GPU:
-the library's decision and per-window offset counts against a numpy restatement of the rules --
-64-row windows, each window's offsets col - row taken as the union over its rows (sorted), every row's
-columns strictly ascending, K <= 32, nonzeros >= min_window_fill x rows x K in each window and >=
-min_fill x 64 x sum K overall; a window is masked when some row lacks one of its offsets or it holds
-fewer than 64 rows.
+the library's decision, per-window offset counts and remainder against a numpy restatement of the rules
+(round 6, windows plus a remainder) -- 64-row windows; every row's columns strictly ascending; a window
+keeps the offsets col - row that >= min(8, its rows) of its rows hold, the 64 most frequent (ties: the
+smaller offset), and drops its rarest kept offsets while they fill < min_window_fill of rows x K; every
+other entry is remainder; the plan holds when sum K > 0, the kept entries fill >= min_fill x 64 x sum K
+and the remainder is <= 5 % of the nonzeros (any share when min_fill is 0); a window is masked when some
+row lacks one of its kept offsets or it holds fewer than 64 rows.
 """
 import numpy as np
 import pytest
@@ -12,31 +14,42 @@ import mspmv
 from test_gpu_dia import band
 
 
-def restate(a, min_fill=0.85, min_window_fill=0.3, kmax=32):
+def restate(a, min_fill=0.85, min_window_fill=0.3, kmax=64, keep_rows=8, max_rem=0.05):
     m = a.num_rows
     ro = a.row_offsets.astype(np.int64)
     ci = a.column_indices.astype(np.int64)
-    if m == 0 or a.num_nonzeros == 0 or np.diff(ro).max() > kmax:
+    if m == 0 or a.num_nonzeros == 0:
         return None
-    ks, masked = [], 0
+    if min_fill <= 0:
+        max_rem = 1.0
+    ks, masked, kept_total = [], 0, 0
     for r0 in range(0, m, 64):
         r1 = min(m, r0 + 64)
+        nr = r1 - r0
         offs = []
         for r in range(r0, r1):
             o = ci[ro[r]:ro[r + 1]] - r
             if o.size > 1 and np.any(np.diff(o) <= 0):
                 return None
             offs.append(o)
-        D = np.unique(np.concatenate(offs)) if any(o.size for o in offs) else np.zeros(0, np.int64)
-        K = D.size
-        nz = int(ro[r1] - ro[r0])
-        if K < 1 or K > kmax or nz < min_window_fill * (r1 - r0) * K:
-            return None
+        allo = np.concatenate(offs) if offs else np.zeros(0, np.int64)
+        vals, counts = np.unique(allo, return_counts=True)  # ascending offsets
+        sel = counts >= min(keep_rows, nr)
+        cand = list(zip(vals[sel].tolist(), counts[sel].tolist()))
+        cand.sort(key=lambda t: -t[1])  # stable: equal counts keep the smaller offset first
+        cand = cand[:kmax]
+        kept = sum(c for _, c in cand)
+        while cand and kept < min_window_fill * nr * len(cand):
+            kept -= cand.pop()[1]
+        K = len(cand)
         ks.append(K)
-        masked += not (r1 - r0 == 64 and nz == 64 * K)
-    if a.num_nonzeros < min_fill * 64 * sum(ks):
+        kept_total += kept
+        masked += not (nr == 64 and kept == 64 * K)
+    rem = a.num_nonzeros - kept_total
+    if sum(ks) == 0 or kept_total < min_fill * 64 * sum(ks) or rem > max_rem * a.num_nonzeros:
         return None
-    return {"windows": len(ks), "sum_offsets": sum(ks), "masked_windows": masked, "k": np.array(ks)}
+    return {"windows": len(ks), "sum_offsets": sum(ks), "masked_windows": masked, "k": np.array(ks),
+            "remainder": rem}
 
 
 def unsorted_tridiag():
@@ -54,8 +67,14 @@ CASES = {
     "rect": (lambda: band(2000, [0, 5, 1700, 3000], 4, n=5001), True),
     "holes": (lambda: band(4000, [-200, -1, 0, 1, 200], 5, drop=0.3), False),   # fill 0.7 < 0.85
     "unsorted": (unsorted_tridiag, False),
-    "fem_blocked": (lambda: mspmv.CsrMatrix.synth_fem_blocked(2400, 126000, 6, 60, seed=3), False),  # rows > 32
-    "banded_random": (lambda: mspmv.CsrMatrix.synth_banded(3000, 3000 * 8, 400, seed=2), False),     # K > 32
+    "fem_blocked": (lambda: mspmv.CsrMatrix.synth_fem_blocked(2400, 126000, 6, 60, seed=3), False),  # no offsets
+    "banded_random": (lambda: mspmv.CsrMatrix.synth_banded(3000, 3000 * 8, 400, seed=2), False),     # kept
+    "perturbed27": (lambda: mspmv.CsrMatrix.synth_stencil_perturbed((17, 12, 9), seed=1, extra_frac=0.02,
+                                                                    long_frac=0.01), True),        # remainder
+    "perturbed_heavy": (lambda: mspmv.CsrMatrix.synth_stencil_perturbed((17, 12, 9), seed=1, extra_frac=0.5,
+                                                                        long_frac=0.1), False),    # > 5 %
+    "kkt": (lambda: mspmv.CsrMatrix.synth_kkt((17, 12, 9), seed=4), True),                         # K 34
+    "wide": (lambda: band(64 * 9, list(range(-20, 21)) + [100, 200], 8), True),                   # K 43
 }
 
 
@@ -70,12 +89,14 @@ def test_offset_windows_plan(name):
         assert got["windows"] == want["windows"]
         assert got["sum_offsets"] == want["sum_offsets"]
         assert got["masked_windows"] == want["masked_windows"]
+        assert got["remainder"] == want["remainder"]
         np.testing.assert_array_equal(got["k"], want["k"])
 
 
 def test_offset_windows_thresholds():
     """Forced thresholds (MSPMV_DIA=1 plans at fill 0): windows with missing offsets and empty rows fit;
-    a window whose nonzeros fall below min_window_fill does not."""
+    a window whose kept entries fall below min_window_fill drops its rarest offsets to the remainder
+    (round 5 rejected the whole plan), which the forced plan takes in any amount."""
     a = CASES["holes"][0]()
     assert mspmv.offset_windows(a, 0.0, 0.0) is not None
     assert mspmv.offset_windows(a, 0.6, 0.3) is not None
@@ -83,7 +104,10 @@ def test_offset_windows_thresholds():
     e = band(3000, [0, 3], 6, drop=0.6)
     got, want = mspmv.offset_windows(e, 0.0, 0.0), restate(e, 0.0, 0.0)
     assert got is not None and got["masked_windows"] == want["masked_windows"] == got["windows"]
-    assert mspmv.offset_windows(e, 0.0, 0.5) is None
+    got, want = mspmv.offset_windows(e, 0.0, 0.5), restate(e, 0.0, 0.5)
+    assert got is not None and got["remainder"] == want["remainder"] > 0
+    np.testing.assert_array_equal(got["k"], want["k"])
+    assert np.any(got["k"] == 0)  # whole windows left to the remainder
 
 
 def test_offset_windows_rejects_bad_input():
