@@ -601,6 +601,7 @@ def run_cg_single(dev, cpu_seconds, do_cpu):
            "status": st, "kernel": kernel}
     if phases:
         out["resident_phases"] = phases
+    out["pipelined_large"] = run_cg_single_pipelined(dev)
     if do_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from _oracle import Oracle
@@ -614,6 +615,39 @@ def run_cg_single(dev, cpu_seconds, do_cpu):
                                "sample": f"oracle CGSolveSingle restatement (the reference's CG headers need "
                                          f"<mkl.h>), {k} iterations in {el:.1f} s"}
     return out
+
+
+CG_LARGE = dict(dims=(75, 76, 75), shift=1e-2)  # 427,500 rows, 11.2 M nonzeros: pwtk's size, SPD
+
+
+def run_cg_single_pipelined(dev):
+    """CGSolveSingle on a pwtk-size SPD matrix (27-point stencil, 11.2 M nonzeros) through the two-kernel
+    pipelined form -- the path a single-RHS matrix takes when it does not fit the register-resident
+    kernel (MSPMV_CG_RESIDENT=0 makes sure of it here).  Every iteration streams the matrix from HBM /
+    the Infinity Cache, so the SURVEY 8(d) bytes per iteration give a real fraction of the roofline."""
+    nx, ny, nz = CG_LARGE["dims"]
+    a = mspmv.CsrMatrix.synth_stencil(1, nx * ny * nz, nx, ny, nz, seed=9, diag_shift=CG_LARGE["shift"])
+    n = a.num_rows
+    b = glibc_rhs(42, n)
+    thr = float(np.sqrt(np.sum(b * b)) * 1e-5)
+    with env_set(MSPMV_CG_RESIDENT="0"), mspmv.GpuCsr(a, device=dev) as g:
+        db, dx = mspmv.DeviceBuffer.from_array(b, dev), mspmv.DeviceBuffer(8 * n, dev)
+        g.cg_dev(db, dx, 1, 10000, thr)
+        t0 = time.perf_counter()
+        it, _, st = g.cg_dev(db, dx, 1, 10000, thr)
+        el = time.perf_counter() - t0
+        kernel = g.cg_kernel_name()
+        db.free()
+        dx.free()
+    ips = it / el
+    return {"workload": f"CGSolveSingle, pwtk-size SPD 27-point stencil (diag shift {CG_LARGE['shift']}) m={n} "
+                        f"nnz={a.num_nonzeros}, srand(42) RHS, tol = 1e-5*||b||; the two-kernel pipelined form "
+                        f"(MSPMV_CG_RESIDENT=0)",
+            "iterations": it, "seconds": round(el, 5), "iters_per_s": round(ips, 1),
+            "us_per_iter": round(el / max(it, 1) * 1e6, 2),
+            "achieved_GBps": round(cg_iter_bytes(n, a.num_nonzeros) * ips / 1e9, 1),
+            "roofline_frac": round(cg_iter_bytes(n, a.num_nonzeros) * ips / 1e9 / HBM_PEAK_GBS, 4),
+            "status": st, "kernel": kernel}
 
 
 def run_cg_multi(d, dev):

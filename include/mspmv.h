@@ -299,6 +299,16 @@ MSPMV_API mspmv_status mspmv_tile_lanes(mspmv_handle h, int L, int *lanes);
 MSPMV_API mspmv_status mspmv_offset_windows(const mspmv_csr_d *a, double min_fill, double min_window_fill, int *ok,
                                             int *num_windows, long long *sum_offsets, int *masked_windows,
                                             int *k_per_window, long long *remainder);
+/* Diagnostic (the small-matrix SpMV's per-tile phases): one plain SpMV y = A x on device
+ * vectors through the stamped instantiation of the merge-tile kernel k_spmv_tile, whose thread 0 records
+ * wall_clock64() (a constant 100 MHz clock) per tile: stamps[t * 6 + i], i = 0 entry, 1 stream and x
+ * gathers issued, 2 staged products in LDS (stream and gathers landed), 3 row ends in LDS, 4 rows reduced
+ * and stored, 5 the HW_ID register of the CU that ran it.  flush_bytes > 0: the cold protocol's read
+ * sweep of that many bytes first (as mspmv_time_spmm_dev).  stamps NULL: only *num_tiles.
+ * MSPMV_ERR_UNSUPPORTED when the matrix's plain SpMV runs another kernel (node blocks, windows, slabs,
+ * one-wave tiles).  No reference counterpart. */
+MSPMV_API mspmv_status mspmv_spmv_tile_stamps(mspmv_handle h, const double *d_x, double *d_y, size_t flush_bytes,
+                                              unsigned long long *stamps, int *num_tiles);
 /* The single-RHS SpMV kernel instantiation launched for this matrix (tuning read once from
  * the MSPMV_SPMV_* environment; nontemporal matrix loads above 128 MiB), e.g.
  * "k_spmv_tile<8,0,true>" -- the name rocprofv3 reports.  Valid until the next call on this
@@ -321,8 +331,8 @@ MSPMV_API const char *mspmv_cg_kernel_name(mspmv_handle h);
  * call this: it synchronizes the handle's stream, clears the word and returns MSPMV_ERR_FAULT if any
  * product since the last check raised it.  No reference counterpart (OpenMP reductions need none). */
 MSPMV_API mspmv_status mspmv_check_faults(mspmv_handle h);
-/* Test hook: the next CG solve on h fills its fold tickets with `value` before its first iteration
- * (MSPMV_POISON_FILL), optionally zeroes them again after the first iteration is enqueued
+/* Test hook: the next CG solve on h fills its fold tickets with `value` after its init, before its first
+ * iteration (MSPMV_POISON_FILL), optionally zeroes them again after the first iteration is enqueued
  * (MSPMV_POISON_LATE_ZERO: the ordering of round 5's unordered null-stream memset) and optionally
  * records the fault without stopping (MSPMV_POISON_NO_STOP: the solve runs to its stop test and then
  * returns MSPMV_ERR_FAULT with the iteration count it reached).  One solve only. */

@@ -33,11 +33,16 @@ __device__ __forceinline__ void store_sc1_2(double *p, double2 v)
 }
 
 // One arrival on a self-resetting ticket (call from one thread; tickets guard the cross-workgroup folds:
-// reduce_slots, publish_partials, close_split_rows, the slab kernels' column groups).  The fetch_add is a
-// release at agent scope: it orders this workgroup's earlier stores (agent-scope, drained) before the
-// arrival.  The arrival that draws `last` -- the group's final one -- takes an agent-scope acquire fence
-// before it reads the others' stores; the other arrivals read nothing, so they skip it (an acquire on
-// every arrival would invalidate the L2's non-coherent lines once per workgroup).  Tickets start at 0
+// reduce_slots, publish_partials, close_split_rows, the slab kernels' column groups).  Every caller has
+// written what the final arrival will read with agent-scope (sc1, write-through) stores and drained them
+// (s_waitcnt vmcnt(0)) before arriving, and the final arrival reads with agent-scope loads.
+// RELEASE: the fetch_add is also a release at agent scope, the memory model's own form of that order --
+// on gfx950 a buffer_wbl2 (the XCD's whole L2 written back) per arrival.  The folds of few workgroups
+// (k_fold_dot, rows split between tiles) take it; the streaming kernels, whose L2 holds the vectors they
+// just wrote, keep the drained-store form (measured with the release on every arrival, r06a: configs[4]'s
+// CG iteration +4.5 %, the sliced-ELL SpMV +10 %).  The arrival that draws `last` -- the group's final
+// one -- takes an agent-scope acquire fence before it reads the others' stores; the other arrivals read
+// nothing, so they skip it.  Tickets start at 0
 // and the final arrival resets them, so a group draws exactly 0 .. last.  A draw > last means the ticket
 // was not 0 when the group began -- its array not zeroed, or zeroed out of stream order, before the
 // launch (round 5's 70-vs-43 iterations): the draw of `last` then falls on an arrival that
@@ -45,9 +50,11 @@ __device__ __forceinline__ void store_sc1_2(double *p, double2 v)
 // stale total).  That draw raises kFaultTicket in *fault (nullable), which a solve returns as
 // MSPMV_ERR_FAULT (a plain product: mspmv_check_faults).
 // *faulted (nullable) tells the caller this arrival raised the fault.
+template <bool RELEASE>
 __device__ __forceinline__ bool ticket_arrive(unsigned *tk, unsigned last, unsigned *fault, bool *faulted = nullptr)
 {
-    const unsigned v = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned v = RELEASE ? __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT)
+                               : __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (v > last && fault)
         __hip_atomic_fetch_or(fault, kFaultTicket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (faulted)
@@ -96,9 +103,9 @@ __device__ __forceinline__ void close_split_rows(const A &a, int t, int4 fx, int
     }
     if (threadIdx.x == 0) {
         int f0 = -1, f1 = -1;
-        if (fx.x >= 0 && ticket_arrive(&a.fix_cnt[fx.x], (unsigned)fx.y, a.fault))
+        if (fx.x >= 0 && ticket_arrive<true>(&a.fix_cnt[fx.x], (unsigned)fx.y, a.fault))
             f0 = fx.x;
-        if (fx.z > 0 && ticket_arrive(&a.fix_cnt[t], (unsigned)fx.z, a.fault))
+        if (fx.z > 0 && ticket_arrive<true>(&a.fix_cnt[t], (unsigned)fx.z, a.fault))
             f1 = t;
         s_fin[0] = f0;
         s_fin[1] = f1;

@@ -51,13 +51,6 @@ struct DiaArgs {
     const CgControl *ctrl;           // CG: return at once when ctrl->done
     double *partials;                // dot mode: x.(A x) per column per window, [windows][L] (launch_fold_dot)
     const double *xr;                // dot mode: x at this matrix's rows (x + row_off * ld for a row-range view)
-    // block CG, p update fused (k_spmm_dia_wg PUPD): x above is p_old; the spans staged are
-    // p = r + beta p_old (CgScalars::beta per column), the window's own rows of p go to pnew and take
-    // the deferred x += alpha p_old (CgScalars::alpha, when ctrl->x_pending: CgVecArgs::lazy_x)
-    const double *r;
-    double *pnew;
-    double *xsol;
-    const CgScalars *scal;
     // the remainder (entries off the window's offset list): a CSR over all rows, summed after the offsets
     const int *rem_ptr;
     const int *rem_col;
@@ -230,19 +223,22 @@ k_spmm_dia(DiaArgs a)
             const long long d0 = off_at(k);
             const long long s0 = r0 + d0;  // the span's first row (wave-uniform)
             if (s0 >= 0 && s0 + 64 + kDiaRun - 2 <= nmax) {  // inside X: a scalar base and per-lane constants
-                const double *sb = xb + s0 * a.ld;
+                const size_t sb = (size_t)s0 * a.ld;
 #pragma unroll
-                for (int q = 0; q < GL; ++q)
-                    nx[q] = *reinterpret_cast<const v2d_t *>(sb + lrow + (size_t)(RS * q) * a.ld);
-                ne = *reinterpret_cast<const v2d_t *>(sb + (size_t)(64 + min(rl, kDiaRun - 2)) * a.ld);
+                for (int q = 0; q < GL; ++q) {
+                    const size_t o = sb + lrow + (size_t)(RS * q) * a.ld;
+                    nx[q] = *reinterpret_cast<const v2d_t *>(xb + o);
+                }
+                const size_t oe = sb + (size_t)(64 + min(rl, kDiaRun - 2)) * a.ld;
+                ne = *reinterpret_cast<const v2d_t *>(xb + oe);
             } else {
 #pragma unroll
                 for (int q = 0; q < GL; ++q) {
-                    const long long xr = min(max(s0 + rl + RS * q, 0LL), nmax);
-                    nx[q] = *reinterpret_cast<const v2d_t *>(xb + xr * a.ld);
+                    const size_t o = (size_t)min(max(s0 + rl + RS * q, 0LL), nmax) * a.ld;
+                    nx[q] = *reinterpret_cast<const v2d_t *>(xb + o);
                 }
-                const long long xe = min(max(s0 + 64 + min(rl, kDiaRun - 2), 0LL), nmax);
-                ne = *reinterpret_cast<const v2d_t *>(xb + xe * a.ld);
+                const size_t oe = (size_t)min(max(s0 + 64 + min(rl, kDiaRun - 2), 0LL), nmax) * a.ld;
+                ne = *reinterpret_cast<const v2d_t *>(xb + oe);
             }
 #pragma unroll
             for (int j = 0; j < kDiaRun; ++j) {
@@ -316,7 +312,8 @@ k_spmm_dia(DiaArgs a)
                 v2d_t ar = v2d_t{0.0, 0.0};
                 for (int j = a.rem_ptr[r]; j < a.rem_ptr[r + 1]; ++j) {
                     const double v = a.rem_val[j];
-                    const v2d_t xv = *reinterpret_cast<const v2d_t *>(xb + (size_t)a.rem_col[j] * a.ld);
+                    const size_t o = (size_t)a.rem_col[j] * a.ld;
+                    const v2d_t xv = *reinterpret_cast<const v2d_t *>(xb + o);
                     ar[0] += v * xv[0];
                     ar[1] += v * xv[1];
                 }
@@ -348,216 +345,6 @@ k_spmm_dia(DiaArgs a)
             }
             if (rl == 0)
                 *reinterpret_cast<v2d_t *>(a.partials + (size_t)w * L + 2 * c) = d;
-        }
-    }
-}
-
-// L = 8, 16: one window per WORKGROUP (four waves) instead of per wave.  The wave form holds L/2 rows
-// of the window per lane (126 VGPRs at L = 8: 4 waves per SIMD, each a serial chain of runs; 28 % of its
-// wave cycles waiting on memory, the rest issue and LDS latency -- r05ad counters).  Here thread t
-// holds row t / (L/2) (L = 8; rows t / 8 and t / 8 + 32 at L = 16) of the window and column pair t % (L/2):
-// the four waves stage each run's span of 64 + g - 1 panel rows in LDS together (one 16-B element per
-// thread and row slot, double-buffered, ONE workgroup barrier per run), each thread loads its own
-// rows' values (no shuffles) and sums its row in CSR order (offsets ascending, mul then add): the
-// products are the wave form's bit for bit.
-// PUPD (the block CG's iteration, CGSolveMultiple no_pretreatment.hpp:93-177 with the p update of
-// :177 moved ahead of the next SpMM): the spans staged are p = r + beta p_old (the reference's
-// update_p_multiple expression, per column), so the separate p update pass (k_dist_pupdate: r, p, x
-// read, p, x written) is gone; the window's own rows of p are written to pnew (ping-pong buffers:
-// other windows still read p_old) and take the deferred x += alpha p_old.
-// DOT: p.(A p) per column per window into partials (launch_fold_dot), p = the staged p (PUPD) or xr.
-template <int L, bool NT, bool DOT, bool PUPD>
-__global__ __launch_bounds__(kDiaThreads) void k_spmm_dia_wg(DiaArgs a)
-{
-    static_assert(L == 8 || L == 16, "workgroup windows: L = 8 or 16");
-    constexpr int GL = L / 2;                       // threads per panel row
-    constexpr int RPI = kDiaThreads / GL;            // panel rows per workgroup instruction
-    constexpr int NR = 64 / RPI;                     // window rows per thread
-    constexpr int SPAN = 64 + kDiaRun - 1;
-    constexpr int EDGE = (kDiaRun - 1) * GL;         // span elements past row 63
-    static_assert(EDGE <= kDiaThreads, "edge rows: one element per thread");
-    __shared__ v2d_t sx[2][SPAN * GL];
-    __shared__ v2d_t s_dot[kDiaWaves][GL];
-    const int w = xcd_tile(blockIdx.x, a.windows);
-    if (a.ctrl && a.ctrl->done)
-        return;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int c = tid % GL, rl = tid / GL;
-    const int4 hd = a.hdr[w];
-    const int K = __builtin_amdgcn_readfirstlane(hd.x) & 0xffff;
-    const bool has_rem = (__builtin_amdgcn_readfirstlane(hd.x) >> 16) != 0;
-    const bool masked = __builtin_amdgcn_readfirstlane(hd.w) >= 0;
-    const int lk = max(min(lane, K - 1), 0);
-    const int offv = K ? a.off[__builtin_amdgcn_readfirstlane(hd.y) + lk] : 0;
-    const unsigned long long mkv = masked && K ? a.mask[__builtin_amdgcn_readfirstlane(hd.w) + lk] : ~0ull;
-    auto off_at = [&](int k) { return __builtin_amdgcn_readlane(offv, k); };
-    auto mask_at = [&](int k) {
-        const unsigned lo = __builtin_amdgcn_readlane((unsigned)mkv, k);
-        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(mkv >> 32), k);
-        return ((unsigned long long)hi << 32) | lo;
-    };
-    int runv = 1;  // run length from offset k (lane k): consecutive offsets, <= kDiaRun, within the list
-    {
-        int step = 1;
-#pragma unroll
-        for (int j = 1; j < kDiaRun; ++j) {
-            const int nxt = __shfl_down(offv, j);
-            step = step && lane + j < K && nxt == offv + j;
-            runv += step;
-        }
-    }
-    const long long r0 = (long long)w * 64;
-    const long long nmax = a.n - 1;
-    const double *__restrict__ vb = a.vt + (size_t)__builtin_amdgcn_readfirstlane(hd.z) * 128;
-    double2 beta = make_double2(0.0, 0.0), alpha = make_double2(0.0, 0.0);
-    bool lag = false;
-    if constexpr (PUPD) {
-        beta = make_double2(a.scal[2 * c].beta, a.scal[2 * c + 1].beta);
-        alpha = make_double2(a.scal[2 * c].alpha, a.scal[2 * c + 1].alpha);
-        lag = a.ctrl->x_pending != 0;
-    }
-    // span element (span row sr, column pair c): p_old, or r + beta p_old
-    auto span_ld = [&](long long xrow) -> v2d_t {
-        const size_t o = (size_t)xrow * a.ld + 2 * c;
-        const v2d_t q = *reinterpret_cast<const v2d_t *>(a.x + o);
-        if constexpr (PUPD) {
-            const v2d_t rv = *reinterpret_cast<const v2d_t *>(a.r + o);
-            return v2d_t{rv[0] + beta.x * q[0], rv[1] + beta.y * q[1]};
-        } else {
-            return q;
-        }
-    };
-    v2d_t nx[NR], ne = v2d_t{0.0, 0.0};
-    double nv[kDiaRun][NR];
-    auto fetch = [&](int k) {  // run k's span (rows clamped into X: outside it they serve absent entries only)
-        const long long s0 = r0 + off_at(k);
-#pragma unroll
-        for (int q = 0; q < NR; ++q)
-            nx[q] = span_ld(min(max(s0 + rl + RPI * q, 0LL), nmax));
-        if (tid < EDGE)
-            ne = span_ld(min(max(s0 + 64 + tid / GL, 0LL), nmax));
-#pragma unroll
-        for (int j = 0; j < kDiaRun; ++j) {
-            const int kk = min(k + j, K - 1);
-#pragma unroll
-            for (int q = 0; q < NR; ++q)
-                nv[j][q] = dia_ld<NT>(vb + (size_t)(kk >> 1) * 128 + 2 * (rl + RPI * q) + (kk & 1));
-        }
-    };
-    auto stage = [&](int buf) {
-#pragma unroll
-        for (int q = 0; q < NR; ++q)
-            sx[buf][(rl + RPI * q) * GL + c] = nx[q];
-        if (tid < EDGE)
-            sx[buf][64 * GL + tid] = ne;
-    };
-    v2d_t acc[NR];
-#pragma unroll
-    for (int q = 0; q < NR; ++q)
-        acc[q] = v2d_t{0.0, 0.0};
-    if (K > 0) {
-        fetch(0);
-        stage(0);
-    }
-    __syncthreads();
-    int buf = 0;
-    for (int k = 0; k < K;) {
-        double cv[kDiaRun][NR];
-#pragma unroll
-        for (int j = 0; j < kDiaRun; ++j)
-#pragma unroll
-            for (int q = 0; q < NR; ++q)
-                cv[j][q] = nv[j][q];
-        const int gk = __builtin_amdgcn_readlane(runv, k), kc = k;
-        k += gk;
-        if (k < K)  // the next run's span and values fly while this one is summed
-            fetch(k);
-#pragma unroll
-        for (int j = 0; j < kDiaRun; ++j) {
-            if (j >= gk)
-                break;
-            const unsigned long long mw = masked ? mask_at(kc + j) : ~0ull;
-#pragma unroll
-            for (int q = 0; q < NR; ++q) {
-                const int row = rl + RPI * q;
-                const v2d_t xv = sx[buf][(row + j) * GL + c];
-                const double v = cv[j][q];
-                if (mw == ~0ull) {  // every row holds this offset (workgroup-uniform): no selects
-                    acc[q][0] += v * xv[0];
-                    acc[q][1] += v * xv[1];
-                } else {
-                    const bool on = (mw >> row) & 1ull;
-                    acc[q][0] += on ? v * xv[0] : 0.0;
-                    acc[q][1] += on ? v * xv[1] : 0.0;
-                }
-            }
-        }
-        if (k < K)
-            stage(buf ^ 1);
-        __syncthreads();  // run kc's reads of sx[buf] and the next span's writes to sx[buf ^ 1] are done
-        buf ^= 1;
-    }
-    if (has_rem) {  // the rows' remainder entries, in CSR order, after their offsets (p at their columns)
-#pragma unroll
-        for (int q = 0; q < NR; ++q) {
-            const long long r = r0 + rl + RPI * q;
-            if (r >= a.m)
-                continue;
-            v2d_t ar = v2d_t{0.0, 0.0};
-            for (int j = a.rem_ptr[r]; j < a.rem_ptr[r + 1]; ++j) {
-                const double v = a.rem_val[j];
-                const v2d_t xv = span_ld(a.rem_col[j]);
-                ar[0] += v * xv[0];
-                ar[1] += v * xv[1];
-            }
-            acc[q][0] = acc[q][0] + ar[0];
-            acc[q][1] = acc[q][1] + ar[1];
-        }
-    }
-    v2d_t d = v2d_t{0.0, 0.0};
-#pragma unroll
-    for (int q = 0; q < NR; ++q) {
-        const long long r = r0 + rl + RPI * q;
-        if (r >= a.m)
-            continue;
-        const size_t o = (size_t)r * a.ld + 2 * c;
-        __builtin_nontemporal_store(acc[q], reinterpret_cast<v2d_t *>(a.y + o));
-        v2d_t pv;
-        if constexpr (PUPD) {  // the window's own rows: p = r + beta p_old to pnew, x += alpha p_old
-            const v2d_t q0 = *reinterpret_cast<const v2d_t *>(a.x + o);
-            const v2d_t rv = *reinterpret_cast<const v2d_t *>(a.r + o);
-            pv = v2d_t{rv[0] + beta.x * q0[0], rv[1] + beta.y * q0[1]};
-            *reinterpret_cast<v2d_t *>(a.pnew + o) = pv;
-            if (lag) {
-                const v2d_t xo = __builtin_nontemporal_load(reinterpret_cast<const v2d_t *>(a.xsol + o));
-                __builtin_nontemporal_store(v2d_t{xo[0] + alpha.x * q0[0], xo[1] + alpha.y * q0[1]},
-                                            reinterpret_cast<v2d_t *>(a.xsol + o));
-            }
-        } else if constexpr (DOT) {
-            pv = *reinterpret_cast<const v2d_t *>(a.xr + o);
-        }
-        if constexpr (DOT) {
-            d[0] += pv[0] * acc[q][0];
-            d[1] += pv[1] * acc[q][1];
-        }
-    }
-    if constexpr (DOT) {  // column pair c: rows in q order, the wave's rows by a fixed butterfly, waves in order
-#pragma unroll
-        for (int off = 32; off >= GL; off >>= 1) {
-            d[0] += __shfl_xor(d[0], off);
-            d[1] += __shfl_xor(d[1], off);
-        }
-        if (lane < GL)
-            s_dot[wv][lane] = d;
-        __syncthreads();
-        if (tid < GL) {
-            v2d_t t = s_dot[0][tid];
-#pragma unroll
-            for (int u = 1; u < kDiaWaves; ++u) {
-                t[0] += s_dot[u][tid][0];
-                t[1] += s_dot[u][tid][1];
-            }
-            *reinterpret_cast<v2d_t *>(a.partials + (size_t)w * L + 2 * tid) = t;
         }
     }
 }
@@ -683,7 +470,7 @@ struct DiaHostPlan {
 // One window's kept offsets (ascending) and their entry count; false when some row's columns do not
 // ascend strictly.  ci[j - cbase] is the column of CSR entry j.
 static bool window_offsets(const int *ro, const int *ci, long long cbase, int r0, int r1, double min_window_fill,
-                           std::vector<std::pair<int, int>> &keep, long long &kept)
+                           std::vector<std::pair<int, int>> &keep, long long &kept, bool all_offsets)
 {
     std::vector<int> d;
     d.reserve((size_t)(ro[r1] - ro[r0]));
@@ -707,7 +494,8 @@ static bool window_offsets(const int *ro, const int *ci, long long cbase, int r0
         cnt.emplace_back(d[i], (int)(e - i));
         i = e;
     }
-    const int keep_min = std::min(kDiaKeepRows, r1 - r0);
+    // all_offsets (the exact plan, dia_plan_host's first attempt): the window keeps its whole offset list
+    const int keep_min = all_offsets ? 1 : std::min(kDiaKeepRows, r1 - r0);
     keep.clear();
     for (const auto &c : cnt)
         if (c.second >= keep_min)
@@ -729,8 +517,20 @@ static bool window_offsets(const int *ro, const int *ci, long long cbase, int r0
     return true;
 }
 
+static bool dia_plan_host_pass(const int *ro, const int *ci, int m, long long nnz, double min_fill,
+                               double min_window_fill, double max_rem_frac, bool all_offsets, DiaHostPlan &out);
+
+// Two passes: first every window keeps its whole offset list (round 5's plan: no remainder, every row
+// summed in CSR order); only when that plan does not hold are the rare offsets left to the remainder.
 static bool dia_plan_host(const int *ro, const int *ci, int m, long long nnz, double min_fill, double min_window_fill,
                           double max_rem_frac, DiaHostPlan &out)
+{
+    return dia_plan_host_pass(ro, ci, m, nnz, min_fill, min_window_fill, 0.0, true, out) ||
+           dia_plan_host_pass(ro, ci, m, nnz, min_fill, min_window_fill, max_rem_frac, false, out);
+}
+
+static bool dia_plan_host_pass(const int *ro, const int *ci, int m, long long nnz, double min_fill,
+                               double min_window_fill, double max_rem_frac, bool all_offsets, DiaHostPlan &out)
 {
     if (m <= 0 || nnz <= 0)
         return false;
@@ -746,7 +546,7 @@ static bool dia_plan_host(const int *ro, const int *ci, int m, long long nnz, do
         const int r0 = w * 64, r1 = std::min(m, r0 + 64);
         std::vector<std::pair<int, int>> keep;
         long long nz = 0;
-        if (!window_offsets(ro, ci, 0, r0, r1, min_window_fill, keep, nz)) {
+        if (!window_offsets(ro, ci, 0, r0, r1, min_window_fill, keep, nz, all_offsets)) {
             bad = 1;
             continue;
         }
@@ -859,7 +659,7 @@ static bool dia_plan_host(const int *ro, const int *ci, int m, long long nnz, do
 // not attempted when their entries would leave twice the remainder allowed or fill the panels clearly
 // less than min_fill (FEM node blocks, random bands and power-law rows fail here in microseconds).
 constexpr int kDiaSamples = 64;
-static mspmv_status dia_sample_ok(const mspmv_handle_s *h, const std::vector<int> &ro, double min_fill,
+static mspmv_status dia_sample_ok(const mspmv_handle_s *h, const int *ro, const int *host_ci, double min_fill,
                                   double min_window_fill, double max_rem_frac, bool *ok)
 {
     const int m = h->m, W = (m + 63) / 64;
@@ -871,14 +671,18 @@ static mspmv_status dia_sample_ok(const mspmv_handle_s *h, const std::vector<int
         const int w = (int)((long long)i * W / S);
         const int r0 = w * 64, r1 = std::min(m, r0 + 64);
         const long long j0 = ro[(size_t)r0], j1 = ro[(size_t)r1];
-        buf.resize((size_t)std::max(j1 - j0, 1LL));
-        if (j1 > j0 && hipMemcpy(buf.data(), h->d_cols + j0, sizeof(int) * (size_t)(j1 - j0), hipMemcpyDeviceToHost) !=
-                           hipSuccess) {
-            set_error("offset-window plan: sample download failed");
-            return MSPMV_ERR_HIP;
+        const int *cw = host_ci ? host_ci + j0 : nullptr;
+        if (!host_ci) {
+            buf.resize((size_t)std::max(j1 - j0, 1LL));
+            if (j1 > j0 &&
+                hipMemcpy(buf.data(), h->d_cols + j0, sizeof(int) * (size_t)(j1 - j0), hipMemcpyDeviceToHost) != hipSuccess) {
+                set_error("offset-window plan: sample download failed");
+                return MSPMV_ERR_HIP;
+            }
+            cw = buf.data();
         }
         long long kw = 0;
-        if (!window_offsets(ro.data(), buf.data(), j0, r0, r1, min_window_fill, keep, kw)) {
+        if (!window_offsets(ro, cw, j0, r0, r1, min_window_fill, keep, kw, false)) {
             *ok = false;
             return MSPMV_OK;
         }
@@ -897,26 +701,34 @@ mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, dou
     if (m <= 0 || h->nnz <= 0)
         return MSPMV_ERR_UNSUPPORTED;
     const double max_rem = min_fill > 0.0 ? kDiaMaxRemFrac : 1.0;  // forced (MSPMV_DIA=1): any remainder
-    std::vector<int> ro((size_t)m + 1);
-    if (hipMemcpy(ro.data(), h->d_row_offsets, sizeof(int) * ro.size(), hipMemcpyDeviceToHost) != hipSuccess) {
-        set_error("offset-window plan: row offsets download failed");
-        return MSPMV_ERR_HIP;
-    }
+    const int *ro = nullptr, *ci = nullptr;
     bool sample_ok = true;
-    const mspmv_status sst = dia_sample_ok(h, ro, min_fill, min_window_fill, max_rem, &sample_ok);
-    if (sst != MSPMV_OK)
-        return sst;
-    if (!sample_ok)
-        return MSPMV_ERR_UNSUPPORTED;
-    std::vector<int> ci((size_t)h->nnz);
-    if (hipMemcpy(ci.data(), h->d_cols, sizeof(int) * ci.size(), hipMemcpyDeviceToHost) != hipSuccess) {
-        set_error("offset-window plan: column download failed");
-        return MSPMV_ERR_HIP;
+    if (host_pattern_resident(h)) {  // the caller's arrays (mspmv_csr_create) or a shared copy: sample there
+        mspmv_status st0 = host_pattern(h, &ro, &ci);
+        if (st0 != MSPMV_OK)
+            return st0;
+        st0 = dia_sample_ok(h, ro, ci, min_fill, min_window_fill, max_rem, &sample_ok);
+        if (st0 != MSPMV_OK)
+            return st0;
+        if (!sample_ok)
+            return MSPMV_ERR_UNSUPPORTED;
+    } else {  // sample the device's columns first: non-stencils never copy the whole pattern
+        std::vector<int> ros((size_t)m + 1);
+        if (hipMemcpy(ros.data(), h->d_row_offsets, sizeof(int) * ros.size(), hipMemcpyDeviceToHost) != hipSuccess) {
+            set_error("offset-window plan: row offsets download failed");
+            return MSPMV_ERR_HIP;
+        }
+        mspmv_status st0 = dia_sample_ok(h, ros.data(), nullptr, min_fill, min_window_fill, max_rem, &sample_ok);
+        if (st0 != MSPMV_OK)
+            return st0;
+        if (!sample_ok)
+            return MSPMV_ERR_UNSUPPORTED;
+        if ((st0 = host_pattern(h, &ro, &ci)) != MSPMV_OK)
+            return st0;
     }
     DiaHostPlan hp;
-    if (!dia_plan_host(ro.data(), ci.data(), m, h->nnz, min_fill, min_window_fill, max_rem, hp))
+    if (!dia_plan_host(ro, ci, m, h->nnz, min_fill, min_window_fill, max_rem, hp))
         return MSPMV_ERR_UNSUPPORTED;
-    std::vector<int>().swap(ci);
     const int W = hp.windows;
     const std::vector<int4> &hdr = hp.hdr;
     const std::vector<int> &offs = hp.offs;
@@ -1008,35 +820,9 @@ mspmv_status build_dia_plan(mspmv_handle_s *h, TilePlan &p, double min_fill, dou
     return MSPMV_OK;
 }
 
-// L = 8, 16 on the workgroup form (k_spmm_dia_wg) unless MSPMV_DIA_WG=0 (A/B against the wave form)
-static bool dia_wg_enabled()
-{
-    static const bool on = [] {
-        const char *e = getenv("MSPMV_DIA_WG");
-        return !(e && *e && atoi(e) == 0);
-    }();
-    return on;
-}
-
 template <int L>
 static void dia_launch_L(const DiaArgs &a, hipStream_t s, bool nt)
 {
-    if constexpr (L == 8 || L == 16) {
-        if (dia_wg_enabled()) {
-            const dim3 grid((unsigned)a.windows), block(kDiaThreads);
-            if (a.partials) {
-                if (nt)
-                    hipLaunchKernelGGL((k_spmm_dia_wg<L, true, true, false>), grid, block, 0, s, a);
-                else
-                    hipLaunchKernelGGL((k_spmm_dia_wg<L, false, true, false>), grid, block, 0, s, a);
-            } else if (nt) {
-                hipLaunchKernelGGL((k_spmm_dia_wg<L, true, false, false>), grid, block, 0, s, a);
-            } else {
-                hipLaunchKernelGGL((k_spmm_dia_wg<L, false, false, false>), grid, block, 0, s, a);
-            }
-            return;
-        }
-    }
     const dim3 grid((unsigned)a.groups), block(kDiaThreads);
     if (a.partials) {
         if (nt)
@@ -1089,60 +875,8 @@ hipError_t launch_dia(mspmv_handle_s *h, const TilePlan &plan, const double *d_X
     return hipGetLastError();
 }
 
-// The block CG's fused iteration SpMM (k_spmm_dia_wg PUPD + DOT): Ap = A p with p = r + beta p_old staged
-// on the fly, p's own rows to pnew, the deferred x += alpha p_old, p.Ap partials per window.
-hipError_t launch_dia_cg(mspmv_handle_s *h, const TilePlan &plan, const double *p_old, const double *r, double *pnew,
-                         double *ap, double *x, int L, CgControl *ctrl, const CgScalars *scal, double *partials)
-{
-    const DiaData *dd = plan.dia;
-    if (!dd || !(L == 8 || L == 16) || !partials || !ctrl || !scal)
-        return hipErrorInvalidValue;
-    if (dd->windows == 0)
-        return hipSuccess;
-    DiaArgs a{};
-    a.hdr = dd->d_hdr;
-    a.off = dd->d_off;
-    a.mask = dd->d_mask;
-    a.vt = dd->d_vt;
-    a.x = p_old;
-    a.y = ap;
-    a.ctrl = ctrl;
-    a.partials = partials;
-    a.windows = dd->windows;
-    a.rem_ptr = dd->d_rem_ptr;
-    a.rem_col = dd->d_rem_col;
-    a.rem_val = dd->d_rem_val;
-    a.xr = p_old;
-    a.groups = (dd->windows + kDiaWaves - 1) / kDiaWaves;
-    a.m = h->m;
-    a.n = h->n;
-    a.ld = L;
-    a.r = r;
-    a.pnew = pnew;
-    a.xsol = x;
-    a.scal = scal;
-    const dim3 grid((unsigned)dd->windows), block(kDiaThreads);
-    const bool nt = stream_nt(h);
-    if (L == 8) {
-        if (nt)
-            hipLaunchKernelGGL((k_spmm_dia_wg<8, true, true, true>), grid, block, 0, h->stream, a);
-        else
-            hipLaunchKernelGGL((k_spmm_dia_wg<8, false, true, true>), grid, block, 0, h->stream, a);
-    } else {
-        if (nt)
-            hipLaunchKernelGGL((k_spmm_dia_wg<16, true, true, true>), grid, block, 0, h->stream, a);
-        else
-            hipLaunchKernelGGL((k_spmm_dia_wg<16, false, true, true>), grid, block, 0, h->stream, a);
-    }
-    return hipGetLastError();
-}
-
-bool dia_cg_fused_available(int L) { return (L == 8 || L == 16) && dia_wg_enabled(); }
-
 std::string dia_kernel_name(const mspmv_handle_s *h, int L)
 {
-    if ((L == 8 || L == 16) && dia_wg_enabled())
-        return "k_spmm_dia_wg<" + std::to_string(L) + "," + (stream_nt(h) ? "true" : "false") + ">";
     return "k_spmm_dia<" + std::to_string(L) + "," + (stream_nt(h) ? "true" : "false") + ">";
 }
 

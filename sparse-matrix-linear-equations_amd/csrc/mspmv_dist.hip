@@ -803,8 +803,6 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
     d->poison_flags = 0;
     // fold tickets: zeroed at every solve's start (a solve that stopped early or faulted may leave some raised)
     D_HIP(hipMemsetAsync(d->d_gtickets, 0, sizeof(unsigned) * d->gtickets_cap, s));
-    if (poison & MSPMV_POISON_FILL)
-        D_HIP(hipMemsetD32Async((hipDeviceptr_t)d->d_gtickets, (int)d->poison_value, d->gtickets_cap, s));
     {
         DistVecArgs a = va;
         a.p = d_B_own;
@@ -814,6 +812,8 @@ static mspmv_status dist_cg_native(mspmv_dist d, const double *d_B_own, double *
         a.red_in = rr;
         D_HIP(launch_dist_vec_mirror(1, a, L, 1, nullptr, s));
     }
+    if (poison & MSPMV_POISON_FILL)  // test hook: the iterations' folds meet dirty tickets (after the init's)
+        D_HIP(hipMemsetD32Async((hipDeviceptr_t)d->d_gtickets, (int)d->poison_value, d->gtickets_cap, s));
     auto iteration = [&]() -> mspmv_status {
         DistVecArgs a = va;
         D_HIP(launch_dist_vec_mirror(2, a, L, nblk, d->d_pext, s));       // p = r + beta p

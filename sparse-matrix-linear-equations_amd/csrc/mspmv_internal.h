@@ -267,6 +267,12 @@ struct mspmv_handle_s {
     // kFault* bits the plain products raise (ticket_arrive: split-row and column-group tickets), read
     // and cleared by mspmv_check_faults (the host-pointer products call it; CG solves use d_ctrl's)
     unsigned *d_fault = nullptr;
+    // The CSR pattern on the host for the plan builders (host_pattern): the caller's arrays while
+    // mspmv_csr_create runs (no copy), else one download shared by every builder of one plan decision and
+    // released after it (PatternScope; ADVICE r05: the window, run and slab builders each copied it)
+    const int *pat_ro_ext = nullptr, *pat_ci_ext = nullptr;
+    std::vector<int> pat_ro, pat_ci;
+    bool pat_scope = false;
     // test hook (mspmv_test_poison_tickets): the next CG solve fills its fold tickets with this value
     unsigned poison_value = 0;
     int poison_flags = 0;  // 0: none pending; MSPMV_POISON_* bits
@@ -298,6 +304,26 @@ struct mspmv_handle_s {
     // mspmv_api.hip dia_decide): -1 not decided yet, 0 no, 1 yes
     int dia = -1;
 };
+
+namespace mspmv {
+// The handle's CSR pattern on the host (see mspmv_handle_s::pat_*): *ro [m + 1], *ci [nnz]
+mspmv_status host_pattern(mspmv_handle_s *h, const int **ro, const int **ci);
+bool host_pattern_resident(const mspmv_handle_s *h);  // available without a download
+// Holds a downloaded pattern for the duration of one plan decision (the outermost scope releases it).
+struct PatternScope {
+    mspmv_handle_s *h;
+    bool own;
+    explicit PatternScope(mspmv_handle_s *hh) : h(hh), own(!hh->pat_scope) { hh->pat_scope = true; }
+    ~PatternScope()
+    {
+        if (own) {
+            h->pat_scope = false;
+            std::vector<int>().swap(h->pat_ro);
+            std::vector<int>().swap(h->pat_ci);
+        }
+    }
+};
+}  // namespace mspmv
 
 // IC(0) factor on the device (mspmv_ic0_create): L and its transpose for the two sync-free
 // triangular solves of the preconditioner apply, their ready flags and the intermediate Y.
@@ -356,11 +382,6 @@ hipError_t launch_dia(mspmv_handle_s *h, const TilePlan &plan, const double *d_X
                       const CgControl *ctrl, double *partials = nullptr, long long row_off = 0,
                       hipStream_t stream = nullptr);
 std::string dia_kernel_name(const mspmv_handle_s *h, int L);
-// The block CG's iteration SpMM with the p update fused (k_spmm_dia_wg: Ap = A p, p = r + beta p_old staged
-// from p_old and r, p's rows to pnew, the deferred x += alpha p_old, p.Ap partials per window); L = 8, 16
-hipError_t launch_dia_cg(mspmv_handle_s *h, const TilePlan &plan, const double *p_old, const double *r, double *pnew,
-                         double *ap, double *x, int L, CgControl *ctrl, const CgScalars *scal, double *partials);
-bool dia_cg_fused_available(int L);
 bool dia_spmm_enabled();  // the L-wide products on the windows too unless MSPMV_DIA_SPMM=0 (mspmv_api.hip)
 // The handle's offset-window plan for width L (decided on first use), or null (mspmv_api.hip)
 mspmv_status dia_plan_for(mspmv_handle_s *h, int L, const TilePlan **out);
@@ -431,6 +452,10 @@ bool supported_L(int L);
 
 // CG pieces
 hipError_t launch_cg_init(mspmv_handle_s *h, const double *d_b, double *d_x, int L, double tol, int nblk);
+// Diagnostic: the plain SpMV's k_spmv_tile in its stamped instantiation (hipErrorNotSupported for plans
+// that run another kernel); d_stamps [num_tiles][6] (mspmv_spmv_tile_stamps)
+hipError_t launch_spmv_tile_stamped(mspmv_handle_s *h, const TilePlan &plan, const double *d_x, double *d_y,
+                                   unsigned long long *d_stamps);
 // splan / dot_fused: the split iteration's plain-product plan and window dot mode, resolved once per
 // solve by cg_solve_native (launch_cg_iteration_split)
 hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, const TilePlan *splan, bool dot_fused,
@@ -456,8 +481,7 @@ void resident_free(ResidentCg *r);
 hipError_t launch_cg_resident(mspmv_handle_s *h, ResidentCg *r, const double *d_b, double *d_x, int max_iters,
                               double tol, unsigned long long *d_stamps = nullptr, int stamp_iters = 0);
 // Split (multi-RHS) CG: the last deferred x += alpha p after the loop (a no-op when none is pending).
-// splan / dot_fused as launch_cg_iteration (the fused form's p alternates buffers).
-hipError_t launch_cg_xflush(mspmv_handle_s *h, double *d_x, int L, int nblk, const TilePlan *splan, bool dot_fused);
+hipError_t launch_cg_xflush(mspmv_handle_s *h, double *d_x, int L, int nblk);
 // Offset (doubles) and count of the partials level a consumer sums: levels of a fan-in
 // kSlotGroup tree are folded while more than `stop` partials would remain.
 inline void consumer_level(int nslots, int stop, int L, long long *off, int *count)

@@ -152,17 +152,19 @@ __device__ __forceinline__ void fold_cols(const double *base, int count, double 
 // One arrival on a fold group's ticket (thread 0 only; ticket_arrive).  A fault also stops a single-GPU
 // solve (done); a sharded one does not (fault_no_stop: the ranks' stop decisions must stay identical, so
 // its host stops on the all-reduced fault word at a batch boundary instead).
+template <bool RELEASE>
 __device__ __forceinline__ bool take_ticket(unsigned *tk, int gsize, CgControl *ctrl)
 {
     bool faulted = false;
-    if (ticket_arrive(tk, (unsigned)gsize - 1, ctrl ? &ctrl->fault : nullptr, &faulted))
+    if (ticket_arrive<RELEASE>(tk, (unsigned)gsize - 1, ctrl ? &ctrl->fault : nullptr, &faulted))
         return true;
     if (faulted && ctrl && !__hip_atomic_load(&ctrl->fault_no_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
         __hip_atomic_store(&ctrl->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return false;
 }
 
-template <int L>
+// RELEASE: the arrivals are agent-scope releases (ticket_arrive; k_fold_dot), else the drained-store form.
+template <int L, bool RELEASE = false>
 __device__ __forceinline__ bool reduce_slots(double *partials, unsigned *tickets, int slot, int nslots,
                                              double *s_tmp, double *s_out, int *s_flag, CgControl *ctrl)
 {
@@ -175,7 +177,7 @@ __device__ __forceinline__ bool reduce_slots(double *partials, unsigned *tickets
         const int gsize = min(kSlotGroup, count - g * kSlotGroup);
         unsigned *tk = &tickets[(size_t)g * kTicketStride];
         if (tid == 0)
-            *s_flag = take_ticket(tk, gsize, ctrl);
+            *s_flag = take_ticket<RELEASE>(tk, gsize, ctrl);
         __syncthreads();
         if (!*s_flag)
             return false;
@@ -242,7 +244,7 @@ __device__ __forceinline__ void publish_partials(double *partials, unsigned *tic
         const int gsize = min(kSlotGroup, count - g * kSlotGroup);
         unsigned *tk = &tickets[(size_t)g * kTicketStride];
         if (tid == 0)
-            *s_flag = take_ticket(tk, gsize, ctrl);
+            *s_flag = take_ticket<false>(tk, gsize, ctrl);
         __syncthreads();
         if (!*s_flag)
             return;
@@ -679,6 +681,7 @@ struct TileArgs {
     // staging (0) -- one dependent round trip fewer per tile (SpmvTuning::early_re)
     int early_re;
     int blk_rows_max;  // node-block plans: the tallest run (TilePlan::blk_rows_max; k_spmm_blk's KR)
+    unsigned long long *stamps;  // k_spmv_tile STAMP (diagnostic): [tile][kTileStamps]
     int tb;            // threads sharing one tile (the plan's lanes: 256, or 64 for one-wave SpMV plans)
     int blk_spmv;      // the plain SpMV runs k_spmv_blk on this plan (TilePlan::blk_spmv; mixed plans too)
     int n;             // columns (x holds n entries)
@@ -1548,7 +1551,12 @@ __device__ __forceinline__ void cg1_publish(const TileArgs &a, SM &sm, int slot,
 // set its VGPR count, so more workgroups fit per CU).
 // FIX: the plan splits rows (close_split_rows); plans that split none -- FEM, CFD, stencils -- run
 // the form without it (fewer SGPRs: 8 workgroups per CU).
-template <int IPT, int MODE, bool NT, int TB = kBlock, bool BLK = true, bool FIX = true>
+// STAMP (diagnostic instantiation only, mspmv_spmv_tile_stamps): thread 0 records wall_clock64() at the
+// tile's phase boundaries into a.stamps[t * kTileStamps + i]: 0 entry, 1 stream and gathers issued, 2 the
+// staged products in LDS (stream and gathers landed), 3 row ends in LDS (after the barrier), 4 rows
+// reduced and stored; slot 5 holds the CU (HW_ID) that ran the tile.
+constexpr int kTileStamps = 6;
+template <int IPT, int MODE, bool NT, int TB = kBlock, bool BLK = true, bool FIX = true, bool STAMP = false>
 __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
 {
     static_assert(TB == kBlock || MODE == kModeSpmv, "one-wave tiles run the plain SpMV only");
@@ -1560,6 +1568,19 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
     // CG: stop flag loaded now, tested after the stream and gathers are issued (see k_spmm_tile)
     const int stopped = (MODE != kModeSpmv || a.ctrl) ? a.ctrl->done : 0;  // MODE 0: a CG's plain SpMM
     const int t = xcd_tile(blockIdx.x, a.num_tiles);
+    auto stamp = [&](int i) {
+        if constexpr (STAMP) {
+            if (tid == 0) {
+                if (i == 0) {
+                    unsigned hw;
+                    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+                    a.stamps[(size_t)t * kTileStamps + 5] = hw;
+                }
+                a.stamps[(size_t)t * kTileStamps + i] = wall_clock64();
+            }
+        }
+    };
+    stamp(0);
     const int2 b0 = a.bounds[t];
     const int2 b1 = a.bounds[t + 1];
     const int r0 = b0.x, n0 = b0.y;
@@ -1634,6 +1655,7 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
         constexpr int NP = (TILE / TB + W - 1) / W;
         GroupRegs<NP, W> st;
         group_issue<NP, W, NT, TB>(a, n0, nnzt, colbase, 0, st);
+        stamp(1);
         head();
         if (go) {
             group_store<NP, W, TB>(st, n0, nnzt, 0, sm.prod);
@@ -1646,6 +1668,7 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
     } else if (nnzt > 0 && nnzt <= TILE) {  // the common case: no snapped-in extra nonzeros
         StageRegs<IPT, CG> st;
         stage_issue<IPT, CG, NT, TB>(a, n0, nnzt, colbase, st);
+        stamp(1);
         head();
         if (go)
             stage_store<IPT, CG, TB>(st, nnzt, beta, sm.prod);
@@ -1660,6 +1683,10 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
     }
     if (!go)
         return;
+    if constexpr (STAMP) {  // the staged products' stores are out (LDS): stamp after they complete
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        stamp(2);
+    }
     // Row ends: issued with the stream by default (TileArgs::early_re; with the pair staging 1-2 %
     // faster, r03ah/r03ai -- with the old striped staging it had measured +0.9 us on pwtk), or here.
     int *rend = sm.rowend(nnzt);
@@ -1673,10 +1700,15 @@ __global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
             rend[i] = a.row_offsets[r0 + 1 + i] - n0;
     }
     tile_sync<TB>();
+    stamp(3);
     double dot = 0.0;
     double xr, pr;
     row_operands<MODE>(a, r0, nrows, xr, pr);
     reduce_tile<IPT, MODE, TB, FIX>(a, sm, t, r0, n0, nrows, nnzt, a.rmode[t], a.split[t + 1] != 0, beta, dot, xr, pr);
+    if constexpr (STAMP) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rows' stores have left
+        stamp(4);
+    }
     if constexpr (FIX)
         close_split_rows<TB>(a, t, fx, 1, 1);
     if constexpr (MODE == kModeCg) {
@@ -2465,7 +2497,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_dot(const double *part, int T, 
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    if (!reduce_slots<L>(lvl, tickets, blockIdx.x, gridDim.x, s_tmp, s_out, &s_last, ctrl))
+    if (!reduce_slots<L, true>(lvl, tickets, blockIdx.x, gridDim.x, s_tmp, s_out, &s_last, ctrl))
         return;
     if (tid < L) {
         const double d = s_out[tid];
@@ -2852,12 +2884,10 @@ __global__ __launch_bounds__(kBlock) void k_dist_pupdate(CgVecArgs a, double *p)
 // once, and a stop in the fold (every column converged or broken) follows a p update that applied
 // the term and a fold that cleared the flag.
 template <int L>
-__global__ __launch_bounds__(kBlock) void k_cg_xflush(CgVecArgs a, const double *p, const double *p_odd)
+__global__ __launch_bounds__(kBlock) void k_cg_xflush(CgVecArgs a, const double *p)
 {
     if (!a.ctrl->x_pending)
         return;
-    if (p_odd && (a.ctrl->iter & 1))  // fused p update: iteration i wrote its p to buffer (i + 1) & 1
-        p = p_odd;
     const long long stride = (long long)gridDim.x * kBlock;
     for (long long i = (long long)blockIdx.x * kBlock + threadIdx.x; i < a.n_elems; i += stride)
         a.x[i] = a.x[i] + a.scal[L == 1 ? 0 : (int)(i % L)].alpha * p[i];
@@ -3464,6 +3494,28 @@ static hipError_t launch_tile(const TileArgs &a, int L, hipStream_t s, bool nt)
     return hipGetLastError();
 }
 
+// Diagnostic: the plain single-RHS SpMV of a plan that runs k_spmv_tile on 256-thread workgroups, in its
+// stamped instantiation (mspmv_spmv_tile_stamps).  hipErrorNotSupported for plans that run another kernel.
+hipError_t launch_spmv_tile_stamped(mspmv_handle_s *h, const TilePlan &plan, const double *d_x, double *d_y,
+                                   unsigned long long *d_stamps)
+{
+    TileArgs a = make_args(h, plan, d_x, d_y, 1);
+    if (a.blk_spmv || a.tb == 64 || plan.dia || plan.slab)
+        return hipErrorNotSupported;
+    a.stamps = d_stamps;
+    const dim3 grid(a.num_tiles), block(kBlock);
+    if (plan.num_tiles == 0)
+        return hipSuccess;
+    const bool nt = stream_nt(h);
+    if (!a.fix)
+        nt ? ggl(k_spmv_tile<kSpmvIpt, kModeSpmv, true, kBlock, true, false, true>, grid, block, h->stream, a)
+           : ggl(k_spmv_tile<kSpmvIpt, kModeSpmv, false, kBlock, true, false, true>, grid, block, h->stream, a);
+    else
+        nt ? ggl(k_spmv_tile<kSpmvIpt, kModeSpmv, true, kBlock, true, true, true>, grid, block, h->stream, a)
+           : ggl(k_spmv_tile<kSpmvIpt, kModeSpmv, false, kBlock, true, true, true>, grid, block, h->stream, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_spmm_tile_only(mspmv_handle_s *h, const TilePlan &plan, const double *d_X, double *d_Y, int L,
                                  int ld)
 {
@@ -3797,16 +3849,12 @@ bool dia_dot_fused()
 // splan: the plan the solve chose for the plain L-wide product (cg_solve_native: the offset-window or
 // column-slab plan, else null -> the tiles of `plan`); dot_fused: the window SpMM takes p.Ap in its dot
 // mode (resolved once per solve, and part of the CG graph's key).
-// Fused form (offset windows in dot mode, L = 8 / 16): the p update runs inside the window SpMM
-// (launch_dia_cg), p alternating between d_p0 and d_p1 by iteration parity -- three launches per
-// iteration (SpMM, fold, update) instead of four.
-static bool cg_split_pupd_fused(const TilePlan *splan, bool dot_fused, int L)
-{
-    return splan && splan->dia && dot_fused && dia_cg_fused_available(L);
-}
-
+// The p update stays its own pass: fused into the window SpMM (the spans staged as r + beta p_old, the
+// window's own rows written to a second p buffer) it measured 0.773-0.779 against 0.657-0.658 ms per
+// configs[4] iteration (r06c): the SpMM then loads r's spans beside p's -- nine times per row through L2
+// -- which costs the issue-bound kernel more than the pass it replaces.
 static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &plan, const TilePlan *splan,
-                                            bool dot_fused, double *d_x, int L, int parity, int nblk, double tol)
+                                            bool dot_fused, double *d_x, int L, int nblk, double tol)
 {
     CgVecArgs va{};
     va.n_elems = (long long)h->m * L;
@@ -3827,20 +3875,8 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
         const char *e = getenv("MSPMV_CG_REV");
         return e ? atoi(e) : 1;
     }();
-    hipError_t e;
-    if (cg_split_pupd_fused(splan, dot_fused, L)) {
-        double *pold = parity ? h->d_p1 : h->d_p0, *pnew = parity ? h->d_p0 : h->d_p1;
-        if ((e = launch_dia_cg(h, *splan, pold, h->d_r, pnew, h->d_ap, d_x, L, h->d_ctrl, h->d_scal, h->d_partials)) !=
-            hipSuccess)
-            return e;
-        if ((e = launch_fold_dot(splan->num_tiles, L, h->d_partials, h->d_gtickets, h->d_red, h->d_scal, h->d_conv,
-                                 h->d_ctrl, -1, h->stream)) != hipSuccess)
-            return e;
-        va.red_in = h->d_red;
-        return dispatch_vec(false, va, L, nblk, h->stream);
-    }
     va.rev = rev;  // the p update (after the forward update) sweeps backwards
-    e = launch_dist_vec(2, va, L, nblk, h->d_p0, h->stream);
+    hipError_t e = launch_dist_vec(2, va, L, nblk, h->d_p0, h->stream);
     va.rev = 0;
     if (e != hipSuccess)
         return e;
@@ -3887,22 +3923,20 @@ static hipError_t launch_cg_iteration_split(mspmv_handle_s *h, const TilePlan &p
     return dispatch_vec(false, va, L, nblk, h->stream);
 }
 
-// After the split iteration's loop: the x += alpha p still pending (CgVecArgs::lazy_x).  The fused
-// form's last p is in d_p0 or d_p1 by the iteration count's parity (chosen on the device).
-hipError_t launch_cg_xflush(mspmv_handle_s *h, double *d_x, int L, int nblk, const TilePlan *splan, bool dot_fused)
+// After the split iteration's loop: the x += alpha p still pending (CgVecArgs::lazy_x).
+hipError_t launch_cg_xflush(mspmv_handle_s *h, double *d_x, int L, int nblk)
 {
-    const double *p_odd = cg_split_pupd_fused(splan, dot_fused, L) ? h->d_p1 : nullptr;
     CgVecArgs va{};
     va.n_elems = (long long)h->m * L;
     va.x = d_x;
     va.scal = h->d_scal;
     va.ctrl = h->d_ctrl;
     switch (L) {
-    case 1: hipLaunchKernelGGL((k_cg_xflush<1>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0, p_odd); break;
-    case 2: hipLaunchKernelGGL((k_cg_xflush<2>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0, p_odd); break;
-    case 4: hipLaunchKernelGGL((k_cg_xflush<4>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0, p_odd); break;
-    case 8: hipLaunchKernelGGL((k_cg_xflush<8>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0, p_odd); break;
-    case 16: hipLaunchKernelGGL((k_cg_xflush<16>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0, p_odd); break;
+    case 1: hipLaunchKernelGGL((k_cg_xflush<1>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
+    case 2: hipLaunchKernelGGL((k_cg_xflush<2>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
+    case 4: hipLaunchKernelGGL((k_cg_xflush<4>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
+    case 8: hipLaunchKernelGGL((k_cg_xflush<8>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
+    case 16: hipLaunchKernelGGL((k_cg_xflush<16>), dim3(nblk), dim3(kBlock), 0, h->stream, va, h->d_p0); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -3923,7 +3957,7 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, const Ti
                                double *d_x, int L, int parity, int nblk, double tol)
 {
     if (cg_split_iteration(L))
-        return launch_cg_iteration_split(h, plan, splan, dot_fused, d_x, L, parity, nblk, tol);
+        return launch_cg_iteration_split(h, plan, splan, dot_fused, d_x, L, nblk, tol);
     double *rp_old = parity ? h->d_p1 : h->d_p0;  // {r_k, p_{k-1}} interleaved (cg_rp)
     double *rp_new = parity ? h->d_p0 : h->d_p1;  // receives p_k, then r_{k+1}
     TileArgs ta = make_args(h, plan, rp_old, h->d_ap, 1);

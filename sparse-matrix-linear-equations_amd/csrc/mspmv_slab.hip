@@ -78,7 +78,7 @@ __device__ __forceinline__ void group_out(const SlabArgs &a, int b, int r0, int 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this group's partials are out
     __syncthreads();
     if (tid == 0)
-        s_last = ticket_arrive(&a.gcnt[rb], (unsigned)(G - 1), a.fault);
+        s_last = ticket_arrive<false>(&a.gcnt[rb], (unsigned)(G - 1), a.fault);
     __syncthreads();
     if (!s_last)
         return;

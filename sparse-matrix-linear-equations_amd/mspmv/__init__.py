@@ -84,6 +84,7 @@ _SIGS = {
     "mspmv_setup_ms": (_D, [_P]),
     "mspmv_sync": (_I, [_P]),
     "mspmv_check_faults": (_I, [_P]),
+    "mspmv_spmv_tile_stamps": (_I, [_P, _P, _P, ctypes.c_size_t, _P, _PI]),
     "mspmv_test_poison_tickets": (_I, [_P, ctypes.c_uint, _I]),
     "mspmv_dist_test_poison_tickets": (_I, [_P, ctypes.c_uint, _I]),
     "mspmv_set_cu_limit": (_I, [_P, _I]),
@@ -467,6 +468,16 @@ class GpuCsr:
 
     def sync(self):
         _check(lib.mspmv_sync(self.h), "sync")
+
+    def spmv_tile_stamps(self, dX: "DeviceBuffer", dY: "DeviceBuffer", flush_bytes: int = 0) -> np.ndarray:
+        """mspmv_spmv_tile_stamps: per-tile wall_clock64() phase stamps of one plain SpMV, [tiles][6]
+        (flush_bytes > 0: after the cold protocol's read sweep)."""
+        nt = ctypes.c_int()
+        _check(lib.mspmv_spmv_tile_stamps(self.h, None, None, 0, None, ctypes.byref(nt)), "spmv_tile_stamps")
+        st = np.zeros((max(nt.value, 1), 6), np.uint64)
+        _check(lib.mspmv_spmv_tile_stamps(self.h, dX.ptr, dY.ptr, flush_bytes, _ptr(st), ctypes.byref(nt)),
+               "spmv_tile_stamps")
+        return st[: nt.value]
 
     def check_faults(self):
         """mspmv_check_faults: raises MspmvError(FAULT) if a product since the last check drew a ticket

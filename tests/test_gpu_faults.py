@@ -96,11 +96,11 @@ def test_poisoned_tickets_dist(orc, monkeypatch, value):
 @pytest.mark.parametrize("value", [32, 0x7FFFFFFF])
 def test_dirty_tickets_mechanism(orc, monkeypatch, value, capsys):
     """Round 5's failure, made deterministic: the sharded CG at L = 3 on the windows with its fold
-    tickets dirty for the FIRST iteration only (filled, then zeroed right after the first iteration is
-    enqueued -- the unordered memset landing late) and the guard recording instead of stopping.  The
-    solve then runs to its own stop test with a wrong iteration count or history (one stale or
-    partial p.Ap, b.b and r.r fold in that iteration: CG loses conjugacy and recovers slowly), and the
-    fault word is what reports it."""
+    tickets dirty for the FIRST iteration only (filled after the init, zeroed right after the first
+    iteration is enqueued -- the unordered memset landing late) and the guard recording instead of
+    stopping.  No fold of that iteration completes, so its alpha comes from a stale p.Ap and its stop
+    test and beta from a stale r.r (the init's b.b); CG loses conjugacy and recovers slowly, running to
+    its own stop test with a wrong iteration count or history -- and the fault word reports it."""
     import mspmv
     monkeypatch.delenv("MSPMV_DIA", raising=False)
     a = _stencil()

@@ -41,6 +41,11 @@ def full_cases():
         "nlpkkt120": lambda: mspmv.CsrMatrix.synth_stencil(1, 160 * 135 * 164, 160, 135, 164, diag_shift=1e-2),
         # SURVEY 8(d)'s skewed variant, bench.py's spmv_shapes power-law leg (the sliced-ELL SpMV)
         "powerlaw": lambda: mspmv.CsrMatrix.synth_powerlaw(PWTK["m"], PWTK["m"], PWTK["nnz"], 1.2, 3),
+        # bench.py's window_shapes legs (round 6): the nlpkkt120-size stencil with off-pattern columns (the
+        # windows plus a remainder) and the KKT saddle point of nlpkkt120's block structure (34 offsets)
+        "stencil27_perturbed": lambda: mspmv.CsrMatrix.synth_stencil_perturbed(
+            (160, 135, 164), seed=5, diag_shift=1e-2, extra_frac=0.01, long_frac=0.001),
+        "kkt": lambda: mspmv.CsrMatrix.synth_kkt((120, 120, 123), seed=6, eps=1e-2),
     }
 
 
@@ -55,6 +60,9 @@ def test_spmv_full_size(orc, name):
         if name == "powerlaw":
             assert g.kernel_name().startswith("k_spmv_sell<"), g.kernel_name()
             assert y.tobytes() == g.spmv(x).tobytes()  # fixed order: repeats bit-identical
+        if name in ("stencil27_perturbed", "kkt"):  # both on the offset windows
+            assert g.kernel_name().startswith("k_spmm_dia<1,"), g.kernel_name()
+            assert y.tobytes() == g.spmv(x).tobytes()
 
 
 @pytest.mark.parametrize("name", ["cant", "pwtk"])

@@ -1,7 +1,8 @@
 """Offset-window planning on the host (mspmv_offset_windows; csrc/mspmv_dia.hip dia_plan_host), no GPU:
 the library's decision, per-window offset counts and remainder against a numpy restatement of the rules
-(round 6, windows plus a remainder) -- 64-row windows; every row's columns strictly ascending; a window
-keeps the offsets col - row that >= min(8, its rows) of its rows hold, the 64 most frequent (ties: the
+(round 6, windows plus a remainder) -- 64-row windows; every row's columns strictly ascending; first
+every window keeping its whole offset list with no remainder (the exact plan), else a window keeps the
+offsets col - row that >= min(8, its rows) of its rows hold, the 64 most frequent (ties: the
 smaller offset), and drops its rarest kept offsets while they fill < min_window_fill of rows x K; every
 other entry is remainder; the plan holds when sum K > 0, the kept entries fill >= min_fill x 64 x sum K
 and the remainder is <= 5 % of the nonzeros (any share when min_fill is 0); a window is masked when some
@@ -15,13 +16,20 @@ from test_gpu_dia import band
 
 
 def restate(a, min_fill=0.85, min_window_fill=0.3, kmax=64, keep_rows=8, max_rem=0.05):
+    """Two passes, as dia_plan_host: every window's whole offset list (no remainder allowed), then the
+    frequency rule with the remainder."""
+    if min_fill <= 0:
+        max_rem = 1.0
+    return (restate_pass(a, min_fill, min_window_fill, kmax, 1, 0.0, True)
+            or restate_pass(a, min_fill, min_window_fill, kmax, keep_rows, max_rem, False))
+
+
+def restate_pass(a, min_fill, min_window_fill, kmax, keep_rows, max_rem, exact):
     m = a.num_rows
     ro = a.row_offsets.astype(np.int64)
     ci = a.column_indices.astype(np.int64)
     if m == 0 or a.num_nonzeros == 0:
         return None
-    if min_fill <= 0:
-        max_rem = 1.0
     ks, masked, kept_total = [], 0, 0
     for r0 in range(0, m, 64):
         r1 = min(m, r0 + 64)

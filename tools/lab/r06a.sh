@@ -25,3 +25,5 @@ for i in 1 2; do
     echo "$v $i $(python -c "import json;d=json.load(open('$OUT/cg_multi_${v}_$i.json'));print(d['ms_per_iter'],d['roofline_frac'],d['iterations'],d['spmv_nlpkkt120_size']['kernel_ms'])") $(python -c "import json;d=json.load(open('$OUT/head_${v}_$i.json'));print(d['roofline']['frac'])") $(python -c "import json;d=json.load(open('$OUT/spmv_shapes_${v}_$i.json'));print(d['powerlaw']['frac'], d['cant']['frac'], d['rma10']['frac'])" | cut -c1-80)"
   done
 done
+timeout -k 10 300 python tools/tile_stamps.py > $OUT/tile_stamps.jsonl 2>$OUT/tile_stamps.err || { echo "stamps rc=$?"; tail -3 $OUT/tile_stamps.err; exit 1; }
+echo stamps done
