@@ -333,6 +333,8 @@ mspmv_status plan_split_rows(TilePlan &p, const std::vector<int2> &hb, const std
 }
 }  // namespace mspmv
 
+constexpr int kSpmvMinFillTile = 512;  // the smallest tile the one-generation fill cuts (merge items)
+
 static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes,
                                const std::vector<int2> *fixed)
 {
@@ -354,7 +356,19 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         // close_split_rows).  (Measured against nominal tiles in round 3: kept.)
         const long long slots = (long long)h->num_cus * spmv_tile_blocks_per_cu();
         const long long t0 = (total + tile - 1) / tile;
-        if (slots > 0 && t0 > slots) {
+        static const bool fill = [] {  // lab (r06e A/B): MSPMV_SPMV_FILL=0 keeps nominal tiles below one generation
+            const char *e = getenv("MSPMV_SPMV_FILL");
+            return !(e && *e && atoi(e) == 0);
+        }();
+        if (fill && slots > 0 && t0 < slots && total >= slots * (long long)kSpmvMinFillTile) {
+            // Fewer tiles than one generation of slots (cant: 1,988 on 2,048; rma10: 1,183): the matrix runs
+            // as ONE generation whose time is the slowest CU's share, and a CU holding 5 nominal tiles
+            // where the mean is 4.6 sets it.  Cut the path into exactly one tile per slot instead -- every
+            // CU the same share, every slot a workgroup of loads in flight (tools/tile_stamps.py: these
+            // kernels are single-generation, bound by their tiles' stream-and-gather latency).
+            step = (int)((total + slots - 1) / slots);
+            snap = std::max(16, step / kSnapDiv);
+        } else if (slots > 0 && t0 > slots) {
             const long long fewer = (t0 + slots - 1) / slots - 1;  // generations after stretching
             const long long fit = (total + fewer * slots - 1) / (fewer * slots);
             if (fit + 16 <= tile + tile / kSnapDiv) {

@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""CGSolveSingle on bench.py's pwtk-size SPD matrix (27-point stencil, 427,500 rows, 11.2 M nonzeros: too
+large for the register-resident kernel): us per iteration (best of 5 solves after a warm one) of the form
+the environment selects (MSPMV_CG_RESIDENT=0: the two-kernel pipelined form; MSPMV_CG_SPLIT=1: the
+multi-RHS split iteration at L = 1, on the offset windows).  One JSON line."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "sparse-matrix-linear-equations_amd")]
+import mspmv  # noqa: E402
+from bench import CG_LARGE, glibc_rhs  # noqa: E402
+
+nx, ny, nz = CG_LARGE["dims"]
+a = mspmv.CsrMatrix.synth_stencil(1, nx * ny * nz, nx, ny, nz, seed=9, diag_shift=CG_LARGE["shift"])
+n = a.num_rows
+b = glibc_rhs(42, n)
+thr = float(np.sqrt(np.sum(b * b)) * 1e-5)
+out = {"env": {k: v for k, v in os.environ.items() if k.startswith("MSPMV_")}}
+with mspmv.GpuCsr(a) as g:
+    db, dx = mspmv.DeviceBuffer.from_array(b), mspmv.DeviceBuffer(8 * n)
+    g.cg_dev(db, dx, 1, 10000, thr)
+    best = None
+    for _ in range(5):
+        t0 = time.perf_counter()
+        it, _, st = g.cg_dev(db, dx, 1, 10000, thr)
+        el = time.perf_counter() - t0
+        best = el / it if best is None else min(best, el / it)
+    out.update(kernel=g.cg_kernel_name(), spmv_kernel=g.kernel_name(), iterations=it, status=st,
+               us_per_iter=round(best * 1e6, 3))
+print(json.dumps(out), flush=True)
