@@ -333,8 +333,6 @@ mspmv_status plan_split_rows(TilePlan &p, const std::vector<int2> &hb, const std
 }
 }  // namespace mspmv
 
-constexpr int kSpmvMinFillTile = 512;  // the smallest tile the one-generation fill cuts (merge items)
-
 static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, int lanes,
                                const std::vector<int2> *fixed)
 {
@@ -356,19 +354,9 @@ static mspmv_status build_plan(mspmv_handle_s *h, int L, const TilePlan **out, i
         // close_split_rows).  (Measured against nominal tiles in round 3: kept.)
         const long long slots = (long long)h->num_cus * spmv_tile_blocks_per_cu();
         const long long t0 = (total + tile - 1) / tile;
-        static const bool fill = [] {  // lab (r06e A/B): MSPMV_SPMV_FILL=0 keeps nominal tiles below one generation
-            const char *e = getenv("MSPMV_SPMV_FILL");
-            return !(e && *e && atoi(e) == 0);
-        }();
-        if (fill && slots > 0 && t0 < slots && total >= slots * (long long)kSpmvMinFillTile) {
-            // Fewer tiles than one generation of slots (cant: 1,988 on 2,048; rma10: 1,183): the matrix runs
-            // as ONE generation whose time is the slowest CU's share, and a CU holding 5 nominal tiles
-            // where the mean is 4.6 sets it.  Cut the path into exactly one tile per slot instead -- every
-            // CU the same share, every slot a workgroup of loads in flight (tools/tile_stamps.py: these
-            // kernels are single-generation, bound by their tiles' stream-and-gather latency).
-            step = (int)((total + slots - 1) / slots);
-            snap = std::max(16, step / kSnapDiv);
-        } else if (slots > 0 && t0 > slots) {
+        // Below one generation (cant: 1,988 tiles on 2,048 slots; rma10: 1,183) the nominal tiles stay: cut
+        // into exactly one tile per slot they measured the same (r06e).
+        if (slots > 0 && t0 > slots) {
             const long long fewer = (t0 + slots - 1) / slots - 1;  // generations after stretching
             const long long fit = (total + fewer * slots - 1) / (fewer * slots);
             if (fit + 16 <= tile + tile / kSnapDiv) {
@@ -1591,15 +1579,18 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
     if (h->m == 0)
         return MSPMV_OK;
     const TilePlan *plan = nullptr, *mplan = nullptr, *splan = nullptr;
-    ST_TRY(get_plan(h, L, &plan));
-    if (!hm && !ic && cg_split_iteration(L)) {
+    if (!hm && !ic) {
         // the split iteration's plain SpMM runs on the handle's offset-window or column-slab plan when
-        // the plain product takes one: decided here, before any graph capture (it may copy the matrix to
-        // the host); launch_cg_iteration_split finds it by the handle's decisions
+        // the plain product takes one, the pipelined single-RHS iteration's SpMV on its offset windows
+        // (k_cg1_dia): decided here, before any graph capture (it may copy the matrix to the host)
         ST_TRY(get_plan(h, L, &splan, true));
-        if (!splan->slab && !splan->dia)
+        if (!(splan->dia || (splan->slab && cg_split_iteration(L))))
             splan = nullptr;
     }
+    if (splan && splan->dia && !cg_split_iteration(L))
+        plan = splan;  // the pipelined form on the windows needs no merge tiles
+    else
+        ST_TRY(get_plan(h, L, &plan));
     const bool dot_fused = dia_dot_fused();  // once per solve (an environment switch; in the graph key)
     if (hm) {
         ST_TRY(get_plan(hm, L, &mplan));
@@ -1629,8 +1620,10 @@ static mspmv_status cg_solve_native(mspmv_handle_s *h, const double *d_b, double
             stalled = true;
         }
     }
-    h->last_cg_kernel = pipelined ? (stalled ? "pipelined (k_spmv_tile MODE 1 + k_cg1_update) after a resident-CG stall"
-                                             : "pipelined (k_spmv_tile MODE 1 + k_cg1_update)")
+    const bool on_windows = pipelined && splan && splan->dia;
+    h->last_cg_kernel = pipelined ? std::string(on_windows ? "pipelined (k_cg1_dia + k_cg1_update)"
+                                                           : "pipelined (k_spmv_tile MODE 1 + k_cg1_update)") +
+                                        (stalled ? " after a resident-CG stall" : "")
                         : hm      ? "SPAI-PCG (split)"
                         : ic      ? "IC0-PCG (split)"
                                   : "split (p update, SpMM, p.Ap, update)";

@@ -133,4 +133,186 @@ __device__ __forceinline__ void close_split_rows(const A &a, int t, int4 fx, int
     }
 }
 
+// ---- cross-workgroup sums shared by the tile kernels and the offset windows' CG (mspmv_dia.hip) ----
+// Lane 0 of each wave holds a deterministic butterfly sum; wave totals are combined in
+// wave order.  Call uniformly from every thread of the block; returns the total in all.
+__device__ __forceinline__ double block_sum(double v, double *s_red)
+{
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        v += __shfl_xor(v, off);
+    __syncthreads();  // s_red may still be read by a previous call
+    if ((threadIdx.x & 63) == 0)
+        s_red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    double t = s_red[0];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w)
+        t += s_red[w];
+    return t;
+}
+
+// Sum of column j over rows q, q + kBlock/L, ... < count of a [count][L] array written by
+// other workgroups (agent-scope loads), in row order; eight loads in flight per batch.
+template <int L>
+__device__ __forceinline__ double fold_col_strided(const double *base, int count, int j, int q)
+{
+    constexpr int TPC = kBlock / L;
+    double v = 0.0;
+    int i = q;
+    for (; i + 7 * TPC < count; i += 8 * TPC) {
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            t[u] = load_sc1(&base[(size_t)(i + u * TPC) * L + j]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            v += t[u];
+    }
+    for (; i < count; i += TPC)
+        v += load_sc1(&base[(size_t)i * L + j]);
+    return v;
+}
+
+// Column totals of a [count][L] partials array in a fixed order (per-thread strided rows,
+// then threads in order) -> s_out[0..L).  Call uniformly from every thread.
+template <int L>
+__device__ __forceinline__ void fold_cols(const double *base, int count, double *s_tmp, double *s_out)
+{
+    constexpr int TPC = kBlock / L;
+    const int tid = threadIdx.x;
+    s_tmp[tid] = fold_col_strided<L>(base, count, tid % L, tid / L);
+    __syncthreads();
+    if (tid < L) {
+        double w = s_tmp[tid];
+        for (int u = 1; u < TPC; ++u)
+            w += s_tmp[u * L + tid];
+        s_out[tid] = w;
+    }
+    __syncthreads();
+}
+
+// One arrival on a fold group's ticket (thread 0 only; ticket_arrive).  A fault also stops a single-GPU
+// solve (done); a sharded one does not (fault_no_stop: the ranks' stop decisions must stay identical, so
+// its host stops on the all-reduced fault word at a batch boundary instead).
+template <bool RELEASE>
+__device__ __forceinline__ bool take_ticket(unsigned *tk, int gsize, CgControl *ctrl)
+{
+    bool faulted = false;
+    if (ticket_arrive<RELEASE>(tk, (unsigned)gsize - 1, ctrl ? &ctrl->fault : nullptr, &faulted))
+        return true;
+    if (faulted && ctrl && !__hip_atomic_load(&ctrl->fault_no_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        __hip_atomic_store(&ctrl->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+}
+
+// Consumer-side reduction (single-RHS pipelined CG).  A producer kernel leaves one partial per
+// workgroup; EVERY workgroup of the consumer kernel sums them itself, in one fixed order (thread
+// tid adds elements tid, tid + 256, ... ascending, then block_sum's fixed tree), so all agree
+// bit for bit and no ticket chain sits in the producer's tail.  The loads are issued early
+// (part_load) and summed late (part_sum), under the consumer's own streaming loads.
+template <int NR>
+struct PartRegs {
+    double v[NR];
+};
+template <int NR>
+__device__ __forceinline__ void part_load(const double *p, int n, PartRegs<NR> &r)
+{
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+        const int i = (int)threadIdx.x + j * kBlock;
+        r.v[j] = i < n ? p[i] : 0.0;
+    }
+}
+template <int NR>
+__device__ __forceinline__ double part_sum(const PartRegs<NR> &r, double *s_red)
+{
+    double v = r.v[0];
+#pragma unroll
+    for (int j = 1; j < NR; ++j)
+        v += r.v[j];
+    return block_sum(v, s_red);
+}
+
+// Publish this workgroup's partial (already stored at partials[slot], agent scope, vmcnt
+// drained, block synchronised) for a consumer kernel that sums at most `stop` of them: while
+// more would remain, groups of kSlotGroup are folded into the next level by their last arriver
+// (reduce_slots' tickets), down to the level consumer_level() names.
+template <int L>
+__device__ __forceinline__ void publish_partials(double *partials, unsigned *tickets, int slot, int nslots, int stop,
+                                                 double *s_tmp, double *s_out, int *s_flag, CgControl *ctrl)
+{
+    const int tid = threadIdx.x;
+    double *lvl = partials;
+    int idx = slot, count = nslots;
+    while (count > stop) {
+        const int g = idx / kSlotGroup;
+        const int ngroups = (count + kSlotGroup - 1) / kSlotGroup;
+        const int gsize = min(kSlotGroup, count - g * kSlotGroup);
+        unsigned *tk = &tickets[(size_t)g * kTicketStride];
+        if (tid == 0)
+            *s_flag = take_ticket<false>(tk, gsize, ctrl);
+        __syncthreads();
+        if (!*s_flag)
+            return;
+        fold_cols<L>(lvl + (size_t)g * kSlotGroup * L, gsize, s_tmp, s_out);
+        if (tid == 0)
+            __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        double *next = lvl + (size_t)count * L;
+        if (tid < L) {
+            store_sc1(&next[(size_t)g * L + tid], s_out[tid]);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        tickets += (size_t)ngroups * kTicketStride;
+        lvl = next;
+        idx = g;
+        count = ngroups;
+    }
+}
+
+// Pipelined single-RHS CG, head of iteration k (MODE 1).  Every workgroup sums the previous
+// update's r.r partials itself (rs_k; at k = 0 the init's b.b), so the stop test and beta need
+// no ticket chain: the reference's check after iteration k-1 (single_strategy.hpp:150-156:
+// sqrt(rs_new)/||b|| < tol -> iterations = k) is taken here, then beta = rs_k / rs_{k-1}
+// (:158-160).  Workgroup 0 records the history and hands rs_k and k+1 on by parity.  Returns
+// false when the solve has stopped (converged): the caller returns at once.
+template <typename A>  // TileArgs (k_spmv_tile, k_spmv_blk) or Cg1DiaArgs (k_cg1_dia)
+__device__ __forceinline__ bool cg1_head(const A &a, double rs, double &beta)
+{
+    CgScalars &s = a.scal[0];
+    CgControl *c = a.ctrl;
+    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+    const int k = c->iter_par[a.parity];
+    if (k == 0) {  // r = p = b: no stop test before the first iteration
+        beta = 0.0;
+        if (lead) {
+            const double bn = sqrt(rs);
+            s.b_norm = bn == 0.0 ? 1.0 : bn;  // single_strategy.hpp:124-129
+            s.rs_par[0] = rs;
+            c->iter_par[1] = 1;
+        }
+        return true;
+    }
+    const double rel = sqrt(rs) / s.b_norm;
+    if (lead) {
+        if (a.hist && k - 1 < a.hist_cap)
+            a.hist[k - 1] = rel;
+        c->iter = k;
+    }
+    if (rel < a.tol) {
+        if (lead) {
+            c->iters_out = k;
+            c->done = 1;
+        }
+        return false;
+    }
+    beta = rs / s.rs_par[a.parity ^ 1];
+    if (lead) {
+        s.rs_par[a.parity] = rs;
+        c->iter_par[a.parity ^ 1] = k + 1;
+    }
+    return true;
+}
+
 }  // namespace mspmv

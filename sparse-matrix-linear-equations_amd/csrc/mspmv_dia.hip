@@ -349,6 +349,199 @@ k_spmm_dia(DiaArgs a)
     }
 }
 
+// ---- pipelined single-RHS CG on the offset windows -----------------------------------------------
+// The two-kernel pipelined CG (mspmv_kernels.hip: [SpMV MODE 1] -> [k_cg1_update]) with its SpMV on the
+// windows instead of the merge tiles, for the single-RHS matrices the register-resident kernel does not
+// hold: a 27-point stencil of pwtk's size runs the plain product in 20 us on the windows against 60 us on
+// the tiles, and the tiles' CG form took 78 us (r06f).  One launch of iteration k:
+//  * head: every workgroup sums the update's <= kUpdateMaxBlocks r.r partials in one fixed order
+//    (part_sum), so all take the same stop test and beta = rs_k / rs_{k-1} (cg1_head; no ticket chain);
+//  * products: x = p_k = r_k + beta p_{k-1}, formed at each load from the {r, p_{k-1}} pair (cg_rp: one
+//    16-B load per lane, contiguous across the window's rows) -- UpdatePSingle fused into the SpMV as the
+//    tile form does -- summed per row in D order then the remainder, as k_spmm_dia<1>;
+//  * own rows: p_k stored into the next {r, p} buffer's p slot, Ap, and the deferred x += alpha_{k-1}
+//    p_{k-1} (cg1_lag_*: alpha from scal[0].alpha, p_{k-1} the pair's second element);
+//  * one p.Ap partial per workgroup (its four windows' rows by wave butterflies, then waves in order),
+//    summed by k_cg1_update -- folded by group tickets first only beyond kConsumeTile workgroups.
+struct Cg1DiaArgs {
+    const double *rp;  // {r_k, p_{k-1}} interleaved
+    double *rp_new;    // receives p_k at the odd slots (k_cg1_update then writes r_{k+1} at the even ones)
+    double *xsol;
+    double *ap;
+    CgScalars *scal;
+    CgControl *ctrl;
+    const double *part_in;  // the update's (or init's) r.r partials
+    int n_part_in;
+    double *partials;       // [groups] p.Ap partials (+ fold levels beyond kConsumeTile)
+    unsigned *gtickets;
+    int parity;
+    double tol;
+    double *hist;
+    int hist_cap;
+};
+
+template <bool NT>
+__global__ __launch_bounds__(kDiaThreads) void k_cg1_dia(DiaArgs a, Cg1DiaArgs c)
+{
+    constexpr int U = 8;
+    static_assert(kDiaThreads == kBlock, "block_sum / publish_partials assume kBlock threads");
+    __shared__ double s_red[kBlock / 64];
+    __shared__ double s_tmp[kBlock];
+    __shared__ double s_out[1];
+    __shared__ int s_flag;
+    if (c.ctrl->done)  // block-uniform
+        return;
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    const int g = xcd_tile(blockIdx.x, a.groups);
+    const int w = g * kDiaWaves + wv;
+    const bool live = w < a.windows;  // a wave past the last window still joins the block's sums
+    const int lane = threadIdx.x & 63;
+    PartRegs<kUpdateMaxBlocks / kBlock> pin;
+    part_load(c.part_in, c.n_part_in, pin);
+    const long long r = (long long)w * 64 + lane;
+    const bool own = live && r < a.m;
+    const v2d_t *__restrict__ rp2 = reinterpret_cast<const v2d_t *>(c.rp);
+    // the deferred x term's operands and this row's own {r_k, p_{k-1}}, loaded under the head's sum
+    const int kit = c.ctrl->iter_par[c.parity];
+    const double alpha_prev = c.scal[0].alpha;
+    v2d_t rpo = v2d_t{0.0, 0.0};
+    double xo = 0.0;
+    if (own) {
+        rpo = rp2[r];
+        xo = c.xsol[r];
+    }
+    const int4 hd = live ? a.hdr[w] : make_int4(0, 0, 0, -1);
+    const int K = __builtin_amdgcn_readfirstlane(hd.x) & 0xffff;
+    const bool has_rem = (__builtin_amdgcn_readfirstlane(hd.x) >> 16) != 0;
+    const bool masked = __builtin_amdgcn_readfirstlane(hd.w) >= 0;
+    const int lk = max(min(lane, K - 1), 0);
+    const int offv = K ? a.off[__builtin_amdgcn_readfirstlane(hd.y) + lk] : 0;
+    const unsigned long long mkv = masked && K ? a.mask[__builtin_amdgcn_readfirstlane(hd.w) + lk] : ~0ull;
+    const v2d_t *__restrict__ vp = reinterpret_cast<const v2d_t *>(a.vt) + (size_t)__builtin_amdgcn_readfirstlane(hd.z) * 64;
+    const int KP = (K + 1) >> 1;
+    auto off_at = [&](int k) { return __builtin_amdgcn_readlane(offv, k); };
+    auto mask_at = [&](int k) {
+        const unsigned lo = __builtin_amdgcn_readlane((unsigned)mkv, k);
+        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(mkv >> 32), k);
+        return ((unsigned long long)hi << 32) | lo;
+    };
+    auto pair_at = [&](int p) { return dia_ld2<NT>(vp + (size_t)min(p, KP - 1) * 64 + lane); };
+    double beta = 0.0;
+    if (!cg1_head(c, part_sum(pin, s_red), beta))  // block-uniform: converged
+        return;
+    auto pk = [&](v2d_t q) { return q.x + beta * q.y; };  // p_k from {r_k, p_{k-1}}: one expression everywhere
+    double acc = 0.0;
+    // (k_spmm_dia<1>'s batches.  Issuing the first batch's loads ahead of the head's sum measured no faster:
+    // 37.4 vs 37.0 us per iteration, r06h.)
+    auto batch = [&](int k0, auto masked_c, auto guard_c, auto u_c) {
+        constexpr bool MASKED = decltype(masked_c)::value, GUARD = decltype(guard_c)::value;
+        constexpr int UU = decltype(u_c)::value;
+        v2d_t v[UU / 2];
+        v2d_t xq[UU];
+        bool on[UU];
+#pragma unroll
+        for (int u = 0; u < UU / 2; ++u)
+            v[u] = pair_at((k0 >> 1) + u);
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+            const int kk = GUARD ? min(k0 + u, K - 1) : k0 + u;
+            on[u] = MASKED ? ((mask_at(kk) >> lane) & 1ull) != 0 : true;
+            xq[u] = rp2[MASKED ? (on[u] ? r + off_at(kk) : 0) : r + off_at(kk)];
+        }
+#pragma unroll
+        for (int u = 0; u < UU; ++u) {
+            const double pv = (u & 1 ? v[u >> 1].y : v[u >> 1].x) * pk(xq[u]);
+            const bool use = (!MASKED || on[u]) && (!GUARD || k0 + u < K);
+            acc += use ? pv : 0.0;
+        }
+    };
+    using U8 = std::integral_constant<int, U>;
+    using U4 = std::integral_constant<int, U / 2>;
+    const int kfull = K - K % U;
+    auto windows = [&](auto masked_c) {
+        for (int k0 = 0; k0 < kfull; k0 += U)
+            batch(k0, masked_c, std::false_type{}, U8{});
+        if (K - kfull > U / 2)
+            batch(kfull, masked_c, std::true_type{}, U8{});
+        else if (kfull < K)
+            batch(kfull, masked_c, std::true_type{}, U4{});
+    };
+    if (masked)
+        windows(std::true_type{});
+    else
+        windows(std::false_type{});
+    if (has_rem && own) {
+        double ar = 0.0;
+        for (int j = a.rem_ptr[r]; j < a.rem_ptr[r + 1]; ++j)
+            ar += a.rem_val[j] * pk(rp2[a.rem_col[j]]);
+        acc = acc + ar;
+    }
+    double dot = 0.0;
+    if (own) {
+        const double p = pk(rpo);
+        c.rp_new[2 * r + 1] = p;
+        c.ap[r] = acc;
+        dot = p * acc;
+        if (kit >= 1)  // iteration 0: x = 0 and nothing is pending
+            c.xsol[r] = xo + alpha_prev * rpo.y;
+    }
+    const double tsum = block_sum(dot, s_red);
+    if (a.groups <= kConsumeTile) {  // k_cg1_update sums them: the launch boundary orders the store
+        if (threadIdx.x == 0)
+            c.partials[g] = tsum;
+        return;
+    }
+    if (threadIdx.x == 0) {  // a ticket tree folds them first: published at agent scope, drained
+        store_sc1(&c.partials[g], tsum);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    publish_partials<1>(c.partials, c.gtickets, g, a.groups, kConsumeTile, s_tmp, s_out, &s_flag, c.ctrl);
+}
+
+hipError_t launch_cg1_dia(mspmv_handle_s *h, const TilePlan &plan, const double *rp_old, double *rp_new, double *d_x,
+                          int parity, int nblk, double tol, int *nslots)
+{
+    const DiaData *dd = plan.dia;
+    if (!dd || dd->windows == 0 || nblk > kUpdateMaxBlocks)
+        return hipErrorInvalidValue;
+    DiaArgs a{};
+    a.hdr = dd->d_hdr;
+    a.off = dd->d_off;
+    a.mask = dd->d_mask;
+    a.vt = dd->d_vt;
+    a.windows = dd->windows;
+    a.rem_ptr = dd->d_rem_ptr;
+    a.rem_col = dd->d_rem_col;
+    a.rem_val = dd->d_rem_val;
+    a.groups = (dd->windows + kDiaWaves - 1) / kDiaWaves;
+    a.m = h->m;
+    a.n = h->n;
+    a.ld = 1;
+    Cg1DiaArgs c{};
+    c.rp = rp_old;
+    c.rp_new = rp_new;
+    c.xsol = d_x;
+    c.ap = h->d_ap;
+    c.scal = h->d_scal;
+    c.ctrl = h->d_ctrl;
+    c.part_in = h->d_partials_b;
+    c.n_part_in = nblk;
+    c.partials = h->d_partials;
+    c.gtickets = h->d_gtickets;
+    c.parity = parity;
+    c.tol = tol;
+    c.hist = h->d_hist;
+    c.hist_cap = h->hist_cap;
+    *nslots = a.groups;
+    const dim3 grid((unsigned)a.groups), block(kDiaThreads);
+    if (stream_nt(h))
+        hipLaunchKernelGGL((k_cg1_dia<true>), grid, block, 0, h->stream, a, c);
+    else
+        hipLaunchKernelGGL((k_cg1_dia<false>), grid, block, 0, h->stream, a, c);
+    return hipGetLastError();
+}
+
 // Plan time: each window's values into its lane-major panel.  One workgroup per window streams the
 // window's CSR entries coalesced (its row offsets and offset list in LDS; an entry finds its row and its
 // offset index by binary searches there); entries off the list are the remainder's (k_dia_rem_fill).  The

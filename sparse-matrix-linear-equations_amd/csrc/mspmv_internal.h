@@ -382,6 +382,11 @@ hipError_t launch_dia(mspmv_handle_s *h, const TilePlan &plan, const double *d_X
                       const CgControl *ctrl, double *partials = nullptr, long long row_off = 0,
                       hipStream_t stream = nullptr);
 std::string dia_kernel_name(const mspmv_handle_s *h, int L);
+// The pipelined single-RHS CG's SpMV (iteration `parity`) on the windows of `plan` (k_cg1_dia): reads
+// {r_k, p_{k-1}} from rp_old, writes p_k into rp_new, Ap into h->d_ap, the deferred x term into d_x and one
+// p.Ap partial per workgroup into h->d_partials; *nslots = that count, for k_cg1_update's consumer level.
+hipError_t launch_cg1_dia(mspmv_handle_s *h, const TilePlan &plan, const double *rp_old, double *rp_new, double *d_x,
+                          int parity, int nblk, double tol, int *nslots);
 bool dia_spmm_enabled();  // the L-wide products on the windows too unless MSPMV_DIA_SPMM=0 (mspmv_api.hip)
 // The handle's offset-window plan for width L (decided on first use), or null (mspmv_api.hip)
 mspmv_status dia_plan_for(mspmv_handle_s *h, int L, const TilePlan **out);

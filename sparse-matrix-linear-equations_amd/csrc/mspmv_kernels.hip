@@ -83,64 +83,6 @@ __device__ __forceinline__ void lds_search(int d, const int *s_rowend, int a_len
     y = d - lo;
 }
 
-// Lane 0 of each wave holds a deterministic butterfly sum; wave totals are combined in
-// wave order.  Call uniformly from every thread of the block; returns the total in all.
-__device__ __forceinline__ double block_sum(double v, double *s_red)
-{
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1)
-        v += __shfl_xor(v, off);
-    __syncthreads();  // s_red may still be read by a previous call
-    if ((threadIdx.x & 63) == 0)
-        s_red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    double t = s_red[0];
-#pragma unroll
-    for (int w = 1; w < kBlock / 64; ++w)
-        t += s_red[w];
-    return t;
-}
-
-// Sum of column j over rows q, q + kBlock/L, ... < count of a [count][L] array written by
-// other workgroups (agent-scope loads), in row order; eight loads in flight per batch.
-template <int L>
-__device__ __forceinline__ double fold_col_strided(const double *base, int count, int j, int q)
-{
-    constexpr int TPC = kBlock / L;
-    double v = 0.0;
-    int i = q;
-    for (; i + 7 * TPC < count; i += 8 * TPC) {
-        double t[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            t[u] = load_sc1(&base[(size_t)(i + u * TPC) * L + j]);
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            v += t[u];
-    }
-    for (; i < count; i += TPC)
-        v += load_sc1(&base[(size_t)i * L + j]);
-    return v;
-}
-
-// Column totals of a [count][L] partials array in a fixed order (per-thread strided rows,
-// then threads in order) -> s_out[0..L).  Call uniformly from every thread.
-template <int L>
-__device__ __forceinline__ void fold_cols(const double *base, int count, double *s_tmp, double *s_out)
-{
-    constexpr int TPC = kBlock / L;
-    const int tid = threadIdx.x;
-    s_tmp[tid] = fold_col_strided<L>(base, count, tid % L, tid / L);
-    __syncthreads();
-    if (tid < L) {
-        double w = s_tmp[tid];
-        for (int u = 1; u < TPC; ++u)
-            w += s_tmp[u * L + tid];
-        s_out[tid] = w;
-    }
-    __syncthreads();
-}
-
 // Deterministic multi-level "last block done" reduction of per-slot column partials.  The
 // caller has stored partials[slot][0..L) (agent scope, vmcnt drained) and synchronised.  Slots
 // form groups of kSlotGroup; the last of a group to arrive (one agent-scope ticket per group)
@@ -149,20 +91,6 @@ __device__ __forceinline__ void fold_cols(const double *base, int count, double 
 // block does).  Tickets reset themselves for the next launch.  Why a tree of small groups on
 // separate 256-B lines: agent-scope atomics on one address serialise at the memory side
 // (~10 ns each), so 2 k blocks on one ticket cost ~22 us; fan-in 32 keeps each chain short.
-// One arrival on a fold group's ticket (thread 0 only; ticket_arrive).  A fault also stops a single-GPU
-// solve (done); a sharded one does not (fault_no_stop: the ranks' stop decisions must stay identical, so
-// its host stops on the all-reduced fault word at a batch boundary instead).
-template <bool RELEASE>
-__device__ __forceinline__ bool take_ticket(unsigned *tk, int gsize, CgControl *ctrl)
-{
-    bool faulted = false;
-    if (ticket_arrive<RELEASE>(tk, (unsigned)gsize - 1, ctrl ? &ctrl->fault : nullptr, &faulted))
-        return true;
-    if (faulted && ctrl && !__hip_atomic_load(&ctrl->fault_no_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        __hip_atomic_store(&ctrl->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return false;
-}
-
 // RELEASE: the arrivals are agent-scope releases (ticket_arrive; k_fold_dot), else the drained-store form.
 template <int L, bool RELEASE = false>
 __device__ __forceinline__ bool reduce_slots(double *partials, unsigned *tickets, int slot, int nslots,
@@ -186,71 +114,6 @@ __device__ __forceinline__ bool reduce_slots(double *partials, unsigned *tickets
             __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (ngroups == 1)
             return true;
-        double *next = lvl + (size_t)count * L;
-        if (tid < L) {
-            store_sc1(&next[(size_t)g * L + tid], s_out[tid]);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        tickets += (size_t)ngroups * kTicketStride;
-        lvl = next;
-        idx = g;
-        count = ngroups;
-    }
-}
-
-// Consumer-side reduction (single-RHS pipelined CG).  A producer kernel leaves one partial per
-// workgroup; EVERY workgroup of the consumer kernel sums them itself, in one fixed order (thread
-// tid adds elements tid, tid + 256, ... ascending, then block_sum's fixed tree), so all agree
-// bit for bit and no ticket chain sits in the producer's tail.  The loads are issued early
-// (part_load) and summed late (part_sum), under the consumer's own streaming loads.
-template <int NR>
-struct PartRegs {
-    double v[NR];
-};
-template <int NR>
-__device__ __forceinline__ void part_load(const double *p, int n, PartRegs<NR> &r)
-{
-#pragma unroll
-    for (int j = 0; j < NR; ++j) {
-        const int i = (int)threadIdx.x + j * kBlock;
-        r.v[j] = i < n ? p[i] : 0.0;
-    }
-}
-template <int NR>
-__device__ __forceinline__ double part_sum(const PartRegs<NR> &r, double *s_red)
-{
-    double v = r.v[0];
-#pragma unroll
-    for (int j = 1; j < NR; ++j)
-        v += r.v[j];
-    return block_sum(v, s_red);
-}
-
-// Publish this workgroup's partial (already stored at partials[slot], agent scope, vmcnt
-// drained, block synchronised) for a consumer kernel that sums at most `stop` of them: while
-// more would remain, groups of kSlotGroup are folded into the next level by their last arriver
-// (reduce_slots' tickets), down to the level consumer_level() names.
-template <int L>
-__device__ __forceinline__ void publish_partials(double *partials, unsigned *tickets, int slot, int nslots, int stop,
-                                                 double *s_tmp, double *s_out, int *s_flag, CgControl *ctrl)
-{
-    const int tid = threadIdx.x;
-    double *lvl = partials;
-    int idx = slot, count = nslots;
-    while (count > stop) {
-        const int g = idx / kSlotGroup;
-        const int ngroups = (count + kSlotGroup - 1) / kSlotGroup;
-        const int gsize = min(kSlotGroup, count - g * kSlotGroup);
-        unsigned *tk = &tickets[(size_t)g * kTicketStride];
-        if (tid == 0)
-            *s_flag = take_ticket<false>(tk, gsize, ctrl);
-        __syncthreads();
-        if (!*s_flag)
-            return;
-        fold_cols<L>(lvl + (size_t)g * kSlotGroup * L, gsize, s_tmp, s_out);
-        if (tid == 0)
-            __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         double *next = lvl + (size_t)count * L;
         if (tid < L) {
             store_sc1(&next[(size_t)g * L + tid], s_out[tid]);
@@ -1439,49 +1302,6 @@ __device__ __forceinline__ void dot_epilogue(const TileArgs &a, SM &sm, int slot
     const double tsum = block_sum(dot, sm.red);
     if (threadIdx.x == 0)
         a.partials[slot] = tsum;
-}
-
-// Pipelined single-RHS CG, head of iteration k (MODE 1).  Every workgroup sums the previous
-// update's r.r partials itself (rs_k; at k = 0 the init's b.b), so the stop test and beta need
-// no ticket chain: the reference's check after iteration k-1 (single_strategy.hpp:150-156:
-// sqrt(rs_new)/||b|| < tol -> iterations = k) is taken here, then beta = rs_k / rs_{k-1}
-// (:158-160).  Workgroup 0 records the history and hands rs_k and k+1 on by parity.  Returns
-// false when the solve has stopped (converged): the caller returns at once.
-__device__ __forceinline__ bool cg1_head(const TileArgs &a, double rs, double &beta)
-{
-    CgScalars &s = a.scal[0];
-    CgControl *c = a.ctrl;
-    const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
-    const int k = c->iter_par[a.parity];
-    if (k == 0) {  // r = p = b: no stop test before the first iteration
-        beta = 0.0;
-        if (lead) {
-            const double bn = sqrt(rs);
-            s.b_norm = bn == 0.0 ? 1.0 : bn;  // single_strategy.hpp:124-129
-            s.rs_par[0] = rs;
-            c->iter_par[1] = 1;
-        }
-        return true;
-    }
-    const double rel = sqrt(rs) / s.b_norm;
-    if (lead) {
-        if (a.hist && k - 1 < a.hist_cap)
-            a.hist[k - 1] = rel;
-        c->iter = k;
-    }
-    if (rel < a.tol) {
-        if (lead) {
-            c->iters_out = k;
-            c->done = 1;
-        }
-        return false;
-    }
-    beta = rs / s.rs_par[a.parity ^ 1];
-    if (lead) {
-        s.rs_par[a.parity] = rs;
-        c->iter_par[a.parity ^ 1] = k + 1;
-    }
-    return true;
 }
 
 // Pipelined single-RHS CG, deferred solution update.  x += alpha_{k-1} p_{k-1} (AxpySingle,
@@ -3575,9 +3395,13 @@ hipError_t launch_spmm(mspmv_handle_s *h, const TilePlan &plan, const double *d_
 // r04af).
 int cg_update_blocks(long long elems, int num_cus)
 {
+    // ~12 pairs per thread on long vectors, capped at 3 workgroups per CU.  Below that (a single-RHS
+    // vector of a few hundred thousand rows: 70 workgroups at 12 pairs) one pair per thread up to the
+    // cap instead: the passes are latency bound on a quarter of the CUs otherwise -- 15.4 us per pass
+    // on the 427,500-row CG (r06e trace).
     const long long pairs = (elems + 1) / 2;
-    long long b = (pairs + kBlock * 12 - 1) / (kBlock * 12);
     const long long cap = 3LL * std::max(num_cus, 1);
+    long long b = std::max((pairs + kBlock * 12 - 1) / (kBlock * 12), std::min((pairs + kBlock - 1) / kBlock, cap));
     if (b < 1)
         b = 1;
     if (b > cap)
@@ -3960,21 +3784,27 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, const Ti
         return launch_cg_iteration_split(h, plan, splan, dot_fused, d_x, L, nblk, tol);
     double *rp_old = parity ? h->d_p1 : h->d_p0;  // {r_k, p_{k-1}} interleaved (cg_rp)
     double *rp_new = parity ? h->d_p0 : h->d_p1;  // receives p_k, then r_{k+1}
-    TileArgs ta = make_args(h, plan, rp_old, h->d_ap, 1);
-    ta.p_new = rp_new;
-    ta.xsol = d_x;
-    ta.scal = h->d_scal;
-    ta.ctrl = h->d_ctrl;
-    ta.fault = &h->d_ctrl->fault;
-    ta.partials = h->d_partials;
-    ta.gtickets = h->d_gtickets;
-    ta.part_in = h->d_partials_b;
-    ta.n_part_in = nblk;
-    ta.parity = parity;
-    ta.tol = tol;
-    ta.hist = h->d_hist;
-    ta.hist_cap = h->hist_cap;
-    hipError_t e = launch_tile<kModeCg>(ta, 1, h->stream, stream_nt(h));
+    int nslots = plan.num_tiles;                   // the SpMV's p.Ap partials
+    hipError_t e = hipSuccess;
+    if (splan && splan->dia) {  // the SpMV on the offset windows (mspmv_dia.hip, k_cg1_dia)
+        e = launch_cg1_dia(h, *splan, rp_old, rp_new, d_x, parity, nblk, tol, &nslots);
+    } else {
+        TileArgs ta = make_args(h, plan, rp_old, h->d_ap, 1);
+        ta.p_new = rp_new;
+        ta.xsol = d_x;
+        ta.scal = h->d_scal;
+        ta.ctrl = h->d_ctrl;
+        ta.fault = &h->d_ctrl->fault;
+        ta.partials = h->d_partials;
+        ta.gtickets = h->d_gtickets;
+        ta.part_in = h->d_partials_b;
+        ta.n_part_in = nblk;
+        ta.parity = parity;
+        ta.tol = tol;
+        ta.hist = h->d_hist;
+        ta.hist_cap = h->hist_cap;
+        e = launch_tile<kModeCg>(ta, 1, h->stream, stream_nt(h));
+    }
     if (e != hipSuccess)
         return e;
     Cg1Args a = cg1_args(h, d_x);
@@ -3982,7 +3812,7 @@ hipError_t launch_cg_iteration(mspmv_handle_s *h, const TilePlan &plan, const Ti
     a.rp_next = rp_new;
     long long off = 0;
     int count = 0;
-    consumer_level(plan.num_tiles, kConsumeTile, 1, &off, &count);
+    consumer_level(nslots, kConsumeTile, 1, &off, &count);
     a.part_in = h->d_partials + off;
     a.n_part_in = count;
     a.part_out = h->d_partials_b;

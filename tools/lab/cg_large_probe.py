@@ -2,7 +2,8 @@
 """CGSolveSingle on bench.py's pwtk-size SPD matrix (27-point stencil, 427,500 rows, 11.2 M nonzeros: too
 large for the register-resident kernel): us per iteration (best of 5 solves after a warm one) of the form
 the environment selects (MSPMV_CG_RESIDENT=0: the two-kernel pipelined form; MSPMV_CG_SPLIT=1: the
-multi-RHS split iteration at L = 1, on the offset windows).  One JSON line."""
+multi-RHS split iteration at L = 1, on the offset windows), beside the plain SpMV's kernel time on the
+same handle (hot).  One JSON line."""
 import json
 import os
 import sys
@@ -23,6 +24,10 @@ thr = float(np.sqrt(np.sum(b * b)) * 1e-5)
 out = {"env": {k: v for k, v in os.environ.items() if k.startswith("MSPMV_")}}
 with mspmv.GpuCsr(a) as g:
     db, dx = mspmv.DeviceBuffer.from_array(b), mspmv.DeviceBuffer(8 * n)
+    dy = mspmv.DeviceBuffer(8 * n)
+    g.time_spmm(db, dy, 1, 5)
+    _, hot, _ = g.time_spmm(db, dy, 1, 50)
+    out.update(spmv_kernel=g.kernel_name(), spmv_hot_us=round(hot * 1e3, 2))
     g.cg_dev(db, dx, 1, 10000, thr)
     best = None
     for _ in range(5):
@@ -30,6 +35,5 @@ with mspmv.GpuCsr(a) as g:
         it, _, st = g.cg_dev(db, dx, 1, 10000, thr)
         el = time.perf_counter() - t0
         best = el / it if best is None else min(best, el / it)
-    out.update(kernel=g.cg_kernel_name(), spmv_kernel=g.kernel_name(), iterations=it, status=st,
-               us_per_iter=round(best * 1e6, 3))
+    out.update(kernel=g.cg_kernel_name(), iterations=it, status=st, us_per_iter=round(best * 1e6, 3))
 print(json.dumps(out), flush=True)
