@@ -132,12 +132,18 @@ k_spmm_dia(DiaArgs a)
     if constexpr (L == 1) {
         constexpr int U = 8;
         const long long r = r0 + lane;
+        const long long nmax1 = (long long)a.n - 1;
         double acc = 0.0;
-        // one batch of U offsets from k0: MASKED selects the absent entries out (acc starts at +0.0 and
-        // never becomes -0.0, so adding +0.0 for them is the identity: the sum is the row's CSR-order
-        // sum bit for bit); GUARD stops at K (the last batch only)
-        auto batch = [&](int k0, auto masked_c, auto guard_c, auto u_c) {
-            constexpr bool MASKED = decltype(masked_c)::value, GUARD = decltype(guard_c)::value;
+        // one batch of U offsets from k0.  MODE 0: every row holds every offset.  MODE 1 (EXACT, masked
+        // windows): the absent entries selected out (acc starts at +0.0 and never becomes -0.0, so adding
+        // +0.0 for them is the identity: the sum is the row's CSR-order sum bit for bit).  MODE 2 (masked
+        // windows, first sweep): every offset summed at a clamped row -- an absent entry's panel value is 0.0,
+        // so its product adds +-0.0, the identity, unless its x is Inf or NaN; a row that comes out non-finite
+        // sends the window through MODE 1 again (the same bits as MODE 1 in every case, without its mask
+        // tests).  GUARD stops at K (the last batch only).
+        auto batch = [&](int k0, auto mode_c, auto guard_c, auto u_c) {
+            constexpr int MODE = decltype(mode_c)::value;
+            constexpr bool GUARD = decltype(guard_c)::value;
             constexpr int U = decltype(u_c)::value;
             v2d_t v[U / 2];
             double xv[U];
@@ -148,15 +154,16 @@ k_spmm_dia(DiaArgs a)
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int kk = GUARD ? min(k0 + u, K - 1) : k0 + u;
-                on[u] = MASKED ? ((mask_at(kk) >> lane) & 1ull) != 0 : true;
-                xv[u] = a.x[MASKED ? (on[u] ? r + off_at(kk) : 0) : r + off_at(kk)];
+                on[u] = MODE == 1 ? ((mask_at(kk) >> lane) & 1ull) != 0 : true;
+                const long long j = r + off_at(kk);
+                xv[u] = a.x[MODE == 1 ? (on[u] ? j : 0) : MODE == 2 ? min(max(j, 0LL), nmax1) : j];
             }
             // (the guard is a select, not a break: a break let the compiler sink the loads under it and
             // issue them one round trip at a time -- K = 7 windows 8.0 -> 9.4 us, r05ab)
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const double pv = (u & 1 ? v[u >> 1].y : v[u >> 1].x) * xv[u];
-                const bool use = (!MASKED || on[u]) && (!GUARD || k0 + u < K);
+                const bool use = (MODE != 1 || on[u]) && (!GUARD || k0 + u < K);
                 acc += use ? pv : 0.0;
             }
         };
@@ -165,18 +172,22 @@ k_spmm_dia(DiaArgs a)
         using U8 = std::integral_constant<int, U>;
         using U4 = std::integral_constant<int, U / 2>;
         const int kfull = K - K % U;
-        auto windows = [&](auto masked_c) {
+        auto windows = [&](auto mode_c) {
+            acc = 0.0;
             for (int k0 = 0; k0 < kfull; k0 += U)
-                batch(k0, masked_c, std::false_type{}, U8{});
+                batch(k0, mode_c, std::false_type{}, U8{});
             if (K - kfull > U / 2)
-                batch(kfull, masked_c, std::true_type{}, U8{});
+                batch(kfull, mode_c, std::true_type{}, U8{});
             else if (kfull < K)
-                batch(kfull, masked_c, std::true_type{}, U4{});
+                batch(kfull, mode_c, std::true_type{}, U4{});
         };
-        if (masked)
-            windows(std::true_type{});
-        else
-            windows(std::false_type{});
+        if (!masked) {
+            windows(std::integral_constant<int, 0>{});
+        } else {
+            windows(std::integral_constant<int, 2>{});
+            if (__any(r < a.m && !__builtin_isfinite(acc)))  // wave-uniform
+                windows(std::integral_constant<int, 1>{});
+        }
         if (has_rem && r < a.m) {  // the row's remainder entries, in CSR order, after its offsets
             double ar = 0.0;
             for (int j = a.rem_ptr[r]; j < a.rem_ptr[r + 1]; ++j)
@@ -255,53 +266,71 @@ k_spmm_dia(DiaArgs a)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         };
         v2d_t acc[GL];
-#pragma unroll
-        for (int q = 0; q < GL; ++q)
-            acc[q] = v2d_t{0.0, 0.0};
-        if (K > 0)
-            fetch(0);
-        for (int k = 0; k < K;) {
-            wave_sync();
+        // EXACT: absent entries (presence mask bit clear) selected out of the sum.  Without it every offset is
+        // summed as if all rows held it: an absent entry's panel value is 0.0, so its product is +-0.0 and adding
+        // it leaves the row sum unchanged (a sum is never -0.0) -- unless the X element it meets is Inf or NaN.
+        // Masked windows therefore run the plain sweep first and again EXACT only when a row came out
+        // non-finite (whatever the cause): the same bits as the select form in every case, without its
+        // 3 + 4 VALU per row per offset.
+        auto sweep = [&](auto exact_c) {
+            constexpr bool EXACT = decltype(exact_c)::value;
 #pragma unroll
             for (int q = 0; q < GL; ++q)
-                sx[(rl + RS * q) * GL + c] = nx[q];
-            if (rl < kDiaRun - 1)
-                sx[(64 + rl) * GL + c] = ne;
-            wave_sync();
-            double cv[kDiaRun];
+                acc[q] = v2d_t{0.0, 0.0};
+            if (K > 0)
+                fetch(0);
+            for (int k = 0; k < K;) {
+                wave_sync();
 #pragma unroll
-            for (int j = 0; j < kDiaRun; ++j)
-                cv[j] = nv[j];
-            const int gk = __builtin_amdgcn_readlane(runv, k), kc = k;
-            k += gk;
-            if (k < K)  // the next run's loads fly while this one is summed
-                fetch(k);
+                for (int q = 0; q < GL; ++q)
+                    sx[(rl + RS * q) * GL + c] = nx[q];
+                if (rl < kDiaRun - 1)
+                    sx[(64 + rl) * GL + c] = ne;
+                wave_sync();
+                double cv[kDiaRun];
 #pragma unroll
-            for (int j = 0; j < kDiaRun; ++j) {
-                if (j >= gk)
-                    break;
-                const unsigned long long mw = masked ? mask_at(kc + j) : ~0ull;
-                if (mw == ~0ull) {  // every row holds this offset (wave-uniform): no selects
+                for (int j = 0; j < kDiaRun; ++j)
+                    cv[j] = nv[j];
+                const int gk = __builtin_amdgcn_readlane(runv, k), kc = k;
+                k += gk;
+                if (k < K)  // the next run's loads fly while this one is summed
+                    fetch(k);
 #pragma unroll
-                    for (int q = 0; q < GL; ++q) {
-                        const int row = rl + RS * q;
-                        const double v = __shfl(cv[j], row);
-                        const v2d_t xv = sx[(row + j) * GL + c];
-                        acc[q].x += v * xv.x;
-                        acc[q].y += v * xv.y;
-                    }
-                } else {
+                for (int j = 0; j < kDiaRun; ++j) {
+                    if (j >= gk)
+                        break;
+                    const unsigned long long mw = EXACT && masked ? mask_at(kc + j) : ~0ull;
+                    if (mw == ~0ull) {  // every row holds this offset (wave-uniform), or the plain sweep
 #pragma unroll
-                    for (int q = 0; q < GL; ++q) {
-                        const int row = rl + RS * q;
-                        const double v = __shfl(cv[j], row);
-                        const v2d_t xv = sx[(row + j) * GL + c];
-                        const bool on = (mw >> row) & 1ull;
-                        acc[q].x += on ? v * xv.x : 0.0;
-                        acc[q].y += on ? v * xv.y : 0.0;
+                        for (int q = 0; q < GL; ++q) {
+                            const int row = rl + RS * q;
+                            const double v = __shfl(cv[j], row);
+                            const v2d_t xv = sx[(row + j) * GL + c];
+                            acc[q].x += v * xv.x;
+                            acc[q].y += v * xv.y;
+                        }
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < GL; ++q) {
+                            const int row = rl + RS * q;
+                            const double v = __shfl(cv[j], row);
+                            const v2d_t xv = sx[(row + j) * GL + c];
+                            const bool on = (mw >> row) & 1ull;
+                            acc[q].x += on ? v * xv.x : 0.0;
+                            acc[q].y += on ? v * xv.y : 0.0;
+                        }
                     }
                 }
             }
+        };
+        sweep(std::false_type{});
+        if (masked) {
+            bool bad = false;
+#pragma unroll
+            for (int q = 0; q < GL; ++q)
+                bad |= !(__builtin_isfinite(acc[q].x) && __builtin_isfinite(acc[q].y));
+            if (__any(bad))  // wave-uniform
+                sweep(std::true_type{});
         }
         if (has_rem) {  // the rows' remainder entries, in CSR order, after their offsets
 #pragma unroll
@@ -400,6 +429,7 @@ __global__ __launch_bounds__(kDiaThreads) void k_cg1_dia(DiaArgs a, Cg1DiaArgs c
     part_load(c.part_in, c.n_part_in, pin);
     const long long r = (long long)w * 64 + lane;
     const bool own = live && r < a.m;
+    const long long nmax1 = (long long)a.n - 1;
     const v2d_t *__restrict__ rp2 = reinterpret_cast<const v2d_t *>(c.rp);
     // the deferred x term's operands and this row's own {r_k, p_{k-1}}, loaded under the head's sum
     const int kit = c.ctrl->iter_par[c.parity];
@@ -433,8 +463,9 @@ __global__ __launch_bounds__(kDiaThreads) void k_cg1_dia(DiaArgs a, Cg1DiaArgs c
     double acc = 0.0;
     // (k_spmm_dia<1>'s batches.  Issuing the first batch's loads ahead of the head's sum measured no faster:
     // 37.4 vs 37.0 us per iteration, r06h.)
-    auto batch = [&](int k0, auto masked_c, auto guard_c, auto u_c) {
-        constexpr bool MASKED = decltype(masked_c)::value, GUARD = decltype(guard_c)::value;
+    auto batch = [&](int k0, auto mode_c, auto guard_c, auto u_c) {  // MODE as k_spmm_dia<1>'s batches
+        constexpr int MODE = decltype(mode_c)::value;
+        constexpr bool GUARD = decltype(guard_c)::value;
         constexpr int UU = decltype(u_c)::value;
         v2d_t v[UU / 2];
         v2d_t xq[UU];
@@ -445,31 +476,36 @@ __global__ __launch_bounds__(kDiaThreads) void k_cg1_dia(DiaArgs a, Cg1DiaArgs c
 #pragma unroll
         for (int u = 0; u < UU; ++u) {
             const int kk = GUARD ? min(k0 + u, K - 1) : k0 + u;
-            on[u] = MASKED ? ((mask_at(kk) >> lane) & 1ull) != 0 : true;
-            xq[u] = rp2[MASKED ? (on[u] ? r + off_at(kk) : 0) : r + off_at(kk)];
+            on[u] = MODE == 1 ? ((mask_at(kk) >> lane) & 1ull) != 0 : true;
+            const long long j = r + off_at(kk);
+            xq[u] = rp2[MODE == 1 ? (on[u] ? j : 0) : MODE == 2 ? min(max(j, 0LL), nmax1) : j];
         }
 #pragma unroll
         for (int u = 0; u < UU; ++u) {
             const double pv = (u & 1 ? v[u >> 1].y : v[u >> 1].x) * pk(xq[u]);
-            const bool use = (!MASKED || on[u]) && (!GUARD || k0 + u < K);
+            const bool use = (MODE != 1 || on[u]) && (!GUARD || k0 + u < K);
             acc += use ? pv : 0.0;
         }
     };
     using U8 = std::integral_constant<int, U>;
     using U4 = std::integral_constant<int, U / 2>;
     const int kfull = K - K % U;
-    auto windows = [&](auto masked_c) {
+    auto windows = [&](auto mode_c) {
+        acc = 0.0;
         for (int k0 = 0; k0 < kfull; k0 += U)
-            batch(k0, masked_c, std::false_type{}, U8{});
+            batch(k0, mode_c, std::false_type{}, U8{});
         if (K - kfull > U / 2)
-            batch(kfull, masked_c, std::true_type{}, U8{});
+            batch(kfull, mode_c, std::true_type{}, U8{});
         else if (kfull < K)
-            batch(kfull, masked_c, std::true_type{}, U4{});
+            batch(kfull, mode_c, std::true_type{}, U4{});
     };
-    if (masked)
-        windows(std::true_type{});
-    else
-        windows(std::false_type{});
+    if (!masked) {
+        windows(std::integral_constant<int, 0>{});
+    } else {  // the clamped sweep first, the exact one when a row came out non-finite (k_spmm_dia<1>)
+        windows(std::integral_constant<int, 2>{});
+        if (__any(own && !__builtin_isfinite(acc)))
+            windows(std::integral_constant<int, 1>{});
+    }
     if (has_rem && own) {
         double ar = 0.0;
         for (int j = a.rem_ptr[r]; j < a.rem_ptr[r + 1]; ++j)

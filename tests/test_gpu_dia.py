@@ -36,10 +36,9 @@ def _windows_every_width(monkeypatch):
 
 
 def is_dia(name, L=None):
-    """The offset-window kernels: k_spmm_dia<L, ...> (one window per wave) or k_spmm_dia_wg<L, ...> (one
-    window per workgroup, L = 8 / 16)."""
-    m = re.match(r"k_spmm_dia(_wg)?<(\d+),", name)
-    return m is not None and (L is None or int(m.group(2)) == L)
+    """The offset-window kernel k_spmm_dia<L, ...> (one window per wave)."""
+    m = re.match(r"k_spmm_dia<(\d+),", name)
+    return m is not None and (L is None or int(m.group(1)) == L)
 
 
 def band(m, offsets, seed, n=None, drop=0.0):
@@ -159,6 +158,41 @@ def test_dia_cu_limit_and_inf(orc, monkeypatch):
     assert np.array_equal(np.isfinite(y2), np.isfinite(gold))
     fin = np.isfinite(gold)
     assert y2[fin].tobytes() == gold[fin].tobytes()
+
+
+@pytest.mark.parametrize("L", [1, 2, 8, 16])
+@pytest.mark.parametrize("name", ["partial", "stencil27"])
+def test_dia_nonfinite_x_exact_fallback(orc, monkeypatch, name, L):
+    """Masked windows are summed first as if every row held every offset (an absent entry's 0.0 adds +-0.0)
+    and again with the absent entries selected out when a row comes out non-finite.  Inf and NaN in x/X --
+    at columns read only through absent entries of masked windows and at columns rows do read -- give the
+    oracle's rows exactly: the same non-finite rows (NaN where it has NaN) and every finite row bit-equal."""
+    monkeypatch.delenv("MSPMV_DIA", raising=False)
+    a = CASES[name]()
+    rng = np.random.default_rng(17 + L)
+    X = rng.uniform(-1, 1, (a.num_cols, L))
+    bad = rng.choice(a.num_cols, 6, replace=False)
+    X[bad[:2]] = np.inf
+    X[bad[2:4]] = -np.inf
+    X[bad[4:]] = np.nan
+    X[0] = np.inf  # the partial band: column 0 is read by rows 0, 3 and 70 only
+    with mspmv.GpuCsr(a) as g:
+        if L == 1:
+            Y = g.spmv(X[:, 0].copy())
+            gold = orc.spmv_gold(a, X[:, 0].copy())
+            assert is_dia(g.kernel_name(), 1), g.kernel_name()
+        else:
+            Y = g.spmm(X)
+            gold = orc.csr_spmm_t(a, X)
+            assert is_dia(g.spmm_kernel_name(L), L), g.spmm_kernel_name(L)
+    assert np.array_equal(np.isnan(Y), np.isnan(gold))
+    assert np.array_equal(np.isfinite(Y), np.isfinite(gold))
+    fin = np.isfinite(gold)
+    assert fin.sum() > 0.9 * fin.size
+    assert np.array_equal(Y[~fin & ~np.isnan(gold)], gold[~fin & ~np.isnan(gold)])  # the infinities' signs
+    if name in REMAINDER:
+        return
+    assert Y[fin].tobytes() == gold[fin].tobytes()
 
 
 @pytest.mark.parametrize("L", [24, 12, 5])
