@@ -230,6 +230,13 @@ k_spmm_dia(DiaArgs a)
         // small part of their traffic; 8-B loads keep the run's values in registers without pair selects)
         const double *__restrict__ vd = reinterpret_cast<const double *>(vp) + 2 * lane;
         const size_t lrow = (size_t)rl * a.ld;  // this lane's first span row, as an element offset
+        auto fetch_vals = [&](int k, double (&dst)[kDiaRun]) {  // the values of the run from offset k
+#pragma unroll
+            for (int j = 0; j < kDiaRun; ++j) {
+                const int kk = min(k + j, K - 1);
+                dst[j] = dia_ld<NT>(vd + (size_t)(kk >> 1) * 128 + (kk & 1));
+            }
+        };
         auto fetch = [&](int k) {  // the run's panel span (clamped into X: rows outside it serve absent entries only)
             const long long d0 = off_at(k);
             const long long s0 = r0 + d0;  // the span's first row (wave-uniform)
@@ -251,11 +258,7 @@ k_spmm_dia(DiaArgs a)
                 const size_t oe = (size_t)min(max(s0 + 64 + min(rl, kDiaRun - 2), 0LL), nmax) * a.ld;
                 ne = *reinterpret_cast<const v2d_t *>(xb + oe);
             }
-#pragma unroll
-            for (int j = 0; j < kDiaRun; ++j) {
-                const int kk = min(k + j, K - 1);
-                nv[j] = dia_ld<NT>(vd + (size_t)(kk >> 1) * 128 + (kk & 1));
-            }
+            fetch_vals(k, nv);
         };
         // Lanes read panel rows other lanes of the wave wrote.  The hardware runs a wave's DS operations in
         // order; the compiler, reasoning per lane, could move a read of another lane's row above the write
@@ -277,9 +280,10 @@ k_spmm_dia(DiaArgs a)
 #pragma unroll
             for (int q = 0; q < GL; ++q)
                 acc[q] = v2d_t{0.0, 0.0};
-            if (K > 0)
-                fetch(0);
-            for (int k = 0; k < K;) {
+            // one run: its span to LDS, its values from buf; the next run's span and values in flight while it is
+            // summed.  (Values loaded two runs ahead, two buffers alternating, measured even: L = 8 364-368 us
+            // either way, r06l.)
+            auto run = [&](int &k, double (&buf)[kDiaRun]) {
                 wave_sync();
 #pragma unroll
                 for (int q = 0; q < GL; ++q)
@@ -290,10 +294,10 @@ k_spmm_dia(DiaArgs a)
                 double cv[kDiaRun];
 #pragma unroll
                 for (int j = 0; j < kDiaRun; ++j)
-                    cv[j] = nv[j];
+                    cv[j] = buf[j];
                 const int gk = __builtin_amdgcn_readlane(runv, k), kc = k;
                 k += gk;
-                if (k < K)  // the next run's loads fly while this one is summed
+                if (k < K)
                     fetch(k);
 #pragma unroll
                 for (int j = 0; j < kDiaRun; ++j) {
@@ -321,7 +325,11 @@ k_spmm_dia(DiaArgs a)
                         }
                     }
                 }
-            }
+            };
+            if (K > 0)
+                fetch(0);
+            for (int k = 0; k < K;)
+                run(k, nv);
         };
         sweep(std::false_type{});
         if (masked) {
