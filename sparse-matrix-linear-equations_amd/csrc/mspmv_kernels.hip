@@ -3393,14 +3393,16 @@ hipError_t launch_spmm(mspmv_handle_s *h, const TilePlan &plan, const double *d_
 // longer-lived workgroups stream faster here: configs[4] (nlpkkt120 size, L = 8) 0.915 -> 0.886 ms
 // per iteration against the old 2,048 (~4 pairs per thread); 4 and 2 per CU 0.895 / 0.893 (r04ae,
 // r04af).
-int cg_update_blocks(long long elems, int num_cus)
+int cg_update_blocks(long long elems, int /*num_cus*/)
 {
-    // ~12 pairs per thread on long vectors, capped at 3 workgroups per CU.  Below that (a single-RHS
-    // vector of a few hundred thousand rows: 70 workgroups at 12 pairs) one pair per thread up to the
-    // cap instead: the passes are latency bound on a quarter of the CUs otherwise -- 15.4 us per pass
-    // on the 427,500-row CG (r06e trace).
+    // ~12 pairs per thread on long vectors, capped at 768 workgroups (3 per CU of the whole chip).  Below that
+    // (a single-RHS vector of a few hundred thousand rows: 70 workgroups at 12 pairs) one pair per thread up to
+    // the cap instead: the passes are latency bound on a quarter of the CUs otherwise -- 15.4 us per pass on
+    // the 427,500-row CG (r06e trace).  The grid -- and so every partial sum's order -- does not depend on the
+    // handle's CU limit: a CU mask changes the speed of a solve, never its iterates (tests/test_parallel_
+    // efficiency.py; round 5's cap of 3 per *available* CU made it depend on them).
+    constexpr long long cap = 768;
     const long long pairs = (elems + 1) / 2;
-    const long long cap = 3LL * std::max(num_cus, 1);
     long long b = std::max((pairs + kBlock * 12 - 1) / (kBlock * 12), std::min((pairs + kBlock - 1) / kBlock, cap));
     if (b < 1)
         b = 1;

@@ -69,7 +69,9 @@ def cg_loop_times(trace, iterations):
     for r in recs:
         k = short_name(r["Kernel_Name"])
         calls[k] = calls.get(k, 0) + 1
-    loop = {k for k, c in calls.items() if c >= iterations}
+    loop = {k for k, c in calls.items() if c >= iterations and not k.startswith("__amd")}  # not the runtime's copies
+    if any(k.startswith("k_cg_resident") for k in calls):  # the resident CG's leg (its pipelined_large solves too)
+        loop = set()
     if not loop:  # the register-resident CG: the whole solve is ONE cooperative launch (the last one is timed)
         # launches: the warm solve, the timed one, then (bench's resident_phases) a stamped one
         res = [r for r in recs if short_name(r["Kernel_Name"]).startswith("k_cg_resident")]
@@ -169,17 +171,42 @@ def main(src, dst):
                          f"{'us' if 'us_per_iter' in lj else 'ms'}/iter, wall) | span frac {frac(nb, span):.4f} "
                          f"({span:.2f} us/iter); kernel-busy frac {frac(nb, busy):.4f} ({busy:.2f} us/iter) | "
                          f"{', '.join(loop)} |")
+            pl = lj.get("pipelined_large") if leg == "cg_single" else None
+            if isinstance(pl, dict) and "workload" in pl:
+                # the two-kernel pipelined CG on the pwtk-size stencil (bench cg_single.pipelined_large): the median
+                # launch of each loop kernel (a solve also launches up to 2 graph batches past convergence, which
+                # return at their stop test: the medians are the iterations' own launches)
+                pm = int(pl["workload"].split(" m=")[1].split()[0])
+                pnnz = int(pl["workload"].split(" nnz=")[1].split(",")[0].split()[0])
+                med = {}
+                for r in rows:
+                    k = r["kernel"]
+                    if k.startswith(("k_cg1_dia", "k_cg1_update")) or (k.startswith("k_spmv_tile<8,1,")):
+                        if r["calls"] >= pl["iterations"] and (k not in med or r["calls"] > med[k][1]):
+                            med[k] = (r["median_us"], r["calls"])
+                if med:
+                    per = sum(v[0] for v in med.values())
+                    lines.append(f"| cg_single.pipelined_large | roofline_frac {pl['roofline_frac']} ({pl['us_per_iter']} "
+                                 f"us/iter, wall) | kernel frac {frac(cg_iter_bytes(pm, pnnz), per):.4f} ({per:.2f} us/iter: "
+                                 f"{' + '.join(f'{v[0]}' for v in med.values())} us, median launches) | "
+                                 f"{', '.join(f'{k} x{v[1]}' for k, v in med.items())} |")
             if leg == "cg_multi" and bench and isinstance(bench.get("spmv_nlpkkt120_size"), dict):
                 # SURVEY 8(d)'s named 70 % case: the nlpkkt120-size single-RHS SpMV timed in the same leg
                 # (back-to-back launches) against its rows in this trace
                 sl = bench["spmv_nlpkkt120_size"]
-                sp = [r for r in rows if r["kernel"].startswith(("k_spmv", "k_spmm_dia<1,")) and r["calls"] >= 40]
-                if sp:
-                    r = max(sp, key=lambda q: q["grid"])
-                    own = lj0.get("spmv_nlpkkt120_size") if isinstance(lj0, dict) else None
-                    own_s = f"; this profiled run's own events: kernel_ms {own['kernel_ms']}" if own else ""
-                    lines.append(f"| spmv_nlpkkt120_size | frac {sl['frac']} (kernel_ms {sl['kernel_ms']}{own_s}) | frac "
-                                 f"{frac(sl['bytes_per_launch'], r['avg_us']):.4f} (avg {r['avg_us']} us, median "
+                own = lj0.get("spmv_nlpkkt120_size") if isinstance(lj0, dict) else None
+                for label, ent, oent in (("", sl, own), (" merge_path", sl.get("merge_path"),
+                                                          own.get("merge_path") if isinstance(own, dict) else None)):
+                    if not isinstance(ent, dict) or "kernel" not in ent:
+                        continue
+                    pre = ent["kernel"].rstrip(">")  # the bench's name leaves out default template arguments
+                    sp = [r for r in rows if r["kernel"].startswith(pre) and r["calls"] >= 40]
+                    if not sp:
+                        continue
+                    r = max(sp, key=lambda q: q["calls"])
+                    own_s = f"; this profiled run's own events: kernel_ms {oent['kernel_ms']}" if isinstance(oent, dict) else ""
+                    lines.append(f"| spmv_nlpkkt120_size{label} | frac {ent['frac']} (kernel_ms {ent['kernel_ms']}{own_s}) | "
+                                 f"frac {frac(sl['bytes_per_launch'], r['avg_us']):.4f} (avg {r['avg_us']} us, median "
                                  f"{r['median_us']} us) | {r['kernel']} grid {r['grid']} x{r['calls']} |")
     lines += ["", "hot rows include the untimed warm-up launches; cold rows are the launches right after bench's "
               "512 MiB flush kernel.  CG: span = the timed solve's first-to-last loop-kernel time / iterations "
