@@ -1377,7 +1377,7 @@ __device__ __forceinline__ void cg1_publish(const TileArgs &a, SM &sm, int slot,
 // reduced and stored; slot 5 holds the CU (HW_ID) that ran the tile.
 constexpr int kTileStamps = 6;
 template <int IPT, int MODE, bool NT, int TB = kBlock, bool BLK = true, bool FIX = true, bool STAMP = false>
-__global__ __launch_bounds__(TB) void k_spmv_tile(TileArgs a)
+__global__ __launch_bounds__(TB) __attribute__((amdgpu_waves_per_eu(STAMP ? 8 : 1))) void k_spmv_tile(TileArgs a)
 {
     static_assert(TB == kBlock || MODE == kModeSpmv, "one-wave tiles run the plain SpMV only");
     constexpr bool CG = MODE == kModeCg;

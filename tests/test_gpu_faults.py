@@ -119,3 +119,53 @@ def test_dirty_tickets_mechanism(orc, monkeypatch, value, capsys):
               f"max history deviation {dev:.3e}")
     assert it != it_o or dev > 1e-10
     d.close()
+
+
+_PIPE_FAULT_CHILD = r"""
+import sys, numpy as np
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+import mspmv
+from test_gpu_cg import big_window_case
+a = big_window_case()
+b = np.random.default_rng(5).uniform(-1, 1, a.num_rows)
+with mspmv.GpuCsr(a) as g:
+    g.test_poison_tickets(int(sys.argv[4]), mspmv.POISON_FILL)
+    try:
+        g.cg_single(b, 150, 1e-30, hist_cap=150)
+        status = 0
+    except mspmv.MspmvError as e:
+        status = e.status
+    kern = g.cg_kernel_name()
+    x, it, h, st = g.cg_single(b, 150, 1e-30, hist_cap=150)
+np.savez(sys.argv[3], status=status, x=x, it=it, h=h, st=st, kern=np.array(kern))
+"""
+
+
+@pytest.mark.parametrize("value", [32, 0x7FFFFFFF])
+def test_poisoned_tickets_pipelined_windows(orc, tmp_path, value):
+    """The pipelined single-RHS CG on the offset windows past the consumer limit (1.1 M rows: 4,297 window
+    workgroups, so k_cg1_dia folds its p.Ap partials one level by group tickets before k_cg1_update sums
+    them) with every fold ticket dirty: MSPMV_ERR_FAULT, then a clean solve equal to the oracle's.  In a child
+    process (MSPMV_CG_RESIDENT=0 and MSPMV_DIA=1 read fresh)."""
+    import os
+    import subprocess
+    import sys
+    import mspmv
+    from test_gpu_cg import big_window_case, iter_match
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = str(tmp_path / "f.npz")
+    e = dict(os.environ, MSPMV_CG_RESIDENT="0", MSPMV_DIA="1")
+    r = subprocess.run([sys.executable, "-c", _PIPE_FAULT_CHILD, os.path.join(root, "sparse-matrix-linear-equations_amd"),
+                        os.path.join(root, "tests"), out, str(value)], env=e, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = np.load(out)
+    assert "k_cg1_dia" in str(d["kern"]), str(d["kern"])
+    assert int(d["status"]) == mspmv.FAULT
+    a = big_window_case()
+    b = np.random.default_rng(5).uniform(-1, 1, a.num_rows)
+    xo, it_o, ho = orc.cg_single(a, b, 150, 1e-30, hist_cap=150)
+    assert int(d["st"]) == 0 and iter_match(int(d["it"]), it_o, ho, 1e-30)
+    k = min(len(d["h"]), len(ho))
+    np.testing.assert_allclose(d["h"][:k], ho[:k], rtol=0, atol=1e-10)
+    assert np.linalg.norm(d["x"] - xo) <= 1e-8 * np.linalg.norm(xo)

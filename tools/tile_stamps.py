@@ -9,6 +9,10 @@ flush (cold, as the bench prices the fraction), this prints one JSON object: til
 the first tile's entry to the last tile's end, tile-lifetime quantiles, the median of each phase, the
 resident-tile profile over the span (how many tiles are live at once, per 1 us), and the tail after the
 last tile entered.
+The stamped instantiation is held to the production kernel's 8 workgroups per CU (amdgpu_waves_per_eu(8):
+64 VGPRs, no spills; round 6's first stamped build held 70 VGPRs and ran 7 per CU, so its cant profile had
+196 tiles in a second generation the production kernel does not have).  Dictionary tiles stage in one pass
+and record no stamp 1: their "issue" phase is 0 and "stream_and_gathers_land" covers entry -> products in LDS.
   usage: python tools/tile_stamps.py [--device D] [--reps N]
 """
 import argparse
@@ -30,6 +34,9 @@ TICK_US = 0.01  # wall_clock64: 100 MHz
 
 def analyse(st):
     t0 = st[:, 0].astype(np.int64)
+    st = st.copy()
+    no_issue = st[:, 1] == 0  # dictionary tiles stage in one pass (no stamp 1): entry -> products in LDS whole
+    st[no_issue, 1] = st[no_issue, 0]
     ph = np.diff(st[:, :5].astype(np.int64), axis=1) * TICK_US  # [tiles][4] us
     life = (st[:, 4].astype(np.int64) - t0) * TICK_US
     start, end = int(t0.min()), int(st[:, 4].max())
@@ -38,7 +45,8 @@ def analyse(st):
     live = [int(np.sum((t0 <= g) & (st[:, 4].astype(np.int64) > g))) for g in grid]
     last_entry = (int(t0.max()) - start) * TICK_US
     cus = len(np.unique(st[:, 5] & 0xFFFF))
-    return {"tiles": int(st.shape[0]), "cus_seen": cus, "span_us": round(span, 2),
+    return {"tiles": int(st.shape[0]), "tiles_without_issue_stamp": int(no_issue.sum()), "cus_seen": cus,
+            "max_resident": int(max(live)) if live else 0, "span_us": round(span, 2),
             "tile_life_us": {q: round(float(np.percentile(life, p)), 2) for q, p in
                              (("p10", 10), ("median", 50), ("p90", 90), ("max", 100))},
             "phase_median_us": {"issue": round(float(np.median(ph[:, 0])), 2),
