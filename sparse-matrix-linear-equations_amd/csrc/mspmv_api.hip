@@ -622,6 +622,24 @@ static mspmv_status spmv_slab_decide(mspmv_handle_s *h, const TilePlan *wg)
     }
     if (!cand)
         return MSPMV_OK;
+    if (sw < 0 && (double)h->nnz >= kSlabAutoNnzPerBlock * kSlabBlocksPerCu * h->num_cus) {
+        // line-bound gathers over a band (rows whose columns scatter within a window of a few slabs): the
+        // sliced-ELL kernel with ONE column group -- whole-row blocks, each staging only its band's slabs --
+        // before the merge-path slab blocks: bench's scattered band 41.5-42.0 -> 36.3 us (r06r / r06t, with slabs
+        // cut from each block's first column; with the power-law variant's 4 groups three of every four blocks of
+        // a band would be empty: 118 us, r05).  At the slab blocks' own size bar (cant, 4 M nonzeros, stays on the
+        // tiles: 14.2 us on these against 13.9)
+        TilePlan q;
+        const mspmv_status st = build_slab_plan(h, q, kSellAutoNnzPerBlock, 2, true, 1);
+        if (st == MSPMV_OK && q.slab->x_bytes_per_nnz <= kSlabAutoBytes) {
+            h->plans.emplace(kSlabPlanKey, q);
+            h->spmv_slab = 1;
+            return MSPMV_OK;
+        }
+        free_plan(q);  // optional plan: any failure keeps trying the slab blocks, then the tiles
+        set_error("");
+        (void)hipGetLastError();
+    }
     TilePlan p;
     // automatic: the blocks-per-nonzero test runs inside the builder before anything past the bounds is
     // copied or allocated, and any failure (an allocation near capacity included) means "no slab plan":

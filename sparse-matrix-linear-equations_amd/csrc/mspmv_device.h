@@ -37,8 +37,8 @@ __device__ __forceinline__ void store_sc1_2(double *p, double2 v)
 // written what the final arrival will read with agent-scope (sc1, write-through) stores and drained them
 // (s_waitcnt vmcnt(0)) before arriving, and the final arrival reads with agent-scope loads.
 // RELEASE: the fetch_add is also a release at agent scope, the memory model's own form of that order --
-// on gfx950 a buffer_wbl2 (the XCD's whole L2 written back) per arrival.  The folds of few workgroups
-// (k_fold_dot, rows split between tiles) take it; the streaming kernels, whose L2 holds the vectors they
+// on gfx950 a buffer_wbl2 (the XCD's whole L2 written back) per arrival.  The fold of few workgroups
+// (k_fold_dot) takes it; rows split between tiles do not (close_split_rows); the streaming kernels, whose L2 holds the vectors they
 // just wrote, keep the drained-store form (measured with the release on every arrival, r06a: configs[4]'s
 // CG iteration +4.5 %, the sliced-ELL SpMV +10 %).  The arrival that draws `last` -- the group's final
 // one -- takes an agent-scope acquire fence before it reads the others' stores; the other arrivals read
@@ -102,10 +102,15 @@ __device__ __forceinline__ void close_split_rows(const A &a, int t, int4 fx, int
         __syncthreads();
     }
     if (threadIdx.x == 0) {
+        // The drained-store form (the carries and the head were published with drained write-through stores
+        // above): a release is a write-back of the XCD's whole L2 per arrival, and on the one-wave tiles of a
+        // power-law matrix -- thousands of rows split over 2 to ~425 tiles -- releases took the skewed SpMV from
+        // 80 to 525 us (r06t), still 291 us with releases kept for rows of <= 8 carries (r06u).
+        auto arrive = [&](unsigned *tk, int carries) { return ticket_arrive<false>(tk, (unsigned)carries, a.fault); };
         int f0 = -1, f1 = -1;
-        if (fx.x >= 0 && ticket_arrive<true>(&a.fix_cnt[fx.x], (unsigned)fx.y, a.fault))
+        if (fx.x >= 0 && arrive(&a.fix_cnt[fx.x], fx.y))
             f0 = fx.x;
-        if (fx.z > 0 && ticket_arrive<true>(&a.fix_cnt[t], (unsigned)fx.z, a.fault))
+        if (fx.z > 0 && arrive(&a.fix_cnt[t], fx.z))
             f1 = t;
         s_fin[0] = f0;
         s_fin[1] = f1;

@@ -77,7 +77,7 @@ struct SlabData {
     int groups = 1;                     // SpMV column groups (cfg 1): blocks = row blocks x groups
     double *d_part = nullptr;           // [groups][m] the groups' partial row sums (groups > 1)
     unsigned *d_gcnt = nullptr;         // [row blocks] tickets of the fold (self-resetting)
-    // sliced-ELL (cfg 2): d_chunk holds the (block, slab) segments {slab, slice0, slice1, piece0} (+ sentinel)
+    // sliced-ELL (cfg 2): d_chunk holds the (block, slab) segments {first column, slice0, slice1, piece0} (+ sentinel)
     int2 *d_slice = nullptr;            // [slices] {value base, slots per lane | medium << 16}
     unsigned *d_sent = nullptr;         // [slices][64] row in block | run length << 16 (0: no run)
     int4 *d_long = nullptr;             // [long-run pieces] {value base, length <= 512, row in block,
@@ -353,7 +353,7 @@ constexpr int kRunPlanKey = -2;  // the run-balanced node-block SpMV plan (mspmv
 // min_nnz_per_block nonzeros on average; p is freed by the caller on any error.
 // cfg: the block shape (kSlabCfgs); groups (always for cfg 1): column-group blocks instead of merge-path ones.
 mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p, double min_nnz_per_block = 0.0, int cfg = 0,
-                             bool groups = false);
+                             bool groups = false, int num_groups = 0);  // num_groups 0: MSPMV_SLAB_GROUPS or kSlabGroups
 void free_slab(SlabData *s);
 hipError_t launch_slab(mspmv_handle_s *h, const TilePlan &plan, const double *d_x, double *d_y);
 std::string slab_kernel_name(const mspmv_handle_s *h);  // the handle's plain-SpMV slab plan's kernel

@@ -284,8 +284,7 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
                          __builtin_amdgcn_readfirstlane(c.z), __builtin_amdgcn_readfirstlane(c.w));
     };
     double xq[XPT];
-    auto fetch_x = [&](int slab) {
-        const int c0 = slab * C.cols;
+    auto fetch_x = [&](int c0) {  // the segment's slab of x: C.cols columns from its first column c0
 #pragma unroll
         for (int j = 0; j < XPT; ++j) {
             const int col = c0 + tid + j * TB;
@@ -807,28 +806,32 @@ struct SellBlockOut {
 static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, const std::vector<double> &va, int r0,
                        int r1, int lo, int hi, SellBlockOut &o)
 {
+    // Slabs are cut from the block's own first column (round 6), not from column 0: a band block's
+    // 2 x band + rows columns then take ceil(width / W) slabs, where globally aligned ones took one more about
+    // half the time.
     const int W = kSlabCfgs[2].cols;
     std::vector<int> ks, kr;
-    int smin = 0x7fffffff, smax = -1;
+    int cmin = 0x7fffffff, cmax = -1;
     for (int r = r0; r < r1; ++r)
         for (int k = ro[(size_t)r]; k < ro[(size_t)r + 1]; ++k)
             if (ci[(size_t)k] >= lo && ci[(size_t)k] < hi) {
                 ks.push_back(k);
                 kr.push_back(r - r0);
-                smin = std::min(smin, ci[(size_t)k] / W);
-                smax = std::max(smax, ci[(size_t)k] / W);
+                cmin = std::min(cmin, ci[(size_t)k]);
+                cmax = std::max(cmax, ci[(size_t)k]);
             }
     if (ks.empty())
         return;
-    const int ns = smax - smin + 1;
+    auto slab_of = [&](int c) { return (c - cmin) / W; };
+    const int ns = slab_of(cmax) + 1;
     std::vector<int> off((size_t)ns + 1, 0);
     for (int k : ks)
-        ++off[(size_t)(ci[(size_t)k] / W - smin) + 1];
+        ++off[(size_t)slab_of(ci[(size_t)k]) + 1];
     for (int s = 0; s < ns; ++s)
         off[(size_t)s + 1] += off[(size_t)s];
     std::vector<int> ord(ks.size()), put(off.begin(), off.end() - 1);
     for (size_t i = 0; i < ks.size(); ++i)
-        ord[(size_t)put[(size_t)(ci[(size_t)ks[i]] / W - smin)]++] = (int)i;  // stable: CSR order per slab
+        ord[(size_t)put[(size_t)slab_of(ci[(size_t)ks[i]])]++] = (int)i;  // stable: CSR order per slab
     struct Run {
         int row, first, len;
     };
@@ -844,11 +847,11 @@ static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, c
             runs.push_back({kr[(size_t)ord[(size_t)q]], q, e - q});
             q = e;
         }
-        const int slab = smin + s;
+        const int base = cmin + s * W;  // the segment's first column
         auto put_val = [&](size_t at, int q) {
             const int k = ks[(size_t)ord[(size_t)q]];
             o.val[at] = va[(size_t)k];
-            o.col[at] = (unsigned short)(ci[(size_t)k] - slab * W);
+            o.col[at] = (unsigned short)(ci[(size_t)k] - base);
         };
         const int slice0 = (int)o.slices.size(), long0 = (int)o.longs.size();
         std::vector<Run> shorts, mediums;
@@ -909,7 +912,7 @@ static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, c
             }
             o.slices.push_back(make_int2((int)base, Lm | (1 << 16)));
         }
-        o.segs.push_back(make_int4(slab, slice0, (int)o.slices.size(), long0));
+        o.segs.push_back(make_int4(base, slice0, (int)o.slices.size(), long0));
         o.staged += (long long)W * 8;
     }
 }
@@ -991,12 +994,14 @@ static mspmv_status sell_finish(mspmv_handle_s *h, TilePlan &p, const std::vecto
 // R = the resident blocks / groups, each crossed with the groups' column ranges (consecutive slabs);
 // block t = row block t / G, group t % G.  The reported bounds give each row block to its first group
 // (the others span nothing), so the plan reads as monotone merge-path tiles.
-static mspmv_status build_slab_group_plan(mspmv_handle_s *h, TilePlan &p, double min_nnz_per_block, int cfg)
+static mspmv_status build_slab_group_plan(mspmv_handle_s *h, TilePlan &p, double min_nnz_per_block, int cfg,
+                                          int num_groups)
 {
     const SlabCfg &C = kSlabCfgs[cfg];
     const int nslabs = (h->n + C.cols - 1) / C.cols;
-    const char *ge = getenv("MSPMV_SLAB_GROUPS");  // lab: the column-group count
-    const int G = std::max(1, std::min(std::min(ge && *ge ? atoi(ge) : kSlabGroups, kSlabMaxGroups), nslabs));
+    const char *ge = getenv("MSPMV_SLAB_GROUPS");  // lab: the column-group count (over num_groups too)
+    const int want = ge && *ge ? atoi(ge) : num_groups > 0 ? num_groups : kSlabGroups;
+    const int G = std::max(1, std::min(std::min(want, kSlabMaxGroups), nslabs));
     const int spg = (nslabs + G - 1) / G;  // slabs per group
     const long long R0 = std::max(1, h->num_cus * C.per_cu / G);
     std::vector<int> ro, ci;
@@ -1102,12 +1107,13 @@ static mspmv_status build_slab_group_plan(mspmv_handle_s *h, TilePlan &p, double
     return slab_finish(h, p, cfg, G, blk, outs, oval, ocol, hb, hs);
 }
 
-mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p, double min_nnz_per_block, int cfg, bool groups)
+mspmv_status build_slab_plan(mspmv_handle_s *h, TilePlan &p, double min_nnz_per_block, int cfg, bool groups,
+                             int num_groups)
 {
     if (h->m <= 0 || h->nnz <= 0)
         return MSPMV_ERR_UNSUPPORTED;
     if (cfg >= 1 || groups)
-        return build_slab_group_plan(h, p, min_nnz_per_block, cfg);
+        return build_slab_group_plan(h, p, min_nnz_per_block, cfg, num_groups);
     std::vector<int2> hb;
     std::vector<unsigned char> hs;
     long long step = 0;

@@ -7,8 +7,9 @@ handle first decides its plain-SpMV plan) on shapes with
 scattered, skewed, split, empty and rectangular rows; checked against the oracle's SpmvGold
 (cpu_spmv.cpp:241-265) within the reordering bound (the slab order is a reordered CSR sum:
 mspmv_tile_modes reports every block as 255), bit-identical on repeats and under a CU limit's
-rebuilt plan against the oracle again.  The default choice (scattered band: slab; large power-law:
-sliced-ELL column groups; FEM, stencil, cant, small power-law: tiles) is checked on its own.
+rebuilt plan against the oracle again.  The default choice (scattered band: sliced-ELL with one column
+group; large power-law: sliced-ELL with four; FEM, stencil, cant, small power-law: tiles) is checked on its
+own.
 """
 import numpy as np
 import pytest
@@ -19,14 +20,20 @@ from gpu_common import check_parity
 pytestmark = pytest.mark.gpu
 
 
-SLAB_KERNEL = {"1": "k_spmv_slab<{nt},0>", "2": "k_spmv_slab<{nt},1>", "4": "k_spmv_sell<{nt}>"}
+SLAB_KERNEL = {"1": "k_spmv_slab<{nt},0>", "2": "k_spmv_slab<{nt},1>", "4": "k_spmv_sell<{nt}>",
+               "4g1": "k_spmv_sell<{nt}>"}
 
 
-@pytest.fixture(params=["1", "2", "4"], ids=["band", "groups", "sell"])
+@pytest.fixture(params=["1", "2", "4", "4g1"], ids=["band", "groups", "sell", "sell_one_group"])
 def slab_on(monkeypatch, request):
     """1: merge-path blocks (kSlabCfgs[0]); 2: column-group blocks (kSlabCfgs[1], partials folded);
-    4: the column-group blocks in sliced-ELL form (k_spmv_sell)."""
-    monkeypatch.setenv("MSPMV_SPMV_SLAB", request.param)
+    4: the column-group blocks in sliced-ELL form (k_spmv_sell, 4 groups); 4g1: the same with one column
+    group (whole-row blocks staging their own slabs: the default for line-bound bands, round 6)."""
+    monkeypatch.setenv("MSPMV_SPMV_SLAB", request.param[0])
+    if request.param == "4g1":
+        monkeypatch.setenv("MSPMV_SLAB_GROUPS", "1")
+    else:
+        monkeypatch.delenv("MSPMV_SLAB_GROUPS", raising=False)
     return request.param
 
 
@@ -108,12 +115,14 @@ def test_slab_device_buffers_and_cg_unaffected(orc, slab_on):
 
 
 def test_slab_default_choice(orc, monkeypatch):
-    """The default plain-SpMV choice: scattered band -> slab blocks; power-law rows at >= 12,288
-    nonzeros per CU -> the sliced-ELL column groups (checked against the oracle here too); a smaller
-    power-law matrix -> one-wave tiles; FEM, stencil, cant -> tiles."""
+    """The default plain-SpMV choice: scattered band at >= 12,288 nonzeros per CU -> the sliced-ELL kernel
+    with one column group (round 6; the slab blocks before); power-law rows at >= 12,288 nonzeros per CU ->
+    the sliced-ELL column groups (both checked against the oracle here too); a smaller power-law matrix ->
+    one-wave tiles; FEM, stencil, cant -> tiles."""
     monkeypatch.delenv("MSPMV_SPMV_SLAB", raising=False)
+    monkeypatch.delenv("MSPMV_SLAB_GROUPS", raising=False)
     want = {
-        "scatter": (lambda: scatter_band(217918, 53, 10000, 77), "k_spmv_slab<"),
+        "scatter": (lambda: scatter_band(217918, 53, 10000, 77), "k_spmv_sell<"),
         "powerlaw": (lambda: mspmv.CsrMatrix.synth_powerlaw(120000, 120000, 4000000, exponent=1.2, seed=9),
                      "k_spmv_sell<"),
         "powerlaw_small": (lambda: mspmv.CsrMatrix.synth_powerlaw(60000, 60000, 1800000, exponent=1.2, seed=7),
@@ -130,7 +139,7 @@ def test_slab_default_choice(orc, monkeypatch):
                 assert not k.startswith(("k_spmv_slab<", "k_spmv_sell<")), (name, k)
             else:
                 assert k.startswith(prefix), (name, k)
-            if name == "powerlaw":
+            if name in ("powerlaw", "scatter"):
                 x = np.random.default_rng(4).uniform(-1, 1, a.num_cols)
                 y = g.spmv(x)
                 check_parity(a, y, orc.spmv_gold(a, x), x, g.tile_plan(1), 1)
