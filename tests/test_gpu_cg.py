@@ -341,15 +341,27 @@ _PIPE_CHILD = r"""
 import sys, numpy as np
 sys.path[:0] = [sys.argv[1], sys.argv[2]]
 import mspmv
-from test_gpu_cg import spd_cases, big_window_case
+from test_gpu_cg import spd_cases, big_window_case, perturbed_spd
 name, tol, cap = sys.argv[4], float(sys.argv[5]), int(sys.argv[6])
-a = big_window_case() if name == "big2d" else spd_cases()[name]()
+a = big_window_case() if name == "big2d" else perturbed_spd() if name == "perturbed27" else spd_cases()[name]()
 b = np.random.default_rng(5).uniform(-1, 1, a.num_rows)
 with mspmv.GpuCsr(a) as g:
     x, it, h, st = g.cg_single(b, cap, tol, hist_cap=cap)
     kern = g.cg_kernel_name()
 np.savez(sys.argv[3], x=x, it=it, h=h, st=st, kern=np.array(kern))
 """
+
+
+def perturbed_spd():
+    """The 27-point stencil with off-pattern columns, symmetrised and made diagonally dominant (SPD): its
+    windows carry a remainder (2,276 entries at this size), which k_cg1_dia sums after each row's offsets."""
+    import scipy.sparse as sp
+    a = mspmv.CsrMatrix.synth_stencil_perturbed((24, 22, 20), seed=2, extra_frac=0.02, long_frac=0.01)
+    A = sp.csr_matrix((a.values, a.column_indices, a.row_offsets), shape=(a.num_rows, a.num_cols))
+    S = (abs(A) + abs(A).T) * 0.5
+    S = sp.csr_matrix(-S + sp.diags(np.asarray(abs(S).sum(axis=1)).ravel() * 2 + 1.0))
+    S.sort_indices()
+    return mspmv.CsrMatrix.from_arrays(S.shape[1], S.indptr.astype(np.int32), S.indices.astype(np.int32), S.data)
 
 
 def big_window_case():
@@ -360,7 +372,8 @@ def big_window_case():
 
 @pytest.mark.parametrize("tiles", [False, True])
 @pytest.mark.parametrize("name,tol,cap", [("fem2d", 1e-10, 5000), ("fem2d_partial_row", 1e-10, 5000),
-                                          ("stencil27", 1e-10, 5000), ("big2d", 1e-30, 150)])
+                                          ("stencil27", 1e-10, 5000), ("perturbed27", 1e-10, 5000),
+                                          ("big2d", 1e-30, 150)])
 def test_cg_pipelined_on_windows_vs_oracle(orc, tmp_path, tiles, name, tol, cap):
     """The two-kernel pipelined single-RHS CG (MSPMV_CG_RESIDENT=0) with its SpMV on the offset windows
     (k_cg1_dia: p = r + beta p_old formed at each {r, p} load, Ap, p.Ap per workgroup; MSPMV_DIA=1 puts even
@@ -379,7 +392,9 @@ def test_cg_pipelined_on_windows_vs_oracle(orc, tmp_path, tiles, name, tol, cap)
     d = np.load(out)
     kern = str(d["kern"])
     assert ("k_spmv_tile MODE 1" if tiles else "k_cg1_dia") in kern, kern
-    a = big_window_case() if name == "big2d" else spd_cases()[name]()
+    a = big_window_case() if name == "big2d" else perturbed_spd() if name == "perturbed27" else spd_cases()[name]()
+    if name == "perturbed27" and not tiles:
+        assert mspmv.offset_windows(a)["remainder"] > 0  # the windows' remainder path is exercised
     b = np.random.default_rng(5).uniform(-1, 1, a.num_rows)
     xo, it_o, ho = orc.cg_single(a, b, cap, tol, hist_cap=cap)
     it_g, st = int(d["it"]), int(d["st"])
