@@ -7,6 +7,8 @@
 
 #include <cstdio>
 #include <vector>
+#include <cstdlib>
+#include <algorithm>
 
 #define CK(x)                                                                                      \
     do {                                                                                           \
@@ -107,8 +109,14 @@ __global__ __launch_bounds__(256) void k_glds(const v2d *__restrict__ a, long lo
         out[0] = 1.0;
 }
 
-int main()
+int main(int argc, char **argv)
 {
+    std::vector<size_t> sizes = {(size_t)1 << 30, (size_t)142651548};
+    if (argc > 1) {  // sizes in bytes (copies rotate through > 512 MiB, so every launch reads from HBM)
+        sizes.clear();
+        for (int i = 1; i < argc; ++i)
+            sizes.push_back((size_t)atoll(argv[i]));
+    }
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     double *out;
@@ -116,8 +124,8 @@ int main()
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (size_t bytes : {(size_t)1 << 30, (size_t)142651548}) {
-        const int NB = bytes < ((size_t)256 << 20) ? 4 : 1;
+    for (size_t bytes : sizes) {
+        const int NB = bytes < ((size_t)256 << 20) ? (int)std::max<size_t>(4, ((size_t)600 << 20) / bytes + 1) : 1;
         const long long n16 = (long long)(bytes / 16);
         std::vector<v2d *> bufs(NB);
         for (auto &p : bufs) {
