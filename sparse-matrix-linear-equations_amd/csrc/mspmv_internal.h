@@ -78,8 +78,8 @@ struct SlabData {
     double *d_part = nullptr;           // [groups][m] the groups' partial row sums (groups > 1)
     unsigned *d_gcnt = nullptr;         // [row blocks] tickets of the fold (self-resetting)
     // sliced-ELL (cfg 2): d_chunk holds the (block, slab) segments {first column, slice0, slice1, piece0} (+ sentinel)
-    int2 *d_slice = nullptr;            // [slices] {value base, slots per lane | medium << 16}
-    unsigned *d_sent = nullptr;         // [slices][64] row in block | run length << 16 (0: no run)
+    int4 *d_slice = nullptr;            // [slices] {value base, slots per lane | medium << 16, run-word base, 0}
+    unsigned *d_sent = nullptr;         // run words: row in block | run length << 16 (0: no run), 64 per short-run slice, 8 per medium
     int4 *d_long = nullptr;             // [long-run pieces] {value base, length <= 512, row in block,
                                         //  the run's first piece in the segment | pieces << 16}
     int num_chunks = 0, num_entries = 0;

@@ -43,7 +43,7 @@ struct SlabArgs {
     int m;
     double *part;               // [groups][m] partial row sums (groups > 1)
     unsigned *gcnt;             // [row blocks] fold tickets
-    const int2 *slice;          // sliced-ELL (k_spmv_sell): SlabData::d_slice, d_sent, d_long
+    const int4 *slice;          // sliced-ELL (k_spmv_sell): SlabData::d_slice, d_sent, d_long
     const unsigned *sent;
     const int4 *lng;
     // split rows (close_split_rows reads these names)
@@ -295,18 +295,25 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
         double v[8];
         unsigned short c[8];
     };
-    auto meta = [&](int qq, int2 &hq, unsigned &ev) {  // qq < 0: none
-        hq = qq >= 0 ? a.slice[qq] : make_int2(0, 0);
-        ev = qq >= 0 ? a.sent[(size_t)qq * 64 + lane] : 0u;
+    auto meta = [&](int qq) { return qq >= 0 ? a.slice[qq] : make_int4(0, 0, 0, 0); };  // qq < 0: none
+    auto runword = [&](const int4 &hq) {  // this lane's run: one word per lane (short runs) or per 8 lanes (medium)
+        return (hq.y & 0xffff) ? a.sent[hq.z + ((hq.y >> 16) ? lane >> 3 : lane)] : 0u;
     };
-    auto load8 = [&](const int2 &hq, Sl &d) {  // slot pairs: one 16-B value load, one 4-B column load
+    auto load8 = [&](const int4 &hq, Sl &d) {  // slot pairs: one 16-B value load, one 4-B column load; an odd last slot alone
+        const int Lm = hq.y & 0xffff, pairs = Lm >> 1;  // wave-uniform
         const v2d_t *vp = reinterpret_cast<const v2d_t *>(a.val + hq.x) + lane;
         const unsigned *cp = reinterpret_cast<const unsigned *>(a.col + hq.x) + lane;
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
-            const bool in = 2 * p < (hq.y & 0xffff);  // wave-uniform: the slice's slot pairs
-            const v2d_t v = in ? slab_stream<NT>(vp + 64 * p) : v2d_t{0.0, 0.0};
-            const unsigned c = in ? slab_stream<NT>(cp + 64 * p) : 0u;
+            v2d_t v = v2d_t{0.0, 0.0};
+            unsigned c = 0u;
+            if (p < pairs) {
+                v = slab_stream<NT>(vp + 64 * p);
+                c = slab_stream<NT>(cp + 64 * p);
+            } else if (p == pairs && (Lm & 1)) {
+                v.x = slab_stream<NT>(a.val + hq.x + 128 * p + lane);
+                c = slab_stream<NT>(a.col + hq.x + 128 * p + lane);
+            }
             d.v[2 * p] = v.x;
             d.v[2 * p + 1] = v.y;
             d.c[2 * p] = (unsigned short)(c & 0xffffu);
@@ -332,8 +339,8 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
         }
     };
     int qa = -1, sa = -1, qb = -1, sb = -1;
-    int2 h0 = make_int2(0, 0), h1 = make_int2(0, 0);
-    unsigned e0 = 0, e1 = 0;
+    int4 h0 = make_int4(0, 0, 0, 0), h1 = make_int4(0, 0, 0, 0);
+    unsigned e0 = 0;
     Sl d0, d1;
     if (bd.z < bd.w)
         fetch_x(segd(bd.z).x);
@@ -371,23 +378,23 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
                 lpart[u - p0] = s;
         }
         // slices, software-pipelined per wave and across segments: while slice qa computes, the wave's
-        // next slice's values and the one after's header and runs are in flight -- at a segment's end
+        // next slice's values and run words and the one after's header are in flight -- at a segment's end
         // those are the next segment's first slices, so the pipeline refills during the x-stage barriers
         if (sa != sg) {  // prime: the wave's first slice of this segment
             qa = seg.y + wave < seg.z ? seg.y + wave : -1;
             sa = sg;
-            meta(qa, h0, e0);
+            h0 = meta(qa);
             load8(h0, d0);
+            e0 = runword(h0);
             nxt(qa, sa, qb, sb);
-            meta(qb, h1, e1);
+            h1 = meta(qb);
         }
         while (qa >= 0 && sa == sg) {  // wave-uniform
             load8(h1, d1);
+            const unsigned e1 = runword(h1);
             int qc, sc;
-            int2 h2;
-            unsigned e2;
             nxt(qb, sb, qc, sc);
-            meta(qc, h2, e2);
+            const int4 h2 = meta(qc);
             const int row = (int)(e0 & 0xffffu), len = (int)(e0 >> 16);
             if (!(h0.y >> 16)) {  // wave-uniform: a slice of 64 short runs, lane = run, in CSR order
                 double acc = len > 0 ? yacc[row] : 0.0;
@@ -419,7 +426,6 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
             qb = qc;
             sb = sc;
             h1 = h2;
-            e1 = e2;
         }
         if (p1 > p0) {  // block-uniform: each run's pieces, in order, onto its row
             __syncthreads();
@@ -790,11 +796,13 @@ static mspmv_status slab_finish(mspmv_handle_s *h, TilePlan &p, int cfg, int gro
 // slab order, its runs of one row (CSR order); runs longer than kSellLongRun stored contiguously and
 // listed apart in pieces of <= 512 values, the others sorted by length (longest first, rows ascending among equals) and cut into
 // slices of 64, value j of the slice's run i at slot j of lane i -- slots in pairs, pair p of lane i at
-// 2 (64 p + i): one 16-B value load and one 4-B column load per pair (slots past a run's length: zeros, never
-// added).  Bases relative to the block.
+// 2 (64 p + i): one 16-B value load and one 4-B column load per pair; an odd last slot alone, lane i at
+// 128 p + i (slots past a run's length: zeros, never added).  Each slice's header {value base, slots per
+// lane | medium << 16, run-word base}; run words (row | length << 16) one per lane for slices of short
+// runs, one per run (8) for medium ones.  Bases relative to the block.
 struct SellBlockOut {
     std::vector<int4> segs;
-    std::vector<int2> slices;
+    std::vector<int4> slices;
     std::vector<unsigned> sents;
     std::vector<int4> longs;
     std::vector<double> val;
@@ -853,6 +861,11 @@ static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, c
             o.val[at] = va[(size_t)k];
             o.col[at] = (unsigned short)(ci[(size_t)k] - base);
         };
+        // slot s of lane i in a slice of Lm slots per lane: pairs, then an odd last slot alone
+        auto slot_at = [](size_t b, int Lm, int s, int i) {
+            const int pairs = Lm >> 1;
+            return s < 2 * pairs ? b + (size_t)(s >> 1) * 128 + 2 * i + (s & 1) : b + (size_t)pairs * 128 + i;
+        };
         const int slice0 = (int)o.slices.size(), long0 = (int)o.longs.size();
         std::vector<Run> shorts, mediums;
         for (const Run &r : runs) {
@@ -877,10 +890,10 @@ static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, c
         std::stable_sort(shorts.begin(), shorts.end(), [](const Run &x, const Run &y) { return x.len > y.len; });
         for (size_t i0 = 0; i0 < shorts.size(); i0 += 64) {
             const int n = (int)std::min<size_t>(64, shorts.size() - i0);
-            const int Lm = shorts[i0].len;
+            const int Lm = shorts[i0].len, e0 = (int)o.sents.size();
             const size_t base = o.val.size();
-            o.val.resize(base + (size_t)(Lm + (Lm & 1)) * 64, 0.0);
-            o.col.resize(base + (size_t)(Lm + (Lm & 1)) * 64, 0);
+            o.val.resize(base + (size_t)Lm * 64, 0.0);
+            o.col.resize(base + (size_t)Lm * 64, 0);
             for (int i = 0; i < 64; ++i) {
                 if (i >= n) {
                     o.sents.push_back(0u);
@@ -888,29 +901,28 @@ static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, c
                 }
                 const Run &r = shorts[i0 + (size_t)i];
                 for (int j = 0; j < r.len; ++j)
-                    put_val(base + (size_t)(j / 2) * 128 + 2 * i + (j & 1), r.first + j);
+                    put_val(slot_at(base, Lm, j, i), r.first + j);
                 o.sents.push_back((unsigned)r.row | ((unsigned)r.len << 16));
             }
-            o.slices.push_back(make_int2((int)base, Lm));
+            o.slices.push_back(make_int4((int)base, Lm, e0, 0));
         }
-        // medium runs: 8 per slice, 8 lanes each (slot pairs as above) -- value j of the slice's run r at slot j / 8, lane
+        // medium runs: 8 per slice, 8 lanes each (slots as above) -- value j of the slice's run r at slot j / 8, lane
         // 8 r + j % 8 (header length | 1 << 16: slots per lane, the medium flag)
         std::stable_sort(mediums.begin(), mediums.end(), [](const Run &x, const Run &y) { return x.len > y.len; });
         for (size_t i0 = 0; i0 < mediums.size(); i0 += 8) {
             const int n = (int)std::min<size_t>(8, mediums.size() - i0);
-            const int Lm = (mediums[i0].len + 7) / 8;
+            const int Lm = (mediums[i0].len + 7) / 8, e0 = (int)o.sents.size();
             const size_t base = o.val.size();
-            o.val.resize(base + (size_t)(Lm + (Lm & 1)) * 64, 0.0);
-            o.col.resize(base + (size_t)(Lm + (Lm & 1)) * 64, 0);
+            o.val.resize(base + (size_t)Lm * 64, 0.0);
+            o.col.resize(base + (size_t)Lm * 64, 0);
             for (int i = 0; i < 8; ++i) {
                 const Run *r = i < n ? &mediums[i0 + (size_t)i] : nullptr;
                 if (r)
                     for (int j = 0; j < r->len; ++j)
-                        put_val(base + (size_t)(j / 16) * 128 + 2 * (8 * i + j % 8) + (j / 8) % 2, r->first + j);
-                for (int l = 0; l < 8; ++l)
-                    o.sents.push_back(r ? (unsigned)r->row | ((unsigned)r->len << 16) : 0u);
+                        put_val(slot_at(base, Lm, j / 8, 8 * i + j % 8), r->first + j);
+                o.sents.push_back(r ? (unsigned)r->row | ((unsigned)r->len << 16) : 0u);
             }
-            o.slices.push_back(make_int2((int)base, Lm | (1 << 16)));
+            o.slices.push_back(make_int4((int)base, Lm | (1 << 16), e0, 0));
         }
         o.segs.push_back(make_int4(base, slice0, (int)o.slices.size(), long0));
         o.staged += (long long)W * 8;
@@ -934,21 +946,22 @@ static mspmv_status sell_finish(mspmv_handle_s *h, TilePlan &p, const std::vecto
         const int lo = (int)((long long)g * h->n / G), hi = g == G - 1 ? 0x7fffffff : (int)((long long)(g + 1) * h->n / G);
         sell_block(ro, ci, va, rbs[(size_t)rb], rbs[(size_t)rb + 1], lo, hi, outs[(size_t)t]);
     }
-    std::vector<int4> blk((size_t)T), segs, longs;
-    std::vector<int2> slices;
+    std::vector<int4> blk((size_t)T), segs, longs, slices;
     std::vector<unsigned> sents;
     std::vector<double> val;
     std::vector<unsigned short> col;
     long long staged = 0;
     for (int t = 0; t < T; ++t) {
         const SellBlockOut &o = outs[(size_t)t];
-        if (o.too_many || (int)o.segs.size() > kSellMaxSegs || val.size() + o.val.size() > (size_t)0x7fffff00)
+        if (o.too_many || (int)o.segs.size() > kSellMaxSegs || val.size() + o.val.size() > (size_t)0x7fffff00 ||
+            sents.size() + o.sents.size() > (size_t)0x7fffff00)
             return MSPMV_ERR_UNSUPPORTED;
         const int vb = (int)val.size(), sb = (int)slices.size(), lb = (int)longs.size(), g0 = (int)segs.size();
+        const int eb = (int)sents.size();
         for (int4 s : o.segs)
             segs.push_back(make_int4(s.x, s.y + sb, s.z + sb, s.w + lb));
-        for (int2 s : o.slices)
-            slices.push_back(make_int2(s.x + vb, s.y));
+        for (int4 s : o.slices)
+            slices.push_back(make_int4(s.x + vb, s.y, s.z + eb, 0));
         for (int4 l : o.longs)
             longs.push_back(make_int4(l.x + vb, l.y, l.z, l.w));
         sents.insert(sents.end(), o.sents.begin(), o.sents.end());
