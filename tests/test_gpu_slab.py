@@ -89,6 +89,36 @@ def test_slab_parity(orc, slab_on, name):
     assert y3.tobytes() == y4.tobytes()
 
 
+
+@pytest.mark.parametrize("name", ["scatter_band", "powerlaw", "hub_rect"])
+def test_slab_nonfinite_x(orc, slab_on, name):
+    """Inf and NaN in x, column 0 among them (the sliced-ELL pad slots hold value 0 at column 0 and are
+    selected out by their run's length): the oracle's non-finite rows exactly (NaN where it has NaN, the
+    infinities' signs), and every other row bit-equal to the same plan's product with the bad columns
+    zeroed, itself within the reordering bound."""
+    a = CASES[name]()
+    rng = np.random.default_rng(21)
+    x = rng.uniform(-1, 1, a.num_cols)
+    bad = rng.choice(a.num_cols, 6, replace=False)
+    x[bad[:2]] = np.inf
+    x[bad[2:4]] = -np.inf
+    x[bad[4:]] = np.nan
+    x[0] = np.inf
+    clean = np.where(np.isfinite(x), x, 0.0)
+    gold = orc.spmv_gold(a, x)
+    with mspmv.GpuCsr(a) as g:
+        y = g.spmv(x)
+        assert slab_kernel_ok(g.kernel_name(), slab_on), g.kernel_name()
+        yc = g.spmv(clean)
+        check_parity(a, yc, orc.spmv_gold(a, clean), clean, g.tile_plan(1), 1)
+    assert np.array_equal(np.isnan(y), np.isnan(gold))
+    assert np.array_equal(np.isfinite(y), np.isfinite(gold))
+    inf = ~np.isfinite(gold) & ~np.isnan(gold)
+    assert np.array_equal(y[inf], gold[inf])
+    fin = np.isfinite(gold)
+    assert 0 < (~fin).sum() and fin.sum() > 0.5 * fin.size
+    assert y[fin].tobytes() == yc[fin].tobytes()
+
 def test_slab_device_buffers_and_cg_unaffected(orc, slab_on):
     """The slab plan serves the plain product only: the CG on the same handle runs its tile plan."""
     a = scatter_band(20000, 12, 3000, 8)
