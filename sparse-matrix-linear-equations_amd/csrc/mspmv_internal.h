@@ -69,17 +69,20 @@ constexpr int kSellLongRun = 64;     // up to this long 8 per slice (8 lanes eac
                                      // in pieces of <= 512
 constexpr int kSellMaxPieces = 1024;  // long-run pieces per (block, slab) segment (their sums sit in LDS)
 constexpr int kSellMaxSegs = 255;     // segments per block (their descriptors sit in LDS)
+// short runs packed per lane by the slice's longest run (<= 4): {runs per lane K, slots per run}
+constexpr int2 kSellPack[5] = {{1, 1}, {8, 1}, {4, 2}, {2, 3}, {2, 4}};
 constexpr int kSlabLongRun = 64;  // runs longer than this are summed by whole waves (listed first in a chunk)
 struct SlabData {
     int L = 1;                          // 1: the SpMV's plan (k_spmv_slab); 8 / 16: an SpMM plan (k_spmm_slab)
     int cfg = 0;                        // the kernel configuration the plan was cut for (SpMV: kSlabCfgs;
                                         // SpMM: slab_mm_cfg)
     int groups = 1;                     // SpMV column groups (cfg 1): blocks = row blocks x groups
+    bool pack = false;                  // sliced-ELL: short runs packed per lane (column groups > 1; k_spmv_sell<., true>)
     double *d_part = nullptr;           // [groups][m] the groups' partial row sums (groups > 1)
     unsigned *d_gcnt = nullptr;         // [row blocks] tickets of the fold (self-resetting)
     // sliced-ELL (cfg 2): d_chunk holds the (block, slab) segments {first column, slice0, slice1, piece0} (+ sentinel)
     int4 *d_slice = nullptr;            // [slices] {value base, slots per lane | medium << 16, run-word base, 0}
-    unsigned *d_sent = nullptr;         // run words: row in block | run length << 16 (0: no run), 64 per short-run slice, 8 per medium
+    unsigned short *d_sent = nullptr;   // 16-bit run words (mspmv_slab.hip sell_block; 0: no run)
     int4 *d_long = nullptr;             // [long-run pieces] {value base, length <= 512, row in block,
                                         //  the run's first piece in the segment | pieces << 16}
     int num_chunks = 0, num_entries = 0;

@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 namespace mspmv {
@@ -44,7 +45,7 @@ struct SlabArgs {
     double *part;               // [groups][m] partial row sums (groups > 1)
     unsigned *gcnt;             // [row blocks] fold tickets
     const int4 *slice;          // sliced-ELL (k_spmv_sell): SlabData::d_slice, d_sent, d_long
-    const unsigned *sent;
+    const unsigned short *sent;
     const int4 *lng;
     // split rows (close_split_rows reads these names)
     const int2 *bounds;
@@ -257,7 +258,7 @@ __global__ __launch_bounds__(kSlabCfgs[CFG].threads) void k_spmv_slab(SlabArgs a
 // runs follow slab order: within a group the row sum is the CSR-order sum when its columns ascend).
 // Runs longer than kSellLongRun come in pieces of <= 512 values, one wave each (8 loads per lane, xor
 // butterfly) into lpart; after a barrier each run's pieces are added to its row in piece order.
-template <bool NT>
+template <bool NT, bool PACK>
 __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
 {
     constexpr SlabCfg C = kSlabCfgs[2];
@@ -296,8 +297,28 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
         unsigned short c[8];
     };
     auto meta = [&](int qq) { return qq >= 0 ? a.slice[qq] : make_int4(0, 0, 0, 0); };  // qq < 0: none
-    auto runword = [&](const int4 &hq) {  // this lane's run: one word per lane (short runs) or per 8 lanes (medium)
-        return (hq.y & 0xffff) ? a.sent[hq.z + ((hq.y >> 16) ? lane >> 3 : lane)] : 0u;
+    // this lane's run words (wave-uniform shape): K 16-bit words (short runs), or {row, length} of its
+    // medium run (8 lanes each)
+    auto runword = [&](const int4 &hq) {
+        uint4 e = make_uint4(0u, 0u, 0u, 0u);
+        if (!(hq.y & 0xffff))
+            return e;
+        const unsigned short *w = a.sent + hq.z;
+        if (hq.y >> 16)
+            e.x = reinterpret_cast<const unsigned *>(w)[lane >> 3];
+        else if (!PACK)
+            e.x = w[lane];
+        else if (hq.w == 8)
+            e = reinterpret_cast<const uint4 *>(w)[lane];
+        else if (hq.w == 4) {
+            const uint2 u = reinterpret_cast<const uint2 *>(w)[lane];
+            e.x = u.x;
+            e.y = u.y;
+        } else if (hq.w == 2)
+            e.x = reinterpret_cast<const unsigned *>(w)[lane];
+        else
+            e.x = w[lane];
+        return e;
     };
     auto load8 = [&](const int4 &hq, Sl &d) {  // slot pairs: one 16-B value load, one 4-B column load; an odd last slot alone
         const int Lm = hq.y & 0xffff, pairs = Lm >> 1;  // wave-uniform
@@ -340,7 +361,7 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
     };
     int qa = -1, sa = -1, qb = -1, sb = -1;
     int4 h0 = make_int4(0, 0, 0, 0), h1 = make_int4(0, 0, 0, 0);
-    unsigned e0 = 0;
+    uint4 e0 = make_uint4(0u, 0u, 0u, 0u);
     Sl d0, d1;
     if (bd.z < bd.w)
         fetch_x(segd(bd.z).x);
@@ -391,20 +412,41 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
         }
         while (qa >= 0 && sa == sg) {  // wave-uniform
             load8(h1, d1);
-            const unsigned e1 = runword(h1);
+            const uint4 e1 = runword(h1);
             int qc, sc;
             nxt(qb, sb, qc, sc);
             const int4 h2 = meta(qc);
-            const int row = (int)(e0 & 0xffffu), len = (int)(e0 >> 16);
-            if (!(h0.y >> 16)) {  // wave-uniform: a slice of 64 short runs, lane = run, in CSR order
-                double acc = len > 0 ? yacc[row] : 0.0;
+            // K short runs of <= ST slots per lane, each continuing its row's sum in CSR order
+            auto short_runs = [&](auto KC, auto STC) {
+                constexpr int K = decltype(KC)::value, ST = decltype(STC)::value;
+                const unsigned ew[4] = {e0.x, e0.y, e0.z, e0.w};
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    const double pv = d0.v[j] * xs[d0.c[j]];
-                    acc += j < len ? pv : 0.0;  // acc never -0.0 (sums start at +0.0): adding +0.0 is exact
+                for (int k = 0; k < K; ++k) {
+                    const unsigned wd = (ew[k >> 1] >> (16 * (k & 1))) & 0xffffu;
+                    const int row = (int)(wd & 0xfffu), len = (int)(wd >> 12);
+                    double acc = len > 0 ? yacc[row] : 0.0;
+#pragma unroll
+                    for (int j = 0; j < ST; ++j) {
+                        const double pv = d0.v[k * ST + j] * xs[d0.c[k * ST + j]];
+                        acc += j < len ? pv : 0.0;  // acc never -0.0 (sums start at +0.0): adding +0.0 is exact
+                    }
+                    if (len > 0)
+                        yacc[row] = acc;
                 }
-                if (len > 0)
-                    yacc[row] = acc;
+            };
+            const int row = (int)(e0.x & 0xffffu), len = (int)(e0.x >> 16);  // medium
+            if (!(h0.y >> 16)) {  // wave-uniform: a slice of short runs, K per lane, in CSR order
+                const int pk = PACK ? h0.w : 1;
+                if (pk == 8)
+                    short_runs(std::integral_constant<int, 8>{}, std::integral_constant<int, 1>{});
+                else if (pk == 4)
+                    short_runs(std::integral_constant<int, 4>{}, std::integral_constant<int, 2>{});
+                else if (pk == 2 && (h0.y & 0xffff) == 6)
+                    short_runs(std::integral_constant<int, 2>{}, std::integral_constant<int, 3>{});
+                else if (pk == 2)
+                    short_runs(std::integral_constant<int, 2>{}, std::integral_constant<int, 4>{});
+                else
+                    short_runs(std::integral_constant<int, 1>{}, std::integral_constant<int, 8>{});
             } else {  // 8 medium runs, 8 lanes each: lane-strided sums, a fixed xor butterfly
                 double s = 0.0;
 #pragma unroll
@@ -483,10 +525,15 @@ hipError_t launch_slab(mspmv_handle_s *h, const TilePlan &plan, const double *d_
     const bool nt = stream_nt(h);
     const dim3 grid(plan.num_tiles);
     if (s.cfg == 2) {
-        if (nt)
-            hipLaunchKernelGGL((k_spmv_sell<true>), grid, dim3(kSlabCfgs[2].threads), 0, h->stream, a);
+        const dim3 tb(kSlabCfgs[2].threads);
+        if (nt && s.pack)
+            hipLaunchKernelGGL((k_spmv_sell<true, true>), grid, tb, 0, h->stream, a);
+        else if (nt)
+            hipLaunchKernelGGL((k_spmv_sell<true, false>), grid, tb, 0, h->stream, a);
+        else if (s.pack)
+            hipLaunchKernelGGL((k_spmv_sell<false, true>), grid, tb, 0, h->stream, a);
         else
-            hipLaunchKernelGGL((k_spmv_sell<false>), grid, dim3(kSlabCfgs[2].threads), 0, h->stream, a);
+            hipLaunchKernelGGL((k_spmv_sell<false, false>), grid, tb, 0, h->stream, a);
         return hipGetLastError();
     }
     const dim3 b1(kSlabCfgs[1].threads), b0(kSlabCfgs[0].threads);
@@ -504,9 +551,10 @@ hipError_t launch_slab(mspmv_handle_s *h, const TilePlan &plan, const double *d_
 std::string slab_kernel_name(const mspmv_handle_s *h)
 {
     const auto it = h->plans.find(kSlabPlanKey);
-    const int cfg = it != h->plans.end() && it->second.slab ? it->second.slab->cfg : 0;
+    const SlabData *sd = it != h->plans.end() ? it->second.slab : nullptr;
+    const int cfg = sd ? sd->cfg : 0;
     if (cfg == 2)
-        return std::string("k_spmv_sell<") + (stream_nt(h) ? "true" : "false") + ">";
+        return std::string("k_spmv_sell<") + (stream_nt(h) ? "true" : "false") + "," + (sd->pack ? "true" : "false") + ">";
     return std::string("k_spmv_slab<") + (stream_nt(h) ? "true" : "false") + "," + std::to_string(cfg) + ">";
 }
 
@@ -797,13 +845,18 @@ static mspmv_status slab_finish(mspmv_handle_s *h, TilePlan &p, int cfg, int gro
 // listed apart in pieces of <= 512 values, the others sorted by length (longest first, rows ascending among equals) and cut into
 // slices of 64, value j of the slice's run i at slot j of lane i -- slots in pairs, pair p of lane i at
 // 2 (64 p + i): one 16-B value load and one 4-B column load per pair; an odd last slot alone, lane i at
-// 128 p + i (slots past a run's length: zeros, never added).  Each slice's header {value base, slots per
-// lane | medium << 16, run-word base}; run words (row | length << 16) one per lane for slices of short
-// runs, one per run (8) for medium ones.  Bases relative to the block.
+// 128 p + i (slots past a run's length: zeros, never added).  With `pack` (the skewed plans' column groups;
+// a band's runs are mostly medium, and its kernel measured 5 % slower with the unpacking) short runs of
+// length <= 4 are packed K to a lane (kSellPack: 1 -> 8 runs of 1 slot, 2 -> 4 of 2, 3 -> 2 of 3, 4 -> 2 of 4; run k of lane i in slots
+// [k stride, (k + 1) stride)), so a slice of 64 K runs still fills ~8 slots per lane: a power-law block's
+// slices then hold 3x the bytes each and a wave's pipeline keeps that much more in flight.  Each slice's
+// header {value base, slots per lane | medium << 16, run-word base, K}; run words are 16-bit: short runs
+// row | length << 12, lane i's K words at i K + k; medium runs two per run, {row, length}.  Bases
+// relative to the block; run-word bases multiples of 8 (the K = 8 words are one 16-B load).
 struct SellBlockOut {
     std::vector<int4> segs;
     std::vector<int4> slices;
-    std::vector<unsigned> sents;
+    std::vector<unsigned short> sents;
     std::vector<int4> longs;
     std::vector<double> val;
     std::vector<unsigned short> col;
@@ -812,7 +865,7 @@ struct SellBlockOut {
 };
 
 static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, const std::vector<double> &va, int r0,
-                       int r1, int lo, int hi, SellBlockOut &o)
+                       int r1, int lo, int hi, bool pack, SellBlockOut &o)
 {
     // Slabs are cut from the block's own first column (round 6), not from column 0: a band block's
     // 2 x band + rows columns then take ceil(width / W) slabs, where globally aligned ones took one more about
@@ -888,30 +941,36 @@ static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, c
         if ((int)o.longs.size() - long0 > kSellMaxPieces)
             o.too_many = true;
         std::stable_sort(shorts.begin(), shorts.end(), [](const Run &x, const Run &y) { return x.len > y.len; });
-        for (size_t i0 = 0; i0 < shorts.size(); i0 += 64) {
-            const int n = (int)std::min<size_t>(64, shorts.size() - i0);
-            const int Lm = shorts[i0].len, e0 = (int)o.sents.size();
+        for (size_t i0 = 0; i0 < shorts.size();) {
+            const int Lmax = shorts[i0].len;
+            const bool pk = pack && Lmax <= 4;
+            const int K = pk ? kSellPack[Lmax].x : 1, stride = pk ? kSellPack[Lmax].y : Lmax;
+            const int S = K * stride;  // slots per lane
+            const int n = (int)std::min<size_t>((size_t)64 * K, shorts.size() - i0);
+            o.sents.resize((o.sents.size() + 7) & ~(size_t)7, 0);
+            const int e0 = (int)o.sents.size();
+            o.sents.resize(o.sents.size() + (size_t)64 * K, 0);
             const size_t base = o.val.size();
-            o.val.resize(base + (size_t)Lm * 64, 0.0);
-            o.col.resize(base + (size_t)Lm * 64, 0);
-            for (int i = 0; i < 64; ++i) {
-                if (i >= n) {
-                    o.sents.push_back(0u);
-                    continue;
-                }
-                const Run &r = shorts[i0 + (size_t)i];
+            o.val.resize(base + (size_t)S * 64, 0.0);
+            o.col.resize(base + (size_t)S * 64, 0);
+            for (int t = 0; t < n; ++t) {  // run t: lane t % 64, its k = t / 64
+                const Run &r = shorts[i0 + (size_t)t];
+                const int i = t % 64, k = t / 64;
                 for (int j = 0; j < r.len; ++j)
-                    put_val(slot_at(base, Lm, j, i), r.first + j);
-                o.sents.push_back((unsigned)r.row | ((unsigned)r.len << 16));
+                    put_val(slot_at(base, S, k * stride + j, i), r.first + j);
+                o.sents[(size_t)e0 + (size_t)i * K + k] = (unsigned short)(r.row | (r.len << 12));
             }
-            o.slices.push_back(make_int4((int)base, Lm, e0, 0));
+            o.slices.push_back(make_int4((int)base, S, e0, K));
+            i0 += (size_t)n;
         }
         // medium runs: 8 per slice, 8 lanes each (slots as above) -- value j of the slice's run r at slot j / 8, lane
         // 8 r + j % 8 (header length | 1 << 16: slots per lane, the medium flag)
         std::stable_sort(mediums.begin(), mediums.end(), [](const Run &x, const Run &y) { return x.len > y.len; });
         for (size_t i0 = 0; i0 < mediums.size(); i0 += 8) {
             const int n = (int)std::min<size_t>(8, mediums.size() - i0);
-            const int Lm = (mediums[i0].len + 7) / 8, e0 = (int)o.sents.size();
+            const int Lm = (mediums[i0].len + 7) / 8;
+            o.sents.resize((o.sents.size() + 7) & ~(size_t)7, 0);
+            const int e0 = (int)o.sents.size();
             const size_t base = o.val.size();
             o.val.resize(base + (size_t)Lm * 64, 0.0);
             o.col.resize(base + (size_t)Lm * 64, 0);
@@ -920,9 +979,10 @@ static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, c
                 if (r)
                     for (int j = 0; j < r->len; ++j)
                         put_val(slot_at(base, Lm, j / 8, 8 * i + j % 8), r->first + j);
-                o.sents.push_back(r ? (unsigned)r->row | ((unsigned)r->len << 16) : 0u);
+                o.sents.push_back(r ? (unsigned short)r->row : (unsigned short)0);
+                o.sents.push_back(r ? (unsigned short)r->len : (unsigned short)0);
             }
-            o.slices.push_back(make_int4((int)base, Lm | (1 << 16), e0, 0));
+            o.slices.push_back(make_int4((int)base, Lm | (1 << 16), e0, 1));
         }
         o.segs.push_back(make_int4(base, slice0, (int)o.slices.size(), long0));
         o.staged += (long long)W * 8;
@@ -944,10 +1004,10 @@ static mspmv_status sell_finish(mspmv_handle_s *h, TilePlan &p, const std::vecto
         (void)spg;
         (void)W;
         const int lo = (int)((long long)g * h->n / G), hi = g == G - 1 ? 0x7fffffff : (int)((long long)(g + 1) * h->n / G);
-        sell_block(ro, ci, va, rbs[(size_t)rb], rbs[(size_t)rb + 1], lo, hi, outs[(size_t)t]);
+        sell_block(ro, ci, va, rbs[(size_t)rb], rbs[(size_t)rb + 1], lo, hi, G > 1, outs[(size_t)t]);
     }
     std::vector<int4> blk((size_t)T), segs, longs, slices;
-    std::vector<unsigned> sents;
+    std::vector<unsigned short> sents;
     std::vector<double> val;
     std::vector<unsigned short> col;
     long long staged = 0;
@@ -957,11 +1017,12 @@ static mspmv_status sell_finish(mspmv_handle_s *h, TilePlan &p, const std::vecto
             sents.size() + o.sents.size() > (size_t)0x7fffff00)
             return MSPMV_ERR_UNSUPPORTED;
         const int vb = (int)val.size(), sb = (int)slices.size(), lb = (int)longs.size(), g0 = (int)segs.size();
+        sents.resize((sents.size() + 7) & ~(size_t)7, 0);  // run-word bases stay multiples of 8
         const int eb = (int)sents.size();
         for (int4 s : o.segs)
             segs.push_back(make_int4(s.x, s.y + sb, s.z + sb, s.w + lb));
         for (int4 s : o.slices)
-            slices.push_back(make_int4(s.x + vb, s.y, s.z + eb, 0));
+            slices.push_back(make_int4(s.x + vb, s.y, s.z + eb, s.w));
         for (int4 l : o.longs)
             longs.push_back(make_int4(l.x + vb, l.y, l.z, l.w));
         sents.insert(sents.end(), o.sents.begin(), o.sents.end());
@@ -975,6 +1036,7 @@ static mspmv_status sell_finish(mspmv_handle_s *h, TilePlan &p, const std::vecto
     SlabData *s = new SlabData();
     s->cfg = 2;
     s->groups = G;
+    s->pack = G > 1;
     s->num_chunks = (int)segs.size() - 1;
     s->num_entries = (int)longs.size();
     s->x_bytes_per_nnz = (double)staged / (double)h->nnz;

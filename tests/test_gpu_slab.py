@@ -20,8 +20,8 @@ from gpu_common import check_parity
 pytestmark = pytest.mark.gpu
 
 
-SLAB_KERNEL = {"1": "k_spmv_slab<{nt},0>", "2": "k_spmv_slab<{nt},1>", "4": "k_spmv_sell<{nt}>",
-               "4g1": "k_spmv_sell<{nt}>"}
+SLAB_KERNEL = {"1": "k_spmv_slab<{nt},0>", "2": "k_spmv_slab<{nt},1>", "4": "k_spmv_sell<{nt},true>",
+               "4g1": "k_spmv_sell<{nt},false>"}
 
 
 @pytest.fixture(params=["1", "2", "4", "4g1"], ids=["band", "groups", "sell", "sell_one_group"])
