@@ -301,13 +301,15 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
     // medium run (8 lanes each)
     auto runword = [&](const int4 &hq) {
         uint4 e = make_uint4(0u, 0u, 0u, 0u);
+        const unsigned short *w = a.sent + hq.z;
+        if (!PACK) {  // one {row, length} word per lane or per medium run: one load, no branches (r06hh: 5 % on bands)
+            e.x = (hq.y & 0xffff) ? reinterpret_cast<const unsigned *>(w)[(hq.y >> 16) ? lane >> 3 : lane] : 0u;
+            return e;
+        }
         if (!(hq.y & 0xffff))
             return e;
-        const unsigned short *w = a.sent + hq.z;
         if (hq.y >> 16)
             e.x = reinterpret_cast<const unsigned *>(w)[lane >> 3];
-        else if (!PACK)
-            e.x = w[lane];
         else if (hq.w == 8)
             e = reinterpret_cast<const uint4 *>(w)[lane];
         else if (hq.w == 4) {
@@ -434,9 +436,18 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
                         yacc[row] = acc;
                 }
             };
-            const int row = (int)(e0.x & 0xffffu), len = (int)(e0.x >> 16);  // medium
-            if (!(h0.y >> 16)) {  // wave-uniform: a slice of short runs, K per lane, in CSR order
-                const int pk = PACK ? h0.w : 1;
+            const int row = (int)(e0.x & 0xffffu), len = (int)(e0.x >> 16);  // medium, or short unpacked
+            if (!PACK && !(h0.y >> 16)) {  // wave-uniform: a slice of 64 short runs, lane = run, in CSR order
+                double acc = len > 0 ? yacc[row] : 0.0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const double pv = d0.v[j] * xs[d0.c[j]];
+                    acc += j < len ? pv : 0.0;  // acc never -0.0 (sums start at +0.0): adding +0.0 is exact
+                }
+                if (len > 0)
+                    yacc[row] = acc;
+            } else if (!(h0.y >> 16)) {  // wave-uniform: a slice of short runs, K per lane, in CSR order
+                const int pk = h0.w;
                 if (pk == 8)
                     short_runs(std::integral_constant<int, 8>{}, std::integral_constant<int, 1>{});
                 else if (pk == 4)
@@ -850,8 +861,9 @@ static mspmv_status slab_finish(mspmv_handle_s *h, TilePlan &p, int cfg, int gro
 // length <= 4 are packed K to a lane (kSellPack: 1 -> 8 runs of 1 slot, 2 -> 4 of 2, 3 -> 2 of 3, 4 -> 2 of 4; run k of lane i in slots
 // [k stride, (k + 1) stride)), so a slice of 64 K runs still fills ~8 slots per lane: a power-law block's
 // slices then hold 3x the bytes each and a wave's pipeline keeps that much more in flight.  Each slice's
-// header {value base, slots per lane | medium << 16, run-word base, K}; run words are 16-bit: short runs
-// row | length << 12, lane i's K words at i K + k; medium runs two per run, {row, length}.  Bases
+// header {value base, slots per lane | medium << 16, run-word base, K}; run words are 16-bit: packed short
+// runs row | length << 12, lane i's K words at i K + k; unpacked short runs and medium runs two per run,
+// {row, length}.  Bases
 // relative to the block; run-word bases multiples of 8 (the K = 8 words are one 16-B load).
 struct SellBlockOut {
     std::vector<int4> segs;
@@ -949,7 +961,7 @@ static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, c
             const int n = (int)std::min<size_t>((size_t)64 * K, shorts.size() - i0);
             o.sents.resize((o.sents.size() + 7) & ~(size_t)7, 0);
             const int e0 = (int)o.sents.size();
-            o.sents.resize(o.sents.size() + (size_t)64 * K, 0);
+            o.sents.resize(o.sents.size() + (size_t)64 * (pack ? K : 2), 0);
             const size_t base = o.val.size();
             o.val.resize(base + (size_t)S * 64, 0.0);
             o.col.resize(base + (size_t)S * 64, 0);
@@ -958,7 +970,12 @@ static void sell_block(const std::vector<int> &ro, const std::vector<int> &ci, c
                 const int i = t % 64, k = t / 64;
                 for (int j = 0; j < r.len; ++j)
                     put_val(slot_at(base, S, k * stride + j, i), r.first + j);
-                o.sents[(size_t)e0 + (size_t)i * K + k] = (unsigned short)(r.row | (r.len << 12));
+                if (pack) {
+                    o.sents[(size_t)e0 + (size_t)i * K + k] = (unsigned short)(r.row | (r.len << 12));
+                } else {  // {row, length}, as the medium runs' words
+                    o.sents[(size_t)e0 + 2 * (size_t)i] = (unsigned short)r.row;
+                    o.sents[(size_t)e0 + 2 * (size_t)i + 1] = (unsigned short)r.len;
+                }
             }
             o.slices.push_back(make_int4((int)base, S, e0, K));
             i0 += (size_t)n;
