@@ -258,6 +258,23 @@ __global__ __launch_bounds__(kSlabCfgs[CFG].threads) void k_spmv_slab(SlabArgs a
 // runs follow slab order: within a group the row sum is the CSR-order sum when its columns ascend).
 // Runs longer than kSellLongRun come in pieces of <= 512 values, one wave each (8 loads per lane, xor
 // butterfly) into lpart; after a barrier each run's pieces are added to its row in piece order.
+constexpr int kSellLabStampsEnd = 19;
+#ifdef MSPMV_SELL_LAB_STAMPS
+// Lab build only (tools/lab/sell_stamps.sh): thread 0 of each block records wall_clock64() at entry, per segment
+// (<= 6) after the x stage, after its wave's long pieces and after its wave's slices, and at exit.
+constexpr int kSellLabStamps = 20, kSellLabBlocks = 1024;
+__device__ unsigned long long g_sell_lab_stamps[kSellLabBlocks * kSellLabStamps];
+#define SELL_STAMP(b, i)                                                                              \
+    do {                                                                                              \
+        if (threadIdx.x == 0 && (b) < kSellLabBlocks && (i) < kSellLabStamps)                         \
+            g_sell_lab_stamps[(size_t)(b) * kSellLabStamps + (i)] = wall_clock64();                   \
+    } while (0)
+#else
+#define SELL_STAMP(b, i) \
+    do {                 \
+    } while (0)
+#endif
+
 template <bool NT, bool PACK>
 __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
 {
@@ -270,6 +287,7 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int b = xcd_tile(blockIdx.x, a.num_tiles);
+    SELL_STAMP(b, 0);
     const int4 bd = a.blk[b];  // {first row, rows, segment0, segment1}
     const int nrows = bd.y;
     // the block's segment descriptors (and the next one's piece start) in LDS: a scalar load at each
@@ -375,6 +393,7 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
         for (int j = 0; j < XPT; ++j)
             xs[tid + j * TB] = xq[j];
         __syncthreads();
+        SELL_STAMP(b, 1 + 3 * (sg - bd.z));
         if (sg + 1 < bd.w)
             fetch_x(segd(sg + 1).x);
         // long runs first (their loads in flight behind the slices of other waves): pieces of <= 512 values
@@ -400,6 +419,7 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
             if (lane == 0)
                 lpart[u - p0] = s;
         }
+        SELL_STAMP(b, 2 + 3 * (sg - bd.z));
         // slices, software-pipelined per wave and across segments: while slice qa computes, the wave's
         // next slice's values and run words and the one after's header are in flight -- at a segment's end
         // those are the next segment's first slices, so the pipeline refills during the x-stage barriers
@@ -480,6 +500,7 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
             sb = sc;
             h1 = h2;
         }
+        SELL_STAMP(b, 3 + 3 * (sg - bd.z));
         if (p1 > p0) {  // block-uniform: each run's pieces, in order, onto its row
             __syncthreads();
             for (int i = tid; i < p1 - p0; i += TB) {
@@ -497,10 +518,12 @@ __global__ __launch_bounds__(kSlabCfgs[2].threads) void k_spmv_sell(SlabArgs a)
     __syncthreads();
     if (a.groups > 1) {  // block-uniform
         group_out<TB>(a, b, bd.x, nrows, yacc);
+        SELL_STAMP(b, kSellLabStampsEnd);
         return;
     }
     for (int i = tid; i < nrows; i += TB)
         a.y[bd.x + i] = yacc[i];
+    SELL_STAMP(b, kSellLabStampsEnd);
 }
 
 hipError_t launch_slab(mspmv_handle_s *h, const TilePlan &plan, const double *d_x, double *d_y)
@@ -558,6 +581,16 @@ hipError_t launch_slab(mspmv_handle_s *h, const TilePlan &plan, const double *d_
         hipLaunchKernelGGL((k_spmv_slab<false, 0>), grid, b0, 0, h->stream, a);
     return hipGetLastError();
 }
+
+#ifdef MSPMV_SELL_LAB_STAMPS
+extern "C" __attribute__((visibility("default"))) int mspmv_lab_sell_stamps(unsigned long long *host, int n)
+{
+    const int m = std::min(n, kSellLabBlocks * kSellLabStamps);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sell_lab_stamps), sizeof(unsigned long long) * (size_t)m) == hipSuccess
+               ? m
+               : -1;
+}
+#endif
 
 std::string slab_kernel_name(const mspmv_handle_s *h)
 {
