@@ -258,8 +258,8 @@ __global__ __launch_bounds__(kSlabCfgs[CFG].threads) void k_spmv_slab(SlabArgs a
 // runs follow slab order: within a group the row sum is the CSR-order sum when its columns ascend).
 // Runs longer than kSellLongRun come in pieces of <= 512 values, one wave each (8 loads per lane, xor
 // butterfly) into lpart; after a barrier each run's pieces are added to its row in piece order.
-constexpr int kSellLabStampsEnd = 19;
 #ifdef MSPMV_SELL_LAB_STAMPS
+constexpr int kSellLabStampsEnd = 19;
 // Lab build only (tools/lab/sell_stamps.sh): thread 0 of each block records wall_clock64() at entry, per segment
 // (<= 6) after the x stage, after its wave's long pieces and after its wave's slices, and at exit.
 constexpr int kSellLabStamps = 20, kSellLabBlocks = 1024;
@@ -586,7 +586,12 @@ hipError_t launch_slab(mspmv_handle_s *h, const TilePlan &plan, const double *d_
 extern "C" __attribute__((visibility("default"))) int mspmv_lab_sell_stamps(unsigned long long *host, int n)
 {
     const int m = std::min(n, kSellLabBlocks * kSellLabStamps);
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sell_lab_stamps), sizeof(unsigned long long) * (size_t)m) == hipSuccess
+    static const std::vector<unsigned long long> zero((size_t)kSellLabBlocks * kSellLabStamps, 0ull);
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sell_lab_stamps), sizeof(unsigned long long) * (size_t)m) != hipSuccess)
+        return -1;
+    // cleared for the next matrix (a block with fewer segments leaves the earlier matrix's slots otherwise)
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_sell_lab_stamps), zero.data(), sizeof(unsigned long long) * zero.size()) ==
+                   hipSuccess
                ? m
                : -1;
 }

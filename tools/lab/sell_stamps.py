@@ -31,6 +31,7 @@ def analyse(name, a):
     x = np.random.default_rng(3).uniform(-1, 1, a.num_cols)
     with mspmv.GpuCsr(a) as g:
         for _ in range(6):
+            stamps()  # cleared: the last launch's stamps only
             g.spmv(x)
         S = stamps()
         kname = g.kernel_name()
